@@ -1,0 +1,115 @@
+"""Parameter tree of one RRIN U-Net, key-compatible with the reference.
+
+The reference U-Net (`/root/reference/unet.py:9-95`) is only used here for
+its *parameter naming*: a checkpoint written by the reference `train.py:158-161`
+must load with ``load_state_dict(strict=True)`` (`convert.py:103`).  The
+arithmetic is NOT done by these modules — `rrin_amd.engine` walks the tree and
+launches HIP kernels with the packed weights.  The modules therefore carry no
+``forward``; they are plain containers whose attribute paths reproduce the
+reference key layout:
+
+    down_path.{i}.block.{0,2}.{weight,bias}          unet.py:23-28, 59-63
+    midconv.{weight,bias}                            unet.py:29
+    up_path.{j}.up.1.{weight,bias}                   unet.py:31-36, 76-79
+    up_path.{j}.conv_block.block.{0,2}.{weight,bias} unet.py:80, 59-63
+    last.{weight,bias}                               unet.py:38
+
+Channel plan (``wf=5``): level i has ``2**(5+i)`` channels (unet.py:26).
+"""
+from __future__ import annotations
+
+import torch
+from torch import nn
+
+WF = 5                 # unet.py:15 default width factor
+LEAKY_SLOPE = 0.1      # unet.py:47,60,63
+
+
+def level_channels(i: int) -> int:
+    return 2 ** (WF + i)
+
+
+def _conv3x3(cin: int, cout: int) -> nn.Conv2d:
+    return nn.Conv2d(cin, cout, kernel_size=3, padding=1)
+
+
+class _TwoConv(nn.Module):
+    """conv3x3 -> leaky -> conv3x3 -> leaky; params at ``block.0`` / ``block.2``
+    (reference UNetConvBlock, unet.py:54-69)."""
+
+    def __init__(self, cin: int, cout: int):
+        super().__init__()
+        self.block = nn.Sequential(_conv3x3(cin, cout), nn.LeakyReLU(LEAKY_SLOPE),
+                                   _conv3x3(cout, cout), nn.LeakyReLU(LEAKY_SLOPE))
+
+
+class _UpStage(nn.Module):
+    """bilinear x2 -> conv3x3 (no act), concat with bridge, _TwoConv
+    (reference UNetUpBlock, unet.py:72-95)."""
+
+    def __init__(self, cin: int, cout: int):
+        super().__init__()
+        self.up = nn.Sequential(nn.Upsample(mode="bilinear", scale_factor=2),
+                                _conv3x3(cin, cout))
+        self.conv_block = _TwoConv(cin, cout)
+
+
+class UNet(nn.Module):
+    """Same constructor contract as reference ``UNet(in_channels, n_classes,
+    depth, wf=5, padding=True)`` (unet.py:10-17)."""
+
+    def __init__(self, in_channels: int = 1, n_classes: int = 2, depth: int = 5,
+                 wf: int = WF, padding: bool = True):
+        super().__init__()
+        if wf != WF or not padding:
+            raise ValueError("RRIN uses wf=5 and padding=True only")
+        self.in_channels = in_channels
+        self.n_classes = n_classes
+        self.depth = depth
+        widths = [level_channels(i) for i in range(depth)]
+        ins = [in_channels] + widths[:-1]
+        self.down_path = nn.ModuleList(_TwoConv(a, b) for a, b in zip(ins, widths))
+        self.midconv = _conv3x3(widths[-1], widths[-1])
+        self.up_path = nn.ModuleList(
+            _UpStage(widths[i + 1], widths[i]) for i in reversed(range(depth - 1)))
+        self.last = _conv3x3(widths[0], n_classes)
+
+    # -- helpers used by the engine --------------------------------------
+    def conv_list(self):
+        """All convs in execution order with a role tag (used for packing)."""
+        out = []
+        for i, d in enumerate(self.down_path):
+            out.append((f"down{i}.a", d.block[0]))
+            out.append((f"down{i}.b", d.block[2]))
+        out.append(("mid", self.midconv))
+        for j, u in enumerate(self.up_path):
+            out.append((f"up{j}.up", u.up[1]))
+            out.append((f"up{j}.a", u.conv_block.block[0]))
+            out.append((f"up{j}.b", u.conv_block.block[2]))
+        out.append(("last", self.last))
+        return out
+
+    def forward(self, x):  # pragma: no cover - guarded
+        raise RuntimeError("rrin_amd.UNet is a parameter container; run rrin_amd.Net "
+                           "(HIP engine) instead of calling a sub-UNet directly")
+
+
+def conv_flops(unet: UNet, h: int, w: int) -> int:
+    """Algorithmic FLOPs (2*MAC) of one UNet forward at input size h x w."""
+    total = 0
+    for tag, conv in unet.conv_list():
+        lvl = _level_of(unet, tag)
+        hh, ww = h >> lvl, w >> lvl
+        total += 2 * conv.out_channels * conv.in_channels * 9 * hh * ww
+    return total
+
+
+def _level_of(unet: UNet, tag: str) -> int:
+    if tag.startswith("down"):
+        return int(tag[4:tag.index(".")])
+    if tag == "mid":
+        return unet.depth - 1
+    if tag.startswith("up"):
+        j = int(tag[2:tag.index(".")])
+        return unet.depth - 2 - j
+    return 0  # last
