@@ -1,0 +1,188 @@
+#!/usr/bin/env python3
+"""RRIN inference throughput on MI355X (BASELINE.json metric).
+
+One step = one ``Net.forward`` over this rank's batch of synthetic 1280x720
+fp32 frame pairs (inputs already resident in HBM) + the RCCL all-gather that
+reassembles the interpolated frames of all ranks (rrin_amd.shard).  Weak
+scaling: every rank owns ``--batch`` pairs per step.
+
+  python bench.py [--gpus N --steps K --warmup W --batch B --height H --width W]
+  torchrun --nproc-per-node N bench.py --gpus N ...   (driver, N > 1)
+
+Rank 0 prints one JSON line.  ``roofline`` is for the dominant kernel (the
+MFMA conv3x3 family): algorithmic conv FLOPs / summed conv launch time, both
+measured live with HIP events recorded around every launch of the timed
+steps; ``cpu_baseline`` times the CPU oracle (oracle/, a restatement of the
+reference op sequence) on a bounded sample on this host.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+from rrin_amd import Net, _lib  # noqa: E402
+from rrin_amd.shard import gather_frames  # noqa: E402
+from rrin_amd.synthetic import keyed_state_dict, synthetic_batch  # noqa: E402
+from rrin_amd.unet import conv_flops  # noqa: E402
+
+FP32_PEAK_TFLOPS = 157.3   # MI355X dense fp32 (MFMA 32x32x2 f32 = VALU rate), MI355X_MICROARCH.md
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=4, help="frame pairs per GPU per step")
+    ap.add_argument("--height", type=int, default=720)
+    ap.add_argument("--width", type=int, default=1280)
+    ap.add_argument("--t", type=float, default=0.5)
+    ap.add_argument("--no-prof", action="store_true", help="skip the per-launch event profiler")
+    ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
+    ap.add_argument("--cpu-pairs", type=int, default=2, help="pairs timed on the CPU baseline")
+    return ap.parse_args()
+
+
+def cpu_baseline(sd, h, w, pairs):
+    from oracle.ref_net import net_forward  # checker / baseline only
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    i0, i1 = synthetic_batch(1, h, w, first_index=0)
+    with torch.no_grad():
+        net_forward(sd, i0[:, :, :64, :64].contiguous(), i1[:, :, :64, :64].contiguous(), 0.5)  # warm
+        t0 = time.perf_counter()
+        for _ in range(pairs):
+            net_forward(sd, i0, i1, 0.5)
+        dt = time.perf_counter() - t0
+    return {"value": pairs / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
+            "sample": f"{pairs} x Net.forward {w}x{h} N=1 fp32 on PyTorch-CPU (oracle/ref_net.py), "
+                      f"{dt:.1f} s"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    net = Net()
+    sd = keyed_state_dict(net.state_dict())
+    net.load_state_dict(sd, strict=True)
+    net = net.to(dev).eval()
+    B, H, W = args.batch, args.height, args.width
+    i0, i1 = synthetic_batch(B, H, W, first_index=rank * B)
+    i0, i1 = i0.to(dev), i1.to(dev)
+    gathered = torch.empty((world * B, 3, H, W), device=dev) if world > 1 else None
+    eng = net.engine()
+    lib = _lib.lib()
+
+    def step(prof=None):
+        with torch.no_grad():
+            out = eng.forward(i0, i1, args.t, prof=prof)
+            if world > 1:
+                gather_frames(out, out=gathered)
+        return out
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+
+    prof = None
+    cap = 0
+    if not args.no_prof:
+        cap = 100 * args.steps
+        h = C.c_void_p()
+        _lib.check(lib.rrin_prof_create(cap, C.byref(h)), "rrin_prof_create")
+        prof = h.value
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(prof)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    roofline = None
+    conv_ms_step = head_ms_step = None
+    if prof is not None:
+        kinds = (C.c_int32 * cap)()
+        ms = (C.c_float * cap)()
+        fl = (C.c_double * cap)()
+        cnt = C.c_int32()
+        _lib.check(lib.rrin_prof_read(prof, kinds, ms, fl, cap, C.byref(cnt)), "rrin_prof_read")
+        n = cnt.value
+        conv_ms = sum(ms[i] for i in range(n) if kinds[i] == 0)
+        conv_fl = sum(fl[i] for i in range(n) if kinds[i] == 0)
+        head_ms = sum(ms[i] for i in range(n) if kinds[i] == 1)
+        conv_launches = sum(1 for i in range(n) if kinds[i] == 0)
+        lib.rrin_prof_destroy(prof)
+        conv_ms_step = conv_ms / args.steps
+        head_ms_step = head_ms / args.steps
+        achieved = conv_fl / (conv_ms * 1e-3) / 1e12
+        roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS,
+                    "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": None,
+                    "kernel": "conv3x3_mfma_kernel (all 77 body convs, v_mfma_f32_32x32x2_f32)",
+                    "flops_per_launch_avg": conv_fl / max(conv_launches, 1),
+                    "avg_launch_ms": conv_ms / max(conv_launches, 1),
+                    "conv_ms_per_step": round(conv_ms_step, 3),
+                    "head_ms_per_step": round(head_ms_step, 3)}
+
+    pairs = world * B * args.steps
+    value = pairs / elapsed
+    res = {
+        "metric": "interpolated frames/sec at 1280x720 fp32 (Net.forward, frame pairs/s)",
+        "value": round(value, 3),
+        "unit": "frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (key-seeded weights, randint/255 frame pairs; SURVEY §8c-d)",
+        "config": {"workload": f"RRIN Net.forward {W}x{H} fp32, {B} pairs/GPU/step, t={args.t}, "
+                               f"+ all-gather of outputs",
+                   "global_batch": world * B, "height": H, "width": W,
+                   "parallelism": f"frame-batch dp{world}",
+                   "gflop_per_pair": round(sum(conv_flops(getattr(net, u), H, W)
+                                               for u in ("Flow", "refine_flow", "Mask", "final")) / 1e9, 1)},
+        "roofline": roofline,
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and args.cpu_baseline == "auto":
+        res["cpu_baseline"] = cpu_baseline({k: v.detach().cpu() for k, v in sd.items()}, H, W, args.cpu_pairs)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,177 @@
+/*
+ * rrin_hip.h — C ABI of librrin_hip.so, the MI355X (gfx950) kernels of the
+ * RRIN inference hot path (reference `Net.forward`, /root/reference/model.py:59-65).
+ *
+ * Rules of the boundary:
+ *   - plain C types only: device pointers, sizes, a hipStream_t passed as void*;
+ *   - no allocation inside the library: every buffer (activations, workspace,
+ *     packed weights) is owned by the caller (the Python host layer uses the
+ *     PyTorch caching allocator);
+ *   - every entry returns int: 0 = ok, > 0 = a hipError_t, < 0 = RRIN_E_* for a
+ *     violated shape/argument precondition; rrin_strerror() decodes it;
+ *   - stateless and stream-ordered: calls only enqueue work on `stream`.
+ *
+ * Activation layout used between kernels ("padded planar", PP): per image and
+ * channel a plane of hp x wp fp32 with hp = round_up(h,16)+2, wp = round_up(w,32)+8;
+ * pixel (y,x) lives at (y+1)*wp + (x+4); everything else is zero and is never
+ * written.  See DESIGN.md §3.
+ */
+#ifndef RRIN_HIP_H
+#define RRIN_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RRIN_ABI_VERSION 1
+
+#define RRIN_OK 0
+#define RRIN_E_SHAPE (-1)     /* H or W not a multiple of 16, or N < 1          */
+#define RRIN_E_ARG (-2)       /* null pointer / bad enum / channel range         */
+#define RRIN_E_WORKSPACE (-3) /* workspace smaller than rrin_net_workspace_bytes */
+#define RRIN_E_CONFIG (-4)    /* no kernel instance for the requested tile cfg   */
+
+/* ---- Planar geometry --------------------------------------------------- */
+typedef struct rrin_geom {
+  int32_t h, w;      /* logical size                       */
+  int32_t hp, wp;    /* padded plane size (see header)      */
+  int64_t plane;     /* hp*wp (floats)                      */
+} rrin_geom;
+
+/* Fill a geometry for an h x w level. */
+int rrin_make_geom(int32_t h, int32_t w, rrin_geom* g);
+
+/* A PP tensor view: base points at channel 0 of image 0. */
+typedef struct rrin_pp {
+  float* base;
+  int64_t img_stride; /* floats between images   */
+  int32_t ch_off;     /* first channel of the view */
+  int32_t channels;   /* channels in the view     */
+  rrin_geom g;
+} rrin_pp;
+
+/* ---- Conv 3x3 (MFMA, exact fp32) ---------------------------------------- */
+/* Replaces nn.Conv2d(k=3,pad=1)+bias (unet.py:29,59,62,78), LeakyReLU(0.1)
+ * (unet.py:47,60,63), F.avg_pool2d(x,2) (unet.py:46, fused as a second output),
+ * nn.Upsample(bilinear,x2) (unet.py:77, fused into the input staging) and
+ * torch.cat(up,bridge) (unet.py:93, by channel-offset addressing). */
+enum rrin_src_mode { RRIN_SRC_DIRECT = 0, RRIN_SRC_UPSAMPLE2X = 1 };
+enum rrin_epi_mode { RRIN_EPI_LINEAR = 0, RRIN_EPI_LEAKY = 1, RRIN_EPI_LEAKY_POOL = 2 };
+
+typedef struct rrin_conv_desc {
+  int32_t n;            /* images                                              */
+  int32_t cin, cout;    /* real channel counts                                  */
+  int32_t cfg;          /* tile config id (rrin_conv_cfg_bm); pack with same bm */
+  int32_t src_mode;     /* rrin_src_mode; UPSAMPLE2X: src is at (h/2, w/2)      */
+  int32_t epi_mode;     /* rrin_epi_mode                                        */
+  float slope;          /* leaky slope (0.1)                                    */
+  rrin_pp src;          /* input view (cin channels from src.ch_off)           */
+  rrin_pp dst;          /* output view (cout channels from dst.ch_off), h x w  */
+  rrin_pp pool;         /* EPI_LEAKY_POOL: pooled output (h/2 x w/2)           */
+  const float* wpack;   /* rrin_pack_conv3x3 output for this cfg              */
+  const float* bias;    /* padded bias (rrin_pack_conv3x3 output)              */
+} rrin_conv_desc;
+
+int rrin_conv_cfg_count(void);
+int rrin_conv_cfg_bm(int32_t cfg);          /* output-channel tile of a config  */
+int rrin_conv_cfg_th(int32_t cfg);          /* output-row tile of a config       */
+int rrin_conv3x3_fwd(const rrin_conv_desc* d, void* stream);
+
+/* Host-side weight packing (CPU memory).  w: OIHW [cout][cin][3][3] fp32,
+ * b: [cout].  perm (nullable): packed input channel c reads reference channel
+ * perm[c].  Output sizes from rrin_pack_conv3x3_floats(). */
+int64_t rrin_pack_conv3x3_floats(int32_t cout, int32_t cin, int32_t bm);
+int64_t rrin_pack_bias_floats(int32_t cout, int32_t bm);
+int rrin_pack_conv3x3(const float* w, const float* b, int32_t cout, int32_t cin, int32_t bm,
+                      const int32_t* perm, float* wpack, float* bpack);
+
+/* ---- Head convs (Cout <= 4) with the fused Net glue ---------------------- */
+/* One VALU conv3x3 32->{4,4,2,3} fused with the model.py glue that consumes it:
+ *   FLOW   (Flow.last)        : t-blend of flows, model.py:37-39
+ *   REFINE (refine_flow.last) : flow residual + two backwarps, model.py:44-48,8-21
+ *   MASK   (Mask.last)        : sigmoid + weighted blend, model.py:52-55
+ *   FINAL  (final.last)       : residual add + clamp to the NCHW output, model.py:62-63
+ * g16 is the 16-channel Net buffer [x0(3) x1(3) Ft0(2) Ft1(2) xt1(3) xt2(3)]. */
+enum rrin_head_mode { RRIN_HEAD_PLAIN = 0, RRIN_HEAD_FLOW = 1, RRIN_HEAD_REFINE = 2,
+                      RRIN_HEAD_MASK = 3, RRIN_HEAD_FINAL = 4 };
+
+typedef struct rrin_head_desc {
+  int32_t n, cin, cout, mode;
+  rrin_pp src;           /* cin-channel PP input                              */
+  rrin_pp g16;           /* Net buffer (modes FLOW..FINAL); PLAIN: dst view    */
+  const float* w;        /* OIHW [cout][cin][3][3] (unpacked)                 */
+  const float* bias;     /* [cout]                                            */
+  const float* coef;     /* [n][8] per-image t coefficients   */
+  float* out;            /* FINAL: NCHW [n][3][h][w] contiguous               */
+} rrin_head_desc;
+
+int rrin_head_fwd(const rrin_head_desc* d, void* stream);
+
+/* ---- Layout kernels ------------------------------------------------------- */
+/* NCHW contiguous [n][c][h][w] <-> PP view (c channels at dst.ch_off). */
+int rrin_nchw_to_pp(const float* src, int32_t n, int32_t c, const rrin_pp* dst, void* stream);
+int rrin_pp_to_nchw(const rrin_pp* src, int32_t n, int32_t c, float* dst, void* stream);
+
+/* Standalone backwarp (model.py:8-21): out = grid_sample(img, grid(flow)),
+ * NCHW contiguous fp32; same device code as the fused REFINE head. */
+int rrin_warp_fwd(const float* img, const float* flow, float* out, int32_t n, int32_t c,
+                  int32_t h, int32_t w, void* stream);
+
+/* ---- Whole forward (native schedule) ------------------------------------- */
+/* Per-conv weight table entry, in Net conv order (rrin_net_conv_count). */
+typedef struct rrin_conv_weights {
+  const float* wpack;   /* packed with bm = rrin_conv_cfg_bm(cfg)   */
+  const float* bias;    /* packed bias                              */
+  int32_t cfg;
+  int32_t pad_;
+} rrin_conv_weights;
+
+typedef struct rrin_head_weights {
+  const float* w;       /* OIHW, unpacked */
+  const float* bias;
+} rrin_head_weights;
+
+/* Optional launch profiler: HIP events recorded around every kernel the
+ * schedule enqueues (bench.py uses it to time the MFMA conv kernels inside the
+ * timed region).  Opaque; created/destroyed by the caller. */
+typedef struct rrin_prof rrin_prof;
+enum rrin_launch_kind { RRIN_KIND_CONV = 0, RRIN_KIND_HEAD = 1, RRIN_KIND_LAYOUT = 2 };
+
+int rrin_prof_create(int32_t capacity, rrin_prof** out);
+int rrin_prof_destroy(rrin_prof* p);
+int rrin_prof_reset(rrin_prof* p);
+/* After the stream has synchronised: per recorded launch its kind, elapsed
+ * milliseconds and algorithmic FLOPs (2*MAC of the conv; 0 for layout). */
+int rrin_prof_read(rrin_prof* p, int32_t* kinds, float* ms, double* flops, int32_t cap, int32_t* count);
+
+typedef struct rrin_net_desc {
+  int32_t n, h, w, pad_;
+  const float* i0;      /* NCHW [n][3][h][w] */
+  const float* i1;
+  float* out;           /* NCHW [n][3][h][w] */
+  const float* coef;    /* device [n][8] t coefficients */
+  /* 4 UNets in execution order Flow, refine_flow, Mask, final; convs of each
+   * in UNet order (down a/b per level, mid, up/a/b per level; `last` excluded) */
+  const rrin_conv_weights* convs;  /* host array, rrin_net_conv_count() entries */
+  const rrin_head_weights* heads;  /* host array of 4 */
+  void* workspace;      /* device, >= rrin_net_workspace_bytes, zero-filled once */
+  int64_t workspace_bytes;
+  int32_t skip_flow;    /* 1: reuse the Ft0/Ft1 already in the workspace (same pair) */
+  int32_t pad2_;
+  rrin_prof* prof;      /* nullable: record events around every launch */
+} rrin_net_desc;
+
+int rrin_net_conv_count(void);                 /* 77 = 81 convs - 4 heads      */
+int64_t rrin_net_workspace_bytes(int32_t n, int32_t h, int32_t w);
+int rrin_net_fwd(const rrin_net_desc* d, void* stream);
+
+/* ---- Misc ---------------------------------------------------------------- */
+int rrin_abi_version(void);
+const char* rrin_strerror(int code);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RRIN_HIP_H */

@@ -1,0 +1,121 @@
+"""ctypes binding of ``librrin_hip.so`` (C ABI declared in include/rrin_hip.h).
+
+The library is built in-tree (``make`` or ``__graft_entry__.build()``) and
+loaded from ``rrin_amd/librrin_hip.so``.  There is no fallback: if the library
+is missing or its ABI version differs, ``lib()`` raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+ABI_VERSION = 1
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "librrin_hip.so")
+
+# enums (rrin_hip.h)
+SRC_DIRECT, SRC_UPSAMPLE2X = 0, 1
+EPI_LINEAR, EPI_LEAKY, EPI_LEAKY_POOL = 0, 1, 2
+HEAD_PLAIN, HEAD_FLOW, HEAD_REFINE, HEAD_MASK, HEAD_FINAL = 0, 1, 2, 3, 4
+
+
+class Geom(C.Structure):
+    _fields_ = [("h", C.c_int32), ("w", C.c_int32), ("hp", C.c_int32), ("wp", C.c_int32),
+                ("plane", C.c_int64)]
+
+
+class PP(C.Structure):
+    _fields_ = [("base", C.c_void_p), ("img_stride", C.c_int64), ("ch_off", C.c_int32),
+                ("channels", C.c_int32), ("g", Geom)]
+
+
+class ConvDesc(C.Structure):
+    _fields_ = [("n", C.c_int32), ("cin", C.c_int32), ("cout", C.c_int32), ("cfg", C.c_int32),
+                ("src_mode", C.c_int32), ("epi_mode", C.c_int32), ("slope", C.c_float),
+                ("src", PP), ("dst", PP), ("pool", PP), ("wpack", C.c_void_p), ("bias", C.c_void_p)]
+
+
+class HeadDesc(C.Structure):
+    _fields_ = [("n", C.c_int32), ("cin", C.c_int32), ("cout", C.c_int32), ("mode", C.c_int32),
+                ("src", PP), ("g16", PP), ("w", C.c_void_p), ("bias", C.c_void_p),
+                ("coef", C.c_void_p), ("out", C.c_void_p)]
+
+
+class ConvWeights(C.Structure):
+    _fields_ = [("wpack", C.c_void_p), ("bias", C.c_void_p), ("cfg", C.c_int32), ("pad_", C.c_int32)]
+
+
+class HeadWeights(C.Structure):
+    _fields_ = [("w", C.c_void_p), ("bias", C.c_void_p)]
+
+
+class NetDesc(C.Structure):
+    _fields_ = [("n", C.c_int32), ("h", C.c_int32), ("w", C.c_int32), ("pad_", C.c_int32),
+                ("i0", C.c_void_p), ("i1", C.c_void_p), ("out", C.c_void_p), ("coef", C.c_void_p),
+                ("convs", C.POINTER(ConvWeights)), ("heads", C.POINTER(HeadWeights)),
+                ("workspace", C.c_void_p), ("workspace_bytes", C.c_int64),
+                ("skip_flow", C.c_int32), ("pad2_", C.c_int32), ("prof", C.c_void_p)]
+
+
+# every symbol include/rrin_hip.h declares: name -> (restype, argtypes)
+SIGNATURES = {
+    "rrin_make_geom": (C.c_int, [C.c_int32, C.c_int32, C.POINTER(Geom)]),
+    "rrin_conv_cfg_count": (C.c_int, []),
+    "rrin_conv_cfg_bm": (C.c_int, [C.c_int32]),
+    "rrin_conv_cfg_th": (C.c_int, [C.c_int32]),
+    "rrin_conv3x3_fwd": (C.c_int, [C.POINTER(ConvDesc), C.c_void_p]),
+    "rrin_pack_conv3x3_floats": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32]),
+    "rrin_pack_bias_floats": (C.c_int64, [C.c_int32, C.c_int32]),
+    "rrin_pack_conv3x3": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32,
+                                    C.c_void_p, C.c_void_p, C.c_void_p]),
+    "rrin_head_fwd": (C.c_int, [C.POINTER(HeadDesc), C.c_void_p]),
+    "rrin_nchw_to_pp": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.POINTER(PP), C.c_void_p]),
+    "rrin_pp_to_nchw": (C.c_int, [C.POINTER(PP), C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]),
+    "rrin_warp_fwd": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_int32,
+                                C.c_int32, C.c_int32, C.c_void_p]),
+    "rrin_net_conv_count": (C.c_int, []),
+    "rrin_net_workspace_bytes": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32]),
+    "rrin_net_fwd": (C.c_int, [C.POINTER(NetDesc), C.c_void_p]),
+    "rrin_prof_create": (C.c_int, [C.c_int32, C.POINTER(C.c_void_p)]),
+    "rrin_prof_destroy": (C.c_int, [C.c_void_p]),
+    "rrin_prof_reset": (C.c_int, [C.c_void_p]),
+    "rrin_prof_read": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32,
+                                 C.POINTER(C.c_int32)]),
+    "rrin_abi_version": (C.c_int, []),
+    "rrin_strerror": (C.c_char_p, [C.c_int]),
+}
+
+_LIB = None
+
+
+class RRINError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load (once) and return the library; raises if it is absent."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise RRINError(f"{LIB_PATH} not built: run `make -j16` (or __graft_entry__.build()); "
+                            "rrin_amd has no non-HIP fallback")
+        h = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(h, name)
+            f.restype = res
+            f.argtypes = args
+        if h.rrin_abi_version() != ABI_VERSION:
+            raise RRINError(f"librrin_hip ABI {h.rrin_abi_version()} != expected {ABI_VERSION}")
+        _LIB = h
+    return _LIB
+
+
+def check(rc: int, what: str = "rrin"):
+    if rc != 0:
+        msg = lib().rrin_strerror(rc)
+        raise RRINError(f"{what} failed ({rc}): {msg.decode() if msg else '?'}")
+
+
+def geom(h: int, w: int) -> Geom:
+    g = Geom()
+    check(lib().rrin_make_geom(h, w, C.byref(g)), "rrin_make_geom")
+    return g

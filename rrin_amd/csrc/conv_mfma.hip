@@ -1,0 +1,417 @@
+// conv3x3 (pad 1) + bias [+ LeakyReLU] [+ fused 2x2 avg-pool output]
+// [+ fused bilinear x2 upsample of the input] as an implicit GEMM on the gfx950
+// f32-input matrix cores (v_mfma_f32_32x32x2_f32: exact fp32, fmaf chain).
+//
+// Replaces, per SURVEY.md §8(a) rows a6-a9:
+//   nn.Conv2d(k=3,pad=1)       /root/reference/unet.py:29,59,62,78
+//   LeakyReLU(0.1)             unet.py:47,60,63  (epilogue)
+//   F.avg_pool2d(x,2)          unet.py:46        (second output of the epilogue)
+//   nn.Upsample(bilinear,x2)   unet.py:77        (input staging)
+//   torch.cat((up,bridge),1)   unet.py:93        (channel-offset addressing)
+//
+// GEMM view: D[co][p] = sum_k W[co][k] * X[k][p], k = (ci, ky, kx).
+// A block owns BM output channels x (TH rows x 32 cols) output pixels and walks
+// K in chunks of 8 input channels x 9 taps.  Per chunk it stages into LDS
+//   input  [8 ch][TH+2 rows][40 cols]  (cols x0-4 .. x0+35, 16-B vector loads)
+//   weight [8 ch][9 taps][BM]          (pre-packed, one contiguous slab)
+// double-buffered with register prefetch of chunk c+1 during the MFMAs of c.
+// One 32x32x2 MFMA covers a channel PAIR at one tap: lanes 0-31 carry channel
+// 2p, lanes 32-63 channel 2p+1, so every operand read is one conflict-free
+// ds_read_b32 with a compile-time immediate offset.
+#include "common.hpp"
+
+namespace rrin {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+struct ConvArgs {
+  const float* src;
+  int64_t src_img, src_plane;
+  int src_wp, src_h, src_w;     // src logical size (h/2,w/2 when upsampling)
+  int cin, nchunks;
+  float* dst;
+  int64_t dst_img, dst_plane;
+  int dst_wp, cout;
+  float* pool;
+  int64_t pool_img, pool_plane;
+  int pool_wp;
+  const float* wpack;
+  const float* bias;
+  int h, w;                     // output size
+  int co_blocks, tiles_x, tiles_y, n;
+  float slope;
+};
+
+constexpr int CK = 8;     // input channels per K chunk
+constexpr int LC = 40;    // LDS row length (floats): cols x0-4 .. x0+35
+
+template <int WAVES_M, int WAVES_N, int WM, int WN>
+struct Tile {
+  static constexpr int BM = 32 * WM * WAVES_M;
+  static constexpr int TH = WN * WAVES_N;
+  static constexpr int ROWS = TH + 2;
+  static constexpr int IN_F = CK * ROWS * LC;
+  static constexpr int W_F = CK * 9 * BM;
+  static constexpr int IN_V4 = IN_F / 4;
+  static constexpr int W_V4 = W_F / 4;
+  static constexpr int IN_IT = (IN_V4 + 255) / 256;
+  static constexpr int W_IT = (W_V4 + 255) / 256;
+  static constexpr size_t LDS_BYTES = 2 * (size_t)(IN_F + W_F) * sizeof(float);
+  static_assert(WAVES_M * WAVES_N == 4, "4 waves per block");
+  static_assert(16 % TH == 0, "TH must divide the 16-row plane padding");
+};
+
+// Bilinear x2 (align_corners=False) source index along one axis:
+// src = max((d + 0.5) * 0.5 - 0.5, 0); i0 = floor(src); i1 = min(i0 + 1, n - 1).
+__device__ inline void up_axis(int d, int n, int& i0, int& i1, float& l1) {
+  float s = fmaxf(((float)d + 0.5f) * 0.5f - 0.5f, 0.0f);
+  i0 = (int)s;
+  l1 = s - (float)i0;
+  i1 = min(i0 + 1, n - 1);
+}
+
+template <int WAVES_M, int WAVES_N, int WM, int WN, int SRC, int EPI>
+__global__ void __launch_bounds__(256) conv3x3_mfma_kernel(ConvArgs a) {
+  using T = Tile<WAVES_M, WAVES_N, WM, WN>;
+  constexpr int BM = T::BM, TH = T::TH, ROWS = T::ROWS;
+  constexpr int IN_F = T::IN_F, W_F = T::W_F;
+
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* s_in = smem;            // [2][IN_F]
+  float* s_w = smem + 2 * IN_F;  // [2][W_F]
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave % WAVES_M;
+  const int wn = wave / WAVES_M;
+  const int j = lane & 31;
+  const int hh = lane >> 5;
+
+  int bid = blockIdx.x;
+  const int cob = bid % a.co_blocks;
+  bid /= a.co_blocks;
+  const int tx = bid % a.tiles_x;
+  bid /= a.tiles_x;
+  const int ty = bid % a.tiles_y;
+  const int img = bid / a.tiles_y;
+  const int x0 = tx * 32;
+  const int y0 = ty * TH;
+
+  const float* src_img = a.src + img * a.src_img;
+  const float* wsrc = a.wpack + (int64_t)cob * a.nchunks * W_F;
+
+  float4 rin[T::IN_IT];
+  float4 rw[T::W_IT];
+
+  auto load_w = [&](int c) {
+    const float4* g = reinterpret_cast<const float4*>(wsrc + (int64_t)c * W_F);
+#pragma unroll
+    for (int it = 0; it < T::W_IT; ++it) {
+      const int idx = tid + 256 * it;
+      if (idx < T::W_V4) rw[it] = g[idx];
+    }
+  };
+  auto store_w = [&](int buf) {
+    float4* s = reinterpret_cast<float4*>(s_w + buf * W_F);
+#pragma unroll
+    for (int it = 0; it < T::W_IT; ++it) {
+      const int idx = tid + 256 * it;
+      if (idx < T::W_V4) s[idx] = rw[it];
+    }
+  };
+  // DIRECT: rectangular copy of padded rows y0..y0+ROWS-1, cols x0..x0+39.
+  auto load_in = [&](int c) {
+#pragma unroll
+    for (int it = 0; it < T::IN_IT; ++it) {
+      const int idx = tid + 256 * it;
+      if (idx < T::IN_V4) {
+        const int ci = idx / (ROWS * 10);
+        const int rem = idx - ci * (ROWS * 10);
+        const int r = rem / 10;
+        const int q = rem - r * 10;
+        const int ch = c * CK + ci;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (ch < a.cin)
+          v = *reinterpret_cast<const float4*>(src_img + (int64_t)ch * a.src_plane +
+                                               (int64_t)(y0 + r) * a.src_wp + x0 + 4 * q);
+        rin[it] = v;
+      }
+    }
+  };
+  auto store_in = [&](int buf) {
+    float4* s = reinterpret_cast<float4*>(s_in + buf * IN_F);
+#pragma unroll
+    for (int it = 0; it < T::IN_IT; ++it) {
+      const int idx = tid + 256 * it;
+      if (idx < T::IN_V4) s[idx] = rin[it];
+    }
+  };
+  // UPSAMPLE2X: value at hi-res (Y,X) = bilinear x2 of the low-res source,
+  // zero outside [0,h)x[0,w) (the conv's zero padding).
+  auto stage_up = [&](int c, int buf) {
+    float4* s = reinterpret_cast<float4*>(s_in + buf * IN_F);
+#pragma unroll
+    for (int it = 0; it < T::IN_IT; ++it) {
+      const int idx = tid + 256 * it;
+      if (idx < T::IN_V4) {
+        const int ci = idx / (ROWS * 10);
+        const int rem = idx - ci * (ROWS * 10);
+        const int r = rem / 10;
+        const int q = rem - r * 10;
+        const int ch = c * CK + ci;
+        const int Y = y0 - 1 + r;
+        float o[4] = {0.f, 0.f, 0.f, 0.f};
+        if (ch < a.cin && Y >= 0 && Y < a.h) {
+          int ya, yb;
+          float ly;
+          up_axis(Y, a.src_h, ya, yb, ly);
+          const float* p = src_img + (int64_t)ch * a.src_plane;
+          const float* ra = p + (int64_t)(ya + 1) * a.src_wp + 4;
+          const float* rb = p + (int64_t)(yb + 1) * a.src_wp + 4;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int X = x0 - 4 + 4 * q + e;
+            if (X >= 0 && X < a.w) {
+              int xa, xb;
+              float lx;
+              up_axis(X, a.src_w, xa, xb, lx);
+              const float top = (1.f - lx) * ra[xa] + lx * ra[xb];
+              const float bot = (1.f - lx) * rb[xa] + lx * rb[xb];
+              o[e] = (1.f - ly) * top + ly * bot;
+            }
+          }
+        }
+        s[idx] = make_float4(o[0], o[1], o[2], o[3]);
+      }
+    }
+  };
+
+  floatx16 acc[WM][WN];
+#pragma unroll
+  for (int mt = 0; mt < WM; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < WN; ++nt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[mt][nt][i] = 0.f;
+
+  auto compute = [&](int buf) {
+    const float* si = s_in + buf * IN_F + hh * ROWS * LC + (wn * WN) * LC + j + 3;
+    const float* sw = s_w + buf * W_F + hh * 9 * BM + (wm * WM) * 32 + j;
+#pragma unroll
+    for (int cp = 0; cp < CK / 2; ++cp) {
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky) {
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          float av[WM], bv[WN];
+#pragma unroll
+          for (int mt = 0; mt < WM; ++mt) av[mt] = sw[(2 * cp * 9 + ky * 3 + kx) * BM + mt * 32];
+#pragma unroll
+          for (int nt = 0; nt < WN; ++nt) bv[nt] = si[(2 * cp * ROWS + nt + ky) * LC + kx];
+#pragma unroll
+          for (int mt = 0; mt < WM; ++mt)
+#pragma unroll
+            for (int nt = 0; nt < WN; ++nt)
+              acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[mt], bv[nt], acc[mt][nt], 0, 0, 0);
+        }
+      }
+    }
+  };
+
+  // ---- prologue: chunk 0 into buffer 0
+  load_w(0);
+  if constexpr (SRC == RRIN_SRC_DIRECT) {
+    load_in(0);
+    store_in(0);
+  } else {
+    stage_up(0, 0);
+  }
+  store_w(0);
+  __syncthreads();
+
+  // ---- main K loop: prefetch c+1 into registers while the MFMAs run on c
+  for (int c = 0; c < a.nchunks; ++c) {
+    const int buf = c & 1;
+    const bool more = (c + 1) < a.nchunks;
+    if (more) {
+      load_w(c + 1);
+      if constexpr (SRC == RRIN_SRC_DIRECT) load_in(c + 1);
+    }
+    compute(buf);
+    if (more) {
+      if constexpr (SRC == RRIN_SRC_DIRECT)
+        store_in(buf ^ 1);
+      else
+        stage_up(c + 1, buf ^ 1);
+      store_w(buf ^ 1);
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue: bias, leaky, store (+ 2x2 average pool)
+  const int yb = y0 + wn * WN;
+  const int x = x0 + j;
+#pragma unroll
+  for (int mt = 0; mt < WM; ++mt) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int co = cob * BM + (wm * WM + mt) * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+      const float bias = a.bias[co];
+      float v[WN];
+#pragma unroll
+      for (int nt = 0; nt < WN; ++nt) {
+        float t = acc[mt][nt][i] + bias;
+        if constexpr (EPI != RRIN_EPI_LINEAR) t = t > 0.f ? t : t * a.slope;
+        v[nt] = t;
+        const int y = yb + nt;
+        if (co < a.cout && y < a.h && x < a.w)
+          a.dst[img * a.dst_img + (int64_t)co * a.dst_plane + (int64_t)(y + 1) * a.dst_wp + x + 4] = t;
+      }
+      if constexpr (EPI == RRIN_EPI_LEAKY_POOL) {
+#pragma unroll
+        for (int p = 0; p < WN / 2; ++p) {
+          float s = v[2 * p] + v[2 * p + 1];
+          s += __shfl_xor(s, 1);
+          const int y = yb + 2 * p;
+          if (!(j & 1) && co < a.cout && y < a.h && x < a.w)
+            a.pool[img * a.pool_img + (int64_t)co * a.pool_plane + (int64_t)(y / 2 + 1) * a.pool_wp +
+                   x / 2 + 4] = 0.25f * s;
+        }
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------
+// Config table.  cfg -> (WAVES_M, WAVES_N, WM, WN)
+//   0: BM 32,  TH 8   (1x4 waves, 32co x 2 rows each)
+//   1: BM 64,  TH 8   (1x4 waves, 64co x 2 rows each)
+//   2: BM 128, TH 4   (2x2 waves, 64co x 2 rows each)
+//   3: BM 32,  TH 16  (1x4 waves, 32co x 4 rows each)
+//   4: BM 64,  TH 4   (2x2 waves, 32co x 2 rows each)
+//   5: BM 128, TH 8   (1x4 waves, 128co x 2 rows each)
+#define RRIN_CONV_CFGS(X) \
+  X(0, 1, 4, 1, 2)        \
+  X(1, 1, 4, 2, 2)        \
+  X(2, 2, 2, 2, 2)        \
+  X(3, 1, 4, 1, 4)        \
+  X(4, 2, 2, 1, 2)        \
+  X(5, 1, 4, 4, 2)
+
+struct CfgInfo {
+  int bm, th;
+  size_t lds;
+};
+
+static const CfgInfo kCfg[] = {
+#define X(id, a, b, c, d) {Tile<a, b, c, d>::BM, Tile<a, b, c, d>::TH, Tile<a, b, c, d>::LDS_BYTES},
+    RRIN_CONV_CFGS(X)
+#undef X
+};
+static constexpr int kNumCfg = sizeof(kCfg) / sizeof(kCfg[0]);
+
+template <int A, int B, int C, int D, int SRC, int EPI>
+static int launch_t(const ConvArgs& args, int grid, hipStream_t st) {
+  using T = Tile<A, B, C, D>;
+  auto k = conv3x3_mfma_kernel<A, B, C, D, SRC, EPI>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)T::LDS_BYTES);
+    if (e != hipSuccess) return (int)e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(k, dim3(grid), dim3(256), T::LDS_BYTES, st, args);
+  return hip_code(hipGetLastError());
+}
+
+template <int A, int B, int C, int D>
+static int launch_cfg(const ConvArgs& args, int src, int epi, int grid, hipStream_t st) {
+  if (src == RRIN_SRC_DIRECT) {
+    if (epi == RRIN_EPI_LINEAR) return launch_t<A, B, C, D, RRIN_SRC_DIRECT, RRIN_EPI_LINEAR>(args, grid, st);
+    if (epi == RRIN_EPI_LEAKY) return launch_t<A, B, C, D, RRIN_SRC_DIRECT, RRIN_EPI_LEAKY>(args, grid, st);
+    return launch_t<A, B, C, D, RRIN_SRC_DIRECT, RRIN_EPI_LEAKY_POOL>(args, grid, st);
+  }
+  if (epi == RRIN_EPI_LINEAR) return launch_t<A, B, C, D, RRIN_SRC_UPSAMPLE2X, RRIN_EPI_LINEAR>(args, grid, st);
+  if (epi == RRIN_EPI_LEAKY) return launch_t<A, B, C, D, RRIN_SRC_UPSAMPLE2X, RRIN_EPI_LEAKY>(args, grid, st);
+  return launch_t<A, B, C, D, RRIN_SRC_UPSAMPLE2X, RRIN_EPI_LEAKY_POOL>(args, grid, st);
+}
+
+}  // namespace rrin
+
+using namespace rrin;
+
+extern "C" int rrin_conv_cfg_count(void) { return kNumCfg; }
+extern "C" int rrin_conv_cfg_bm(int32_t cfg) { return (cfg >= 0 && cfg < kNumCfg) ? kCfg[cfg].bm : RRIN_E_CONFIG; }
+extern "C" int rrin_conv_cfg_th(int32_t cfg) { return (cfg >= 0 && cfg < kNumCfg) ? kCfg[cfg].th : RRIN_E_CONFIG; }
+
+extern "C" int rrin_conv3x3_fwd(const rrin_conv_desc* d, void* stream) {
+  if (!d || !d->src.base || !d->dst.base || !d->wpack || !d->bias) return RRIN_E_ARG;
+  if (d->cfg < 0 || d->cfg >= kNumCfg) return RRIN_E_CONFIG;
+  if (d->n < 1 || d->cin < 1 || d->cout < 1) return RRIN_E_ARG;
+  if (d->src_mode != RRIN_SRC_DIRECT && d->src_mode != RRIN_SRC_UPSAMPLE2X) return RRIN_E_ARG;
+  if (d->epi_mode < RRIN_EPI_LINEAR || d->epi_mode > RRIN_EPI_LEAKY_POOL) return RRIN_E_ARG;
+  const CfgInfo& ci = kCfg[d->cfg];
+  const int h = d->dst.g.h, w = d->dst.g.w;
+  if (d->cin > d->src.channels || d->cout > d->dst.channels) return RRIN_E_ARG;
+  if (d->src_mode == RRIN_SRC_DIRECT) {
+    if (d->src.g.h != h || d->src.g.w != w) return RRIN_E_SHAPE;
+  } else {
+    if (d->src.g.h * 2 != h || d->src.g.w * 2 != w) return RRIN_E_SHAPE;
+  }
+  if (d->epi_mode == RRIN_EPI_LEAKY_POOL) {
+    if (!d->pool.base || (h & 1) || (w & 1) || d->pool.g.h * 2 != h || d->pool.g.w * 2 != w ||
+        d->cout > d->pool.channels)
+      return RRIN_E_SHAPE;
+  }
+  // plane geometry must be the library's (reads past w/h rely on the padding)
+  const rrin_geom gs = make_geom(d->src.g.h, d->src.g.w);
+  const rrin_geom gd = make_geom(h, w);
+  if (gs.wp != d->src.g.wp || gs.hp != d->src.g.hp || gd.wp != d->dst.g.wp || gd.hp != d->dst.g.hp)
+    return RRIN_E_SHAPE;
+
+  ConvArgs a;
+  a.src = d->src.base + (int64_t)d->src.ch_off * d->src.g.plane;
+  a.src_img = d->src.img_stride;
+  a.src_plane = d->src.g.plane;
+  a.src_wp = d->src.g.wp;
+  a.src_h = d->src.g.h;
+  a.src_w = d->src.g.w;
+  a.cin = d->cin;
+  a.nchunks = (d->cin + CK - 1) / CK;
+  a.dst = d->dst.base + (int64_t)d->dst.ch_off * d->dst.g.plane;
+  a.dst_img = d->dst.img_stride;
+  a.dst_plane = d->dst.g.plane;
+  a.dst_wp = d->dst.g.wp;
+  a.cout = d->cout;
+  a.pool = nullptr;
+  a.pool_img = a.pool_plane = 0;
+  a.pool_wp = 0;
+  if (d->epi_mode == RRIN_EPI_LEAKY_POOL) {
+    a.pool = d->pool.base + (int64_t)d->pool.ch_off * d->pool.g.plane;
+    a.pool_img = d->pool.img_stride;
+    a.pool_plane = d->pool.g.plane;
+    a.pool_wp = d->pool.g.wp;
+  }
+  a.wpack = d->wpack;
+  a.bias = d->bias;
+  a.h = h;
+  a.w = w;
+  a.co_blocks = (d->cout + ci.bm - 1) / ci.bm;
+  a.tiles_x = (w + 31) / 32;
+  a.tiles_y = (h + ci.th - 1) / ci.th;
+  a.n = d->n;
+  a.slope = d->slope;
+  const int64_t grid = (int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n;
+  if (grid > 0x7fffffff) return RRIN_E_SHAPE;
+  hipStream_t st = (hipStream_t)stream;
+  switch (d->cfg) {
+#define X(id, A, B, C, D) \
+  case id:                \
+    return launch_cfg<A, B, C, D>(a, d->src_mode, d->epi_mode, (int)grid, st);
+    RRIN_CONV_CFGS(X)
+#undef X
+  }
+  return RRIN_E_CONFIG;
+}

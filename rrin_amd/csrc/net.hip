@@ -1,0 +1,342 @@
+// Native forward schedule of RRIN Net (reference model.py:32-65, unet.py:40-51):
+// carves the caller's workspace into padded-planar activation buffers and
+// enqueues the 77 MFMA convs + 4 fused head convs + 1 input pack on one stream.
+// Also: host-side weight packing, error strings, ABI version.
+#include <string.h>
+
+#include <vector>
+
+#include "common.hpp"
+
+using namespace rrin;
+
+struct rrin_prof {
+  std::vector<hipEvent_t> ev;  // 2 per launch
+  std::vector<int32_t> kind;
+  std::vector<double> flops;
+  int count = 0;
+};
+
+namespace {
+
+// The four U-Nets in execution order (model.py:35,42,51,62) with the input
+// channel count they read from the 16-channel Net buffer g16 (starting at 0).
+struct UNetSpec {
+  int in_ch, out_ch, depth, head_mode;
+};
+constexpr UNetSpec kUNets[4] = {
+    {6, 4, 5, RRIN_HEAD_FLOW},     // Flow        = UNet(6, 4, 5)   model.py:28
+    {10, 4, 4, RRIN_HEAD_REFINE},  // refine_flow = UNet(10, 4, 4)  model.py:29
+    {16, 2, 4, RRIN_HEAD_MASK},    // Mask        = UNet(16, 2, 4)  model.py:27
+    {9, 3, 4, RRIN_HEAD_FINAL},    // final       = UNet(9, 3, 4)   model.py:30
+};
+constexpr int kMaxDepth = 5;
+
+inline int chans(int level) { return 32 << level; }  // unet.py:26, wf=5
+inline int convs_of(int depth) { return 2 * depth + 1 + 3 * (depth - 1); }
+
+struct Buf {
+  float* base;
+  int ch;
+  rrin_geom g;
+};
+
+// Workspace plan: offsets are identical in size query and forward.
+struct Plan {
+  int n;
+  rrin_geom g[kMaxDepth];
+  Buf G;                  // 16 ch at level 0
+  Buf X[kMaxDepth];       // level input (L >= 1): C_{L-1} ch
+  Buf T[kMaxDepth];       // first conv of a block: C_L ch
+  Buf CAT[kMaxDepth - 1]; // [up | bridge]: 2 C_L ch  (levels 0..3)
+  Buf BOT;                // Flow bottom (level 4) conv-b output: 512 ch
+  int64_t bytes;
+};
+
+int64_t align256(int64_t b) { return (b + 255) & ~(int64_t)255; }
+
+void make_plan(int n, int h, int w, char* base, Plan& p) {
+  p.n = n;
+  int64_t off = 0;
+  auto take = [&](int ch, const rrin_geom& g) {
+    Buf b;
+    b.base = base ? reinterpret_cast<float*>(base + off) : nullptr;
+    b.ch = ch;
+    b.g = g;
+    off += align256((int64_t)n * ch * g.plane * (int64_t)sizeof(float));
+    return b;
+  };
+  for (int L = 0; L < kMaxDepth; ++L) p.g[L] = make_geom(h >> L, w >> L);
+  p.G = take(16, p.g[0]);
+  for (int L = 0; L < kMaxDepth; ++L) {
+    p.X[L] = L ? take(chans(L - 1), p.g[L]) : Buf{nullptr, 0, p.g[0]};
+    p.T[L] = take(chans(L), p.g[L]);
+    if (L < kMaxDepth - 1) p.CAT[L] = take(2 * chans(L), p.g[L]);
+  }
+  p.BOT = take(chans(kMaxDepth - 1), p.g[kMaxDepth - 1]);
+  p.bytes = off;
+}
+
+rrin_pp view(const Buf& b, int n, int ch_off, int channels) {
+  rrin_pp v;
+  v.base = b.base;
+  v.img_stride = (int64_t)b.ch * b.g.plane;
+  v.ch_off = ch_off;
+  v.channels = channels;
+  v.g = b.g;
+  (void)n;
+  return v;
+}
+
+// Bracket one launch with profiler events (no-op without a profiler).
+struct ProfScope {
+  rrin_prof* p;
+  hipStream_t st;
+  int slot;
+  ProfScope(rrin_prof* p_, hipStream_t s, int kind, double flops) : p(p_), st(s), slot(-1) {
+    if (p && p->count < (int)p->kind.size()) {
+      slot = p->count++;
+      p->kind[slot] = kind;
+      p->flops[slot] = flops;
+      (void)hipEventRecord(p->ev[2 * slot], st);
+    }
+  }
+  ~ProfScope() {
+    if (slot >= 0) (void)hipEventRecord(p->ev[2 * slot + 1], st);
+  }
+};
+
+rrin_prof* g_prof = nullptr;  // set for the duration of one rrin_net_fwd call
+
+int conv(const Plan& p, const rrin_conv_weights& cw, int cin, int cout, int src_mode, int epi,
+         const rrin_pp& src, const rrin_pp& dst, const rrin_pp* pool, hipStream_t st) {
+  ProfScope ps(g_prof, st, RRIN_KIND_CONV, 2.0 * 9 * cin * cout * (double)dst.g.h * dst.g.w * p.n);
+  rrin_conv_desc d;
+  memset(&d, 0, sizeof(d));
+  d.n = p.n;
+  d.cin = cin;
+  d.cout = cout;
+  d.cfg = cw.cfg;
+  d.src_mode = src_mode;
+  d.epi_mode = epi;
+  d.slope = 0.1f;
+  d.src = src;
+  d.dst = dst;
+  if (pool) d.pool = *pool;
+  d.wpack = cw.wpack;
+  d.bias = cw.bias;
+  return rrin_conv3x3_fwd(&d, st);
+}
+
+#define RRIN_TRY(x)          \
+  do {                       \
+    int _rc = (x);           \
+    if (_rc != 0) return _rc; \
+  } while (0)
+
+// One U-Net (unet.py:40-51) from g16 channels [0, in_ch) to its head.
+int run_unet(const Plan& p, const UNetSpec& u, const rrin_conv_weights* cw, const rrin_head_weights& hw,
+             const rrin_net_desc* nd, hipStream_t st) {
+  const int D = u.depth;
+  int k = 0;
+  // ---- down path (unet.py:42-46)
+  for (int L = 0; L < D; ++L) {
+    const int C = chans(L);
+    const rrin_pp in = L ? view(p.X[L], p.n, 0, chans(L - 1)) : view(p.G, p.n, 0, u.in_ch);
+    const int cin = L ? chans(L - 1) : u.in_ch;
+    const rrin_pp t = view(p.T[L], p.n, 0, C);
+    RRIN_TRY(conv(p, cw[k++], cin, C, RRIN_SRC_DIRECT, RRIN_EPI_LEAKY, in, t, nullptr, st));
+    if (L < D - 1) {
+      const rrin_pp bridge = view(p.CAT[L], p.n, C, C);  // cat's second half (unet.py:93)
+      const rrin_pp pooled = view(p.X[L + 1], p.n, 0, C);
+      RRIN_TRY(conv(p, cw[k++], C, C, RRIN_SRC_DIRECT, RRIN_EPI_LEAKY_POOL, t, bridge, &pooled, st));
+    } else {
+      const Buf& bot = (L == kMaxDepth - 1) ? p.BOT : p.CAT[L];  // CAT[3] is free at depth 4
+      RRIN_TRY(conv(p, cw[k++], C, C, RRIN_SRC_DIRECT, RRIN_EPI_LEAKY, t, view(bot, p.n, 0, C), nullptr, st));
+      // midconv + leaky (unet.py:47) back into T[bottom]
+      RRIN_TRY(conv(p, cw[k++], C, C, RRIN_SRC_DIRECT, RRIN_EPI_LEAKY, view(bot, p.n, 0, C), t, nullptr, st));
+    }
+  }
+  // ---- up path (unet.py:48-49, 72-95)
+  rrin_pp x = view(p.T[D - 1], p.n, 0, chans(D - 1));
+  for (int L = D - 2; L >= 0; --L) {
+    const int C = chans(L);
+    const rrin_pp up = view(p.CAT[L], p.n, 0, C);
+    RRIN_TRY(conv(p, cw[k++], chans(L + 1), C, RRIN_SRC_UPSAMPLE2X, RRIN_EPI_LINEAR, x, up, nullptr, st));
+    const rrin_pp cat = view(p.CAT[L], p.n, 0, 2 * C);
+    const rrin_pp t = view(p.T[L], p.n, 0, C);
+    RRIN_TRY(conv(p, cw[k++], 2 * C, C, RRIN_SRC_DIRECT, RRIN_EPI_LEAKY, cat, t, nullptr, st));
+    RRIN_TRY(conv(p, cw[k++], C, C, RRIN_SRC_DIRECT, RRIN_EPI_LEAKY, t, up, nullptr, st));  // U_L
+    x = up;
+  }
+  // ---- last conv fused with the Net glue (unet.py:51 + model.py)
+  rrin_head_desc hd;
+  memset(&hd, 0, sizeof(hd));
+  hd.n = p.n;
+  hd.cin = 32;
+  hd.cout = u.out_ch;
+  hd.mode = u.head_mode;
+  hd.src = x;
+  hd.g16 = view(p.G, p.n, 0, 16);
+  hd.w = hw.w;
+  hd.bias = hw.bias;
+  hd.coef = nd->coef;
+  hd.out = nd->out;
+  ProfScope ps(g_prof, st, RRIN_KIND_HEAD, 2.0 * 9 * 32 * u.out_ch * (double)x.g.h * x.g.w * p.n);
+  return rrin_head_fwd(&hd, st);
+}
+
+}  // namespace
+
+extern "C" int rrin_make_geom(int32_t h, int32_t w, rrin_geom* g) {
+  if (!g || h < 1 || w < 1) return RRIN_E_ARG;
+  *g = make_geom(h, w);
+  return 0;
+}
+
+extern "C" int rrin_net_conv_count(void) {
+  int c = 0;
+  for (const auto& u : kUNets) c += convs_of(u.depth);
+  return c;
+}
+
+extern "C" int64_t rrin_net_workspace_bytes(int32_t n, int32_t h, int32_t w) {
+  if (n < 1 || h < 16 || w < 16 || (h % 16) || (w % 16)) return RRIN_E_SHAPE;
+  Plan p;
+  make_plan(n, h, w, nullptr, p);
+  return p.bytes;
+}
+
+extern "C" int rrin_net_fwd(const rrin_net_desc* d, void* stream) {
+  if (!d || !d->i0 || !d->i1 || !d->out || !d->coef || !d->convs || !d->heads || !d->workspace)
+    return RRIN_E_ARG;
+  if (d->n < 1 || d->h < 16 || d->w < 16 || (d->h % 16) || (d->w % 16)) return RRIN_E_SHAPE;
+  Plan p;
+  make_plan(d->n, d->h, d->w, reinterpret_cast<char*>(d->workspace), p);
+  if (d->workspace_bytes < p.bytes) return RRIN_E_WORKSPACE;
+  hipStream_t st = (hipStream_t)stream;
+
+  // x = cat(x0, x1) into g16 channels 0-5 (model.py:33)
+  const rrin_pp gx0 = view(p.G, p.n, 0, 3);
+  const rrin_pp gx1 = view(p.G, p.n, 3, 3);
+  if (d->skip_flow) return RRIN_E_ARG;  // Flow reuse across t: not built yet
+  g_prof = d->prof;
+  int rc = 0;
+  {
+    ProfScope ps(g_prof, st, RRIN_KIND_LAYOUT, 0.0);
+    rc = rrin_nchw_to_pp(d->i0, d->n, 3, &gx0, st);
+    if (!rc) rc = rrin_nchw_to_pp(d->i1, d->n, 3, &gx1, st);
+  }
+  int k = 0;
+  for (int u = 0; u < 4 && !rc; ++u) {
+    rc = run_unet(p, kUNets[u], d->convs + k, d->heads[u], d, st);
+    k += convs_of(kUNets[u].depth);
+  }
+  g_prof = nullptr;
+  return rc;
+}
+
+extern "C" int rrin_prof_create(int32_t capacity, rrin_prof** out) {
+  if (!out || capacity < 1) return RRIN_E_ARG;
+  rrin_prof* p = new rrin_prof();
+  p->ev.resize(2 * (size_t)capacity);
+  p->kind.resize(capacity);
+  p->flops.resize(capacity);
+  for (auto& e : p->ev) {
+    hipError_t r = hipEventCreate(&e);
+    if (r != hipSuccess) {
+      delete p;
+      return (int)r;
+    }
+  }
+  *out = p;
+  return 0;
+}
+
+extern "C" int rrin_prof_destroy(rrin_prof* p) {
+  if (!p) return RRIN_E_ARG;
+  for (auto& e : p->ev)
+    if (e) (void)hipEventDestroy(e);
+  delete p;
+  return 0;
+}
+
+extern "C" int rrin_prof_reset(rrin_prof* p) {
+  if (!p) return RRIN_E_ARG;
+  p->count = 0;
+  return 0;
+}
+
+extern "C" int rrin_prof_read(rrin_prof* p, int32_t* kinds, float* ms, double* flops, int32_t cap,
+                              int32_t* count) {
+  if (!p || !count) return RRIN_E_ARG;
+  const int n = p->count < cap ? p->count : cap;
+  for (int i = 0; i < n; ++i) {
+    if (kinds) kinds[i] = p->kind[i];
+    if (flops) flops[i] = p->flops[i];
+    if (ms) {
+      hipError_t r = hipEventElapsedTime(&ms[i], p->ev[2 * i], p->ev[2 * i + 1]);
+      if (r != hipSuccess) return (int)r;
+    }
+  }
+  *count = n;
+  return 0;
+}
+
+// ---- weight packing (host) ------------------------------------------------
+// wpack[cob][chunk][ci8][tap][bm]: the slab a block stages per K chunk is
+// contiguous; zero rows/cols pad cin to 8 and cout to bm.
+extern "C" int64_t rrin_pack_conv3x3_floats(int32_t cout, int32_t cin, int32_t bm) {
+  if (cout < 1 || cin < 1 || bm < 32 || bm % 32) return RRIN_E_ARG;
+  const int64_t cob = (cout + bm - 1) / bm, nch = (cin + 7) / 8;
+  return cob * nch * 8 * 9 * bm;
+}
+
+extern "C" int64_t rrin_pack_bias_floats(int32_t cout, int32_t bm) {
+  if (cout < 1 || bm < 32 || bm % 32) return RRIN_E_ARG;
+  return (int64_t)((cout + bm - 1) / bm) * bm;
+}
+
+extern "C" int rrin_pack_conv3x3(const float* w, const float* b, int32_t cout, int32_t cin, int32_t bm,
+                                 const int32_t* perm, float* wpack, float* bpack) {
+  if (!w || !b || !wpack || !bpack || cout < 1 || cin < 1 || bm < 32 || bm % 32) return RRIN_E_ARG;
+  if (perm)
+    for (int c = 0; c < cin; ++c)
+      if (perm[c] < 0 || perm[c] >= cin) return RRIN_E_ARG;
+  const int cob_n = (cout + bm - 1) / bm, nch = (cin + 7) / 8;
+  int64_t o = 0;
+  for (int cob = 0; cob < cob_n; ++cob)
+    for (int c = 0; c < nch; ++c)
+      for (int ci = 0; ci < 8; ++ci)
+        for (int tap = 0; tap < 9; ++tap)
+          for (int col = 0; col < bm; ++col) {
+            const int co = cob * bm + col, ch = c * 8 + ci;
+            float v = 0.f;
+            if (co < cout && ch < cin) {
+              const int src_ch = perm ? perm[ch] : ch;
+              v = w[((int64_t)co * cin + src_ch) * 9 + tap];
+            }
+            wpack[o++] = v;
+          }
+  for (int co = 0; co < cob_n * bm; ++co) bpack[co] = co < cout ? b[co] : 0.f;
+  return 0;
+}
+
+extern "C" int rrin_abi_version(void) { return RRIN_ABI_VERSION; }
+
+extern "C" const char* rrin_strerror(int code) {
+  switch (code) {
+    case RRIN_OK:
+      return "ok";
+    case RRIN_E_SHAPE:
+      return "rrin: shape precondition violated (H, W must be multiples of 16; N >= 1; views must match)";
+    case RRIN_E_ARG:
+      return "rrin: invalid argument (null pointer, mode or channel range)";
+    case RRIN_E_WORKSPACE:
+      return "rrin: workspace smaller than rrin_net_workspace_bytes()";
+    case RRIN_E_CONFIG:
+      return "rrin: unknown conv tile config";
+  }
+  if (code > 0) return hipGetErrorString((hipError_t)code);
+  return "rrin: unknown error";
+}

@@ -1,0 +1,173 @@
+"""HIP execution engine behind ``rrin_amd.Net.forward``.
+
+Responsibilities (host side only — every FLOP runs in librrin_hip.so):
+
+* pack the 77 body convs once per weight version into the MFMA slab layout
+  (``rrin_pack_conv3x3``, CPU) and upload them as one device blob; the first
+  convs of ``refine_flow`` and ``Mask`` get an input-channel permutation so
+  they can read the 16-channel Net buffer in its own order;
+* keep one zero-initialised workspace per (device, n, h, w) — the padding
+  of every padded-planar buffer stays zero because kernels never write it;
+* turn ``t`` into the per-image coefficient table with the reference's own
+  rounding (Python-float t: double then fp32; tensor t: fp32 tensor ops);
+* call ``rrin_net_fwd`` on torch's current stream.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from collections import OrderedDict
+
+import numpy as np
+import torch
+
+from . import _lib
+
+UNET_ORDER = ("Flow", "refine_flow", "Mask", "final")
+
+# g16 = [x0 0-2 | x1 3-5 | Ft0 6-7 | Ft1 8-9 | xt1 10-12 | xt2 13-15]; reference input orders:
+#   refine_flow: cat(Ft0, Ft1, x)            model.py:41
+#   Mask:        cat(Ft0, Ft1, x, xt1, xt2)  model.py:50
+# perm[c] = reference input channel read by buffer channel c.
+FIRST_CONV_PERM = {
+    "Flow": None,
+    "refine_flow": [4, 5, 6, 7, 8, 9, 0, 1, 2, 3],
+    "Mask": [4, 5, 6, 7, 8, 9, 0, 1, 2, 3, 10, 11, 12, 13, 14, 15],
+    "final": None,
+}
+
+
+def choose_cfg(cin: int, cout: int, level: int) -> int:
+    """Tile config id for one conv (see conv_mfma.hip config table)."""
+    if cout <= 32:
+        return 0        # BM 32 x TH 8
+    return 1            # BM 64 x TH 8
+
+
+def t_coefficients(t, n: int) -> torch.Tensor:
+    """[n, 8] fp32: -(1-t)t, t*t, (1-t)^2, t(1-t), 1-t, t, 0, 0 (model.py:38-39,54)."""
+    if isinstance(t, torch.Tensor) and t.numel() > 1:
+        tt = t.detach().to("cpu", torch.float32).reshape(-1)
+        if tt.numel() != n:
+            raise ValueError(f"t has {tt.numel()} elements for a batch of {n}")
+        one_m = 1 - tt
+        cols = [(-one_m) * tt, tt * tt, one_m * one_m, tt * one_m, one_m, tt]
+        c = torch.stack(cols + [torch.zeros_like(tt)] * 2, dim=1)
+    else:
+        tf = float(t.item()) if isinstance(t, torch.Tensor) else float(t)
+        if isinstance(t, torch.Tensor):  # 0-dim tensor: fp32 tensor arithmetic
+            tt = torch.tensor([tf], dtype=torch.float32)
+            one_m = 1 - tt
+            row = torch.cat([(-one_m) * tt, tt * tt, one_m * one_m, tt * one_m, one_m, tt,
+                             torch.zeros(2)])
+        else:  # Python float: double arithmetic, rounded once to fp32 (scalar * tensor)
+            row = torch.tensor([-(1 - tf) * tf, tf * tf, (1 - tf) * (1 - tf), tf * (1 - tf),
+                                1 - tf, tf, 0.0, 0.0], dtype=torch.float64).float()
+        c = row.view(1, 8).expand(n, 8).contiguous()
+    return c
+
+
+class RRINEngine:
+    MAX_WORKSPACES = 2
+
+    def __init__(self, net):
+        self.lib = _lib.lib()
+        params = list(net.parameters())
+        self.device = params[0].device
+        if self.device.type != "cuda":
+            raise RuntimeError("rrin_amd.Net: move the model to a ROCm device (net.cuda()) before "
+                               "forward — the HIP kernels are the only implementation")
+        L = self.lib
+        blobs, meta = [], []
+        off = 0
+        self.heads_t = []
+        for name in UNET_ORDER:
+            unet = getattr(net, name)
+            convs = unet.conv_list()
+            for idx, (tag, conv) in enumerate(convs):
+                w = conv.weight.detach().to("cpu", torch.float32).contiguous().numpy()
+                b = conv.bias.detach().to("cpu", torch.float32).contiguous().numpy()
+                cout, cin = w.shape[0], w.shape[1]
+                if tag == "last":
+                    self.heads_t.append((torch.from_numpy(w.copy()).to(self.device),
+                                         torch.from_numpy(b.copy()).to(self.device)))
+                    continue
+                level = int(tag[4]) if tag.startswith("down") else 0
+                cfg = choose_cfg(cin, cout, level)
+                bm = L.rrin_conv_cfg_bm(cfg)
+                nw = L.rrin_pack_conv3x3_floats(cout, cin, bm)
+                nb = L.rrin_pack_bias_floats(cout, bm)
+                wp = np.empty(nw, np.float32)
+                bp = np.empty(nb, np.float32)
+                perm = FIRST_CONV_PERM[name] if idx == 0 else None
+                perm_arr = np.asarray(perm, np.int32) if perm is not None else None
+                _lib.check(L.rrin_pack_conv3x3(w.ctypes.data, b.ctypes.data, cout, cin, bm,
+                                               perm_arr.ctypes.data if perm_arr is not None else None,
+                                               wp.ctypes.data, bp.ctypes.data), "rrin_pack_conv3x3")
+                meta.append((off, off + nw, cfg))
+                blobs += [wp, bp]
+                off += nw + nb
+                # keep 16-B alignment of every slab
+                pad = (-off) % 4
+                if pad:
+                    blobs.append(np.zeros(pad, np.float32))
+                    off += pad
+        if len(meta) != L.rrin_net_conv_count():
+            raise RuntimeError(f"packed {len(meta)} convs, library expects {L.rrin_net_conv_count()}")
+        self.blob = torch.from_numpy(np.concatenate(blobs)).to(self.device)
+        base = self.blob.data_ptr()
+        self.conv_table = (_lib.ConvWeights * len(meta))()
+        for i, (wo, bo, cfg) in enumerate(meta):
+            self.conv_table[i].wpack = base + 4 * wo
+            self.conv_table[i].bias = base + 4 * bo
+            self.conv_table[i].cfg = cfg
+        self.head_table = (_lib.HeadWeights * 4)()
+        for i, (w, b) in enumerate(self.heads_t):
+            self.head_table[i].w = w.data_ptr()
+            self.head_table[i].bias = b.data_ptr()
+        self.cfgs = [m[2] for m in meta]
+        self._ws = OrderedDict()
+
+    def workspace(self, n: int, h: int, w: int) -> torch.Tensor:
+        key = (n, h, w)
+        ws = self._ws.get(key)
+        if ws is None:
+            nbytes = self.lib.rrin_net_workspace_bytes(n, h, w)
+            if nbytes < 0:
+                _lib.check(int(nbytes), "rrin_net_workspace_bytes")
+            while len(self._ws) >= self.MAX_WORKSPACES:
+                self._ws.popitem(last=False)
+            ws = torch.zeros(int(nbytes), dtype=torch.uint8, device=self.device)
+            self._ws[key] = ws
+        else:
+            self._ws.move_to_end(key)
+        return ws
+
+    def forward(self, i0: torch.Tensor, i1: torch.Tensor, t=0.5, prof=None) -> torch.Tensor:
+        if i0.device != self.device or i1.device != self.device:
+            raise RuntimeError(f"inputs on {i0.device}/{i1.device}, model on {self.device}")
+        if i0.dtype != torch.float32 or i1.dtype != torch.float32:
+            raise TypeError("rrin_amd.Net computes in fp32; inputs must be float32")
+        if i0.dim() != 4 or i0.shape != i1.shape or i0.shape[1] != 3:
+            raise ValueError(f"expected two [N,3,H,W] tensors, got {tuple(i0.shape)} / {tuple(i1.shape)}")
+        n, _, h, w = i0.shape
+        if h % 16 or w % 16 or n < 1:
+            raise RuntimeError(f"H and W must be multiples of 16 (the Flow U-Net pools 4 times); "
+                               f"got {h}x{w} (reference fails at model.py:41)")
+        i0 = i0.contiguous()
+        i1 = i1.contiguous()
+        out = torch.empty_like(i0)
+        coef = t_coefficients(t, n).to(self.device, non_blocking=True)
+        with torch.cuda.device(self.device):
+            ws = self.workspace(n, h, w)
+            d = _lib.NetDesc()
+            d.n, d.h, d.w = n, h, w
+            d.i0, d.i1, d.out, d.coef = i0.data_ptr(), i1.data_ptr(), out.data_ptr(), coef.data_ptr()
+            d.convs = self.conv_table
+            d.heads = self.head_table
+            d.workspace = ws.data_ptr()
+            d.workspace_bytes = ws.numel()
+            d.skip_flow = 0
+            d.prof = prof
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+            _lib.check(self.lib.rrin_net_fwd(C.byref(d), C.c_void_p(stream)), "rrin_net_fwd")
+        return out

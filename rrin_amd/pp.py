@@ -1,0 +1,56 @@
+"""Padded-planar (PP) activation tensors on the device (layout: DESIGN.md §3).
+
+A PP tensor is a torch allocation ``[n, c, hp, wp]`` fp32 with
+``hp = round_up(h,16)+2``, ``wp = round_up(w,32)+8`` and pixel (y,x) at
+``[.., y+1, x+4]``; the padding is zero and never written by the kernels.
+Conversions to/from NCHW run the library's HIP layout kernels.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from . import _lib
+
+
+class PPTensor:
+    def __init__(self, n: int, c: int, h: int, w: int, device):
+        self.n, self.c, self.h, self.w = n, c, h, w
+        self.g = _lib.geom(h, w)
+        self.t = torch.zeros((n, c, self.g.hp, self.g.wp), dtype=torch.float32, device=device)
+
+    def view(self, ch_off: int = 0, channels: int | None = None) -> _lib.PP:
+        v = _lib.PP()
+        v.base = self.t.data_ptr()
+        v.img_stride = self.c * self.g.plane
+        v.ch_off = ch_off
+        v.channels = self.c - ch_off if channels is None else channels
+        v.g = self.g
+        return v
+
+    @classmethod
+    def from_nchw(cls, x: torch.Tensor, c_alloc: int | None = None, ch_off: int = 0) -> "PPTensor":
+        x = x.contiguous()
+        n, c, h, w = x.shape
+        pp = cls(n, c_alloc or c + ch_off, h, w, x.device)
+        pp.load(x, ch_off)
+        return pp
+
+    def load(self, x: torch.Tensor, ch_off: int = 0):
+        x = x.contiguous().float()
+        v = self.view(ch_off, x.shape[1])
+        _lib.check(_lib.lib().rrin_nchw_to_pp(C.c_void_p(x.data_ptr()), x.shape[0], x.shape[1],
+                                              C.byref(v), _stream(x.device)), "rrin_nchw_to_pp")
+
+    def to_nchw(self, ch_off: int = 0, channels: int | None = None) -> torch.Tensor:
+        channels = self.c - ch_off if channels is None else channels
+        out = torch.empty((self.n, channels, self.h, self.w), dtype=torch.float32, device=self.t.device)
+        v = self.view(ch_off, channels)
+        _lib.check(_lib.lib().rrin_pp_to_nchw(C.byref(v), self.n, channels, C.c_void_p(out.data_ptr()),
+                                              _stream(out.device)), "rrin_pp_to_nchw")
+        return out
+
+
+def _stream(device) -> C.c_void_p:
+    return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)

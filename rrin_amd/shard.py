@@ -1,0 +1,50 @@
+"""Frame-batch data parallelism: one process per GPU.
+
+Replaces the single-device dispatch of the reference caller
+(`/root/reference/convert.py:90-92,110,130`: ``model.cuda()`` and
+``model(img1.cuda(), img2.cuda(), t)``).  Frame pairs are independent, so a
+global batch of B pairs is split into contiguous shards of B/W pairs; each rank
+runs the HIP ``Net`` on its shard and the only exchange is one all-gather that
+reassembles the ``[B,3,H,W]`` output sequence in order (RCCL over xGMI with
+backend "nccl" on ROCm; gloo in the CPU tests).
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+def shard_bounds(global_batch: int, rank: int, world: int):
+    """Contiguous shard [lo, hi) of rank ``rank``; B must divide evenly so the
+    all-gather moves equal-size messages."""
+    if global_batch % world:
+        raise ValueError(f"global batch {global_batch} is not divisible by world size {world}")
+    per = global_batch // world
+    return rank * per, (rank + 1) * per
+
+
+def gather_frames(local: torch.Tensor, group=None, out: torch.Tensor | None = None) -> torch.Tensor:
+    """All-gather equal shards ``local`` [b,...] into ``[world*b, ...]`` (rank order)."""
+    world = dist.get_world_size(group)
+    if world == 1:
+        return local if out is None else out.copy_(local)
+    local = local.contiguous()
+    if out is None:
+        out = torch.empty((world * local.shape[0],) + tuple(local.shape[1:]),
+                          dtype=local.dtype, device=local.device)
+    if dist.get_backend(group) == "gloo":
+        parts = list(out.chunk(world))
+        dist.all_gather(parts, local, group=group)
+        if not all(p.data_ptr() == q.data_ptr() for p, q in zip(parts, out.chunk(world))):
+            out.copy_(torch.cat(parts))
+    else:
+        dist.all_gather_into_tensor(out, local, group=group)
+    return out
+
+
+def interpolate_sharded(net, i0_local: torch.Tensor, i1_local: torch.Tensor, t=0.5, group=None,
+                        out: torch.Tensor | None = None) -> torch.Tensor:
+    """Run ``net`` on this rank's pairs and return the whole gathered batch."""
+    with torch.no_grad():
+        local = net(i0_local, i1_local, t)
+    return gather_frames(local, group=group, out=out)

@@ -43,9 +43,7 @@ import model as ref_model  # noqa: E402  (reference)
 import unet as ref_unet    # noqa: E402  (reference)
 from rrin_amd.synthetic import keyed_state_dict, keyed_tensor  # noqa: E402
 
-CONV_CLASSES = [(6, 32), (10, 32), (16, 32), (9, 32), (32, 32), (64, 32), (32, 4), (32, 2),
-                (32, 3), (32, 64), (64, 64), (128, 64), (64, 128), (128, 128), (256, 128),
-                (128, 256), (256, 256), (512, 256), (256, 512), (512, 512)]
+from tests.golden.spec import CONV_CLASSES  # noqa: E402
 
 
 def f32(t):

@@ -1,0 +1,97 @@
+"""GPU: the drop-in ``rrin_amd.Net`` (HIP path, librrin_hip.so) against the
+reference goldens and the CPU oracle.  Gate (BASELINE.json north_star):
+max-abs <= 1e-3 fp32 per pixel; the default-weight cases also hold 1e-4."""
+import numpy as np
+import pytest
+import torch
+
+from oracle.ref_net import net_forward
+from rrin_amd import Net
+from rrin_amd.synthetic import keyed_state_dict, synthetic_batch
+
+pytestmark = pytest.mark.gpu
+GATE = 1e-3
+
+
+def make_net(dev, stress=False):
+    net = Net()
+    net.load_state_dict(keyed_state_dict(net.state_dict(), stress=stress), strict=True)
+    return net.to(dev).eval()
+
+
+@pytest.fixture(scope="module")
+def nets(gpu):
+    return {"default": make_net(gpu), "stress": make_net(gpu, True)}
+
+
+def maxabs(a, b):
+    return float(np.abs(np.asarray(a, np.float64) - np.asarray(b, np.float64)).max())
+
+
+@pytest.mark.parametrize("which", ["default", "stress"])
+def test_net_golden(gpu, golden, nets, which):
+    g = golden("net_" + which)
+    net = nets[which]
+    i0, i1 = torch.from_numpy(g["i0"]).to(gpu), torch.from_numpy(g["i1"]).to(gpu)
+    tight = 1e-4 if which == "default" else GATE
+    with torch.no_grad():
+        for t, key in [(0.5, "out_t050"), (0.25, "out_t025"),
+                       (torch.from_numpy(g["t_tensor"]).view(-1, 1, 1, 1).to(gpu), "out_ttensor")]:
+            out = net(i0, i1, t=t)
+            assert out.shape == i0.shape and out.dtype == torch.float32 and out.device == i0.device
+            err = maxabs(out.cpu(), g[key])
+            assert err <= tight, f"{which} {key}: max-abs {err:.3e}"
+
+
+def test_net_golden_odd_levels(gpu, golden, nets):
+    g = golden("net_odd")  # 80x112: 5x7 at the Flow bottom
+    with torch.no_grad():
+        out = nets["default"](torch.from_numpy(g["i0"]).to(gpu), torch.from_numpy(g["i1"]).to(gpu), 0.5)
+    assert maxabs(out.cpu(), g["out_t050"]) <= 1e-4
+
+
+@pytest.mark.parametrize("h,w,n,which", [(256, 256, 1, "stress"), (368, 640, 1, "default"),
+                                         (720, 1280, 1, "default")])
+def test_net_vs_oracle(gpu, nets, h, w, n, which):
+    """Larger sizes against the CPU oracle (same torch-op sequence as the reference)."""
+    i0, i1 = synthetic_batch(n, h, w, first_index=17)
+    sd = {k: v.detach().cpu() for k, v in nets[which].state_dict().items()}
+    with torch.no_grad():
+        ref = net_forward(sd, i0, i1, 0.5)
+        out = nets[which](i0.to(gpu), i1.to(gpu), 0.5).cpu()
+    err = maxabs(out, ref)
+    assert err <= GATE, f"{h}x{w}: {err:.3e}"
+    mse = float(((out.double() - ref.double()) ** 2).mean())
+    assert mse == 0 or 10 * np.log10(1.0 / mse) > 80  # PSNR vs CPU ref
+
+
+def test_batch_equals_per_sample_and_deterministic(gpu, nets):
+    i0, i1 = synthetic_batch(3, 64, 96, first_index=3)
+    i0, i1 = i0.to(gpu), i1.to(gpu)
+    net = nets["stress"]
+    with torch.no_grad():
+        full = net(i0, i1, 0.5)
+        again = net(i0, i1, 0.5)
+        parts = torch.cat([net(i0[k:k + 1], i1[k:k + 1], 0.5) for k in range(3)])
+    assert torch.equal(full, again)
+    assert torch.equal(full, parts)
+
+
+def test_weight_reload_repacks(gpu):
+    net = make_net(gpu)
+    i0, i1 = synthetic_batch(1, 64, 64)
+    i0, i1 = i0.to(gpu), i1.to(gpu)
+    with torch.no_grad():
+        a = net(i0, i1)
+        net.load_state_dict(keyed_state_dict(net.state_dict(), stress=True))
+        b = net(i0, i1)
+    assert not torch.equal(a, b)
+
+
+def test_net_errors(gpu, nets):
+    net = nets["default"]
+    with torch.no_grad():
+        with pytest.raises(RuntimeError, match="multiples of 16"):
+            net(torch.zeros(1, 3, 72, 72, device=gpu), torch.zeros(1, 3, 72, 72, device=gpu))
+        with pytest.raises(TypeError):
+            net(torch.zeros(1, 3, 64, 64, device=gpu).half(), torch.zeros(1, 3, 64, 64, device=gpu).half())

@@ -1,0 +1,84 @@
+"""CPU: host-side logic of the drop-in boundary (no kernel launches)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from rrin_amd import Net
+from rrin_amd.engine import FIRST_CONV_PERM, t_coefficients
+from rrin_amd.synthetic import keyed_state_dict, synthetic_batch, synthetic_pair
+from rrin_amd.unet import conv_flops
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def test_state_dict_keys_match_reference():
+    keys = [l.strip() for l in open(os.path.join(GOLDEN, "state_dict_keys.txt"))]
+    net = Net()
+    sd = net.state_dict()
+    assert list(sd.keys()) == keys and len(keys) == 162
+    assert tuple(sd["Flow.up_path.0.up.1.weight"].shape) == (256, 512, 3, 3)
+    assert sum(v.numel() for v in sd.values()) == 19_194_445
+    # a reference-style checkpoint dict loads strict (convert.py:103, train.py:158-161)
+    state = {"model": keyed_state_dict(sd), "optim": {}, "epoch": 3}
+    net.load_state_dict(state["model"], strict=True)
+
+
+def test_conv_flops_match_survey():
+    net = Net()
+    total = sum(conv_flops(getattr(net, u), 736, 1280) for u in ("Flow", "refine_flow", "Mask", "final"))
+    assert abs(total / 1e9 - 1635.5) < 0.1
+    total720 = sum(conv_flops(getattr(net, u), 720, 1280) for u in ("Flow", "refine_flow", "Mask", "final"))
+    assert abs(total720 / 1e9 - 1600.0) < 0.1
+
+
+def test_forward_requires_no_grad():
+    net = Net()
+    x = torch.zeros(1, 3, 16, 16)
+    with pytest.raises(RuntimeError, match="no_grad"):
+        net(x, x)
+
+
+def test_forward_requires_rocm_device():
+    net = Net()
+    x = torch.zeros(1, 3, 16, 16)
+    with torch.no_grad(), pytest.raises(RuntimeError, match="ROCm device"):
+        net(x, x)
+
+
+@pytest.mark.parametrize("t", [0.5, 0.25, 1 / 3, 0.9])
+def test_t_coefficients_python_float(t):
+    c = t_coefficients(t, 3)
+    assert c.shape == (3, 8) and c.dtype == torch.float32
+    # scalar*tensor in the reference: the Python double is rounded to fp32 once
+    f = torch.ones(1)
+    exp = [(-(1 - t) * t * f).item(), (t * t * f).item(), ((1 - t) * (1 - t) * f).item(),
+           (t * (1 - t) * f).item(), ((1 - t) * f).item(), (t * f).item()]
+    assert c[1, :6].tolist() == exp
+
+
+def test_t_coefficients_tensor():
+    tt = torch.tensor([0.3, 0.7]).view(2, 1, 1, 1)
+    c = t_coefficients(tt, 2)
+    f = torch.ones(2, 1, 1, 1)
+    exp0 = (-(1 - tt) * tt * f).view(-1)
+    assert torch.equal(c[:, 0], exp0)
+    assert torch.equal(c[:, 3], (tt * (1 - tt) * f).view(-1))
+    with pytest.raises(ValueError):
+        t_coefficients(torch.tensor([0.1, 0.2, 0.3]), 2)
+
+
+def test_channel_permutations_are_bijective():
+    assert sorted(FIRST_CONV_PERM["refine_flow"]) == list(range(10))
+    assert sorted(FIRST_CONV_PERM["Mask"]) == list(range(16))
+
+
+def test_synthetic_pairs_deterministic():
+    a0, a1 = synthetic_pair(32, 48, 5)
+    b0, b1 = synthetic_pair(32, 48, 5)
+    assert torch.equal(a0, b0) and torch.equal(a1, b1)
+    assert torch.all((a0 * 255).round() == a0 * 255)  # ToTensor quantisation
+    assert 0 <= a1.min() and a1.max() <= 1
+    x0, _ = synthetic_batch(3, 32, 48, first_index=4)
+    assert torch.equal(x0[1:2], a0)

@@ -1,0 +1,23 @@
+#!/bin/bash
+# One GPU session: parity tests, smoke, short bench, rocprof kernel stats.
+# Each GPU step has its own time limit; stop at the first crash/timeout
+# (exit codes 124/134/137/139 or >128), continue past plain test failures (1).
+set -u
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+run() {  # name limit cmd...
+  local name=$1 lim=$2; shift 2
+  echo "=== $name" | tee -a gpurun_out/steps.log
+  timeout -k 10 "$lim" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" | tee -a gpurun_out/steps.log
+  tail -5 "gpurun_out/$name.log"
+  if [ $rc -ge 124 ]; then echo "fatal rc $rc in $name; stopping"; exit $rc; fi
+  return 0
+}
+STEPS=${STEPS:-tests,smoke,bench,prof}
+[[ $STEPS == *tests* ]] && run tests 900 python -m pytest tests -m gpu -x -q
+[[ $STEPS == *smoke* ]] && run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+[[ $STEPS == *bench* ]] && run bench 600 python bench.py --steps 5 --warmup 2
+[[ $STEPS == *prof* ]] && run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --cpu-baseline off
+exit 0
