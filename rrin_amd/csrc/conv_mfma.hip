@@ -56,19 +56,15 @@ struct Tile {
   static constexpr int W_V4 = W_F / 4;
   static constexpr int IN_IT = (IN_V4 + 255) / 256;
   static constexpr int W_IT = (W_V4 + 255) / 256;
+  static constexpr int LR_ROWS = TH / 2 + 2;
+  static constexpr int LR_COLS = 20;
+  static constexpr int LR_F = CK * LR_ROWS * LR_COLS;
+  static constexpr int LR_IT = (LR_F + 255) / 256;
   static constexpr size_t LDS_BYTES = 2 * (size_t)(IN_F + W_F) * sizeof(float);
+  static constexpr size_t LDS_BYTES_UP = LDS_BYTES + (size_t)LR_F * sizeof(float);
   static_assert(WAVES_M * WAVES_N == 4, "4 waves per block");
   static_assert(16 % TH == 0, "TH must divide the 16-row plane padding");
 };
-
-// Bilinear x2 (align_corners=False) source index along one axis:
-// src = max((d + 0.5) * 0.5 - 0.5, 0); i0 = floor(src); i1 = min(i0 + 1, n - 1).
-__device__ inline void up_axis(int d, int n, int& i0, int& i1, float& l1) {
-  float s = fmaxf(((float)d + 0.5f) * 0.5f - 0.5f, 0.0f);
-  i0 = (int)s;
-  l1 = s - (float)i0;
-  i1 = min(i0 + 1, n - 1);
-}
 
 template <int WAVES_M, int WAVES_N, int WM, int WN, int SRC, int EPI>
 __global__ void __launch_bounds__(256) conv3x3_mfma_kernel(ConvArgs a) {
@@ -79,6 +75,7 @@ __global__ void __launch_bounds__(256) conv3x3_mfma_kernel(ConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* s_in = smem;            // [2][IN_F]
   float* s_w = smem + 2 * IN_F;  // [2][W_F]
+  float* s_lr = s_w + 2 * W_F;   // [LR_F] low-res tile (UPSAMPLE2X)
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -147,42 +144,66 @@ __global__ void __launch_bounds__(256) conv3x3_mfma_kernel(ConvArgs a) {
       if (idx < T::IN_V4) s[idx] = rin[it];
     }
   };
-  // UPSAMPLE2X: value at hi-res (Y,X) = bilinear x2 of the low-res source,
-  // zero outside [0,h)x[0,w) (the conv's zero padding).
-  auto stage_up = [&](int c, int buf) {
-    float4* s = reinterpret_cast<float4*>(s_in + buf * IN_F);
+  // UPSAMPLE2X (unet.py:77, bilinear x2, align_corners=False).  The low-res
+  // tile this block needs (TH/2+2 rows x 20 cols per channel, edge-clamped
+  // coordinates) is prefetched into registers during the MFMAs, stored to LDS,
+  // and expanded there into the hi-res input tile, two output columns per item:
+  //   X = 2i   : .25 L[i-1] + .75 L[i]      X = 2i+1 : .75 L[i] + .25 L[i+1]
+  // (rows likewise; clamping is carried by the clamped loads).  Positions
+  // outside the hi-res frame are the conv's zero padding.
+  const int ly0 = y0 / 2 - 1, lx0 = x0 / 2 - 2;
+  float rlr[T::LR_IT];
+  auto load_lr = [&](int c) {
 #pragma unroll
-    for (int it = 0; it < T::IN_IT; ++it) {
+    for (int it = 0; it < T::LR_IT; ++it) {
       const int idx = tid + 256 * it;
-      if (idx < T::IN_V4) {
-        const int ci = idx / (ROWS * 10);
-        const int rem = idx - ci * (ROWS * 10);
-        const int r = rem / 10;
-        const int q = rem - r * 10;
+      if (idx < T::LR_F) {
+        const int ci = idx / (T::LR_ROWS * T::LR_COLS);
+        const int rem = idx - ci * (T::LR_ROWS * T::LR_COLS);
+        const int r = rem / T::LR_COLS;
+        const int q = rem - r * T::LR_COLS;
         const int ch = c * CK + ci;
-        const int Y = y0 - 1 + r;
-        float o[4] = {0.f, 0.f, 0.f, 0.f};
-        if (ch < a.cin && Y >= 0 && Y < a.h) {
-          int ya, yb;
-          float ly;
-          up_axis(Y, a.src_h, ya, yb, ly);
-          const float* p = src_img + (int64_t)ch * a.src_plane;
-          const float* ra = p + (int64_t)(ya + 1) * a.src_wp + 4;
-          const float* rb = p + (int64_t)(yb + 1) * a.src_wp + 4;
+        const int yy = min(max(ly0 + r, 0), a.src_h - 1);
+        const int xx = min(max(lx0 + q, 0), a.src_w - 1);
+        rlr[it] = ch < a.cin ? src_img[(int64_t)ch * a.src_plane + (int64_t)(yy + 1) * a.src_wp + xx + 4] : 0.f;
+      }
+    }
+  };
+  auto expand_up = [&](int buf) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int X = x0 - 4 + 4 * q + e;
-            if (X >= 0 && X < a.w) {
-              int xa, xb;
-              float lx;
-              up_axis(X, a.src_w, xa, xb, lx);
-              const float top = (1.f - lx) * ra[xa] + lx * ra[xb];
-              const float bot = (1.f - lx) * rb[xa] + lx * rb[xb];
-              o[e] = (1.f - ly) * top + ly * bot;
-            }
-          }
+    for (int it = 0; it < T::LR_IT; ++it) {
+      const int idx = tid + 256 * it;
+      if (idx < T::LR_F) s_lr[idx] = rlr[it];
+    }
+    __syncthreads();
+    float* so = s_in + buf * IN_F;
+    constexpr int PAIRS = 18;  // i = x0/2-1 .. x0/2+16 -> X = x0-2 .. x0+33 (LDS cols 2..37)
+    constexpr int ITEMS = CK * ROWS * PAIRS;
+#pragma unroll
+    for (int it = 0; it < (ITEMS + 255) / 256; ++it) {
+      const int idx = tid + 256 * it;
+      if (idx < ITEMS) {
+        const int ci = idx / (ROWS * PAIRS);
+        const int rem = idx - ci * (ROWS * PAIRS);
+        const int r = rem / PAIRS;
+        const int pi = rem - r * PAIRS;
+        const int Y = y0 - 1 + r;
+        const int Xe = x0 - 2 + 2 * pi;  // even output column of the pair
+        float2 o = make_float2(0.f, 0.f);
+        if (Y >= 0 && Y < a.h) {
+          const int iy = Y >> 1;
+          const int ra = (Y & 1) ? iy : iy - 1;         // upper source row
+          const float wa = (Y & 1) ? 0.75f : 0.25f;      // its weight
+          const float* la = s_lr + (ci * T::LR_ROWS + (ra - ly0)) * T::LR_COLS + (x0 / 2 - 1 + pi - lx0);
+          const float* lb = la + T::LR_COLS;
+          const float wb = 1.0f - wa;
+          // horizontal first, then vertical (the order of upsample_bilinear2d)
+          const float ae = 0.25f * la[-1] + 0.75f * la[0], ao = 0.75f * la[0] + 0.25f * la[1];
+          const float be = 0.25f * lb[-1] + 0.75f * lb[0], bo = 0.75f * lb[0] + 0.25f * lb[1];
+          if (Xe >= 0 && Xe < a.w) o.x = wa * ae + wb * be;
+          if (Xe + 1 >= 0 && Xe + 1 < a.w) o.y = wa * ao + wb * bo;
         }
-        s[idx] = make_float4(o[0], o[1], o[2], o[3]);
+        *reinterpret_cast<float2*>(so + (ci * ROWS + r) * LC + 2 + 2 * pi) = o;
       }
     }
   };
@@ -195,27 +216,29 @@ __global__ void __launch_bounds__(256) conv3x3_mfma_kernel(ConvArgs a) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[mt][nt][i] = 0.f;
 
+  // 36 k-steps (4 channel pairs x 9 taps) per chunk; operands of step s+1 are
+  // read from LDS before the MFMAs of step s issue, so the ds_read latency
+  // hides under 64-cycle MFMAs instead of stalling in front of them.
   auto compute = [&](int buf) {
     const float* si = s_in + buf * IN_F + hh * ROWS * LC + (wn * WN) * LC + j + 3;
     const float* sw = s_w + buf * W_F + hh * 9 * BM + (wm * WM) * 32 + j;
+    float av[2][WM], bv[2][WN];
+    auto ld = [&](int st, int slot) {
+      const int cp = st / 9, tap = st % 9, ky = tap / 3, kx = tap % 3;
 #pragma unroll
-    for (int cp = 0; cp < CK / 2; ++cp) {
+      for (int mt = 0; mt < WM; ++mt) av[slot][mt] = sw[(2 * cp * 9 + tap) * BM + mt * 32];
 #pragma unroll
-      for (int ky = 0; ky < 3; ++ky) {
+      for (int nt = 0; nt < WN; ++nt) bv[slot][nt] = si[(2 * cp * ROWS + nt + ky) * LC + kx];
+    };
+    ld(0, 0);
 #pragma unroll
-        for (int kx = 0; kx < 3; ++kx) {
-          float av[WM], bv[WN];
+    for (int st = 0; st < (CK / 2) * 9; ++st) {
+      if (st + 1 < (CK / 2) * 9) ld(st + 1, (st + 1) & 1);
 #pragma unroll
-          for (int mt = 0; mt < WM; ++mt) av[mt] = sw[(2 * cp * 9 + ky * 3 + kx) * BM + mt * 32];
+      for (int mt = 0; mt < WM; ++mt)
 #pragma unroll
-          for (int nt = 0; nt < WN; ++nt) bv[nt] = si[(2 * cp * ROWS + nt + ky) * LC + kx];
-#pragma unroll
-          for (int mt = 0; mt < WM; ++mt)
-#pragma unroll
-            for (int nt = 0; nt < WN; ++nt)
-              acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[mt], bv[nt], acc[mt][nt], 0, 0, 0);
-        }
-      }
+        for (int nt = 0; nt < WN; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[st & 1][mt], bv[st & 1][nt], acc[mt][nt], 0, 0, 0);
     }
   };
 
@@ -225,7 +248,8 @@ __global__ void __launch_bounds__(256) conv3x3_mfma_kernel(ConvArgs a) {
     load_in(0);
     store_in(0);
   } else {
-    stage_up(0, 0);
+    load_lr(0);
+    expand_up(0);
   }
   store_w(0);
   __syncthreads();
@@ -236,14 +260,17 @@ __global__ void __launch_bounds__(256) conv3x3_mfma_kernel(ConvArgs a) {
     const bool more = (c + 1) < a.nchunks;
     if (more) {
       load_w(c + 1);
-      if constexpr (SRC == RRIN_SRC_DIRECT) load_in(c + 1);
+      if constexpr (SRC == RRIN_SRC_DIRECT)
+        load_in(c + 1);
+      else
+        load_lr(c + 1);
     }
     compute(buf);
     if (more) {
       if constexpr (SRC == RRIN_SRC_DIRECT)
         store_in(buf ^ 1);
       else
-        stage_up(c + 1, buf ^ 1);
+        expand_up(buf ^ 1);  // contains one extra barrier (s_lr hand-off)
       store_w(buf ^ 1);
     }
     __syncthreads();
@@ -314,15 +341,15 @@ static constexpr int kNumCfg = sizeof(kCfg) / sizeof(kCfg[0]);
 template <int A, int B, int C, int D, int SRC, int EPI>
 static int launch_t(const ConvArgs& args, int grid, hipStream_t st) {
   using T = Tile<A, B, C, D>;
+  constexpr size_t lds = SRC == RRIN_SRC_UPSAMPLE2X ? T::LDS_BYTES_UP : T::LDS_BYTES;
   auto k = conv3x3_mfma_kernel<A, B, C, D, SRC, EPI>;
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)T::LDS_BYTES);
+    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return (int)e;
     attr_set = true;
   }
-  hipLaunchKernelGGL(k, dim3(grid), dim3(256), T::LDS_BYTES, st, args);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(256), lds, st, args);
   return hip_code(hipGetLastError());
 }
 

@@ -1,0 +1,179 @@
+#!/usr/bin/env python3
+"""Conv kernel lab (GPU).
+
+  python tools/conv_lab.py breakdown [--batch 4 --height 720 --width 1280]
+      per-launch time / TFLOP/s of one Net.forward in schedule order (HIP events)
+  python tools/conv_lab.py tune [--batch 4 ...] [--out gpurun_out/tune.json]
+      every tile config on every distinct conv shape of the Net; best per shape
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+from rrin_amd import Net, _lib  # noqa: E402
+from rrin_amd.pp import PPTensor  # noqa: E402
+from rrin_amd.synthetic import keyed_state_dict, synthetic_batch  # noqa: E402
+
+UNETS = [("Flow", 6, 5), ("refine_flow", 10, 4), ("Mask", 16, 4), ("final", 9, 4)]
+
+
+def schedule(h, w):
+    """(unet, tag, cin, cout, level, src_mode, epi) in rrin_net_fwd launch order."""
+    out = [("-", "pack", 0, 0, 0, -1, -1)]
+    for name, cin0, D in UNETS:
+        for L in range(D):
+            C_ = 32 << L
+            cin = (32 << (L - 1)) if L else cin0
+            out.append((name, f"down{L}.a", cin, C_, L, 0, 1))
+            if L < D - 1:
+                out.append((name, f"down{L}.b", C_, C_, L, 0, 2))
+            else:
+                out.append((name, f"down{L}.b", C_, C_, L, 0, 1))
+                out.append((name, "mid", C_, C_, L, 0, 1))
+        for L in range(D - 2, -1, -1):
+            C_ = 32 << L
+            out.append((name, f"up{L}.up", 2 * C_, C_, L, 1, 0))
+            out.append((name, f"up{L}.a", 2 * C_, C_, L, 0, 1))
+            out.append((name, f"up{L}.b", C_, C_, L, 0, 1))
+        out.append((name, "head", 32, 0, 0, -2, -2))
+    return out
+
+
+def breakdown(args):
+    dev = torch.device("cuda:0")
+    net = Net()
+    net.load_state_dict(keyed_state_dict(net.state_dict()))
+    net = net.to(dev).eval()
+    eng = net.engine()
+    lib = _lib.lib()
+    i0, i1 = synthetic_batch(args.batch, args.height, args.width)
+    i0, i1 = i0.to(dev), i1.to(dev)
+    with torch.no_grad():
+        for _ in range(2):
+            eng.forward(i0, i1)
+    torch.cuda.synchronize()
+    cap = 128
+    h = C.c_void_p()
+    _lib.check(lib.rrin_prof_create(cap, C.byref(h)))
+    reps = args.reps
+    tot = {}
+    for r in range(reps):
+        lib.rrin_prof_reset(h)
+        with torch.no_grad():
+            eng.forward(i0, i1, prof=h.value)
+        torch.cuda.synchronize()
+        kinds = (C.c_int32 * cap)()
+        ms = (C.c_float * cap)()
+        fl = (C.c_double * cap)()
+        cnt = C.c_int32()
+        _lib.check(lib.rrin_prof_read(h, kinds, ms, fl, cap, C.byref(cnt)))
+        for i in range(cnt.value):
+            tot.setdefault(i, []).append((kinds[i], ms[i], fl[i]))
+    lib.rrin_prof_destroy(h)
+    sch = schedule(args.height, args.width)
+    cfgs = [None] + list(eng.cfgs)
+    rows = []
+    conv_i = 0
+    for i, entry in enumerate(sch):
+        vals = sorted(tot[i], key=lambda v: v[1])
+        k, ms_, fl_ = vals[len(vals) // 2]
+        cfg = None
+        if entry[5] >= 0:
+            cfg = eng.cfgs[conv_i]
+            conv_i += 1
+        rows.append(dict(unet=entry[0], tag=entry[1], cin=entry[2], cout=entry[3], level=entry[4],
+                         src=entry[5], epi=entry[6], cfg=cfg, ms=ms_, tflops=fl_ / (ms_ * 1e-3) / 1e12 if ms_ else 0))
+    total = sum(r["ms"] for r in rows)
+    for r in rows:
+        print(f"{r['unet']:12s} {r['tag']:10s} {r['cin']:4d}->{r['cout']:4d} L{r['level']} src{r['src']:2d} "
+              f"epi{r['epi']:2d} cfg {str(r['cfg']):4s} {r['ms']:8.3f} ms {r['tflops']:7.1f} TF "
+              f"{100 * r['ms'] / total:5.1f}%")
+    print(f"total {total:.3f} ms per forward (B={args.batch})")
+    agg = {}
+    for r in rows:
+        key = f"L{r['level']} src{r['src']} epi{r['epi']}"
+        a = agg.setdefault(key, [0.0, 0.0])
+        a[0] += r["ms"]
+        a[1] += r["tflops"] * r["ms"]
+    for k, (m, tw) in sorted(agg.items(), key=lambda kv: -kv[1][0]):
+        print(f"  {k:20s} {m:8.3f} ms  {tw / m if m else 0:6.1f} TF")
+    if args.out:
+        json.dump(rows, open(args.out, "w"), indent=1)
+
+
+def tune(args):
+    dev = torch.device("cuda:0")
+    lib = _lib.lib()
+    ncfg = lib.rrin_conv_cfg_count()
+    shapes = sorted({(e[2], e[3], e[4], e[5], e[6]) for e in schedule(args.height, args.width) if e[5] >= 0})
+    n = args.batch
+    results = []
+    for cin, cout, L, src, epi in shapes:
+        h, w = args.height >> L, args.width >> L
+        hs, ws_ = (h // 2, w // 2) if src == 1 else (h, w)
+        x = PPTensor.from_nchw(torch.rand(n, cin, hs, ws_, device=dev) * 2 - 1)
+        dst = PPTensor(n, cout, h, w, dev)
+        pool = PPTensor(n, cout, h // 2, w // 2, dev) if epi == 2 else None
+        wt = torch.randn(cout, cin, 3, 3) / (3 * cin ** 0.5)
+        b = torch.zeros(cout)
+        best = None
+        line = []
+        for cfg in range(ncfg):
+            bm = lib.rrin_conv_cfg_bm(cfg)
+            if bm > max(32, 2 * cout):
+                continue
+            from tests.hip_helpers import pack
+            wp, bp = pack(wt, b, cfg, dev=dev)
+            d = _lib.ConvDesc()
+            d.n, d.cin, d.cout, d.cfg, d.src_mode, d.epi_mode, d.slope = n, cin, cout, cfg, src, epi, 0.1
+            d.src, d.dst = x.view(0, cin), dst.view(0, cout)
+            if pool is not None:
+                d.pool = pool.view(0, cout)
+            d.wpack, d.bias = wp.data_ptr(), bp.data_ptr()
+            st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+            for _ in range(2):
+                _lib.check(lib.rrin_conv3x3_fwd(C.byref(d), st))
+            ts = []
+            for _ in range(args.reps):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                _lib.check(lib.rrin_conv3x3_fwd(C.byref(d), st))
+                e1.record()
+                e1.synchronize()
+                ts.append(e0.elapsed_time(e1))
+            ms = sorted(ts)[len(ts) // 2]
+            fl = 2 * 9 * cin * cout * h * w * n
+            tf = fl / (ms * 1e-3) / 1e12
+            line.append(f"cfg{cfg}:{ms:.3f}ms/{tf:.0f}TF")
+            results.append(dict(cin=cin, cout=cout, level=L, src=src, epi=epi, cfg=cfg, ms=ms, tflops=tf))
+            if best is None or ms < best[1]:
+                best = (cfg, ms, tf)
+        print(f"{cin:4d}->{cout:4d} L{L} src{src} epi{epi}: best cfg{best[0]} {best[2]:.0f} TF | " + " ".join(line),
+              flush=True)
+    if args.out:
+        json.dump(results, open(args.out, "w"), indent=1)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("mode", choices=["breakdown", "tune"])
+    ap.add_argument("--batch", type=int, default=4)
+    ap.add_argument("--height", type=int, default=720)
+    ap.add_argument("--width", type=int, default=1280)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+    breakdown(args) if args.mode == "breakdown" else tune(args)
+
+
+if __name__ == "__main__":
+    main()
