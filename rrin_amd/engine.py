@@ -37,9 +37,13 @@ FIRST_CONV_PERM = {
 
 
 def choose_cfg(cin: int, cout: int, level: int) -> int:
-    """Tile config id for one conv (see conv_mfma.hip config table)."""
+    """Tile config id for one conv (conv_mfma.hip config table), from the
+    per-shape sweep of tools/conv_lab.py tune at 1280x720, 4 pairs (see
+    profiles/ and DESIGN.md §5)."""
     if cout <= 32:
-        return 0        # BM 32 x TH 8
+        return 3        # BM 32 x TH 16: full-res layers, 85-103 TF vs 75-88 at TH 8
+    if cout >= 512:
+        return 4        # BM 64 x TH 4: 80x45 bottom, more blocks for the small grid
     return 1            # BM 64 x TH 8
 
 
@@ -91,8 +95,7 @@ class RRINEngine:
                     self.heads_t.append((torch.from_numpy(w.copy()).to(self.device),
                                          torch.from_numpy(b.copy()).to(self.device)))
                     continue
-                level = int(tag[4]) if tag.startswith("down") else 0
-                cfg = choose_cfg(cin, cout, level)
+                cfg = choose_cfg(cin, cout, 0)
                 bm = L.rrin_conv_cfg_bm(cfg)
                 nw = L.rrin_pack_conv3x3_floats(cout, cin, bm)
                 nb = L.rrin_pack_bias_floats(cout, bm)
