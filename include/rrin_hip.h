@@ -12,8 +12,8 @@
  *   - stateless and stream-ordered: calls only enqueue work on `stream`.
  *
  * Activation layout used between kernels ("padded planar", PP): per image and
- * channel a plane of hp x wp fp32 with hp = round_up(h,16)+2, wp = round_up(w,32)+8;
- * pixel (y,x) lives at (y+1)*wp + (x+4); everything else is zero and is never
+ * channel a plane of hp x wp fp32 with hp = round_up(h,16)+2, wp = round_up(w,32)+64;
+ * pixel (y,x) lives at (y+1)*wp + (x+32); everything else is zero and is never
  * written.  See DESIGN.md §3.
  */
 #ifndef RRIN_HIP_H

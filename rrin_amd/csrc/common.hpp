@@ -8,8 +8,9 @@
 namespace rrin {
 
 constexpr int kPadRowsAlign = 16;  // hp = round_up(h,16) + 2
-constexpr int kPadColsAlign = 32;  // wp = round_up(w,32) + 8
-constexpr int kPadLeft = 4;        // pixel x at column x+4 (16-B aligned data)
+constexpr int kPadColsAlign = 32;  // wp = round_up(w,32) + 64
+constexpr int kPadLeft = 32;       // pixel x at column x+32: every 32-px output row segment
+                                   // is one whole 128-B line (full-line stores)
 
 __host__ __device__ inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
 
@@ -18,7 +19,7 @@ inline rrin_geom make_geom(int h, int w) {
   g.h = h;
   g.w = w;
   g.hp = round_up(h, kPadRowsAlign) + 2;
-  g.wp = round_up(w, kPadColsAlign) + 8;
+  g.wp = round_up(w, kPadColsAlign) + 2 * kPadLeft;
   g.plane = (int64_t)g.hp * g.wp;
   return g;
 }

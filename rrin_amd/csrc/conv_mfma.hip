@@ -85,7 +85,16 @@ __global__ void __launch_bounds__(256) conv3x3_mfma_kernel(ConvArgs a) {
   const int j = lane & 31;
   const int hh = lane >> 5;
 
-  int bid = blockIdx.x;
+  // XCD-aware remap (bijective): hardware deals blocks round-robin over the 8
+  // XCDs, so give each XCD one contiguous run of logical blocks.  Logical order
+  // has the co-blocks of a tile adjacent, then neighbouring tiles: blocks that
+  // stage the same input rows share one L2.  Placement affects speed only.
+  int bid;
+  {
+    const int nwg = gridDim.x, q = nwg >> 3, r = nwg & 7;
+    const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+  }
   const int cob = bid % a.co_blocks;
   bid /= a.co_blocks;
   const int tx = bid % a.tiles_x;
@@ -131,7 +140,7 @@ __global__ void __launch_bounds__(256) conv3x3_mfma_kernel(ConvArgs a) {
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
         if (ch < a.cin)
           v = *reinterpret_cast<const float4*>(src_img + (int64_t)ch * a.src_plane +
-                                               (int64_t)(y0 + r) * a.src_wp + x0 + 4 * q);
+                                               (int64_t)(y0 + r) * a.src_wp + x0 + (kPadLeft - 4) + 4 * q);
         rin[it] = v;
       }
     }
@@ -165,7 +174,7 @@ __global__ void __launch_bounds__(256) conv3x3_mfma_kernel(ConvArgs a) {
         const int ch = c * CK + ci;
         const int yy = min(max(ly0 + r, 0), a.src_h - 1);
         const int xx = min(max(lx0 + q, 0), a.src_w - 1);
-        rlr[it] = ch < a.cin ? src_img[(int64_t)ch * a.src_plane + (int64_t)(yy + 1) * a.src_wp + xx + 4] : 0.f;
+        rlr[it] = ch < a.cin ? src_img[(int64_t)ch * a.src_plane + (int64_t)(yy + 1) * a.src_wp + xx + kPadLeft] : 0.f;
       }
     }
   };
@@ -293,7 +302,7 @@ __global__ void __launch_bounds__(256) conv3x3_mfma_kernel(ConvArgs a) {
         v[nt] = t;
         const int y = yb + nt;
         if (co < a.cout && y < a.h && x < a.w)
-          a.dst[img * a.dst_img + (int64_t)co * a.dst_plane + (int64_t)(y + 1) * a.dst_wp + x + 4] = t;
+          a.dst[img * a.dst_img + (int64_t)co * a.dst_plane + (int64_t)(y + 1) * a.dst_wp + x + kPadLeft] = t;
       }
       if constexpr (EPI == RRIN_EPI_LEAKY_POOL) {
 #pragma unroll
@@ -303,7 +312,7 @@ __global__ void __launch_bounds__(256) conv3x3_mfma_kernel(ConvArgs a) {
           const int y = yb + 2 * p;
           if (!(j & 1) && co < a.cout && y < a.h && x < a.w)
             a.pool[img * a.pool_img + (int64_t)co * a.pool_plane + (int64_t)(y / 2 + 1) * a.pool_wp +
-                   x / 2 + 4] = 0.25f * s;
+                   x / 2 + kPadLeft] = 0.25f * s;
         }
       }
     }

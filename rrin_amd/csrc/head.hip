@@ -118,7 +118,7 @@ __global__ void __launch_bounds__(256) head_kernel(HeadArgs a) {
         const int rr = rem / 10;
         const int q = rem - rr * 10;
         s4[idx] = *reinterpret_cast<const float4*>(src_img + (int64_t)(c * HC + ci) * a.src_plane +
-                                                   (int64_t)(y0 + rr) * a.src_wp + x0 + 4 * q);
+                                                   (int64_t)(y0 + rr) * a.src_wp + x0 + (kPadLeft - 4) + 4 * q);
       }
     }
     __syncthreads();
@@ -141,7 +141,7 @@ __global__ void __launch_bounds__(256) head_kernel(HeadArgs a) {
   const int y = y0 + r, x = x0 + xl;
   if (y >= a.h || x >= a.w_) return;
   float* gi = a.g + img * a.g_img;
-  const int64_t pix = (int64_t)(y + 1) * a.g_wp + x + 4;
+  const int64_t pix = (int64_t)(y + 1) * a.g_wp + x + kPadLeft;
   auto G = [&](int ch) -> float& { return gi[(int64_t)ch * a.g_plane + pix]; };
   const float* cf = a.coef + img * 8;
 
@@ -163,7 +163,7 @@ __global__ void __launch_bounds__(256) head_kernel(HeadArgs a) {
     G(7) = f0v;
     G(8) = f1u;
     G(9) = f1v;
-    const int64_t off = (int64_t)a.g_wp + 4;  // pixel (0,0) inside a plane
+    const int64_t off = (int64_t)a.g_wp + kPadLeft;  // pixel (0,0) inside a plane
     const WarpTaps t0 = warp_taps(x, y, f0u, f0v, a.h, a.w_);
     const WarpTaps t1 = warp_taps(x, y, f1u, f1v, a.h, a.w_);
 #pragma unroll
@@ -207,7 +207,7 @@ __global__ void nchw_to_pp_kernel(const float* __restrict__ src, float* dst, int
   t /= h;
   const int ch = (int)(t % c);
   const int n = (int)(t / c);
-  dst[n * dst_img + ch * plane + (int64_t)(y + 1) * wp + x + 4] = src[i];
+  dst[n * dst_img + ch * plane + (int64_t)(y + 1) * wp + x + kPadLeft] = src[i];
 }
 
 __global__ void pp_to_nchw_kernel(const float* __restrict__ src, int64_t src_img, int64_t plane,
@@ -220,7 +220,7 @@ __global__ void pp_to_nchw_kernel(const float* __restrict__ src, int64_t src_img
   t /= h;
   const int ch = (int)(t % c);
   const int n = (int)(t / c);
-  dst[i] = src[n * src_img + ch * plane + (int64_t)(y + 1) * wp + x + 4];
+  dst[i] = src[n * src_img + ch * plane + (int64_t)(y + 1) * wp + x + kPadLeft];
 }
 
 __global__ void warp_nchw_kernel(const float* __restrict__ img, const float* __restrict__ flow,

@@ -1,8 +1,8 @@
 """Padded-planar (PP) activation tensors on the device (layout: DESIGN.md §3).
 
 A PP tensor is a torch allocation ``[n, c, hp, wp]`` fp32 with
-``hp = round_up(h,16)+2``, ``wp = round_up(w,32)+8`` and pixel (y,x) at
-``[.., y+1, x+4]``; the padding is zero and never written by the kernels.
+``hp = round_up(h,16)+2``, ``wp = round_up(w,32)+64`` and pixel (y,x) at
+``[.., y+1, x+32]``; the padding is zero and never written by the kernels.
 Conversions to/from NCHW run the library's HIP layout kernels.
 """
 from __future__ import annotations

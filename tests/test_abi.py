@@ -37,10 +37,10 @@ def test_strerror_and_geom():
     for code in (0, -1, -2, -3, -4):
         assert lib.rrin_strerror(code)
     g = _lib.geom(720, 1280)
-    assert (g.h, g.w, g.hp, g.wp) == (720, 1280, 722, 1288)
-    assert g.plane == 722 * 1288
+    assert (g.h, g.w, g.hp, g.wp) == (720, 1280, 722, 1344)
+    assert g.plane == 722 * 1344
     g = _lib.geom(45, 80)
-    assert (g.hp, g.wp) == (50, 104)
+    assert (g.hp, g.wp) == (50, 160)
 
 
 def test_conv_counts_and_workspace():

@@ -41,7 +41,7 @@ def test_layout_roundtrip(gpu):
     t = pp.t
     assert not t[:, 0].any() and not t[:, 6].any()
     assert not t[:, :, 0].any() and not t[:, :, 24:].any()
-    assert not t[:, :, :, :4].any() and not t[:, :, :, 44:].any()
+    assert not t[:, :, :, :32].any() and not t[:, :, :, 72:].any()
 
 
 @pytest.mark.parametrize("cin,cout", CONV_CLASSES)

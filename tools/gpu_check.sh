@@ -22,4 +22,9 @@ STEPS=${STEPS:-tests,smoke,bench,prof}
 [[ $STEPS == *breakdown* ]] && run breakdown 300 python tools/conv_lab.py breakdown --out gpurun_out/breakdown.json
 [[ $STEPS == *tune* ]] && run tune 600 python tools/conv_lab.py tune --out gpurun_out/tune.json
 [[ $STEPS == *prof* ]] && run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --cpu-baseline off
+if [[ $STEPS == *pmc* ]]; then
+  run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 2 --warmup 1 --cpu-baseline off --no-prof
+  run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --steps 2 --warmup 1 --cpu-baseline off --no-prof
+  python tools/pmc_summary.py --fetch gpurun_out/pmc_fetch --write gpurun_out/pmc_write --steps 3 --out gpurun_out/traffic.json > gpurun_out/pmc_summary.log 2>&1; cat gpurun_out/pmc_summary.log
+fi
 exit 0
