@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define RRIN_ABI_VERSION 1
+#define RRIN_ABI_VERSION 2
 
 #define RRIN_OK 0
 #define RRIN_E_SHAPE (-1)     /* H or W not a multiple of 16, or N < 1          */
@@ -119,13 +119,86 @@ int rrin_pp_to_nchw(const rrin_pp* src, int32_t n, int32_t c, float* dst, void* 
 int rrin_warp_fwd(const float* img, const float* flow, float* out, int32_t n, int32_t c,
                   int32_t h, int32_t w, void* stream);
 
+/* ---- Split-fp16 path ("H8" layout) --------------------------------------- */
+/* Precision of a forward / conv:
+ *   F32   exact fp32 (v_mfma_f32_32x32x2_f32), PP layout above;
+ *   F16X3 every fp32 value v is held as hi = f16(v), lo = f16(v - hi)
+ *         (|v - hi - lo| <= 2^-22 |v| for normal lo) and every product as
+ *         hi*hi + hi*lo + lo*hi in v_mfma_f32_32x32x16_f16 with fp32
+ *         accumulation: fp32-class accuracy at ~5x the fp32 MFMA rate;
+ *   F16   hi only (fp16 storage, fp16 products, fp32 accumulation) for the
+ *         fp16 configs of BASELINE.json.
+ * H8 layout: per image, per group of 8 channels, an hp x wp plane of 16-byte
+ * records (8 halfs, channel-innermost); hp = round_up(h,16)+2,
+ * wp = round_up(w,32)+16 records, pixel (y,x) at record (y+1)*wp + x+8.
+ * F16X3 keeps two such tensors (hi, lo) with identical geometry. */
+enum rrin_prec { RRIN_PREC_F32 = 0, RRIN_PREC_F16X3 = 1, RRIN_PREC_F16 = 2 };
+
+int rrin_make_geom_h8(int32_t h, int32_t w, rrin_geom* g); /* plane in records */
+
+typedef struct rrin_h8 {
+  void* hi;           /* records (16 B), group 0 of image 0 of the tensor */
+  void* lo;           /* same geometry; NULL for F16                     */
+  int64_t img_stride; /* records between images                          */
+  int32_t g_off;      /* first 8-channel group of the view               */
+  int32_t groups;     /* groups in the view                              */
+  rrin_geom g;
+} rrin_h8;
+
+typedef struct rrin_conv_h8_desc {
+  int32_t n, cin, cout, cfg;   /* cfg: rrin_conv_h8_cfg_* */
+  int32_t prec;                /* F16X3 or F16 */
+  int32_t epi_mode;            /* rrin_epi_mode */
+  float slope;
+  float inv_wscale;            /* from rrin_pack_conv3x3_h8: weights were scaled by 1/inv_wscale */
+  rrin_h8 src, dst, pool;      /* pool: EPI_LEAKY_POOL only */
+  const void* whi;             /* packed halves (rrin_pack_conv3x3_h8) */
+  const void* wlo;             /* NULL for F16 */
+  const float* bias;           /* padded fp32 bias */
+} rrin_conv_h8_desc;
+
+int rrin_conv_h8_cfg_count(void);
+int rrin_conv_h8_cfg_bm(int32_t cfg);
+int rrin_conv_h8_cfg_th(int32_t cfg);
+int rrin_conv_h8_cfg_ok(int32_t cfg, int32_t prec); /* 1 if the config fits LDS at prec */
+int rrin_conv3x3_h8_fwd(const rrin_conv_h8_desc* d, void* stream);
+
+/* Host packing: [co_block][chunk of 16 ci][tap][half][bm][8] halves, weights
+ * pre-scaled by a power of two so max|w| lands in [2^12, 2^13) (keeps lo
+ * normal); *inv_wscale receives the exact inverse scale. */
+int64_t rrin_pack_conv3x3_h8_halves(int32_t cout, int32_t cin, int32_t bm);
+int rrin_pack_conv3x3_h8(const float* w, const float* b, int32_t cout, int32_t cin, int32_t bm,
+                         const int32_t* perm, int32_t prec, uint16_t* whi, uint16_t* wlo,
+                         float* bpack, float* inv_wscale);
+
+/* nn.Upsample(bilinear, x2) (unet.py:77) of an H8 view into another H8 view. */
+int rrin_upsample2x_h8(const rrin_h8* src, const rrin_h8* dst, int32_t n, int32_t prec, void* stream);
+/* NCHW fp32 <-> H8 view (c channels starting at channel ch_off of the view). */
+int rrin_nchw_to_h8(const float* src, int32_t n, int32_t c, int32_t ch_off, const rrin_h8* dst,
+                    int32_t prec, void* stream);
+int rrin_h8_to_nchw(const rrin_h8* src, int32_t n, int32_t c, int32_t ch_off, float* dst, int32_t prec,
+                    void* stream);
+
+typedef struct rrin_head_h8_desc {
+  int32_t n, cin, cout, mode, prec, pad_;
+  rrin_h8 src;           /* 32-channel input                              */
+  rrin_h8 g16;           /* Net buffer (2 groups); PLAIN: dst view          */
+  const float* w;        /* OIHW fp32 (unpacked)                          */
+  const float* bias;
+  const float* coef;
+  float* out;            /* FINAL: NCHW fp32 */
+} rrin_head_h8_desc;
+int rrin_head_h8_fwd(const rrin_head_h8_desc* d, void* stream);
+
 /* ---- Whole forward (native schedule) ------------------------------------- */
 /* Per-conv weight table entry, in Net conv order (rrin_net_conv_count). */
 typedef struct rrin_conv_weights {
-  const float* wpack;   /* packed with bm = rrin_conv_cfg_bm(cfg)   */
-  const float* bias;    /* packed bias                              */
-  int32_t cfg;
-  int32_t pad_;
+  const float* wpack;   /* F32: packed with bm = rrin_conv_cfg_bm(cfg)        */
+  const float* bias;    /* packed bias (bm of the config of this precision)  */
+  int32_t cfg;          /* F32: rrin_conv_cfg_*; F16*: rrin_conv_h8_cfg_*     */
+  float inv_wscale;     /* F16*: from rrin_pack_conv3x3_h8                    */
+  const void* whi;      /* F16*: packed halves                                */
+  const void* wlo;      /* F16X3: packed lo halves                            */
 } rrin_conv_weights;
 
 typedef struct rrin_head_weights {
@@ -159,12 +232,12 @@ typedef struct rrin_net_desc {
   void* workspace;      /* device, >= rrin_net_workspace_bytes, zero-filled once */
   int64_t workspace_bytes;
   int32_t skip_flow;    /* 1: reuse the Ft0/Ft1 already in the workspace (same pair) */
-  int32_t pad2_;
+  int32_t prec;         /* rrin_prec of the whole forward */
   rrin_prof* prof;      /* nullable: record events around every launch */
 } rrin_net_desc;
 
 int rrin_net_conv_count(void);                 /* 77 = 81 convs - 4 heads      */
-int64_t rrin_net_workspace_bytes(int32_t n, int32_t h, int32_t w);
+int64_t rrin_net_workspace_bytes(int32_t n, int32_t h, int32_t w, int32_t prec);
 int rrin_net_fwd(const rrin_net_desc* d, void* stream);
 
 /* ---- Misc ---------------------------------------------------------------- */

@@ -9,13 +9,15 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "librrin_hip.so")
 
 # enums (rrin_hip.h)
 SRC_DIRECT, SRC_UPSAMPLE2X = 0, 1
 EPI_LINEAR, EPI_LEAKY, EPI_LEAKY_POOL = 0, 1, 2
 HEAD_PLAIN, HEAD_FLOW, HEAD_REFINE, HEAD_MASK, HEAD_FINAL = 0, 1, 2, 3, 4
+PREC_F32, PREC_F16X3, PREC_F16 = 0, 1, 2
+PRECISIONS = {"fp32": PREC_F32, "fp32_split16": PREC_F16X3, "fp16": PREC_F16}
 
 
 class Geom(C.Structure):
@@ -41,7 +43,26 @@ class HeadDesc(C.Structure):
 
 
 class ConvWeights(C.Structure):
-    _fields_ = [("wpack", C.c_void_p), ("bias", C.c_void_p), ("cfg", C.c_int32), ("pad_", C.c_int32)]
+    _fields_ = [("wpack", C.c_void_p), ("bias", C.c_void_p), ("cfg", C.c_int32), ("inv_wscale", C.c_float),
+                ("whi", C.c_void_p), ("wlo", C.c_void_p)]
+
+
+class H8(C.Structure):
+    _fields_ = [("hi", C.c_void_p), ("lo", C.c_void_p), ("img_stride", C.c_int64), ("g_off", C.c_int32),
+                ("groups", C.c_int32), ("g", Geom)]
+
+
+class ConvH8Desc(C.Structure):
+    _fields_ = [("n", C.c_int32), ("cin", C.c_int32), ("cout", C.c_int32), ("cfg", C.c_int32),
+                ("prec", C.c_int32), ("epi_mode", C.c_int32), ("slope", C.c_float), ("inv_wscale", C.c_float),
+                ("src", H8), ("dst", H8), ("pool", H8), ("whi", C.c_void_p), ("wlo", C.c_void_p),
+                ("bias", C.c_void_p)]
+
+
+class HeadH8Desc(C.Structure):
+    _fields_ = [("n", C.c_int32), ("cin", C.c_int32), ("cout", C.c_int32), ("mode", C.c_int32),
+                ("prec", C.c_int32), ("pad_", C.c_int32), ("src", H8), ("g16", H8), ("w", C.c_void_p),
+                ("bias", C.c_void_p), ("coef", C.c_void_p), ("out", C.c_void_p)]
 
 
 class HeadWeights(C.Structure):
@@ -53,7 +74,7 @@ class NetDesc(C.Structure):
                 ("i0", C.c_void_p), ("i1", C.c_void_p), ("out", C.c_void_p), ("coef", C.c_void_p),
                 ("convs", C.POINTER(ConvWeights)), ("heads", C.POINTER(HeadWeights)),
                 ("workspace", C.c_void_p), ("workspace_bytes", C.c_int64),
-                ("skip_flow", C.c_int32), ("pad2_", C.c_int32), ("prof", C.c_void_p)]
+                ("skip_flow", C.c_int32), ("prec", C.c_int32), ("prof", C.c_void_p)]
 
 
 # every symbol include/rrin_hip.h declares: name -> (restype, argtypes)
@@ -73,7 +94,22 @@ SIGNATURES = {
     "rrin_warp_fwd": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_int32,
                                 C.c_int32, C.c_int32, C.c_void_p]),
     "rrin_net_conv_count": (C.c_int, []),
-    "rrin_net_workspace_bytes": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32]),
+    "rrin_net_workspace_bytes": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32, C.c_int32]),
+    "rrin_make_geom_h8": (C.c_int, [C.c_int32, C.c_int32, C.POINTER(Geom)]),
+    "rrin_conv_h8_cfg_count": (C.c_int, []),
+    "rrin_conv_h8_cfg_bm": (C.c_int, [C.c_int32]),
+    "rrin_conv_h8_cfg_th": (C.c_int, [C.c_int32]),
+    "rrin_conv_h8_cfg_ok": (C.c_int, [C.c_int32, C.c_int32]),
+    "rrin_conv3x3_h8_fwd": (C.c_int, [C.POINTER(ConvH8Desc), C.c_void_p]),
+    "rrin_pack_conv3x3_h8_halves": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32]),
+    "rrin_pack_conv3x3_h8": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p,
+                                       C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(C.c_float)]),
+    "rrin_upsample2x_h8": (C.c_int, [C.POINTER(H8), C.POINTER(H8), C.c_int32, C.c_int32, C.c_void_p]),
+    "rrin_nchw_to_h8": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.POINTER(H8), C.c_int32,
+                                  C.c_void_p]),
+    "rrin_h8_to_nchw": (C.c_int, [C.POINTER(H8), C.c_int32, C.c_int32, C.c_int32, C.c_void_p, C.c_int32,
+                                  C.c_void_p]),
+    "rrin_head_h8_fwd": (C.c_int, [C.POINTER(HeadH8Desc), C.c_void_p]),
     "rrin_net_fwd": (C.c_int, [C.POINTER(NetDesc), C.c_void_p]),
     "rrin_prof_create": (C.c_int, [C.c_int32, C.POINTER(C.c_void_p)]),
     "rrin_prof_destroy": (C.c_int, [C.c_void_p]),
@@ -118,4 +154,10 @@ def check(rc: int, what: str = "rrin"):
 def geom(h: int, w: int) -> Geom:
     g = Geom()
     check(lib().rrin_make_geom(h, w, C.byref(g)), "rrin_make_geom")
+    return g
+
+
+def geom_h8(h: int, w: int) -> Geom:
+    g = Geom()
+    check(lib().rrin_make_geom_h8(h, w, C.byref(g)), "rrin_make_geom_h8")
     return g

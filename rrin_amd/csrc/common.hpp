@@ -36,4 +36,80 @@ __host__ __device__ inline float* pp_chan(const rrin_pp& v, int n, int c) {
 
 inline int hip_code(hipError_t e) { return e == hipSuccess ? 0 : (int)e; }
 
+// ---- H8 (channel-blocked fp16 records) geometry -----------------------------
+constexpr int kH8PadLeft = 8;  // records: pixel x at record x+8 (128-B aligned rows)
+
+inline rrin_geom make_geom_h8(int h, int w) {
+  rrin_geom g;
+  g.h = h;
+  g.w = w;
+  g.hp = round_up(h, kPadRowsAlign) + 2;
+  g.wp = round_up(w, kPadColsAlign) + 2 * kH8PadLeft;
+  g.plane = (int64_t)g.hp * g.wp;
+  return g;
+}
+
+// ---- backwarp: grid_sample(bilinear, zeros, align_corners=False) ----------
+// Sampling position follows the reference grid arithmetic in fp32:
+//   x = gx + u;  nx = 2*(x/W - 0.5);  ix = (nx + 1) * (W/2) - 0.5   (CPU unnormalize)
+// then bilinear weights nw = s*e, ne = s*w, sw = n*e, se = n*w with zero taps
+// outside the frame (PyTorch CPU grid sampler order).
+struct WarpTaps {
+  int x0, y0;
+  float nw, ne, sw, se;
+  bool vx0, vx1, vy0, vy1;
+};
+
+#pragma clang fp contract(off)
+__device__ inline WarpTaps warp_taps(int gx, int gy, float u, float v, int H, int W) {
+  WarpTaps t;
+  const float x = (float)gx + u;
+  const float y = (float)gy + v;
+  const float nx = 2.0f * (x / (float)W - 0.5f);
+  const float ny = 2.0f * (y / (float)H - 0.5f);
+  const float ix = (nx + 1.0f) * ((float)W / 2.0f) - 0.5f;
+  const float iy = (ny + 1.0f) * ((float)H / 2.0f) - 0.5f;
+  const float fx = floorf(ix);
+  const float fy = floorf(iy);
+  const float we = ix - fx;  // "w" in the CPU kernel: distance to the west edge
+  const float e = 1.0f - we;
+  const float n = iy - fy;
+  const float s = 1.0f - n;
+  t.nw = s * e;
+  t.ne = s * we;
+  t.sw = n * e;
+  t.se = n * we;
+  // validity tested in float so that huge / non-finite flows never overflow an int
+  t.vx0 = fx >= 0.0f && fx <= (float)(W - 1);
+  t.vx1 = fx >= -1.0f && fx <= (float)(W - 2);
+  t.vy0 = fy >= 0.0f && fy <= (float)(H - 1);
+  t.vy1 = fy >= -1.0f && fy <= (float)(H - 2);
+  t.x0 = (t.vx0 || t.vx1) ? (int)fx : 0;
+  t.y0 = (t.vy0 || t.vy1) ? (int)fy : 0;
+  return t;
+}
+
+// plane: channel base; rs: row stride; off: offset of pixel (0,0)
+__device__ inline float warp_apply(const WarpTaps& t, const float* plane, int64_t rs, int64_t off) {
+  const float* p = plane + off + (int64_t)t.y0 * rs + t.x0;
+  const float a = (t.vy0 && t.vx0) ? p[0] : 0.0f;
+  const float b = (t.vy0 && t.vx1) ? p[1] : 0.0f;
+  const float c = (t.vy1 && t.vx0) ? p[rs] : 0.0f;
+  const float d = (t.vy1 && t.vx1) ? p[rs + 1] : 0.0f;
+  return a * t.nw + b * t.ne + c * t.sw + d * t.se;
+}
+
+// Same, with a value accessor get(y, x) (used for the fp16-split Net buffer).
+template <class F>
+__device__ inline float warp_apply_f(const WarpTaps& t, F get) {
+  const float a = (t.vy0 && t.vx0) ? get(t.y0, t.x0) : 0.0f;
+  const float b = (t.vy0 && t.vx1) ? get(t.y0, t.x0 + 1) : 0.0f;
+  const float c = (t.vy1 && t.vx0) ? get(t.y0 + 1, t.x0) : 0.0f;
+  const float d = (t.vy1 && t.vx1) ? get(t.y0 + 1, t.x0 + 1) : 0.0f;
+  return a * t.nw + b * t.ne + c * t.sw + d * t.se;
+}
+#pragma clang fp contract(on)
+
+
+
 }  // namespace rrin

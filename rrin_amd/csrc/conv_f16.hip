@@ -1,0 +1,869 @@
+// Split-fp16 ("F16X3") and fp16 ("F16") path of the RRIN hot path on the
+// gfx950 f16 matrix cores (v_mfma_f32_32x32x16_f16, fp32 accumulate).
+//
+// Numerics (F16X3): every fp32 value v lives as hi = f16(v), lo = f16(v - hi),
+// so v = hi + lo to 2^-22 |v| (lo normal; absolute 2^-25 floor otherwise).
+// A product a*w is computed as a_hi*w_hi + a_hi*w_lo + a_lo*w_hi — each term
+// exact in fp32 — and accumulated in fp32 by the MFMA; the dropped a_lo*w_lo is
+// <= 2^-22 |a w|.  Weights are pre-scaled by 2^s (exact) so their lo parts stay
+// normal; the epilogue multiplies by 2^-s.  F16 keeps hi only (fp16 configs).
+//
+// Replaces (as conv_mfma.hip): nn.Conv2d(3,pad=1) + LeakyReLU(0.1)
+// (/root/reference/unet.py:29,59-63,78), F.avg_pool2d (unet.py:46, fused second
+// output), torch.cat (unet.py:93, channel-offset views); nn.Upsample(bilinear,x2)
+// (unet.py:77) runs as its own pass (rrin_upsample2x_h8); the head convs +
+// model.py glue as head_h8_kernel.
+//
+// H8 activation layout: per image and 8-channel group an hp x wp plane of
+// 16-B records (8 halves).  A pixel's 8 channels are one record, so the MFMA
+// operands (8 consecutive k per lane) are single ds_read_b128s of the staged
+// tile, and epilogue stores of 32 pixels x 8 B per half-wave are contiguous.
+#include <math.h>
+#include <string.h>
+
+#include "common.hpp"
+
+namespace rrin {
+
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+constexpr int H8_LC = 34;  // staged input row: records of pixels x0-1 .. x0+32
+
+struct ConvH8Args {
+  const uint4* src_hi;
+  const uint4* src_lo;
+  int64_t src_img, src_gp;  // records per image / per group plane
+  int src_wp;
+  int cin, nchunks;         // chunks of 16 input channels
+  uint4* dst_hi;
+  uint4* dst_lo;
+  int64_t dst_img, dst_gp;
+  int dst_wp, cout;
+  uint4* pool_hi;
+  uint4* pool_lo;
+  int64_t pool_img, pool_gp;
+  int pool_wp;
+  const uint4* w_hi;
+  const uint4* w_lo;
+  const float* bias;
+  float inv_wscale, slope;
+  int h, w, co_blocks, tiles_x, tiles_y, n;
+};
+
+template <int NW, int WM, int WN, int PLANES>
+struct TileH8 {
+  static constexpr int NT = 64 * NW;
+  static constexpr int BM = 32 * WM;
+  static constexpr int TH = WN * NW;
+  static constexpr int ROWS = TH + 2;
+  static constexpr int IN_REC = 2 * ROWS * H8_LC;  // per plane: 2 groups x rows x cols
+  static constexpr int W_REC = 9 * 2 * BM;          // per plane: taps x halves x co
+  static constexpr int IN_IT = (IN_REC + NT - 1) / NT;
+  static constexpr int W_IT = (W_REC + NT - 1) / NT;
+  static constexpr size_t LDS = 2 * (size_t)PLANES * (IN_REC + W_REC) * 16;
+  static_assert(16 % TH == 0, "TH must divide the 16-row plane padding");
+};
+
+__device__ inline uint4 mask_halves(uint4 v, int nvalid) {
+  // keep halves [0, nvalid) of a record (nvalid in 1..7)
+  unsigned* d = reinterpret_cast<unsigned*>(&v);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (2 * k >= nvalid)
+      d[k] = 0u;
+    else if (2 * k + 1 >= nvalid)
+      d[k] &= 0xFFFFu;
+  }
+  return v;
+}
+
+template <int NW, int WM, int WN, int PLANES, int EPI>
+__global__ void __launch_bounds__(64 * NW) conv3x3_h8_kernel(ConvH8Args a) {
+  using T = TileH8<NW, WM, WN, PLANES>;
+  constexpr int NT = T::NT, BM = T::BM, TH = T::TH, ROWS = T::ROWS;
+  constexpr int IN_REC = T::IN_REC, W_REC = T::W_REC;
+
+  extern __shared__ __attribute__((aligned(16))) uint4 smem4[];
+  uint4* s_in = smem4;                          // [buf][plane][IN_REC]
+  uint4* s_w = smem4 + 2 * PLANES * IN_REC;     // [buf][plane][W_REC]
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wn = tid >> 6;  // waves stacked along output rows
+  const int j = lane & 31;
+  const int hh = lane >> 5;
+
+  int bid;
+  {  // XCD-aware bijective remap (see conv_mfma.hip)
+    const int nwg = gridDim.x, q = nwg >> 3, r = nwg & 7;
+    const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+  }
+  const int cob = bid % a.co_blocks;
+  bid /= a.co_blocks;
+  const int tx = bid % a.tiles_x;
+  bid /= a.tiles_x;
+  const int ty = bid % a.tiles_y;
+  const int img = bid / a.tiles_y;
+  const int x0 = tx * 32;
+  const int y0 = ty * TH;
+
+  const uint4* src[2] = {a.src_hi + img * a.src_img, PLANES == 2 ? a.src_lo + img * a.src_img : nullptr};
+  const uint4* wsrc[2] = {a.w_hi + (int64_t)cob * a.nchunks * W_REC,
+                          PLANES == 2 ? a.w_lo + (int64_t)cob * a.nchunks * W_REC : nullptr};
+
+  uint4 rin[PLANES][T::IN_IT];
+  uint4 rw[PLANES][T::W_IT];
+
+  auto load_in = [&](int c) {
+#pragma unroll
+    for (int it = 0; it < T::IN_IT; ++it) {
+      const int idx = tid + NT * it;
+      if (idx < IN_REC) {
+        const int g = idx / (ROWS * H8_LC);
+        const int rem = idx - g * (ROWS * H8_LC);
+        const int r = rem / H8_LC;
+        const int col = rem - r * H8_LC;
+        const int gg = c * 2 + g;
+        const int nval = a.cin - gg * 8;
+        const int64_t off = (int64_t)gg * a.src_gp + (int64_t)(y0 + r) * a.src_wp + x0 + (kH8PadLeft - 1) + col;
+#pragma unroll
+        for (int p = 0; p < PLANES; ++p) {
+          uint4 v = make_uint4(0u, 0u, 0u, 0u);
+          if (nval > 0) {
+            v = src[p][off];
+            if (nval < 8) v = mask_halves(v, nval);
+          }
+          rin[p][it] = v;
+        }
+      }
+    }
+  };
+  auto store_in = [&](int buf) {
+#pragma unroll
+    for (int p = 0; p < PLANES; ++p)
+#pragma unroll
+      for (int it = 0; it < T::IN_IT; ++it) {
+        const int idx = tid + NT * it;
+        if (idx < IN_REC) s_in[(buf * PLANES + p) * IN_REC + idx] = rin[p][it];
+      }
+  };
+  auto load_w = [&](int c) {
+#pragma unroll
+    for (int p = 0; p < PLANES; ++p)
+#pragma unroll
+      for (int it = 0; it < T::W_IT; ++it) {
+        const int idx = tid + NT * it;
+        if (idx < W_REC) rw[p][it] = wsrc[p][(int64_t)c * W_REC + idx];
+      }
+  };
+  auto store_w = [&](int buf) {
+#pragma unroll
+    for (int p = 0; p < PLANES; ++p)
+#pragma unroll
+      for (int it = 0; it < T::W_IT; ++it) {
+        const int idx = tid + NT * it;
+        if (idx < W_REC) s_w[(buf * PLANES + p) * W_REC + idx] = rw[p][it];
+      }
+  };
+
+  floatx16 acc[WM][WN];
+#pragma unroll
+  for (int mt = 0; mt < WM; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < WN; ++nt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[mt][nt][i] = 0.f;
+
+  // 9 taps per chunk; one K16 block = 16 input channels at one tap (lanes
+  // 0-31 carry channels 0-7 of the chunk, lanes 32-63 channels 8-15).
+  // Operands of tap t+1 are read before the MFMAs of tap t issue.
+  auto compute = [&](int buf) {
+    const uint4* si[PLANES];
+    const uint4* sw[PLANES];
+#pragma unroll
+    for (int p = 0; p < PLANES; ++p) {
+      si[p] = s_in + (buf * PLANES + p) * IN_REC + (hh * ROWS + wn * WN) * H8_LC + j;
+      sw[p] = s_w + (buf * PLANES + p) * W_REC + hh * BM + j;
+    }
+    half8 av[2][PLANES][WM], bv[2][PLANES][WN];
+    auto ld = [&](int t, int slot) {
+      const int ky = t / 3, kx = t % 3;
+#pragma unroll
+      for (int p = 0; p < PLANES; ++p) {
+#pragma unroll
+        for (int mt = 0; mt < WM; ++mt) av[slot][p][mt] = __builtin_bit_cast(half8, sw[p][t * 2 * BM + mt * 32]);
+#pragma unroll
+        for (int nt = 0; nt < WN; ++nt) bv[slot][p][nt] = __builtin_bit_cast(half8, si[p][(nt + ky) * H8_LC + kx]);
+      }
+    };
+    ld(0, 0);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      if (t + 1 < 9) ld(t + 1, (t + 1) & 1);
+      const int s = t & 1;
+#pragma unroll
+      for (int mt = 0; mt < WM; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < WN; ++nt) {
+          if constexpr (PLANES == 2) {
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[s][1][mt], bv[s][0][nt], acc[mt][nt], 0, 0, 0);
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[s][0][mt], bv[s][1][nt], acc[mt][nt], 0, 0, 0);
+          }
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[s][0][mt], bv[s][0][nt], acc[mt][nt], 0, 0, 0);
+        }
+    }
+  };
+
+  load_w(0);
+  load_in(0);
+  store_in(0);
+  store_w(0);
+  __syncthreads();
+  for (int c = 0; c < a.nchunks; ++c) {
+    const int buf = c & 1;
+    const bool more = (c + 1) < a.nchunks;
+    if (more) {
+      load_w(c + 1);
+      load_in(c + 1);
+    }
+    compute(buf);
+    if (more) {
+      store_in(buf ^ 1);
+      store_w(buf ^ 1);
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue: scale, bias, leaky, split, 8-B half-record stores (+ pool)
+  const int yb = y0 + wn * WN;
+  const int x = x0 + j;
+  uint4* dst[2] = {a.dst_hi + img * a.dst_img, PLANES == 2 ? a.dst_lo + img * a.dst_img : nullptr};
+  uint4* pdst[2] = {nullptr, nullptr};
+  if constexpr (EPI == RRIN_EPI_LEAKY_POOL) {
+    pdst[0] = a.pool_hi + img * a.pool_img;
+    if (PLANES == 2) pdst[1] = a.pool_lo + img * a.pool_img;
+  }
+#pragma unroll
+  for (int mt = 0; mt < WM; ++mt) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int co0 = cob * BM + mt * 32 + 8 * q;  // first channel of the record
+      const int grp = co0 >> 3;
+      float bs[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bs[e] = a.bias[co0 + 4 * hh + e];
+      float v[WN][4];
+#pragma unroll
+      for (int nt = 0; nt < WN; ++nt) {
+        const int y = yb + nt;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float t = acc[mt][nt][4 * q + e] * a.inv_wscale + bs[e];
+          if constexpr (EPI != RRIN_EPI_LINEAR) t = t > 0.f ? t : t * a.slope;
+          v[nt][e] = t;
+        }
+        if (co0 < a.cout && y < a.h && x < a.w) {
+          const int64_t rec = (int64_t)grp * a.dst_gp + (int64_t)(y + 1) * a.dst_wp + x + kH8PadLeft;
+          _Float16 hi[4], lo[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            hi[e] = (_Float16)v[nt][e];
+            lo[e] = (_Float16)(v[nt][e] - (float)hi[e]);
+          }
+          reinterpret_cast<uint2*>(dst[0] + rec)[hh] = __builtin_bit_cast(uint2, hi);
+          if constexpr (PLANES == 2) reinterpret_cast<uint2*>(dst[1] + rec)[hh] = __builtin_bit_cast(uint2, lo);
+        }
+      }
+      if constexpr (EPI == RRIN_EPI_LEAKY_POOL) {
+#pragma unroll
+        for (int p2 = 0; p2 < WN / 2; ++p2) {
+          float s4[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float s = v[2 * p2][e] + v[2 * p2 + 1][e];
+            s4[e] = 0.25f * (s + __shfl_xor(s, 1));
+          }
+          const int y = yb + 2 * p2;
+          if (!(j & 1) && co0 < a.cout && y < a.h && x < a.w) {
+            const int64_t rec = (int64_t)grp * a.pool_gp + (int64_t)(y / 2 + 1) * a.pool_wp + x / 2 + kH8PadLeft;
+            _Float16 hi[4], lo[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              hi[e] = (_Float16)s4[e];
+              lo[e] = (_Float16)(s4[e] - (float)hi[e]);
+            }
+            reinterpret_cast<uint2*>(pdst[0] + rec)[hh] = __builtin_bit_cast(uint2, hi);
+            if constexpr (PLANES == 2) reinterpret_cast<uint2*>(pdst[1] + rec)[hh] = __builtin_bit_cast(uint2, lo);
+          }
+        }
+      }
+    }
+  }
+}
+
+// ---- bilinear x2 upsample pass (unet.py:77, align_corners=False) -------------
+template <int PLANES>
+__global__ void up2x_h8_kernel(const uint4* __restrict__ s_hi, const uint4* __restrict__ s_lo, int64_t s_img,
+                               int64_t s_gp, int s_wp, int sh, int sw, uint4* d_hi, uint4* d_lo, int64_t d_img,
+                               int64_t d_gp, int d_wp, int groups, int64_t total) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int w = 2 * sw, h = 2 * sh;
+  const int x = (int)(i % w);
+  int64_t t = i / w;
+  const int y = (int)(t % h);
+  t /= h;
+  const int g = (int)(t % groups);
+  const int img = (int)(t / groups);
+  // Y even (2i): 0.25 row(i-1) + 0.75 row(i); odd: 0.75 row(i) + 0.25 row(i+1); edges clamp
+  int ra, rb, ca, cb;
+  float wa, wc;
+  if (y & 1) { ra = y >> 1; rb = min(ra + 1, sh - 1); wa = 0.75f; }
+  else { rb = y >> 1; ra = max(rb - 1, 0); wa = 0.25f; }
+  if (x & 1) { ca = x >> 1; cb = min(ca + 1, sw - 1); wc = 0.75f; }
+  else { cb = x >> 1; ca = max(cb - 1, 0); wc = 0.25f; }
+  const float wb = 1.0f - wa, wd = 1.0f - wc;
+  const int64_t base = img * s_img + g * s_gp;
+  const int64_t r00 = base + (int64_t)(ra + 1) * s_wp + ca + kH8PadLeft;
+  const int64_t r01 = base + (int64_t)(ra + 1) * s_wp + cb + kH8PadLeft;
+  const int64_t r10 = base + (int64_t)(rb + 1) * s_wp + ca + kH8PadLeft;
+  const int64_t r11 = base + (int64_t)(rb + 1) * s_wp + cb + kH8PadLeft;
+  half8 q[4][PLANES];
+  const int64_t rr[4] = {r00, r01, r10, r11};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    q[k][0] = __builtin_bit_cast(half8, s_hi[rr[k]]);
+    if constexpr (PLANES == 2) q[k][1] = __builtin_bit_cast(half8, s_lo[rr[k]]);
+  }
+  half8 ohi, olo;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    float v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = (float)q[k][0][e] + (PLANES == 2 ? (float)q[k][PLANES - 1][e] : 0.0f);
+    // horizontal first, then vertical (upsample_bilinear2d order)
+    const float top = wc * v[0] + wd * v[1];
+    const float bot = wc * v[2] + wd * v[3];
+    const float o = wa * top + wb * bot;
+    ohi[e] = (_Float16)o;
+    olo[e] = (_Float16)(o - (float)ohi[e]);
+  }
+  const int64_t drec = img * d_img + g * d_gp + (int64_t)(y + 1) * d_wp + x + kH8PadLeft;
+  d_hi[drec] = __builtin_bit_cast(uint4, ohi);
+  if constexpr (PLANES == 2) d_lo[drec] = __builtin_bit_cast(uint4, olo);
+}
+
+// ---- layout kernels ------------------------------------------------------------
+__device__ inline int64_t h8_half_index(int64_t img_stride, int64_t gp, int wp, int img, int ch, int y, int x) {
+  return ((int64_t)img * img_stride + (int64_t)(ch >> 3) * gp + (int64_t)(y + 1) * wp + x + kH8PadLeft) * 8 +
+         (ch & 7);
+}
+
+__global__ void nchw_to_h8_kernel(const float* __restrict__ src, _Float16* hi, _Float16* lo, int64_t img_stride,
+                                  int64_t gp, int wp, int ch_off, int c, int h, int w, int64_t total) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int x = (int)(i % w);
+  int64_t t = i / w;
+  const int y = (int)(t % h);
+  t /= h;
+  const int ch = (int)(t % c);
+  const int n = (int)(t / c);
+  const float v = src[i];
+  const int64_t k = h8_half_index(img_stride, gp, wp, n, ch_off + ch, y, x);
+  const _Float16 vh = (_Float16)v;
+  hi[k] = vh;
+  if (lo) lo[k] = (_Float16)(v - (float)vh);
+}
+
+__global__ void h8_to_nchw_kernel(const _Float16* __restrict__ hi, const _Float16* __restrict__ lo, int64_t img_stride,
+                                  int64_t gp, int wp, int ch_off, float* dst, int c, int h, int w, int64_t total) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int x = (int)(i % w);
+  int64_t t = i / w;
+  const int y = (int)(t % h);
+  t /= h;
+  const int ch = (int)(t % c);
+  const int n = (int)(t / c);
+  const int64_t k = h8_half_index(img_stride, gp, wp, n, ch_off + ch, y, x);
+  dst[i] = (float)hi[k] + (lo ? (float)lo[k] : 0.0f);
+}
+
+// ---- head conv (Cout <= 4) + Net glue on the H8 Net buffer --------------------
+struct HeadH8Args {
+  const uint4* src_hi;
+  const uint4* src_lo;
+  int64_t src_img, src_gp;
+  int src_wp;
+  _Float16* g_hi;  // g16: 2 groups
+  _Float16* g_lo;
+  int64_t g_img, g_gp;
+  int g_wp;
+  const float* w;
+  const float* bias;
+  const float* coef;
+  float* out;
+  int h, w_, tiles_x, tiles_y;
+};
+
+template <int COUT, int MODE, int PLANES>
+__global__ void __launch_bounds__(256) head_h8_kernel(HeadH8Args a) {
+  constexpr int CIN = 32, HROWS = 10, HLC = 40;
+  __shared__ __attribute__((aligned(16))) float s_in[8 * HROWS * HLC];
+  const int tid = threadIdx.x;
+  int bid = blockIdx.x;
+  const int tx = bid % a.tiles_x;
+  bid /= a.tiles_x;
+  const int ty = bid % a.tiles_y;
+  const int img = bid / a.tiles_y;
+  const int x0 = tx * 32, y0 = ty * 8;
+  const int r = tid >> 5, xl = tid & 31;
+
+  float acc[COUT];
+#pragma unroll
+  for (int co = 0; co < COUT; ++co) acc[co] = a.bias[co];
+
+  for (int g = 0; g < CIN / 8; ++g) {
+    // stage records of rows y0-1..y0+8, cols x0-1..x0+32 -> fp32 planar LDS
+    for (int idx = tid; idx < HROWS * H8_LC; idx += 256) {
+      const int rr = idx / H8_LC, col = idx - rr * H8_LC;
+      const int64_t rec = img * a.src_img + (int64_t)g * a.src_gp + (int64_t)(y0 + rr) * a.src_wp + x0 +
+                          (kH8PadLeft - 1) + col;
+      const half8 vh = __builtin_bit_cast(half8, a.src_hi[rec]);
+      half8 vl = {};
+      if constexpr (PLANES == 2) vl = __builtin_bit_cast(half8, a.src_lo[rec]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        s_in[(e * HROWS + rr) * HLC + col + 3] = (float)vh[e] + (PLANES == 2 ? (float)vl[e] : 0.0f);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ci = 0; ci < 8; ++ci)
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          const float v = s_in[(ci * HROWS + r + ky) * HLC + xl + 3 + kx];
+#pragma unroll
+          for (int co = 0; co < COUT; ++co)
+            acc[co] = fmaf(a.w[((co * CIN) + g * 8 + ci) * 9 + ky * 3 + kx], v, acc[co]);
+        }
+    __syncthreads();
+  }
+
+  const int y = y0 + r, x = x0 + xl;
+  if (y >= a.h || x >= a.w_) return;
+  auto idx_of = [&](int ch, int yy, int xx) { return h8_half_index(a.g_img, a.g_gp, a.g_wp, img, ch, yy, xx); };
+  auto rd = [&](int ch, int yy, int xx) -> float {
+    const int64_t k = idx_of(ch, yy, xx);
+    return (float)a.g_hi[k] + (PLANES == 2 ? (float)a.g_lo[k] : 0.0f);
+  };
+  auto wr = [&](int ch, float v) {
+    const int64_t k = idx_of(ch, y, x);
+    const _Float16 vh = (_Float16)v;
+    a.g_hi[k] = vh;
+    if constexpr (PLANES == 2) a.g_lo[k] = (_Float16)(v - (float)vh);
+  };
+  const float* cf = a.coef + img * 8;
+
+  if constexpr (MODE == RRIN_HEAD_PLAIN) {
+#pragma unroll
+    for (int co = 0; co < COUT; ++co) wr(co, acc[co]);
+  } else if constexpr (MODE == RRIN_HEAD_FLOW) {
+#pragma clang fp contract(off)
+    for (int k = 0; k < 2; ++k) {
+      wr(6 + k, cf[0] * acc[k] + cf[1] * acc[2 + k]);
+      wr(8 + k, cf[2] * acc[k] - cf[3] * acc[2 + k]);
+    }
+  } else if constexpr (MODE == RRIN_HEAD_REFINE) {
+#pragma clang fp contract(off)
+    const float f0u = rd(6, y, x) + acc[0], f0v = rd(7, y, x) + acc[1];
+    const float f1u = rd(8, y, x) + acc[2], f1v = rd(9, y, x) + acc[3];
+    wr(6, f0u);
+    wr(7, f0v);
+    wr(8, f1u);
+    wr(9, f1v);
+    const WarpTaps t0 = warp_taps(x, y, f0u, f0v, a.h, a.w_);
+    const WarpTaps t1 = warp_taps(x, y, f1u, f1v, a.h, a.w_);
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+      wr(10 + ch, warp_apply_f(t0, [&](int yy, int xx) { return rd(ch, yy, xx); }));
+      wr(13 + ch, warp_apply_f(t1, [&](int yy, int xx) { return rd(3 + ch, yy, xx); }));
+    }
+  } else if constexpr (MODE == RRIN_HEAD_MASK) {
+#pragma clang fp contract(off)
+    const float m0 = 1.0f / (1.0f + expf(-acc[0]));
+    const float m1 = 1.0f / (1.0f + expf(-acc[1]));
+    const float w1 = cf[4] * m0, w2 = cf[5] * m1;
+    const float den = w1 + w2 + 1e-8f;
+    float o[3];
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) o[ch] = (w1 * rd(10 + ch, y, x) + w2 * rd(13 + ch, y, x)) / den;
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) wr(6 + ch, o[ch]);
+  } else {  // FINAL
+#pragma clang fp contract(off)
+    float* o = a.out + ((int64_t)img * 3) * a.h * a.w_ + (int64_t)y * a.w_ + x;
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+      const float v = acc[ch] + rd(6 + ch, y, x);
+      o[(int64_t)ch * a.h * a.w_] = v < 0.0f ? 0.0f : (v > 1.0f ? 1.0f : v);
+    }
+  }
+}
+
+// ---- host helpers ------------------------------------------------------------------
+// fp32 -> fp16 bits, round to nearest even (host packing).
+static uint16_t f2h_rne(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  const uint32_t sign = (u >> 16) & 0x8000u;
+  const uint32_t au = u & 0x7FFFFFFFu;
+  if (au >= 0x7F800000u) return (uint16_t)(sign | (au > 0x7F800000u ? 0x7E00u : 0x7C00u));
+  if (au >= 0x477FF000u) return (uint16_t)(sign | 0x7C00u);  // rounds to >= 65520 -> inf
+  if (au < 0x38800000u) {                                     // subnormal / zero in fp16
+    const float af = fabsf(f);
+    const uint32_t m = (uint32_t)lrintf(af * 16777216.0f);     // units of 2^-24, RNE
+    return (uint16_t)(sign | m);
+  }
+  const uint32_t e = ((au >> 23) - 112u) << 10;  // rebias 127 -> 15
+  uint32_t m = (au >> 13) & 0x3FFu;
+  const uint32_t rest = au & 0x1FFFu;
+  uint32_t h = e | m;
+  if (rest > 0x1000u || (rest == 0x1000u && (m & 1u))) h += 1u;
+  return (uint16_t)(sign | h);
+}
+
+static float h2f(uint16_t h) {
+  const uint32_t sign = (uint32_t)(h & 0x8000u) << 16;
+  const uint32_t e = (h >> 10) & 0x1Fu, m = h & 0x3FFu;
+  float f;
+  if (e == 0) {
+    f = ldexpf((float)m, -24);
+  } else if (e == 31) {
+    uint32_t u = sign | 0x7F800000u | (m << 13);
+    memcpy(&f, &u, 4);
+    return f;
+  } else {
+    uint32_t u = ((e + 112u) << 23) | (m << 13);
+    memcpy(&f, &u, 4);
+  }
+  return sign ? -f : f;
+}
+
+// Config table: cfg -> (NW waves along rows, WM co-tiles, WN rows per wave)
+#define RRIN_H8_CFGS(X) \
+  X(0, 8, 2, 2)         \
+  X(1, 8, 1, 2)         \
+  X(2, 4, 2, 2)         \
+  X(3, 4, 1, 4)         \
+  X(4, 4, 2, 1)         \
+  X(5, 8, 4, 2)
+
+struct CfgH8 {
+  int bm, th;
+  size_t lds1, lds2;
+};
+static const CfgH8 kCfgH8[] = {
+#define X(id, nw, wm, wn) {TileH8<nw, wm, wn, 1>::BM, TileH8<nw, wm, wn, 1>::TH, TileH8<nw, wm, wn, 1>::LDS, \
+                           TileH8<nw, wm, wn, 2>::LDS},
+    RRIN_H8_CFGS(X)
+#undef X
+};
+static constexpr int kNumCfgH8 = sizeof(kCfgH8) / sizeof(kCfgH8[0]);
+static constexpr size_t kMaxLds = 160 * 1024;
+
+template <int NW, int WM, int WN, int PLANES, int EPI>
+static int launch_h8_t(const ConvH8Args& args, int grid, hipStream_t st) {
+  using T = TileH8<NW, WM, WN, PLANES>;
+  if constexpr (T::LDS > kMaxLds) {
+    return RRIN_E_CONFIG;
+  } else {
+    auto k = conv3x3_h8_kernel<NW, WM, WN, PLANES, EPI>;
+    static bool attr_set = false;
+    if (!attr_set) {
+      hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)T::LDS);
+      if (e != hipSuccess) return (int)e;
+      attr_set = true;
+    }
+    hipLaunchKernelGGL(k, dim3(grid), dim3(T::NT), T::LDS, st, args);
+    return hip_code(hipGetLastError());
+  }
+}
+
+template <int NW, int WM, int WN>
+static int launch_h8_cfg(const ConvH8Args& args, int planes, int epi, int grid, hipStream_t st) {
+  if (planes == 2) {
+    if (epi == RRIN_EPI_LINEAR) return launch_h8_t<NW, WM, WN, 2, RRIN_EPI_LINEAR>(args, grid, st);
+    if (epi == RRIN_EPI_LEAKY) return launch_h8_t<NW, WM, WN, 2, RRIN_EPI_LEAKY>(args, grid, st);
+    return launch_h8_t<NW, WM, WN, 2, RRIN_EPI_LEAKY_POOL>(args, grid, st);
+  }
+  if (epi == RRIN_EPI_LINEAR) return launch_h8_t<NW, WM, WN, 1, RRIN_EPI_LINEAR>(args, grid, st);
+  if (epi == RRIN_EPI_LEAKY) return launch_h8_t<NW, WM, WN, 1, RRIN_EPI_LEAKY>(args, grid, st);
+  return launch_h8_t<NW, WM, WN, 1, RRIN_EPI_LEAKY_POOL>(args, grid, st);
+}
+
+static bool h8_ok(const rrin_h8& v, int prec) {
+  if (!v.hi || (prec == RRIN_PREC_F16X3 && !v.lo)) return false;
+  const rrin_geom g = make_geom_h8(v.g.h, v.g.w);
+  return g.hp == v.g.hp && g.wp == v.g.wp && g.plane == v.g.plane;
+}
+
+static inline int planes_of(int prec) { return prec == RRIN_PREC_F16X3 ? 2 : 1; }
+
+}  // namespace rrin
+
+using namespace rrin;
+
+extern "C" int rrin_make_geom_h8(int32_t h, int32_t w, rrin_geom* g) {
+  if (!g || h < 1 || w < 1) return RRIN_E_ARG;
+  *g = make_geom_h8(h, w);
+  return 0;
+}
+
+extern "C" int rrin_conv_h8_cfg_count(void) { return kNumCfgH8; }
+extern "C" int rrin_conv_h8_cfg_bm(int32_t cfg) {
+  return (cfg >= 0 && cfg < kNumCfgH8) ? kCfgH8[cfg].bm : RRIN_E_CONFIG;
+}
+extern "C" int rrin_conv_h8_cfg_th(int32_t cfg) {
+  return (cfg >= 0 && cfg < kNumCfgH8) ? kCfgH8[cfg].th : RRIN_E_CONFIG;
+}
+extern "C" int rrin_conv_h8_cfg_ok(int32_t cfg, int32_t prec) {
+  if (cfg < 0 || cfg >= kNumCfgH8) return 0;
+  if (prec != RRIN_PREC_F16X3 && prec != RRIN_PREC_F16) return 0;
+  return (planes_of(prec) == 2 ? kCfgH8[cfg].lds2 : kCfgH8[cfg].lds1) <= kMaxLds ? 1 : 0;
+}
+
+extern "C" int rrin_conv3x3_h8_fwd(const rrin_conv_h8_desc* d, void* stream) {
+  if (!d || !d->whi || !d->bias) return RRIN_E_ARG;
+  if (d->prec != RRIN_PREC_F16X3 && d->prec != RRIN_PREC_F16) return RRIN_E_ARG;
+  if (d->prec == RRIN_PREC_F16X3 && !d->wlo) return RRIN_E_ARG;
+  if (!rrin_conv_h8_cfg_ok(d->cfg, d->prec)) return RRIN_E_CONFIG;
+  if (d->n < 1 || d->cin < 1 || d->cout < 8 || (d->cout & 7)) return RRIN_E_ARG;
+  if (d->epi_mode < RRIN_EPI_LINEAR || d->epi_mode > RRIN_EPI_LEAKY_POOL) return RRIN_E_ARG;
+  if (!h8_ok(d->src, d->prec) || !h8_ok(d->dst, d->prec)) return RRIN_E_SHAPE;
+  const int h = d->dst.g.h, w = d->dst.g.w;
+  if (d->src.g.h != h || d->src.g.w != w) return RRIN_E_SHAPE;
+  if (d->cin > 8 * d->src.groups || d->cout > 8 * d->dst.groups) return RRIN_E_ARG;
+  if (d->epi_mode == RRIN_EPI_LEAKY_POOL) {
+    if (!h8_ok(d->pool, d->prec) || (h & 1) || (w & 1) || d->pool.g.h * 2 != h || d->pool.g.w * 2 != w ||
+        d->cout > 8 * d->pool.groups)
+      return RRIN_E_SHAPE;
+  }
+  const int planes = planes_of(d->prec);
+  const CfgH8& ci = kCfgH8[d->cfg];
+  ConvH8Args a;
+  memset(&a, 0, sizeof(a));
+  const int64_t sg = (int64_t)d->src.g_off * d->src.g.plane;
+  a.src_hi = static_cast<const uint4*>(d->src.hi) + sg;
+  a.src_lo = planes == 2 ? static_cast<const uint4*>(d->src.lo) + sg : nullptr;
+  a.src_img = d->src.img_stride;
+  a.src_gp = d->src.g.plane;
+  a.src_wp = d->src.g.wp;
+  a.cin = d->cin;
+  a.nchunks = (d->cin + 15) / 16;
+  const int64_t dg = (int64_t)d->dst.g_off * d->dst.g.plane;
+  a.dst_hi = static_cast<uint4*>(d->dst.hi) + dg;
+  a.dst_lo = planes == 2 ? static_cast<uint4*>(d->dst.lo) + dg : nullptr;
+  a.dst_img = d->dst.img_stride;
+  a.dst_gp = d->dst.g.plane;
+  a.dst_wp = d->dst.g.wp;
+  a.cout = d->cout;
+  if (d->epi_mode == RRIN_EPI_LEAKY_POOL) {
+    const int64_t pg = (int64_t)d->pool.g_off * d->pool.g.plane;
+    a.pool_hi = static_cast<uint4*>(d->pool.hi) + pg;
+    a.pool_lo = planes == 2 ? static_cast<uint4*>(d->pool.lo) + pg : nullptr;
+    a.pool_img = d->pool.img_stride;
+    a.pool_gp = d->pool.g.plane;
+    a.pool_wp = d->pool.g.wp;
+  }
+  a.w_hi = static_cast<const uint4*>(d->whi);
+  a.w_lo = planes == 2 ? static_cast<const uint4*>(d->wlo) : nullptr;
+  a.bias = d->bias;
+  a.inv_wscale = d->inv_wscale;
+  a.slope = d->slope;
+  a.h = h;
+  a.w = w;
+  a.co_blocks = (d->cout + ci.bm - 1) / ci.bm;
+  a.tiles_x = (w + 31) / 32;
+  a.tiles_y = (h + ci.th - 1) / ci.th;
+  a.n = d->n;
+  const int64_t grid = (int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n;
+  if (grid > 0x7fffffff) return RRIN_E_SHAPE;
+  hipStream_t st = (hipStream_t)stream;
+  switch (d->cfg) {
+#define X(id, nw, wm, wn) \
+  case id:                \
+    return launch_h8_cfg<nw, wm, wn>(a, planes, d->epi_mode, (int)grid, st);
+    RRIN_H8_CFGS(X)
+#undef X
+  }
+  return RRIN_E_CONFIG;
+}
+
+extern "C" int64_t rrin_pack_conv3x3_h8_halves(int32_t cout, int32_t cin, int32_t bm) {
+  if (cout < 1 || cin < 1 || bm < 32 || bm % 32) return RRIN_E_ARG;
+  const int64_t cob = (cout + bm - 1) / bm, nch = (cin + 15) / 16;
+  return cob * nch * 9 * 2 * bm * 8;
+}
+
+extern "C" int rrin_pack_conv3x3_h8(const float* w, const float* b, int32_t cout, int32_t cin, int32_t bm,
+                                    const int32_t* perm, int32_t prec, uint16_t* whi, uint16_t* wlo, float* bpack,
+                                    float* inv_wscale) {
+  if (!w || !b || !whi || !bpack || !inv_wscale || cout < 1 || cin < 1 || bm < 32 || bm % 32) return RRIN_E_ARG;
+  if (prec != RRIN_PREC_F16X3 && prec != RRIN_PREC_F16) return RRIN_E_ARG;
+  if (prec == RRIN_PREC_F16X3 && !wlo) return RRIN_E_ARG;
+  if (perm)
+    for (int c = 0; c < cin; ++c)
+      if (perm[c] < 0 || perm[c] >= cin) return RRIN_E_ARG;
+  float mx = 0.f;
+  const int64_t nw = (int64_t)cout * cin * 9;
+  for (int64_t i = 0; i < nw; ++i) mx = fmaxf(mx, fabsf(w[i]));
+  if (!(mx < INFINITY)) return RRIN_E_ARG;
+  int s = 0;
+  if (mx > 0.f) {
+    int e;
+    frexpf(mx, &e);  // mx in [2^(e-1), 2^e)
+    s = 13 - e;      // scaled max in [2^12, 2^13)
+  }
+  const float scale = ldexpf(1.0f, s);
+  *inv_wscale = ldexpf(1.0f, -s);
+  const int cob_n = (cout + bm - 1) / bm, nch = (cin + 15) / 16;
+  int64_t o = 0;
+  for (int cob = 0; cob < cob_n; ++cob)
+    for (int c = 0; c < nch; ++c)
+      for (int tap = 0; tap < 9; ++tap)
+        for (int hh = 0; hh < 2; ++hh)
+          for (int col = 0; col < bm; ++col)
+            for (int e = 0; e < 8; ++e) {
+              const int co = cob * bm + col, ch = c * 16 + hh * 8 + e;
+              float v = 0.f;
+              if (co < cout && ch < cin) v = w[((int64_t)co * cin + (perm ? perm[ch] : ch)) * 9 + tap] * scale;
+              const uint16_t hbits = f2h_rne(v);
+              whi[o] = hbits;
+              if (prec == RRIN_PREC_F16X3) wlo[o] = f2h_rne(v - h2f(hbits));
+              ++o;
+            }
+  for (int co = 0; co < cob_n * bm; ++co) bpack[co] = co < cout ? b[co] : 0.f;
+  return 0;
+}
+
+extern "C" int rrin_upsample2x_h8(const rrin_h8* src, const rrin_h8* dst, int32_t n, int32_t prec, void* stream) {
+  if (!src || !dst || n < 1 || (prec != RRIN_PREC_F16X3 && prec != RRIN_PREC_F16)) return RRIN_E_ARG;
+  if (!h8_ok(*src, prec) || !h8_ok(*dst, prec)) return RRIN_E_SHAPE;
+  if (dst->g.h != 2 * src->g.h || dst->g.w != 2 * src->g.w || dst->groups < src->groups) return RRIN_E_SHAPE;
+  const int64_t total = (int64_t)n * src->groups * dst->g.h * dst->g.w;
+  const int grid = (int)((total + 255) / 256);
+  const int64_t so = (int64_t)src->g_off * src->g.plane, dof = (int64_t)dst->g_off * dst->g.plane;
+  const uint4* shi = static_cast<const uint4*>(src->hi) + so;
+  uint4* dhi = static_cast<uint4*>(dst->hi) + dof;
+  hipStream_t st = (hipStream_t)stream;
+  if (planes_of(prec) == 2) {
+    hipLaunchKernelGGL(up2x_h8_kernel<2>, dim3(grid), dim3(256), 0, st, shi,
+                       static_cast<const uint4*>(src->lo) + so, src->img_stride, src->g.plane, src->g.wp, src->g.h,
+                       src->g.w, dhi, static_cast<uint4*>(dst->lo) + dof, dst->img_stride, dst->g.plane, dst->g.wp,
+                       src->groups, total);
+  } else {
+    hipLaunchKernelGGL(up2x_h8_kernel<1>, dim3(grid), dim3(256), 0, st, shi, (const uint4*)nullptr,
+                       src->img_stride, src->g.plane, src->g.wp, src->g.h, src->g.w, dhi, (uint4*)nullptr,
+                       dst->img_stride, dst->g.plane, dst->g.wp, src->groups, total);
+  }
+  return hip_code(hipGetLastError());
+}
+
+extern "C" int rrin_nchw_to_h8(const float* src, int32_t n, int32_t c, int32_t ch_off, const rrin_h8* dst,
+                               int32_t prec, void* stream) {
+  if (!src || !dst || n < 1 || c < 1 || ch_off < 0 || ch_off + c > 8 * dst->groups) return RRIN_E_ARG;
+  if (prec != RRIN_PREC_F16X3 && prec != RRIN_PREC_F16) return RRIN_E_ARG;
+  if (!h8_ok(*dst, prec)) return RRIN_E_SHAPE;
+  const int64_t total = (int64_t)n * c * dst->g.h * dst->g.w;
+  const int grid = (int)((total + 255) / 256);
+  const int64_t go = (int64_t)dst->g_off * dst->g.plane * 8;
+  hipLaunchKernelGGL(nchw_to_h8_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, src,
+                     static_cast<_Float16*>(dst->hi) + go,
+                     planes_of(prec) == 2 ? static_cast<_Float16*>(dst->lo) + go : (_Float16*)nullptr,
+                     dst->img_stride, dst->g.plane, dst->g.wp, ch_off, c, dst->g.h, dst->g.w, total);
+  return hip_code(hipGetLastError());
+}
+
+extern "C" int rrin_h8_to_nchw(const rrin_h8* src, int32_t n, int32_t c, int32_t ch_off, float* dst, int32_t prec,
+                               void* stream) {
+  if (!src || !dst || n < 1 || c < 1 || ch_off < 0 || ch_off + c > 8 * src->groups) return RRIN_E_ARG;
+  if (prec != RRIN_PREC_F16X3 && prec != RRIN_PREC_F16) return RRIN_E_ARG;
+  if (!h8_ok(*src, prec)) return RRIN_E_SHAPE;
+  const int64_t total = (int64_t)n * c * src->g.h * src->g.w;
+  const int grid = (int)((total + 255) / 256);
+  const int64_t go = (int64_t)src->g_off * src->g.plane * 8;
+  hipLaunchKernelGGL(h8_to_nchw_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                     static_cast<const _Float16*>(src->hi) + go,
+                     planes_of(prec) == 2 ? static_cast<const _Float16*>(src->lo) + go : (const _Float16*)nullptr,
+                     src->img_stride, src->g.plane, src->g.wp, ch_off, dst, c, src->g.h, src->g.w, total);
+  return hip_code(hipGetLastError());
+}
+
+template <int COUT, int MODE>
+static int head_h8_launch(const HeadH8Args& a, int planes, int grid, hipStream_t st) {
+  if (planes == 2)
+    hipLaunchKernelGGL((head_h8_kernel<COUT, MODE, 2>), dim3(grid), dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((head_h8_kernel<COUT, MODE, 1>), dim3(grid), dim3(256), 0, st, a);
+  return hip_code(hipGetLastError());
+}
+
+extern "C" int rrin_head_h8_fwd(const rrin_head_h8_desc* d, void* stream) {
+  if (!d || !d->w || !d->bias || d->cin != 32 || d->n < 1) return RRIN_E_ARG;
+  if (d->prec != RRIN_PREC_F16X3 && d->prec != RRIN_PREC_F16) return RRIN_E_ARG;
+  if (!h8_ok(d->src, d->prec) || !h8_ok(d->g16, d->prec)) return RRIN_E_SHAPE;
+  const int h = d->src.g.h, w = d->src.g.w;
+  if (d->g16.g.h != h || d->g16.g.w != w || d->src.groups < 4) return RRIN_E_SHAPE;
+  if (d->mode != RRIN_HEAD_PLAIN) {
+    if (d->g16.groups < 2 || d->g16.g_off != 0 || !d->coef) return RRIN_E_ARG;
+  } else if (8 * d->g16.groups < d->cout) {
+    return RRIN_E_ARG;
+  }
+  if (d->mode == RRIN_HEAD_FINAL && !d->out) return RRIN_E_ARG;
+  const int planes = planes_of(d->prec);
+  HeadH8Args a;
+  memset(&a, 0, sizeof(a));
+  const int64_t sg = (int64_t)d->src.g_off * d->src.g.plane;
+  a.src_hi = static_cast<const uint4*>(d->src.hi) + sg;
+  a.src_lo = planes == 2 ? static_cast<const uint4*>(d->src.lo) + sg : nullptr;
+  a.src_img = d->src.img_stride;
+  a.src_gp = d->src.g.plane;
+  a.src_wp = d->src.g.wp;
+  const int64_t gg = (int64_t)d->g16.g_off * d->g16.g.plane * 8;
+  a.g_hi = static_cast<_Float16*>(d->g16.hi) + gg;
+  a.g_lo = planes == 2 ? static_cast<_Float16*>(d->g16.lo) + gg : nullptr;
+  a.g_img = d->g16.img_stride;
+  a.g_gp = d->g16.g.plane;
+  a.g_wp = d->g16.g.wp;
+  a.w = d->w;
+  a.bias = d->bias;
+  a.coef = d->coef;
+  a.out = d->out;
+  a.h = h;
+  a.w_ = w;
+  a.tiles_x = (w + 31) / 32;
+  a.tiles_y = (h + 7) / 8;
+  const int grid = a.tiles_x * a.tiles_y * d->n;
+  hipStream_t st = (hipStream_t)stream;
+  switch (d->mode) {
+    case RRIN_HEAD_PLAIN:
+      if (d->cout == 2) return head_h8_launch<2, RRIN_HEAD_PLAIN>(a, planes, grid, st);
+      if (d->cout == 3) return head_h8_launch<3, RRIN_HEAD_PLAIN>(a, planes, grid, st);
+      if (d->cout == 4) return head_h8_launch<4, RRIN_HEAD_PLAIN>(a, planes, grid, st);
+      return RRIN_E_ARG;
+    case RRIN_HEAD_FLOW:
+      return d->cout == 4 ? head_h8_launch<4, RRIN_HEAD_FLOW>(a, planes, grid, st) : RRIN_E_ARG;
+    case RRIN_HEAD_REFINE:
+      return d->cout == 4 ? head_h8_launch<4, RRIN_HEAD_REFINE>(a, planes, grid, st) : RRIN_E_ARG;
+    case RRIN_HEAD_MASK:
+      return d->cout == 2 ? head_h8_launch<2, RRIN_HEAD_MASK>(a, planes, grid, st) : RRIN_E_ARG;
+    case RRIN_HEAD_FINAL:
+      return d->cout == 3 ? head_h8_launch<3, RRIN_HEAD_FINAL>(a, planes, grid, st) : RRIN_E_ARG;
+  }
+  return RRIN_E_ARG;
+}

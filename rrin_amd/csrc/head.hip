@@ -18,57 +18,6 @@
 
 namespace rrin {
 
-// ---- backwarp: grid_sample(bilinear, zeros, align_corners=False) ----------
-// Sampling position follows the reference grid arithmetic in fp32:
-//   x = gx + u;  nx = 2*(x/W - 0.5);  ix = (nx + 1) * (W/2) - 0.5   (CPU unnormalize)
-// then bilinear weights nw = s*e, ne = s*w, sw = n*e, se = n*w with zero taps
-// outside the frame (PyTorch CPU grid sampler order).
-struct WarpTaps {
-  int x0, y0;
-  float nw, ne, sw, se;
-  bool vx0, vx1, vy0, vy1;
-};
-
-#pragma clang fp contract(off)
-__device__ inline WarpTaps warp_taps(int gx, int gy, float u, float v, int H, int W) {
-  WarpTaps t;
-  const float x = (float)gx + u;
-  const float y = (float)gy + v;
-  const float nx = 2.0f * (x / (float)W - 0.5f);
-  const float ny = 2.0f * (y / (float)H - 0.5f);
-  const float ix = (nx + 1.0f) * ((float)W / 2.0f) - 0.5f;
-  const float iy = (ny + 1.0f) * ((float)H / 2.0f) - 0.5f;
-  const float fx = floorf(ix);
-  const float fy = floorf(iy);
-  const float we = ix - fx;  // "w" in the CPU kernel: distance to the west edge
-  const float e = 1.0f - we;
-  const float n = iy - fy;
-  const float s = 1.0f - n;
-  t.nw = s * e;
-  t.ne = s * we;
-  t.sw = n * e;
-  t.se = n * we;
-  // validity tested in float so that huge / non-finite flows never overflow an int
-  t.vx0 = fx >= 0.0f && fx <= (float)(W - 1);
-  t.vx1 = fx >= -1.0f && fx <= (float)(W - 2);
-  t.vy0 = fy >= 0.0f && fy <= (float)(H - 1);
-  t.vy1 = fy >= -1.0f && fy <= (float)(H - 2);
-  t.x0 = (t.vx0 || t.vx1) ? (int)fx : 0;
-  t.y0 = (t.vy0 || t.vy1) ? (int)fy : 0;
-  return t;
-}
-
-// plane: channel base; rs: row stride; off: offset of pixel (0,0)
-__device__ inline float warp_apply(const WarpTaps& t, const float* plane, int64_t rs, int64_t off) {
-  const float* p = plane + off + (int64_t)t.y0 * rs + t.x0;
-  const float a = (t.vy0 && t.vx0) ? p[0] : 0.0f;
-  const float b = (t.vy0 && t.vx1) ? p[1] : 0.0f;
-  const float c = (t.vy1 && t.vx0) ? p[rs] : 0.0f;
-  const float d = (t.vy1 && t.vx1) ? p[rs + 1] : 0.0f;
-  return a * t.nw + b * t.ne + c * t.sw + d * t.se;
-}
-#pragma clang fp contract(on)
-
 // ---- head conv ----------------------------------------------------------------
 struct HeadArgs {
   const float* src;  // cin-channel PP, channel 0 of image 0

@@ -36,46 +36,73 @@ inline int chans(int level) { return 32 << level; }  // unet.py:26, wf=5
 inline int convs_of(int depth) { return 2 * depth + 1 + 3 * (depth - 1); }
 
 struct Buf {
-  float* base;
+  float* base;  // F32: fp32 PP planes; F16*: hi records
+  void* lo;     // F16X3: lo records
   int ch;
   rrin_geom g;
 };
 
 // Workspace plan: offsets are identical in size query and forward.
 struct Plan {
-  int n;
+  int n, prec;
   rrin_geom g[kMaxDepth];
   Buf G;                  // 16 ch at level 0
   Buf X[kMaxDepth];       // level input (L >= 1): C_{L-1} ch
   Buf T[kMaxDepth];       // first conv of a block: C_L ch
   Buf CAT[kMaxDepth - 1]; // [up | bridge]: 2 C_L ch  (levels 0..3)
   Buf BOT;                // Flow bottom (level 4) conv-b output: 512 ch
+  Buf UPT;                // F16*: upsampled input of an up.1 conv (64 ch at level 0, reused per level)
   int64_t bytes;
 };
 
 int64_t align256(int64_t b) { return (b + 255) & ~(int64_t)255; }
 
-void make_plan(int n, int h, int w, char* base, Plan& p) {
+void make_plan(int n, int h, int w, int prec, char* base, Plan& p) {
   p.n = n;
+  p.prec = prec;
+  const bool f32 = prec == RRIN_PREC_F32;
+  const int planes = prec == RRIN_PREC_F16X3 ? 2 : 1;
   int64_t off = 0;
   auto take = [&](int ch, const rrin_geom& g) {
     Buf b;
+    // F32: ch fp32 planes; F16*: ch/8 record planes of 16 B (same 4 B/value with lo)
+    const int64_t bytes = f32 ? (int64_t)n * ch * g.plane * 4 : (int64_t)n * ((ch + 7) / 8) * g.plane * 16;
     b.base = base ? reinterpret_cast<float*>(base + off) : nullptr;
+    off += align256(bytes);
+    b.lo = nullptr;
+    if (planes == 2) {
+      b.lo = base ? static_cast<void*>(base + off) : nullptr;
+      off += align256(bytes);
+    }
     b.ch = ch;
     b.g = g;
-    off += align256((int64_t)n * ch * g.plane * (int64_t)sizeof(float));
     return b;
   };
-  for (int L = 0; L < kMaxDepth; ++L) p.g[L] = make_geom(h >> L, w >> L);
+  for (int L = 0; L < kMaxDepth; ++L) p.g[L] = f32 ? make_geom(h >> L, w >> L) : make_geom_h8(h >> L, w >> L);
   p.G = take(16, p.g[0]);
   for (int L = 0; L < kMaxDepth; ++L) {
-    p.X[L] = L ? take(chans(L - 1), p.g[L]) : Buf{nullptr, 0, p.g[0]};
+    p.X[L] = L ? take(chans(L - 1), p.g[L]) : Buf{nullptr, nullptr, 0, p.g[0]};
     p.T[L] = take(chans(L), p.g[L]);
     if (L < kMaxDepth - 1) p.CAT[L] = take(2 * chans(L), p.g[L]);
   }
   p.BOT = take(chans(kMaxDepth - 1), p.g[kMaxDepth - 1]);
+  p.UPT = f32 ? Buf{nullptr, nullptr, 0, p.g[0]} : take(2 * chans(0), p.g[0]);
   p.bytes = off;
 }
+
+// H8 view of channels [ch_off, ch_off+channels) of a buffer, at geometry g
+// (g differs from b.g only for the level-shared UPT buffer).
+rrin_h8 hview(const Buf& b, int ch_off, int channels, const rrin_geom& g) {
+  rrin_h8 v;
+  v.hi = b.base;
+  v.lo = b.lo;
+  v.img_stride = (int64_t)((b.ch + 7) / 8) * g.plane;
+  v.g_off = ch_off / 8;
+  v.groups = (channels + 7) / 8;
+  v.g = g;
+  return v;
+}
+rrin_h8 hview(const Buf& b, int ch_off, int channels) { return hview(b, ch_off, channels, b.g); }
 
 rrin_pp view(const Buf& b, int n, int ch_off, int channels) {
   rrin_pp v;
@@ -186,6 +213,83 @@ int run_unet(const Plan& p, const UNetSpec& u, const rrin_conv_weights* cw, cons
   return rrin_head_fwd(&hd, st);
 }
 
+int conv_h8(const Plan& p, const rrin_conv_weights& cw, int cin, int cout, int epi, const rrin_h8& src,
+            const rrin_h8& dst, const rrin_h8* pool, hipStream_t st) {
+  ProfScope ps(g_prof, st, RRIN_KIND_CONV, 2.0 * 9 * cin * cout * (double)dst.g.h * dst.g.w * p.n);
+  rrin_conv_h8_desc d;
+  memset(&d, 0, sizeof(d));
+  d.n = p.n;
+  d.cin = cin;
+  d.cout = cout;
+  d.cfg = cw.cfg;
+  d.prec = p.prec;
+  d.epi_mode = epi;
+  d.slope = 0.1f;
+  d.inv_wscale = cw.inv_wscale;
+  d.src = src;
+  d.dst = dst;
+  if (pool) d.pool = *pool;
+  d.whi = cw.whi;
+  d.wlo = cw.wlo;
+  d.bias = cw.bias;
+  return rrin_conv3x3_h8_fwd(&d, st);
+}
+
+// One U-Net on the split-fp16 path: same dataflow as run_unet, plus an explicit
+// upsample pass (UPT) in front of every up.1 conv.
+int run_unet_h8(const Plan& p, const UNetSpec& u, const rrin_conv_weights* cw, const rrin_head_weights& hw,
+                const rrin_net_desc* nd, hipStream_t st) {
+  const int D = u.depth;
+  int k = 0;
+  for (int L = 0; L < D; ++L) {
+    const int C = chans(L);
+    const int cin = L ? chans(L - 1) : u.in_ch;
+    const rrin_h8 in = L ? hview(p.X[L], 0, cin) : hview(p.G, 0, cin);
+    const rrin_h8 t = hview(p.T[L], 0, C);
+    RRIN_TRY(conv_h8(p, cw[k++], cin, C, RRIN_EPI_LEAKY, in, t, nullptr, st));
+    if (L < D - 1) {
+      const rrin_h8 bridge = hview(p.CAT[L], C, C);
+      const rrin_h8 pooled = hview(p.X[L + 1], 0, C);
+      RRIN_TRY(conv_h8(p, cw[k++], C, C, RRIN_EPI_LEAKY_POOL, t, bridge, &pooled, st));
+    } else {
+      const Buf& bot = (L == kMaxDepth - 1) ? p.BOT : p.CAT[L];
+      RRIN_TRY(conv_h8(p, cw[k++], C, C, RRIN_EPI_LEAKY, t, hview(bot, 0, C), nullptr, st));
+      RRIN_TRY(conv_h8(p, cw[k++], C, C, RRIN_EPI_LEAKY, hview(bot, 0, C), t, nullptr, st));
+    }
+  }
+  rrin_h8 x = hview(p.T[D - 1], 0, chans(D - 1));
+  for (int L = D - 2; L >= 0; --L) {
+    const int C = chans(L);
+    const rrin_h8 upin = hview(p.UPT, 0, 2 * C, p.g[L]);
+    {
+      ProfScope ps(g_prof, st, RRIN_KIND_LAYOUT, 0.0);
+      RRIN_TRY(rrin_upsample2x_h8(&x, &upin, p.n, p.prec, st));
+    }
+    const rrin_h8 up = hview(p.CAT[L], 0, C);
+    RRIN_TRY(conv_h8(p, cw[k++], 2 * C, C, RRIN_EPI_LINEAR, upin, up, nullptr, st));
+    const rrin_h8 cat = hview(p.CAT[L], 0, 2 * C);
+    const rrin_h8 t = hview(p.T[L], 0, C);
+    RRIN_TRY(conv_h8(p, cw[k++], 2 * C, C, RRIN_EPI_LEAKY, cat, t, nullptr, st));
+    RRIN_TRY(conv_h8(p, cw[k++], C, C, RRIN_EPI_LEAKY, t, up, nullptr, st));
+    x = up;
+  }
+  rrin_head_h8_desc hd;
+  memset(&hd, 0, sizeof(hd));
+  hd.n = p.n;
+  hd.cin = 32;
+  hd.cout = u.out_ch;
+  hd.mode = u.head_mode;
+  hd.prec = p.prec;
+  hd.src = x;
+  hd.g16 = hview(p.G, 0, 16);
+  hd.w = hw.w;
+  hd.bias = hw.bias;
+  hd.coef = nd->coef;
+  hd.out = nd->out;
+  ProfScope ps(g_prof, st, RRIN_KIND_HEAD, 2.0 * 9 * 32 * u.out_ch * (double)x.g.h * x.g.w * p.n);
+  return rrin_head_h8_fwd(&hd, st);
+}
+
 }  // namespace
 
 extern "C" int rrin_make_geom(int32_t h, int32_t w, rrin_geom* g) {
@@ -200,10 +304,11 @@ extern "C" int rrin_net_conv_count(void) {
   return c;
 }
 
-extern "C" int64_t rrin_net_workspace_bytes(int32_t n, int32_t h, int32_t w) {
+extern "C" int64_t rrin_net_workspace_bytes(int32_t n, int32_t h, int32_t w, int32_t prec) {
   if (n < 1 || h < 16 || w < 16 || (h % 16) || (w % 16)) return RRIN_E_SHAPE;
+  if (prec < RRIN_PREC_F32 || prec > RRIN_PREC_F16) return RRIN_E_ARG;
   Plan p;
-  make_plan(n, h, w, nullptr, p);
+  make_plan(n, h, w, prec, nullptr, p);
   return p.bytes;
 }
 
@@ -211,10 +316,29 @@ extern "C" int rrin_net_fwd(const rrin_net_desc* d, void* stream) {
   if (!d || !d->i0 || !d->i1 || !d->out || !d->coef || !d->convs || !d->heads || !d->workspace)
     return RRIN_E_ARG;
   if (d->n < 1 || d->h < 16 || d->w < 16 || (d->h % 16) || (d->w % 16)) return RRIN_E_SHAPE;
+  if (d->prec < RRIN_PREC_F32 || d->prec > RRIN_PREC_F16) return RRIN_E_ARG;
   Plan p;
-  make_plan(d->n, d->h, d->w, reinterpret_cast<char*>(d->workspace), p);
+  make_plan(d->n, d->h, d->w, d->prec, reinterpret_cast<char*>(d->workspace), p);
   if (d->workspace_bytes < p.bytes) return RRIN_E_WORKSPACE;
   hipStream_t st = (hipStream_t)stream;
+  if (d->prec != RRIN_PREC_F32) {
+    if (d->skip_flow) return RRIN_E_ARG;
+    g_prof = d->prof;
+    const rrin_h8 gall = hview(p.G, 0, 16);
+    int rc = 0;
+    {
+      ProfScope ps(g_prof, st, RRIN_KIND_LAYOUT, 0.0);
+      rc = rrin_nchw_to_h8(d->i0, d->n, 3, 0, &gall, d->prec, st);
+      if (!rc) rc = rrin_nchw_to_h8(d->i1, d->n, 3, 3, &gall, d->prec, st);
+    }
+    int k = 0;
+    for (int u = 0; u < 4 && !rc; ++u) {
+      rc = run_unet_h8(p, kUNets[u], d->convs + k, d->heads[u], d, st);
+      k += convs_of(kUNets[u].depth);
+    }
+    g_prof = nullptr;
+    return rc;
+  }
 
   // x = cat(x0, x1) into g16 channels 0-5 (model.py:33)
   const rrin_pp gx0 = view(p.G, p.n, 0, 3);

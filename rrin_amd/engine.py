@@ -47,6 +47,13 @@ def choose_cfg(cin: int, cout: int, level: int) -> int:
     return 1            # BM 64 x TH 8
 
 
+def choose_cfg_h8(cin: int, cout: int, prec: int) -> int:
+    """Tile config of the split-fp16 / fp16 conv (conv_f16.hip table)."""
+    if cout <= 32:
+        return 1        # BM 32 x TH 16, 512 threads
+    return 0            # BM 64 x TH 16, 512 threads
+
+
 def t_coefficients(t, n: int) -> torch.Tensor:
     """[n, 8] fp32: -(1-t)t, t*t, (1-t)^2, t(1-t), 1-t, t, 0, 0 (model.py:38-39,54)."""
     if isinstance(t, torch.Tensor) and t.numel() > 1:
@@ -73,17 +80,24 @@ def t_coefficients(t, n: int) -> torch.Tensor:
 class RRINEngine:
     MAX_WORKSPACES = 2
 
-    def __init__(self, net):
+    def __init__(self, net, precision: str = "fp32"):
         self.lib = _lib.lib()
         params = list(net.parameters())
         self.device = params[0].device
         if self.device.type != "cuda":
             raise RuntimeError("rrin_amd.Net: move the model to a ROCm device (net.cuda()) before "
                                "forward — the HIP kernels are the only implementation")
+        if precision not in _lib.PRECISIONS:
+            raise ValueError(f"precision must be one of {sorted(_lib.PRECISIONS)}")
+        self.precision = precision
+        self.prec = _lib.PRECISIONS[precision]
         L = self.lib
         blobs, meta = [], []
         off = 0
         self.heads_t = []
+        if self.prec != _lib.PREC_F32:
+            self._init_h8(net)
+            return
         for name in UNET_ORDER:
             unet = getattr(net, name)
             convs = unet.conv_list()
@@ -130,11 +144,68 @@ class RRINEngine:
         self.cfgs = [m[2] for m in meta]
         self._ws = OrderedDict()
 
+    def _init_h8(self, net):
+        """Pack for the split-fp16 (F16X3) or fp16 (F16) path: [cob][16-ch chunk][tap][half][bm][8]
+        halves (rrin_pack_conv3x3_h8), one device blob of halves + one of fp32 biases."""
+        L = self.lib
+        halves, biases, meta = [], [], []
+        hoff = boff = 0
+        for name in UNET_ORDER:
+            for idx, (tag, conv) in enumerate(getattr(net, name).conv_list()):
+                w = conv.weight.detach().to("cpu", torch.float32).contiguous().numpy()
+                b = conv.bias.detach().to("cpu", torch.float32).contiguous().numpy()
+                cout, cin = w.shape[0], w.shape[1]
+                if tag == "last":
+                    self.heads_t.append((torch.from_numpy(w.copy()).to(self.device),
+                                         torch.from_numpy(b.copy()).to(self.device)))
+                    continue
+                cfg = choose_cfg_h8(cin, cout, self.prec)
+                bm = L.rrin_conv_h8_cfg_bm(cfg)
+                nh = L.rrin_pack_conv3x3_h8_halves(cout, cin, bm)
+                whi = np.empty(nh, np.uint16)
+                wlo = np.empty(nh, np.uint16) if self.prec == _lib.PREC_F16X3 else None
+                bp = np.empty(L.rrin_pack_bias_floats(cout, bm), np.float32)
+                inv = C.c_float()
+                perm = FIRST_CONV_PERM[name] if idx == 0 else None
+                perm_arr = np.asarray(perm, np.int32) if perm is not None else None
+                _lib.check(L.rrin_pack_conv3x3_h8(
+                    w.ctypes.data, b.ctypes.data, cout, cin, bm,
+                    perm_arr.ctypes.data if perm_arr is not None else None, self.prec, whi.ctypes.data,
+                    wlo.ctypes.data if wlo is not None else None, bp.ctypes.data, C.byref(inv)),
+                    "rrin_pack_conv3x3_h8")
+                meta.append((hoff, hoff + nh if wlo is not None else None, boff, cfg, inv.value))
+                halves.append(whi)
+                hoff += nh
+                if wlo is not None:
+                    halves.append(wlo)
+                    hoff += nh
+                biases.append(bp)
+                boff += bp.size
+        if len(meta) != L.rrin_net_conv_count():
+            raise RuntimeError(f"packed {len(meta)} convs, library expects {L.rrin_net_conv_count()}")
+        self.blob = torch.from_numpy(np.concatenate(halves).view(np.int16)).to(self.device)
+        self.bias_blob = torch.from_numpy(np.concatenate(biases)).to(self.device)
+        hb, bb = self.blob.data_ptr(), self.bias_blob.data_ptr()
+        self.conv_table = (_lib.ConvWeights * len(meta))()
+        for i, (ho, lo, bo, cfg, inv) in enumerate(meta):
+            e = self.conv_table[i]
+            e.whi = hb + 2 * ho
+            e.wlo = hb + 2 * lo if lo is not None else None
+            e.bias = bb + 4 * bo
+            e.cfg = cfg
+            e.inv_wscale = inv
+        self.head_table = (_lib.HeadWeights * 4)()
+        for i, (w, b) in enumerate(self.heads_t):
+            self.head_table[i].w = w.data_ptr()
+            self.head_table[i].bias = b.data_ptr()
+        self.cfgs = [m[3] for m in meta]
+        self._ws = OrderedDict()
+
     def workspace(self, n: int, h: int, w: int) -> torch.Tensor:
         key = (n, h, w)
         ws = self._ws.get(key)
         if ws is None:
-            nbytes = self.lib.rrin_net_workspace_bytes(n, h, w)
+            nbytes = self.lib.rrin_net_workspace_bytes(n, h, w, self.prec)
             if nbytes < 0:
                 _lib.check(int(nbytes), "rrin_net_workspace_bytes")
             while len(self._ws) >= self.MAX_WORKSPACES:
@@ -170,6 +241,7 @@ class RRINEngine:
             d.workspace = ws.data_ptr()
             d.workspace_bytes = ws.numel()
             d.skip_flow = 0
+            d.prec = self.prec
             d.prof = prof
             stream = torch.cuda.current_stream(self.device).cuda_stream
             _lib.check(self.lib.rrin_net_fwd(C.byref(d), C.c_void_p(stream)), "rrin_net_fwd")

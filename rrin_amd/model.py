@@ -34,6 +34,11 @@ class Net(nn.Module):
         self._engine = None
         self._engine_version = -1
         self._weights_version = 0
+        # Arithmetic of the HIP path (not part of the reference contract):
+        #   "fp32"         exact fp32 MFMA (v_mfma_f32_32x32x2_f32)
+        #   "fp32_split16" fp32 values as fp16 hi+lo pairs, 3 f16 MFMA products, fp32 accumulate
+        #   "fp16"         fp16 storage and products, fp32 accumulate (BASELINE fp16 configs)
+        self.precision = "fp32"
         self.register_load_state_dict_post_hook(Net._on_load)
 
     # Packed weights are rebuilt after load_state_dict / .to() / param edits.
@@ -51,8 +56,10 @@ class Net(nn.Module):
 
     def engine(self):
         from .engine import RRINEngine
-        if self._engine is None or self._engine_version != self._weights_version:
-            self._engine = RRINEngine(self)
+        if (self._engine is None or self._engine_version != self._weights_version
+                or self._engine.precision != self.precision):
+            self._engine = None  # free the previous packed weights first
+            self._engine = RRINEngine(self, self.precision)
             self._engine_version = self._weights_version
         return self._engine
 

@@ -54,3 +54,51 @@ class PPTensor:
 
 def _stream(device) -> C.c_void_p:
     return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+class H8Tensor:
+    """Channel-blocked fp16 activation tensor (H8 layout, include/rrin_hip.h):
+    ``hi`` (and for fp32_split16 ``lo``) are ``[n, ceil(c/8), hp, wp, 8]``
+    half tensors, pixel (y,x) at ``[.., y+1, x+8, :]``; padding zero."""
+
+    def __init__(self, n: int, c: int, h: int, w: int, device, prec: int):
+        self.n, self.c, self.h, self.w, self.prec = n, c, h, w, prec
+        self.g = _lib.geom_h8(h, w)
+        self.groups = (c + 7) // 8
+        shape = (n, self.groups, self.g.hp, self.g.wp, 8)
+        self.hi = torch.zeros(shape, dtype=torch.float16, device=device)
+        self.lo = torch.zeros(shape, dtype=torch.float16, device=device) if prec == _lib.PREC_F16X3 else None
+
+    def view(self, ch_off: int = 0, channels: int | None = None) -> _lib.H8:
+        channels = self.c - ch_off if channels is None else channels
+        if ch_off % 8:
+            raise ValueError("H8 views start on an 8-channel group")
+        v = _lib.H8()
+        v.hi = self.hi.data_ptr()
+        v.lo = self.lo.data_ptr() if self.lo is not None else None
+        v.img_stride = self.groups * self.g.plane
+        v.g_off = ch_off // 8
+        v.groups = (channels + 7) // 8
+        v.g = self.g
+        return v
+
+    @classmethod
+    def from_nchw(cls, x: torch.Tensor, prec: int, c_alloc: int | None = None, ch_off: int = 0) -> "H8Tensor":
+        n, c, h, w = x.shape
+        t = cls(n, c_alloc or c + ch_off, h, w, x.device, prec)
+        t.load(x, ch_off)
+        return t
+
+    def load(self, x: torch.Tensor, ch_off: int = 0):
+        x = x.contiguous().float()
+        v = self.view(0, self.c)
+        _lib.check(_lib.lib().rrin_nchw_to_h8(C.c_void_p(x.data_ptr()), x.shape[0], x.shape[1], ch_off,
+                                              C.byref(v), self.prec, _stream(x.device)), "rrin_nchw_to_h8")
+
+    def to_nchw(self, ch_off: int = 0, channels: int | None = None) -> torch.Tensor:
+        channels = self.c - ch_off if channels is None else channels
+        out = torch.empty((self.n, channels, self.h, self.w), dtype=torch.float32, device=self.hi.device)
+        v = self.view(0, self.c)
+        _lib.check(_lib.lib().rrin_h8_to_nchw(C.byref(v), self.n, channels, ch_off, C.c_void_p(out.data_ptr()),
+                                              self.prec, _stream(out.device)), "rrin_h8_to_nchw")
+        return out

@@ -46,9 +46,9 @@ def test_strerror_and_geom():
 def test_conv_counts_and_workspace():
     lib = _lib.lib()
     assert lib.rrin_net_conv_count() == 77  # 81 convs - 4 fused heads
-    assert lib.rrin_net_workspace_bytes(1, 720, 1280) > 0
-    assert lib.rrin_net_workspace_bytes(1, 72, 80) < 0   # not /16
-    assert lib.rrin_net_workspace_bytes(4, 736, 1280) > 3 * lib.rrin_net_workspace_bytes(1, 736, 1280)
+    assert lib.rrin_net_workspace_bytes(1, 720, 1280, 0) > 0
+    assert lib.rrin_net_workspace_bytes(1, 72, 80, 0) < 0   # not /16
+    assert lib.rrin_net_workspace_bytes(4, 736, 1280, 1) > 3 * lib.rrin_net_workspace_bytes(1, 736, 1280, 1)
     for cfg in range(lib.rrin_conv_cfg_count()):
         assert lib.rrin_conv_cfg_bm(cfg) % 32 == 0
         assert 16 % lib.rrin_conv_cfg_th(cfg) == 0
@@ -92,3 +92,48 @@ def test_pack_rejects_bad_args():
                                  out.ctypes.data, bo.ctypes.data) == -2
     assert lib.rrin_pack_conv3x3(w.ctypes.data, b.ctypes.data, 32, 6, 48, None,
                                  out.ctypes.data, bo.ctypes.data) == -2
+
+
+def _h2f(bits):
+    return bits.view(np.float16).astype(np.float64)
+
+
+@pytest.mark.parametrize("cout,cin,bm,prec", [(32, 6, 32, 1), (64, 32, 64, 1), (128, 256, 64, 2), (40, 10, 32, 1)])
+def test_pack_h8_layout_and_split(cout, cin, bm, prec):
+    """[cob][16-ch chunk][tap][half][bm][8] halves; weights scaled by 2^s with
+    max|w|*2^s in [2^12, 2^13); hi+lo reproduces w*2^s to 2^-22 (split mode)."""
+    lib = _lib.lib()
+    rng = np.random.default_rng(1)
+    w = (rng.standard_normal((cout, cin, 3, 3)) * 0.05).astype(np.float32)
+    b = rng.standard_normal(cout).astype(np.float32)
+    nh = lib.rrin_pack_conv3x3_h8_halves(cout, cin, bm)
+    whi = np.zeros(nh, np.uint16)
+    wlo = np.zeros(nh, np.uint16)
+    bp = np.zeros(lib.rrin_pack_bias_floats(cout, bm), np.float32)
+    inv = C.c_float()
+    rc = lib.rrin_pack_conv3x3_h8(w.ctypes.data, b.ctypes.data, cout, cin, bm, None, prec, whi.ctypes.data,
+                                  wlo.ctypes.data if prec == 1 else None, bp.ctypes.data, C.byref(inv))
+    assert rc == 0
+    scale = 1.0 / inv.value
+    assert scale == 2.0 ** round(np.log2(scale))
+    assert 2 ** 12 <= np.abs(w).max() * scale < 2 ** 13
+    cob, nch = -(-cout // bm), -(-cin // 16)
+    rec = _h2f(whi) + (_h2f(wlo) if prec == 1 else 0)
+    rec = rec.reshape(cob, nch, 9, 2, bm, 8)
+    # back to [co][ci][tap]
+    got = rec.transpose(0, 4, 1, 3, 5, 2).reshape(cob * bm, nch * 16, 9)[:cout, :cin] / scale
+    ref = w.reshape(cout, cin, 9).astype(np.float64)
+    tol = 2.0 ** -21 if prec == 1 else 2.0 ** -10
+    assert np.abs(got - ref).max() <= tol * np.abs(ref).max()
+    np.testing.assert_array_equal(bp[:cout], b)
+
+
+def test_h8_geometry_and_cfgs():
+    lib = _lib.lib()
+    g = _lib.geom_h8(720, 1280)
+    assert (g.hp, g.wp) == (722, 1296)
+    ok = [lib.rrin_conv_h8_cfg_ok(c, 1) for c in range(lib.rrin_conv_h8_cfg_count())]
+    assert ok[0] == 1 and ok[1] == 1
+    assert all(lib.rrin_conv_h8_cfg_ok(c, 2) for c in range(lib.rrin_conv_h8_cfg_count()))
+    for prec in (0, 1, 2):
+        assert lib.rrin_net_workspace_bytes(2, 64, 96, prec) > 0

@@ -1,0 +1,147 @@
+"""GPU: split-fp16 (fp32_split16) and fp16 paths of librrin_hip.so.
+
+fp32_split16 holds each fp32 value as fp16 hi+lo and forms each product from
+three exact fp16 products with fp32 accumulation (error ~2^-21 relative per
+product), so it is held to the fp32 tolerances.  fp16 is held to the SURVEY
+§8d fp16 gate: max-abs <= 1e-2 and PSNR >= 45 dB vs the fp32 CPU reference."""
+import ctypes as C
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from rrin_amd import _lib
+from rrin_amd.pp import H8Tensor
+from rrin_amd.synthetic import keyed_tensor
+from tests import hip_helpers as H
+from tests.golden.spec import CONV_CLASSES
+
+pytestmark = pytest.mark.gpu
+X3, F16 = _lib.PREC_F16X3, _lib.PREC_F16
+TOL = {X3: dict(rtol=1e-4, atol=1e-4), F16: dict(rtol=2e-2, atol=2e-2)}
+
+
+def ref_conv(x, w, b, slope=None):
+    y = F.conv2d(x.double().cpu(), w.double().cpu(), b.double().cpu(), padding=1)
+    return F.leaky_relu(y, slope) if slope is not None else y
+
+
+def keyed_conv(cin, cout, key="h8"):
+    return (keyed_tensor(f"{key}.{cin}.{cout}.w", (cout, cin, 3, 3), cin * 9),
+            keyed_tensor(f"{key}.{cin}.{cout}.b", (cout,), cin * 9))
+
+
+def cfgs(prec, cout):
+    lib = _lib.lib()
+    return [c for c in range(lib.rrin_conv_h8_cfg_count())
+            if lib.rrin_conv_h8_cfg_ok(c, prec) and lib.rrin_conv_h8_cfg_bm(c) <= max(32, 2 * cout)]
+
+
+def pack_h8(w, b, cfg, prec, dev, perm=None):
+    lib = _lib.lib()
+    w = w.detach().cpu().float().contiguous().numpy()
+    b = b.detach().cpu().float().contiguous().numpy()
+    cout, cin = w.shape[:2]
+    bm = lib.rrin_conv_h8_cfg_bm(cfg)
+    nh = lib.rrin_pack_conv3x3_h8_halves(cout, cin, bm)
+    whi = np.zeros(nh, np.uint16)
+    wlo = np.zeros(nh, np.uint16)
+    bp = np.zeros(lib.rrin_pack_bias_floats(cout, bm), np.float32)
+    inv = C.c_float()
+    pa = np.asarray(perm, np.int32) if perm is not None else None
+    _lib.check(lib.rrin_pack_conv3x3_h8(w.ctypes.data, b.ctypes.data, cout, cin, bm,
+                                        pa.ctypes.data if pa is not None else None, prec, whi.ctypes.data,
+                                        wlo.ctypes.data, bp.ctypes.data, C.byref(inv)))
+    t = lambda a: torch.from_numpy(a.view(np.int16)).to(dev)  # noqa: E731
+    return t(whi), t(wlo), torch.from_numpy(bp).to(dev), inv.value
+
+
+def conv_h8(src: H8Tensor, w, b, cfg, prec, epi=_lib.EPI_LINEAR, dst=None, dst_off=0, pool=None, perm=None,
+            cin=None):
+    dev = src.hi.device
+    cout, cin_w = w.shape[:2]
+    cin = cin or cin_w
+    if dst is None:
+        dst = H8Tensor(src.n, cout + dst_off, src.h, src.w, dev, prec)
+    if epi == _lib.EPI_LEAKY_POOL and pool is None:
+        pool = H8Tensor(src.n, cout, src.h // 2, src.w // 2, dev, prec)
+    whi, wlo, bp, inv = pack_h8(w, b, cfg, prec, dev, perm)
+    d = _lib.ConvH8Desc()
+    d.n, d.cin, d.cout, d.cfg, d.prec, d.epi_mode, d.slope, d.inv_wscale = src.n, cin, cout, cfg, prec, epi, 0.1, inv
+    d.src = src.view(0, cin)
+    d.dst = dst.view(dst_off, cout)
+    if pool is not None:
+        d.pool = pool.view(0, cout)
+    d.whi, d.wlo, d.bias = whi.data_ptr(), wlo.data_ptr() if prec == X3 else None, bp.data_ptr()
+    _lib.check(_lib.lib().rrin_conv3x3_h8_fwd(C.byref(d), H.stream(dev)), "rrin_conv3x3_h8_fwd")
+    torch.cuda.synchronize(dev)
+    return dst, pool
+
+
+@pytest.mark.parametrize("prec", [X3, F16])
+def test_h8_roundtrip(gpu, prec):
+    x = torch.randn(2, 11, 23, 40, device=gpu) * 3
+    t = H8Tensor.from_nchw(x, prec, c_alloc=24, ch_off=3)
+    y = t.to_nchw(3, 11)
+    rel = 2.0 ** -21 if prec == X3 else 2.0 ** -10
+    assert float(((y - x).abs() / x.abs().clamp_min(1e-3)).max()) <= rel
+    assert not t.hi[:, :, 0].any() and not t.hi[:, :, :, :8].any() and not t.hi[:, :, 24:].any()
+
+
+@pytest.mark.parametrize("prec", [X3, F16])
+@pytest.mark.parametrize("cin,cout", CONV_CLASSES)
+def test_h8_conv_golden(gpu, golden, prec, cin, cout):
+    if cout % 8:
+        pytest.skip("heads (Cout 2-4) run on the VALU head kernel")
+    g = golden("ops")
+    w = keyed_tensor(f"golden.conv.{cin}.{cout}.weight", (cout, cin, 3, 3), cin * 9)
+    b = keyed_tensor(f"golden.conv.{cin}.{cout}.bias", (cout,), cin * 9)
+    x = torch.from_numpy(g[f"conv_{cin}_{cout}_in"]).to(gpu)
+    for cfg in cfgs(prec, cout):
+        dst, _ = conv_h8(H8Tensor.from_nchw(x, prec), w, b, cfg, prec)
+        np.testing.assert_allclose(dst.to_nchw().cpu().numpy(), g[f"conv_{cin}_{cout}_out"], **TOL[prec],
+                                   err_msg=f"cfg {cfg}")
+
+
+@pytest.mark.parametrize("prec", [X3, F16])
+@pytest.mark.parametrize("n,cin,cout,h,w", [(2, 64, 32, 40, 72), (1, 128, 64, 46, 80), (1, 256, 256, 12, 20),
+                                            (2, 16, 32, 32, 64)])
+def test_h8_conv_pool(gpu, prec, n, cin, cout, h, w):
+    x = torch.rand(n, cin, h, w, device=gpu) * 2 - 1
+    wt, b = keyed_conv(cin, cout)
+    ref = ref_conv(x, wt, b, 0.1)
+    refp = F.avg_pool2d(ref, 2)
+    for cfg in cfgs(prec, cout):
+        dst, pool = conv_h8(H8Tensor.from_nchw(x, prec), wt, b, cfg, prec, epi=_lib.EPI_LEAKY_POOL, dst_off=cout,
+                            dst=H8Tensor(n, 2 * cout, h, w, gpu, prec))
+        np.testing.assert_allclose(dst.to_nchw(cout, cout).cpu().double().numpy(), ref.numpy(), **TOL[prec])
+        assert not dst.to_nchw(0, cout).any()
+        np.testing.assert_allclose(pool.to_nchw().cpu().double().numpy(), refp.numpy(), **TOL[prec],
+                                   err_msg=f"cfg {cfg}")
+
+
+@pytest.mark.parametrize("prec", [X3, F16])
+def test_h8_conv_partial_channels_and_perm(gpu, prec):
+    x = torch.rand(2, 16, 32, 48, device=gpu)
+    wt, b = keyed_conv(10, 32, "perm")
+    perm = [4, 5, 6, 7, 8, 9, 0, 1, 2, 3]
+    ref = ref_conv(torch.cat([x[:, 6:10], x[:, 0:6]], 1), wt, b)
+    xx = x.clone()
+    xx[:, 10:] = float("nan")  # channels beyond cin must never be read into the sum
+    dst, _ = conv_h8(H8Tensor.from_nchw(xx, prec), wt, b, 1, prec, perm=perm, cin=10)
+    np.testing.assert_allclose(dst.to_nchw().cpu().double().numpy(), ref.numpy(), **TOL[prec])
+
+
+@pytest.mark.parametrize("prec", [X3, F16])
+@pytest.mark.parametrize("n,c,h,w", [(1, 64, 20, 36), (2, 16, 5, 7), (1, 512, 5, 10)])
+def test_h8_upsample(gpu, prec, n, c, h, w):
+    x = torch.rand(n, c, h, w, device=gpu) * 2 - 1
+    src = H8Tensor.from_nchw(x, prec)
+    dst = H8Tensor(n, c, 2 * h, 2 * w, gpu, prec)
+    sv, dv = src.view(), dst.view()
+    _lib.check(_lib.lib().rrin_upsample2x_h8(C.byref(sv), C.byref(dv), n, prec, H.stream(gpu)))
+    torch.cuda.synchronize()
+    ref = F.interpolate(x.double().cpu(), scale_factor=2, mode="bilinear", align_corners=False)
+    tol = 1e-6 if prec == X3 else 2e-3
+    np.testing.assert_allclose(dst.to_nchw().cpu().double().numpy(), ref.numpy(), rtol=0, atol=tol)

@@ -95,3 +95,45 @@ def test_net_errors(gpu, nets):
             net(torch.zeros(1, 3, 72, 72, device=gpu), torch.zeros(1, 3, 72, 72, device=gpu))
         with pytest.raises(TypeError):
             net(torch.zeros(1, 3, 64, 64, device=gpu).half(), torch.zeros(1, 3, 64, 64, device=gpu).half())
+
+
+@pytest.mark.parametrize("which", ["default", "stress"])
+def test_net_golden_split16(gpu, golden, which):
+    """fp32_split16: fp32-class accuracy (three fp16 products per fp32 product)."""
+    g = golden("net_" + which)
+    net = make_net(gpu, which == "stress")
+    net.precision = "fp32_split16"
+    i0, i1 = torch.from_numpy(g["i0"]).to(gpu), torch.from_numpy(g["i1"]).to(gpu)
+    with torch.no_grad():
+        for t, key in [(0.5, "out_t050"), (0.25, "out_t025"),
+                       (torch.from_numpy(g["t_tensor"]).view(-1, 1, 1, 1).to(gpu), "out_ttensor")]:
+            err = maxabs(net(i0, i1, t=t).cpu(), g[key])
+            assert err <= (1e-4 if which == "default" else GATE), f"{which} {key}: {err:.3e}"
+
+
+@pytest.mark.parametrize("h,w", [(64, 96), (368, 640), (720, 1280)])
+def test_net_split16_vs_oracle(gpu, nets, h, w):
+    net = make_net(gpu)
+    net.precision = "fp32_split16"
+    i0, i1 = synthetic_batch(1, h, w, first_index=5)
+    sd = {k: v.detach().cpu() for k, v in net.state_dict().items()}
+    with torch.no_grad():
+        ref = net_forward(sd, i0, i1, 0.5)
+        out = net(i0.to(gpu), i1.to(gpu), 0.5).cpu()
+    assert maxabs(out, ref) <= GATE
+
+
+@pytest.mark.parametrize("which,h,w", [("default", 64, 96), ("stress", 64, 96), ("default", 368, 640)])
+def test_net_fp16_gate(gpu, which, h, w):
+    """fp16 configs: max-abs <= 1e-2 and PSNR >= 45 dB vs the fp32 CPU reference."""
+    net = make_net(gpu, which == "stress")
+    net.precision = "fp16"
+    i0, i1 = synthetic_batch(2, h, w, first_index=9)
+    sd = {k: v.detach().cpu() for k, v in net.state_dict().items()}
+    with torch.no_grad():
+        ref = net_forward(sd, i0, i1, 0.5)
+        out = net(i0.to(gpu), i1.to(gpu), 0.5).cpu()
+    err = maxabs(out, ref)
+    mse = float(((out.double() - ref.double()) ** 2).mean())
+    psnr = 10 * np.log10(1.0 / max(mse, 1e-30))
+    assert err <= 1e-2 and psnr >= 45, f"max-abs {err:.3e} psnr {psnr:.1f}"
