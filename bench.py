@@ -20,6 +20,7 @@ from __future__ import annotations
 import argparse
 import ctypes as C
 import json
+import math
 import os
 import sys
 import time
@@ -36,7 +37,12 @@ from rrin_amd.synthetic import keyed_state_dict, synthetic_batch  # noqa: E402
 from rrin_amd.unet import conv_flops  # noqa: E402
 
 FP32_PEAK_TFLOPS = 157.3   # MI355X dense fp32 (MFMA 32x32x2 f32 = VALU rate), MI355X_MICROARCH.md
+F16_PEAK_TFLOPS = 2500.0   # dense f16 MFMA (v_mfma_f32_32x32x16_f16), no sparsity
 HBM_PEAK_GBS = 8000.0
+# Roofline peak in fp32-equivalent TFLOP/s per precision: the split path spends
+# three f16 MFMA products on every fp32 product.
+PEAK = {"fp32": FP32_PEAK_TFLOPS, "fp32_split16": F16_PEAK_TFLOPS / 3, "fp16": F16_PEAK_TFLOPS}
+MFMA_PRODUCTS = {"fp32": 1, "fp32_split16": 3, "fp16": 1}
 
 
 def parse():
@@ -48,26 +54,34 @@ def parse():
     ap.add_argument("--height", type=int, default=720)
     ap.add_argument("--width", type=int, default=1280)
     ap.add_argument("--t", type=float, default=0.5)
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "fp32_split16", "fp16"],
+                    help="fp32: exact fp32 MFMA; fp32_split16: fp32 values as fp16 hi+lo, 3 fp16 "
+                         "products per fp32 product, fp32 accumulate; fp16: fp16 storage/products")
     ap.add_argument("--no-prof", action="store_true", help="skip the per-launch event profiler")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-pairs", type=int, default=2, help="pairs timed on the CPU baseline")
     return ap.parse_args()
 
 
-def cpu_baseline(sd, h, w, pairs):
+def cpu_baseline(sd, h, w, pairs, t, gpu_out0):
+    """Time the CPU oracle on pair 0 and compare its output with the GPU's."""
     from oracle.ref_net import net_forward  # checker / baseline only
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
     i0, i1 = synthetic_batch(1, h, w, first_index=0)
     with torch.no_grad():
-        net_forward(sd, i0[:, :, :64, :64].contiguous(), i1[:, :, :64, :64].contiguous(), 0.5)  # warm
+        net_forward(sd, i0[:, :, :64, :64].contiguous(), i1[:, :, :64, :64].contiguous(), t)  # warm
         t0 = time.perf_counter()
         for _ in range(pairs):
-            net_forward(sd, i0, i1, 0.5)
+            ref = net_forward(sd, i0, i1, t)
         dt = time.perf_counter() - t0
-    return {"value": pairs / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
-            "sample": f"{pairs} x Net.forward {w}x{h} N=1 fp32 on PyTorch-CPU (oracle/ref_net.py), "
-                      f"{dt:.1f} s"}
+    d = (gpu_out0.double() - ref.double())
+    mse = float((d * d).mean())
+    parity = {"pair": 0, "max_abs": float(d.abs().max()),
+              "psnr_db": (10 * math.log10(1.0 / mse)) if mse > 0 else float("inf"), "gate_max_abs": 1e-3}
+    return ({"value": pairs / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
+             "sample": f"{pairs} x Net.forward {w}x{h} N=1 fp32 on PyTorch-CPU (oracle/ref_net.py), "
+                       f"{dt:.1f} s"}, parity)
 
 
 def main():
@@ -86,6 +100,7 @@ def main():
     sd = keyed_state_dict(net.state_dict())
     net.load_state_dict(sd, strict=True)
     net = net.to(dev).eval()
+    net.precision = args.precision
     B, H, W = args.batch, args.height, args.width
     i0, i1 = synthetic_batch(B, H, W, first_index=rank * B)
     i0, i1 = i0.to(dev), i1.to(dev)
@@ -103,6 +118,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
+    last = [None]
 
     prof = None
     cap = 0
@@ -117,7 +133,7 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step(prof)
+        last[0] = step(prof)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -139,18 +155,24 @@ def main():
         conv_ms = sum(ms[i] for i in range(n) if kinds[i] == 0)
         conv_fl = sum(fl[i] for i in range(n) if kinds[i] == 0)
         head_ms = sum(ms[i] for i in range(n) if kinds[i] == 1)
+        other_ms = sum(ms[i] for i in range(n) if kinds[i] == 2)
         conv_launches = sum(1 for i in range(n) if kinds[i] == 0)
         lib.rrin_prof_destroy(prof)
         conv_ms_step = conv_ms / args.steps
         head_ms_step = head_ms / args.steps
         achieved = conv_fl / (conv_ms * 1e-3) / 1e12
-        roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS,
-                    "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": None,
-                    "kernel": "conv3x3_mfma_kernel (all 77 body convs, v_mfma_f32_32x32x2_f32)",
+        peak = PEAK[args.precision]
+        roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1),
+                    "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None,
+                    "mfma_issued_tflops": round(achieved * MFMA_PRODUCTS[args.precision], 1),
+                    "kernel": ("conv3x3_mfma_kernel (77 body convs, v_mfma_f32_32x32x2_f32)"
+                               if args.precision == "fp32" else
+                               "conv3x3_h8_kernel (77 body convs, v_mfma_f32_32x32x16_f16)"),
                     "flops_per_launch_avg": conv_fl / max(conv_launches, 1),
                     "avg_launch_ms": conv_ms / max(conv_launches, 1),
                     "conv_ms_per_step": round(conv_ms_step, 3),
-                    "head_ms_per_step": round(head_ms_step, 3)}
+                    "head_ms_per_step": round(head_ms_step, 3),
+                    "layout_upsample_ms_per_step": round(other_ms / args.steps, 3)}
 
     pairs = world * B * args.steps
     value = pairs / elapsed
@@ -165,7 +187,8 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": {"fp32": "f32", "fp32_split16": "f32 (fp16 hi+lo split, 3 MFMA products, f32 accumulate)",
+                  "fp16": "f16"}[args.precision],
         "data": "synthetic (key-seeded weights, randint/255 frame pairs; SURVEY §8c-d)",
         "config": {"workload": f"RRIN Net.forward {W}x{H} fp32, {B} pairs/GPU/step, t={args.t}, "
                                f"+ all-gather of outputs",
@@ -175,9 +198,11 @@ def main():
                                                for u in ("Flow", "refine_flow", "Mask", "final")) / 1e9, 1)},
         "roofline": roofline,
         "cpu_baseline": None,
+        "parity": None,
     }
     if rank == 0 and world == 1 and args.cpu_baseline == "auto":
-        res["cpu_baseline"] = cpu_baseline({k: v.detach().cpu() for k, v in sd.items()}, H, W, args.cpu_pairs)
+        res["cpu_baseline"], res["parity"] = cpu_baseline({k: v.detach().cpu() for k, v in sd.items()}, H, W,
+                                                          args.cpu_pairs, args.t, last[0][0:1].cpu())
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:

@@ -105,6 +105,8 @@ typedef struct rrin_head_desc {
   const float* bias;     /* [cout]                                            */
   const float* coef;     /* [n][8] per-image t coefficients   */
   float* out;            /* FINAL: NCHW [n][3][h][w] contiguous               */
+  rrin_pp flow_raw;      /* FLOW (optional, base NULL = skip): raw 4-ch Flow output kept
+                            for reuse across t                    */
 } rrin_head_desc;
 
 int rrin_head_fwd(const rrin_head_desc* d, void* stream);
@@ -187,8 +189,17 @@ typedef struct rrin_head_h8_desc {
   const float* bias;
   const float* coef;
   float* out;            /* FINAL: NCHW fp32 */
+  rrin_h8 flow_raw;      /* FLOW (optional, hi NULL = skip): raw 4-ch Flow output */
 } rrin_head_h8_desc;
 int rrin_head_h8_fwd(const rrin_head_h8_desc* d, void* stream);
+
+/* Flow reuse across t: Ft0/Ft1 of model.py:38-39 recomputed
+ * from a kept raw Flow (4 channels) with new per-image coefficients, written to
+ * g16 channels 6-9.  The U-Net output itself does not depend on t (model.py:35). */
+int rrin_flow_tblend_fwd(const rrin_pp* flow_raw, const rrin_pp* g16, const float* coef, int32_t n,
+                         void* stream);
+int rrin_flow_tblend_h8(const rrin_h8* flow_raw, const rrin_h8* g16, const float* coef, int32_t n,
+                        int32_t prec, void* stream);
 
 /* ---- Whole forward (native schedule) ------------------------------------- */
 /* Per-conv weight table entry, in Net conv order (rrin_net_conv_count). */
@@ -231,7 +242,8 @@ typedef struct rrin_net_desc {
   const rrin_head_weights* heads;  /* host array of 4 */
   void* workspace;      /* device, >= rrin_net_workspace_bytes, zero-filled once */
   int64_t workspace_bytes;
-  int32_t skip_flow;    /* 1: reuse the Ft0/Ft1 already in the workspace (same pair) */
+  int32_t skip_flow;    /* 1: the pair is the one of the previous call on this workspace:
+                           reuse its raw Flow (Flow U-Net skipped, t-blend only)      */
   int32_t prec;         /* rrin_prec of the whole forward */
   rrin_prof* prof;      /* nullable: record events around every launch */
 } rrin_net_desc;

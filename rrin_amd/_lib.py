@@ -39,7 +39,7 @@ class ConvDesc(C.Structure):
 class HeadDesc(C.Structure):
     _fields_ = [("n", C.c_int32), ("cin", C.c_int32), ("cout", C.c_int32), ("mode", C.c_int32),
                 ("src", PP), ("g16", PP), ("w", C.c_void_p), ("bias", C.c_void_p),
-                ("coef", C.c_void_p), ("out", C.c_void_p)]
+                ("coef", C.c_void_p), ("out", C.c_void_p), ("flow_raw", PP)]
 
 
 class ConvWeights(C.Structure):
@@ -62,7 +62,7 @@ class ConvH8Desc(C.Structure):
 class HeadH8Desc(C.Structure):
     _fields_ = [("n", C.c_int32), ("cin", C.c_int32), ("cout", C.c_int32), ("mode", C.c_int32),
                 ("prec", C.c_int32), ("pad_", C.c_int32), ("src", H8), ("g16", H8), ("w", C.c_void_p),
-                ("bias", C.c_void_p), ("coef", C.c_void_p), ("out", C.c_void_p)]
+                ("bias", C.c_void_p), ("coef", C.c_void_p), ("out", C.c_void_p), ("flow_raw", H8)]
 
 
 class HeadWeights(C.Structure):
@@ -110,6 +110,9 @@ SIGNATURES = {
     "rrin_h8_to_nchw": (C.c_int, [C.POINTER(H8), C.c_int32, C.c_int32, C.c_int32, C.c_void_p, C.c_int32,
                                   C.c_void_p]),
     "rrin_head_h8_fwd": (C.c_int, [C.POINTER(HeadH8Desc), C.c_void_p]),
+    "rrin_flow_tblend_fwd": (C.c_int, [C.POINTER(PP), C.POINTER(PP), C.c_void_p, C.c_int32, C.c_void_p]),
+    "rrin_flow_tblend_h8": (C.c_int, [C.POINTER(H8), C.POINTER(H8), C.c_void_p, C.c_int32, C.c_int32,
+                                      C.c_void_p]),
     "rrin_net_fwd": (C.c_int, [C.POINTER(NetDesc), C.c_void_p]),
     "rrin_prof_create": (C.c_int, [C.c_int32, C.POINTER(C.c_void_p)]),
     "rrin_prof_destroy": (C.c_int, [C.c_void_p]),

@@ -406,6 +406,10 @@ struct HeadH8Args {
   const float* bias;
   const float* coef;
   float* out;
+  _Float16* fr_hi;  // FLOW: raw output (1 group), nullable
+  _Float16* fr_lo;
+  int64_t fr_img, fr_gp;
+  int fr_wp;
   int h, w_, tiles_x, tiles_y;
 };
 
@@ -474,6 +478,14 @@ __global__ void __launch_bounds__(256) head_h8_kernel(HeadH8Args a) {
     for (int co = 0; co < COUT; ++co) wr(co, acc[co]);
   } else if constexpr (MODE == RRIN_HEAD_FLOW) {
 #pragma clang fp contract(off)
+    if (a.fr_hi) {
+      for (int k = 0; k < 4; ++k) {
+        const int64_t kk = h8_half_index(a.fr_img, a.fr_gp, a.fr_wp, img, k, y, x);
+        const _Float16 vh = (_Float16)acc[k];
+        a.fr_hi[kk] = vh;
+        if constexpr (PLANES == 2) a.fr_lo[kk] = (_Float16)(acc[k] - (float)vh);
+      }
+    }
     for (int k = 0; k < 2; ++k) {
       wr(6 + k, cf[0] * acc[k] + cf[1] * acc[2 + k]);
       wr(8 + k, cf[2] * acc[k] - cf[3] * acc[2 + k]);
@@ -512,6 +524,39 @@ __global__ void __launch_bounds__(256) head_h8_kernel(HeadH8Args a) {
       const float v = acc[ch] + rd(6 + ch, y, x);
       o[(int64_t)ch * a.h * a.w_] = v < 0.0f ? 0.0f : (v > 1.0f ? 1.0f : v);
     }
+  }
+}
+
+template <int PLANES>
+__global__ void flow_tblend_h8_kernel(const _Float16* __restrict__ fhi, const _Float16* __restrict__ flo,
+                                      int64_t f_img, int64_t f_gp, int f_wp, _Float16* ghi, _Float16* glo,
+                                      int64_t g_img, int64_t g_gp, int g_wp, const float* coef, int h, int w,
+                                      int64_t total) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int x = (int)(i % w);
+  const int64_t t = i / w;
+  const int y = (int)(t % h);
+  const int img = (int)(t / h);
+  const float* cf = coef + img * 8;
+  float f[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int64_t kk = h8_half_index(f_img, f_gp, f_wp, img, k, y, x);
+    f[k] = (float)fhi[kk] + (PLANES == 2 ? (float)flo[kk] : 0.0f);
+  }
+  float o[4];
+  for (int k = 0; k < 2; ++k) {
+#pragma clang fp contract(off)
+    o[k] = cf[0] * f[k] + cf[1] * f[2 + k];
+    o[2 + k] = cf[2] * f[k] - cf[3] * f[2 + k];
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int64_t kk = h8_half_index(g_img, g_gp, g_wp, img, 6 + k, y, x);
+    const _Float16 vh = (_Float16)o[k];
+    ghi[kk] = vh;
+    if constexpr (PLANES == 2) glo[kk] = (_Float16)(o[k] - (float)vh);
   }
 }
 
@@ -844,6 +889,15 @@ extern "C" int rrin_head_h8_fwd(const rrin_head_h8_desc* d, void* stream) {
   a.bias = d->bias;
   a.coef = d->coef;
   a.out = d->out;
+  if (d->mode == RRIN_HEAD_FLOW && d->flow_raw.hi) {
+    if (!h8_ok(d->flow_raw, d->prec) || d->flow_raw.g.h != h || d->flow_raw.g.w != w) return RRIN_E_SHAPE;
+    const int64_t fo = (int64_t)d->flow_raw.g_off * d->flow_raw.g.plane * 8;
+    a.fr_hi = static_cast<_Float16*>(d->flow_raw.hi) + fo;
+    a.fr_lo = planes == 2 ? static_cast<_Float16*>(d->flow_raw.lo) + fo : nullptr;
+    a.fr_img = d->flow_raw.img_stride;
+    a.fr_gp = d->flow_raw.g.plane;
+    a.fr_wp = d->flow_raw.g.wp;
+  }
   a.h = h;
   a.w_ = w;
   a.tiles_x = (w + 31) / 32;
@@ -866,4 +920,27 @@ extern "C" int rrin_head_h8_fwd(const rrin_head_h8_desc* d, void* stream) {
       return d->cout == 3 ? head_h8_launch<3, RRIN_HEAD_FINAL>(a, planes, grid, st) : RRIN_E_ARG;
   }
   return RRIN_E_ARG;
+}
+
+extern "C" int rrin_flow_tblend_h8(const rrin_h8* fr, const rrin_h8* g16, const float* coef, int32_t n, int32_t prec,
+                                   void* stream) {
+  if (!fr || !g16 || !coef || n < 1 || (prec != RRIN_PREC_F16X3 && prec != RRIN_PREC_F16)) return RRIN_E_ARG;
+  if (!h8_ok(*fr, prec) || !h8_ok(*g16, prec) || g16->g_off != 0 || g16->groups < 2) return RRIN_E_SHAPE;
+  if (fr->g.h != g16->g.h || fr->g.w != g16->g.w) return RRIN_E_SHAPE;
+  const int h = g16->g.h, w = g16->g.w;
+  const int64_t total = (int64_t)n * h * w;
+  const int grid = (int)((total + 255) / 256);
+  const int64_t fo = (int64_t)fr->g_off * fr->g.plane * 8;
+  const _Float16* fhi = static_cast<const _Float16*>(fr->hi) + fo;
+  hipStream_t st = (hipStream_t)stream;
+  if (planes_of(prec) == 2)
+    hipLaunchKernelGGL(flow_tblend_h8_kernel<2>, dim3(grid), dim3(256), 0, st, fhi,
+                       static_cast<const _Float16*>(fr->lo) + fo, fr->img_stride, fr->g.plane, fr->g.wp,
+                       static_cast<_Float16*>(g16->hi), static_cast<_Float16*>(g16->lo), g16->img_stride,
+                       g16->g.plane, g16->g.wp, coef, h, w, total);
+  else
+    hipLaunchKernelGGL(flow_tblend_h8_kernel<1>, dim3(grid), dim3(256), 0, st, fhi, (const _Float16*)nullptr,
+                       fr->img_stride, fr->g.plane, fr->g.wp, static_cast<_Float16*>(g16->hi), (_Float16*)nullptr,
+                       g16->img_stride, g16->g.plane, g16->g.wp, coef, h, w, total);
+  return hip_code(hipGetLastError());
 }

@@ -30,6 +30,9 @@ struct HeadArgs {
   const float* bias;
   const float* coef; // [n][8]
   float* out;        // FINAL: NCHW
+  float* flow_raw;   // FLOW: raw output (4 PP planes), nullable
+  int64_t fr_img, fr_plane;
+  int fr_wp;
   int h, w_, tiles_x, tiles_y;
 };
 
@@ -100,6 +103,10 @@ __global__ void __launch_bounds__(256) head_kernel(HeadArgs a) {
   } else if constexpr (MODE == RRIN_HEAD_FLOW) {
     // Ft0 = (-(1-t)t)*F01 + (t*t)*F10 ; Ft1 = ((1-t)^2)*F01 - (t(1-t))*F10
 #pragma clang fp contract(off)
+    if (a.flow_raw) {
+      float* fr = a.flow_raw + img * a.fr_img + (int64_t)(y + 1) * a.fr_wp + x + kPadLeft;
+      for (int k = 0; k < 4; ++k) fr[k * a.fr_plane] = acc[k];
+    }
     for (int k = 0; k < 2; ++k) {
       G(6 + k) = cf[0] * acc[k] + cf[1] * acc[2 + k];
       G(8 + k) = cf[2] * acc[k] - cf[3] * acc[2 + k];
@@ -190,9 +197,42 @@ __global__ void warp_nchw_kernel(const float* __restrict__ img, const float* __r
   }
 }
 
+__global__ void flow_tblend_kernel(const float* __restrict__ fr, int64_t fr_img, int64_t fr_plane, int fr_wp,
+                                   float* g, int64_t g_img, int64_t g_plane, int g_wp, const float* coef, int h,
+                                   int w, int64_t total) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int x = (int)(i % w);
+  const int64_t t = i / w;
+  const int y = (int)(t % h);
+  const int img = (int)(t / h);
+  const float* f = fr + img * fr_img + (int64_t)(y + 1) * fr_wp + x + kPadLeft;
+  float* gp = g + img * g_img + (int64_t)(y + 1) * g_wp + x + kPadLeft;
+  const float* cf = coef + img * 8;
+  for (int k = 0; k < 2; ++k) {
+#pragma clang fp contract(off)
+    const float f01 = f[k * fr_plane], f10 = f[(2 + k) * fr_plane];
+    gp[(6 + k) * g_plane] = cf[0] * f01 + cf[1] * f10;
+    gp[(8 + k) * g_plane] = cf[2] * f01 - cf[3] * f10;
+  }
+}
+
 }  // namespace rrin
 
 using namespace rrin;
+
+extern "C" int rrin_flow_tblend_fwd(const rrin_pp* fr, const rrin_pp* g16, const float* coef, int32_t n,
+                                    void* stream) {
+  if (!fr || !g16 || !fr->base || !g16->base || !coef || n < 1) return RRIN_E_ARG;
+  if (fr->channels < 4 || g16->channels < 16 || g16->ch_off != 0) return RRIN_E_ARG;
+  if (fr->g.h != g16->g.h || fr->g.w != g16->g.w) return RRIN_E_SHAPE;
+  const int64_t total = (int64_t)n * g16->g.h * g16->g.w;
+  hipLaunchKernelGGL(flow_tblend_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, fr->base + (int64_t)fr->ch_off * fr->g.plane, fr->img_stride,
+                     fr->g.plane, fr->g.wp, g16->base, g16->img_stride, g16->g.plane, g16->g.wp, coef,
+                     g16->g.h, g16->g.w, total);
+  return hip_code(hipGetLastError());
+}
 
 extern "C" int rrin_head_fwd(const rrin_head_desc* d, void* stream) {
   if (!d || !d->src.base || !d->g16.base || !d->w || !d->bias) return RRIN_E_ARG;
@@ -222,6 +262,15 @@ extern "C" int rrin_head_fwd(const rrin_head_desc* d, void* stream) {
   a.bias = d->bias;
   a.coef = d->coef;
   a.out = d->out;
+  a.flow_raw = nullptr;
+  if (d->mode == RRIN_HEAD_FLOW && d->flow_raw.base) {
+    if (d->flow_raw.channels < 4 || d->flow_raw.g.h != h || d->flow_raw.g.w != w || d->flow_raw.g.wp != gg.wp)
+      return RRIN_E_SHAPE;
+    a.flow_raw = d->flow_raw.base + (int64_t)d->flow_raw.ch_off * d->flow_raw.g.plane;
+    a.fr_img = d->flow_raw.img_stride;
+    a.fr_plane = d->flow_raw.g.plane;
+    a.fr_wp = d->flow_raw.g.wp;
+  }
   a.h = h;
   a.w_ = w;
   a.tiles_x = (w + 31) / 32;

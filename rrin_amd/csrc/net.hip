@@ -52,6 +52,7 @@ struct Plan {
   Buf CAT[kMaxDepth - 1]; // [up | bridge]: 2 C_L ch  (levels 0..3)
   Buf BOT;                // Flow bottom (level 4) conv-b output: 512 ch
   Buf UPT;                // F16*: upsampled input of an up.1 conv (64 ch at level 0, reused per level)
+  Buf FLOWRAW;            // raw 4-ch Flow output, kept for reuse across t (skip_flow)
   int64_t bytes;
 };
 
@@ -87,6 +88,7 @@ void make_plan(int n, int h, int w, int prec, char* base, Plan& p) {
   }
   p.BOT = take(chans(kMaxDepth - 1), p.g[kMaxDepth - 1]);
   p.UPT = f32 ? Buf{nullptr, nullptr, 0, p.g[0]} : take(2 * chans(0), p.g[0]);
+  p.FLOWRAW = take(f32 ? 4 : 8, p.g[0]);
   p.bytes = off;
 }
 
@@ -209,6 +211,7 @@ int run_unet(const Plan& p, const UNetSpec& u, const rrin_conv_weights* cw, cons
   hd.bias = hw.bias;
   hd.coef = nd->coef;
   hd.out = nd->out;
+  if (u.head_mode == RRIN_HEAD_FLOW) hd.flow_raw = view(p.FLOWRAW, p.n, 0, 4);
   ProfScope ps(g_prof, st, RRIN_KIND_HEAD, 2.0 * 9 * 32 * u.out_ch * (double)x.g.h * x.g.w * p.n);
   return rrin_head_fwd(&hd, st);
 }
@@ -286,6 +289,7 @@ int run_unet_h8(const Plan& p, const UNetSpec& u, const rrin_conv_weights* cw, c
   hd.bias = hw.bias;
   hd.coef = nd->coef;
   hd.out = nd->out;
+  if (u.head_mode == RRIN_HEAD_FLOW) hd.flow_raw = hview(p.FLOWRAW, 0, 4);
   ProfScope ps(g_prof, st, RRIN_KIND_HEAD, 2.0 * 9 * 32 * u.out_ch * (double)x.g.h * x.g.w * p.n);
   return rrin_head_h8_fwd(&hd, st);
 }
@@ -322,7 +326,6 @@ extern "C" int rrin_net_fwd(const rrin_net_desc* d, void* stream) {
   if (d->workspace_bytes < p.bytes) return RRIN_E_WORKSPACE;
   hipStream_t st = (hipStream_t)stream;
   if (d->prec != RRIN_PREC_F32) {
-    if (d->skip_flow) return RRIN_E_ARG;
     g_prof = d->prof;
     const rrin_h8 gall = hview(p.G, 0, 16);
     int rc = 0;
@@ -330,10 +333,14 @@ extern "C" int rrin_net_fwd(const rrin_net_desc* d, void* stream) {
       ProfScope ps(g_prof, st, RRIN_KIND_LAYOUT, 0.0);
       rc = rrin_nchw_to_h8(d->i0, d->n, 3, 0, &gall, d->prec, st);
       if (!rc) rc = rrin_nchw_to_h8(d->i1, d->n, 3, 3, &gall, d->prec, st);
+      if (!rc && d->skip_flow) {
+        const rrin_h8 fr = hview(p.FLOWRAW, 0, 4);
+        rc = rrin_flow_tblend_h8(&fr, &gall, d->coef, d->n, d->prec, st);
+      }
     }
     int k = 0;
     for (int u = 0; u < 4 && !rc; ++u) {
-      rc = run_unet_h8(p, kUNets[u], d->convs + k, d->heads[u], d, st);
+      if (!(u == 0 && d->skip_flow)) rc = run_unet_h8(p, kUNets[u], d->convs + k, d->heads[u], d, st);
       k += convs_of(kUNets[u].depth);
     }
     g_prof = nullptr;
@@ -343,17 +350,21 @@ extern "C" int rrin_net_fwd(const rrin_net_desc* d, void* stream) {
   // x = cat(x0, x1) into g16 channels 0-5 (model.py:33)
   const rrin_pp gx0 = view(p.G, p.n, 0, 3);
   const rrin_pp gx1 = view(p.G, p.n, 3, 3);
-  if (d->skip_flow) return RRIN_E_ARG;  // Flow reuse across t: not built yet
   g_prof = d->prof;
   int rc = 0;
   {
     ProfScope ps(g_prof, st, RRIN_KIND_LAYOUT, 0.0);
     rc = rrin_nchw_to_pp(d->i0, d->n, 3, &gx0, st);
     if (!rc) rc = rrin_nchw_to_pp(d->i1, d->n, 3, &gx1, st);
+    if (!rc && d->skip_flow) {  // Flow U-Net skipped: t-blend of the kept raw Flow
+      const rrin_pp fr = view(p.FLOWRAW, p.n, 0, 4);
+      const rrin_pp g16 = view(p.G, p.n, 0, 16);
+      rc = rrin_flow_tblend_fwd(&fr, &g16, d->coef, d->n, st);
+    }
   }
   int k = 0;
   for (int u = 0; u < 4 && !rc; ++u) {
-    rc = run_unet(p, kUNets[u], d->convs + k, d->heads[u], d, st);
+    if (!(u == 0 && d->skip_flow)) rc = run_unet(p, kUNets[u], d->convs + k, d->heads[u], d, st);
     k += convs_of(kUNets[u].depth);
   }
   g_prof = nullptr;

@@ -143,6 +143,7 @@ class RRINEngine:
             self.head_table[i].bias = b.data_ptr()
         self.cfgs = [m[2] for m in meta]
         self._ws = OrderedDict()
+        self._flow_valid = {}
 
     def _init_h8(self, net):
         """Pack for the split-fp16 (F16X3) or fp16 (F16) path: [cob][16-ch chunk][tap][half][bm][8]
@@ -200,6 +201,7 @@ class RRINEngine:
             self.head_table[i].bias = b.data_ptr()
         self.cfgs = [m[3] for m in meta]
         self._ws = OrderedDict()
+        self._flow_valid = {}
 
     def workspace(self, n: int, h: int, w: int) -> torch.Tensor:
         key = (n, h, w)
@@ -209,14 +211,20 @@ class RRINEngine:
             if nbytes < 0:
                 _lib.check(int(nbytes), "rrin_net_workspace_bytes")
             while len(self._ws) >= self.MAX_WORKSPACES:
-                self._ws.popitem(last=False)
+                old, _ = self._ws.popitem(last=False)
+                self._flow_valid.pop(old, None)
             ws = torch.zeros(int(nbytes), dtype=torch.uint8, device=self.device)
             self._ws[key] = ws
+            self._flow_valid[key] = False
         else:
             self._ws.move_to_end(key)
         return ws
 
-    def forward(self, i0: torch.Tensor, i1: torch.Tensor, t=0.5, prof=None) -> torch.Tensor:
+    def forward(self, i0: torch.Tensor, i1: torch.Tensor, t=0.5, prof=None, reuse_flow: bool = False) -> torch.Tensor:
+        """One Net.forward.  ``reuse_flow=True`` promises that (i0, i1) is the pair
+        of the previous call with the same shape: the Flow U-Net (t-independent,
+        model.py:35, 30 % of the FLOPs) is skipped and its kept raw output is
+        re-blended for this t."""
         if i0.device != self.device or i1.device != self.device:
             raise RuntimeError(f"inputs on {i0.device}/{i1.device}, model on {self.device}")
         if i0.dtype != torch.float32 or i1.dtype != torch.float32:
@@ -233,6 +241,7 @@ class RRINEngine:
         coef = t_coefficients(t, n).to(self.device, non_blocking=True)
         with torch.cuda.device(self.device):
             ws = self.workspace(n, h, w)
+            skip = bool(reuse_flow) and self._flow_valid.get((n, h, w), False)
             d = _lib.NetDesc()
             d.n, d.h, d.w = n, h, w
             d.i0, d.i1, d.out, d.coef = i0.data_ptr(), i1.data_ptr(), out.data_ptr(), coef.data_ptr()
@@ -240,9 +249,10 @@ class RRINEngine:
             d.heads = self.head_table
             d.workspace = ws.data_ptr()
             d.workspace_bytes = ws.numel()
-            d.skip_flow = 0
+            d.skip_flow = 1 if skip else 0
             d.prec = self.prec
             d.prof = prof
             stream = torch.cuda.current_stream(self.device).cuda_stream
             _lib.check(self.lib.rrin_net_fwd(C.byref(d), C.c_void_p(stream)), "rrin_net_fwd")
+            self._flow_valid[(n, h, w)] = True
         return out

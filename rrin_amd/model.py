@@ -63,6 +63,15 @@ class Net(nn.Module):
             self._engine_version = self._weights_version
         return self._engine
 
+    def interpolate(self, input0, input1, ts):
+        """All intermediate frames of one (batch of) pair(s): ``[forward(I0, I1, t) for t in ts]``
+        with the t-independent Flow U-Net computed once (the
+        reference recomputes it per t, convert.py:127-130)."""
+        if torch.is_grad_enabled():
+            raise RuntimeError("rrin_amd.Net.interpolate is inference-only: use torch.no_grad()")
+        eng = self.engine()
+        return [eng.forward(input0, input1, t, reuse_flow=(k > 0)) for k, t in enumerate(ts)]
+
     def forward(self, input0, input1, t=0.5):
         if torch.is_grad_enabled() and (input0.requires_grad or input1.requires_grad or
                                         any(p.requires_grad for p in self.parameters())):

@@ -137,3 +137,18 @@ def test_net_fp16_gate(gpu, which, h, w):
     mse = float(((out.double() - ref.double()) ** 2).mean())
     psnr = 10 * np.log10(1.0 / max(mse, 1e-30))
     assert err <= 1e-2 and psnr >= 45, f"max-abs {err:.3e} psnr {psnr:.1f}"
+
+
+@pytest.mark.parametrize("precision", ["fp32", "fp32_split16", "fp16"])
+def test_interpolate_reuses_flow(gpu, precision):
+    """Net.interpolate == [forward(t) for t in ts] bitwise, with the Flow U-Net run once."""
+    net = make_net(gpu, stress=True)
+    net.precision = precision
+    i0, i1 = synthetic_batch(2, 64, 96, first_index=11)
+    i0, i1 = i0.to(gpu), i1.to(gpu)
+    ts = [0.25, 0.5, 0.75]
+    with torch.no_grad():
+        many = net.interpolate(i0, i1, ts)
+        single = [net(i0, i1, t) for t in ts]
+    for a, b in zip(many, single):
+        assert torch.equal(a, b)
