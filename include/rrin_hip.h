@@ -124,9 +124,9 @@ int rrin_warp_fwd(const float* img, const float* flow, float* out, int32_t n, in
 /* ---- Split-fp16 path ("H8" layout) --------------------------------------- */
 /* Precision of a forward / conv:
  *   F32   exact fp32 (v_mfma_f32_32x32x2_f32), PP layout above;
- *   F16X3 every fp32 value v is held as hi = f16(v), lo = f16(v - hi)
- *         (|v - hi - lo| <= 2^-22 |v| for normal lo) and every product as
- *         hi*hi + hi*lo + lo*hi in v_mfma_f32_32x32x16_f16 with fp32
+ *   F16X3 every fp32 value v is held as hi = f16(v), lo = f16((v - hi) * 2^11)
+ *         (v = hi + lo 2^-11 to ~2^-22 |v|; lo stays normal) and every product as
+ *         hi*hi + 2^-11 (hi*lo + lo*hi) in v_mfma_f32_32x32x16_f16 with fp32
  *         accumulation: fp32-class accuracy at ~5x the fp32 MFMA rate;
  *   F16   hi only (fp16 storage, fp16 products, fp32 accumulation) for the
  *         fp16 configs of BASELINE.json.

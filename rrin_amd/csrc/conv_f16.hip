@@ -1,12 +1,14 @@
 // Split-fp16 ("F16X3") and fp16 ("F16") path of the RRIN hot path on the
 // gfx950 f16 matrix cores (v_mfma_f32_32x32x16_f16, fp32 accumulate).
 //
-// Numerics (F16X3): every fp32 value v lives as hi = f16(v), lo = f16(v - hi),
-// so v = hi + lo to 2^-22 |v| (lo normal; absolute 2^-25 floor otherwise).
-// A product a*w is computed as a_hi*w_hi + a_hi*w_lo + a_lo*w_hi — each term
-// exact in fp32 — and accumulated in fp32 by the MFMA; the dropped a_lo*w_lo is
-// <= 2^-22 |a w|.  Weights are pre-scaled by 2^s (exact) so their lo parts stay
-// normal; the epilogue multiplies by 2^-s.  F16 keeps hi only (fp16 configs).
+// Numerics (F16X3): every fp32 value v lives as hi = f16(v) and a pre-scaled
+// lo' = f16((v - hi) * 2^11), so v = hi + lo' 2^-11 to ~2^-22 |v| and lo' stays
+// a normal fp16 down to |v| ~ 1e-4.  A product a*w is computed as
+// a_hi*w_hi (accumulator acc) + (a_hi*w_lo' + a_lo'*w_hi) (accumulator accx,
+// scaled back by 2^-11 in the epilogue) — every term exact in fp32 — with fp32
+// accumulation in the MFMA; the dropped lo*lo term is <= 2^-22 |a w|.
+// Weights are pre-scaled by 2^s (exact), max |w| 2^s in [2^12, 2^13); the
+// epilogue multiplies by 2^-s.  F16 keeps hi only (fp16 configs).
 //
 // Replaces (as conv_mfma.hip): nn.Conv2d(3,pad=1) + LeakyReLU(0.1)
 // (/root/reference/unet.py:29,59-63,78), F.avg_pool2d (unet.py:46, fused second
@@ -29,6 +31,14 @@ typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 constexpr int H8_LC = 34;  // staged input row: records of pixels x0-1 .. x0+32
+
+// lo halves are stored pre-scaled by 2^11 so they stay normal fp16 for any
+// |v| >= ~1e-4 (unscaled, v - hi ~ 2^-12 v would be subnormal below |v| = 0.125
+// and lose its bits): v = hi + lo * 2^-11.
+constexpr float kLoScale = 2048.0f;
+constexpr float kLoUnscale = 1.0f / 2048.0f;
+__device__ inline _Float16 lo_of(float v, _Float16 hi) { return (_Float16)((v - (float)hi) * kLoScale); }
+__device__ inline float join(_Float16 hi, _Float16 lo) { return fmaf((float)lo, kLoUnscale, (float)hi); }
 
 struct ConvH8Args {
   const uint4* src_hi;
@@ -168,13 +178,17 @@ __global__ void __launch_bounds__(64 * NW) conv3x3_h8_kernel(ConvH8Args a) {
       }
   };
 
-  floatx16 acc[WM][WN];
+  // acc: hi*hi products; accx (F16X3): hi*lo' + lo'*hi, 2^11 too large
+  floatx16 acc[WM][WN], accx[WM][WN];
 #pragma unroll
   for (int mt = 0; mt < WM; ++mt)
 #pragma unroll
     for (int nt = 0; nt < WN; ++nt)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) acc[mt][nt][i] = 0.f;
+      for (int i = 0; i < 16; ++i) {
+        acc[mt][nt][i] = 0.f;
+        accx[mt][nt][i] = 0.f;
+      }
 
   // 9 taps per chunk; one K16 block = 16 input channels at one tap (lanes
   // 0-31 carry channels 0-7 of the chunk, lanes 32-63 channels 8-15).
@@ -208,8 +222,8 @@ __global__ void __launch_bounds__(64 * NW) conv3x3_h8_kernel(ConvH8Args a) {
 #pragma unroll
         for (int nt = 0; nt < WN; ++nt) {
           if constexpr (PLANES == 2) {
-            acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[s][1][mt], bv[s][0][nt], acc[mt][nt], 0, 0, 0);
-            acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[s][0][mt], bv[s][1][nt], acc[mt][nt], 0, 0, 0);
+            accx[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[s][1][mt], bv[s][0][nt], accx[mt][nt], 0, 0, 0);
+            accx[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[s][0][mt], bv[s][1][nt], accx[mt][nt], 0, 0, 0);
           }
           acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[s][0][mt], bv[s][0][nt], acc[mt][nt], 0, 0, 0);
         }
@@ -260,7 +274,9 @@ __global__ void __launch_bounds__(64 * NW) conv3x3_h8_kernel(ConvH8Args a) {
         const int y = yb + nt;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          float t = acc[mt][nt][4 * q + e] * a.inv_wscale + bs[e];
+          float t = acc[mt][nt][4 * q + e];
+          if constexpr (PLANES == 2) t = fmaf(accx[mt][nt][4 * q + e], kLoUnscale, t);
+          t = t * a.inv_wscale + bs[e];
           if constexpr (EPI != RRIN_EPI_LINEAR) t = t > 0.f ? t : t * a.slope;
           v[nt][e] = t;
         }
@@ -270,7 +286,7 @@ __global__ void __launch_bounds__(64 * NW) conv3x3_h8_kernel(ConvH8Args a) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             hi[e] = (_Float16)v[nt][e];
-            lo[e] = (_Float16)(v[nt][e] - (float)hi[e]);
+            lo[e] = lo_of(v[nt][e], hi[e]);
           }
           reinterpret_cast<uint2*>(dst[0] + rec)[hh] = __builtin_bit_cast(uint2, hi);
           if constexpr (PLANES == 2) reinterpret_cast<uint2*>(dst[1] + rec)[hh] = __builtin_bit_cast(uint2, lo);
@@ -292,7 +308,7 @@ __global__ void __launch_bounds__(64 * NW) conv3x3_h8_kernel(ConvH8Args a) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
               hi[e] = (_Float16)s4[e];
-              lo[e] = (_Float16)(s4[e] - (float)hi[e]);
+              lo[e] = lo_of(s4[e], hi[e]);
             }
             reinterpret_cast<uint2*>(pdst[0] + rec)[hh] = __builtin_bit_cast(uint2, hi);
             if constexpr (PLANES == 2) reinterpret_cast<uint2*>(pdst[1] + rec)[hh] = __builtin_bit_cast(uint2, lo);
@@ -342,13 +358,13 @@ __global__ void up2x_h8_kernel(const uint4* __restrict__ s_hi, const uint4* __re
   for (int e = 0; e < 8; ++e) {
     float v[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) v[k] = (float)q[k][0][e] + (PLANES == 2 ? (float)q[k][PLANES - 1][e] : 0.0f);
+    for (int k = 0; k < 4; ++k) v[k] = PLANES == 2 ? join(q[k][0][e], q[k][PLANES - 1][e]) : (float)q[k][0][e];
     // horizontal first, then vertical (upsample_bilinear2d order)
     const float top = wc * v[0] + wd * v[1];
     const float bot = wc * v[2] + wd * v[3];
     const float o = wa * top + wb * bot;
     ohi[e] = (_Float16)o;
-    olo[e] = (_Float16)(o - (float)ohi[e]);
+    olo[e] = lo_of(o, ohi[e]);
   }
   const int64_t drec = img * d_img + g * d_gp + (int64_t)(y + 1) * d_wp + x + kH8PadLeft;
   d_hi[drec] = __builtin_bit_cast(uint4, ohi);
@@ -375,7 +391,7 @@ __global__ void nchw_to_h8_kernel(const float* __restrict__ src, _Float16* hi, _
   const int64_t k = h8_half_index(img_stride, gp, wp, n, ch_off + ch, y, x);
   const _Float16 vh = (_Float16)v;
   hi[k] = vh;
-  if (lo) lo[k] = (_Float16)(v - (float)vh);
+  if (lo) lo[k] = lo_of(v, vh);
 }
 
 __global__ void h8_to_nchw_kernel(const _Float16* __restrict__ hi, const _Float16* __restrict__ lo, int64_t img_stride,
@@ -389,7 +405,7 @@ __global__ void h8_to_nchw_kernel(const _Float16* __restrict__ hi, const _Float1
   const int ch = (int)(t % c);
   const int n = (int)(t / c);
   const int64_t k = h8_half_index(img_stride, gp, wp, n, ch_off + ch, y, x);
-  dst[i] = (float)hi[k] + (lo ? (float)lo[k] : 0.0f);
+  dst[i] = lo ? join(hi[k], lo[k]) : (float)hi[k];
 }
 
 // ---- head conv (Cout <= 4) + Net glue on the H8 Net buffer --------------------
@@ -441,7 +457,7 @@ __global__ void __launch_bounds__(256) head_h8_kernel(HeadH8Args a) {
       if constexpr (PLANES == 2) vl = __builtin_bit_cast(half8, a.src_lo[rec]);
 #pragma unroll
       for (int e = 0; e < 8; ++e)
-        s_in[(e * HROWS + rr) * HLC + col + 3] = (float)vh[e] + (PLANES == 2 ? (float)vl[e] : 0.0f);
+        s_in[(e * HROWS + rr) * HLC + col + 3] = PLANES == 2 ? join(vh[e], vl[e]) : (float)vh[e];
     }
     __syncthreads();
 #pragma unroll
@@ -463,13 +479,13 @@ __global__ void __launch_bounds__(256) head_h8_kernel(HeadH8Args a) {
   auto idx_of = [&](int ch, int yy, int xx) { return h8_half_index(a.g_img, a.g_gp, a.g_wp, img, ch, yy, xx); };
   auto rd = [&](int ch, int yy, int xx) -> float {
     const int64_t k = idx_of(ch, yy, xx);
-    return (float)a.g_hi[k] + (PLANES == 2 ? (float)a.g_lo[k] : 0.0f);
+    return PLANES == 2 ? join(a.g_hi[k], a.g_lo[k]) : (float)a.g_hi[k];
   };
   auto wr = [&](int ch, float v) {
     const int64_t k = idx_of(ch, y, x);
     const _Float16 vh = (_Float16)v;
     a.g_hi[k] = vh;
-    if constexpr (PLANES == 2) a.g_lo[k] = (_Float16)(v - (float)vh);
+    if constexpr (PLANES == 2) a.g_lo[k] = lo_of(v, vh);
   };
   const float* cf = a.coef + img * 8;
 
@@ -483,7 +499,7 @@ __global__ void __launch_bounds__(256) head_h8_kernel(HeadH8Args a) {
         const int64_t kk = h8_half_index(a.fr_img, a.fr_gp, a.fr_wp, img, k, y, x);
         const _Float16 vh = (_Float16)acc[k];
         a.fr_hi[kk] = vh;
-        if constexpr (PLANES == 2) a.fr_lo[kk] = (_Float16)(acc[k] - (float)vh);
+        if constexpr (PLANES == 2) a.fr_lo[kk] = lo_of(acc[k], vh);
       }
     }
     for (int k = 0; k < 2; ++k) {
@@ -543,7 +559,7 @@ __global__ void flow_tblend_h8_kernel(const _Float16* __restrict__ fhi, const _F
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int64_t kk = h8_half_index(f_img, f_gp, f_wp, img, k, y, x);
-    f[k] = (float)fhi[kk] + (PLANES == 2 ? (float)flo[kk] : 0.0f);
+    f[k] = PLANES == 2 ? join(fhi[kk], flo[kk]) : (float)fhi[kk];
   }
   float o[4];
   for (int k = 0; k < 2; ++k) {
@@ -556,7 +572,7 @@ __global__ void flow_tblend_h8_kernel(const _Float16* __restrict__ fhi, const _F
     const int64_t kk = h8_half_index(g_img, g_gp, g_wp, img, 6 + k, y, x);
     const _Float16 vh = (_Float16)o[k];
     ghi[kk] = vh;
-    if constexpr (PLANES == 2) glo[kk] = (_Float16)(o[k] - (float)vh);
+    if constexpr (PLANES == 2) glo[kk] = lo_of(o[k], vh);
   }
 }
 
@@ -789,7 +805,7 @@ extern "C" int rrin_pack_conv3x3_h8(const float* w, const float* b, int32_t cout
               if (co < cout && ch < cin) v = w[((int64_t)co * cin + (perm ? perm[ch] : ch)) * 9 + tap] * scale;
               const uint16_t hbits = f2h_rne(v);
               whi[o] = hbits;
-              if (prec == RRIN_PREC_F16X3) wlo[o] = f2h_rne(v - h2f(hbits));
+              if (prec == RRIN_PREC_F16X3) wlo[o] = f2h_rne((v - h2f(hbits)) * 2048.0f);
               ++o;
             }
   for (int co = 0; co < cob_n * bm; ++co) bpack[co] = co < cout ? b[co] : 0.f;

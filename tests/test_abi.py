@@ -118,7 +118,7 @@ def test_pack_h8_layout_and_split(cout, cin, bm, prec):
     assert scale == 2.0 ** round(np.log2(scale))
     assert 2 ** 12 <= np.abs(w).max() * scale < 2 ** 13
     cob, nch = -(-cout // bm), -(-cin // 16)
-    rec = _h2f(whi) + (_h2f(wlo) if prec == 1 else 0)
+    rec = _h2f(whi) + (_h2f(wlo) / 2048.0 if prec == 1 else 0)
     rec = rec.reshape(cob, nch, 9, 2, bm, 8)
     # back to [co][ci][tap]
     got = rec.transpose(0, 4, 1, 3, 5, 2).reshape(cob * bm, nch * 16, 9)[:cout, :cin] / scale

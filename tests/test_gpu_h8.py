@@ -85,7 +85,8 @@ def test_h8_roundtrip(gpu, prec):
     t = H8Tensor.from_nchw(x, prec, c_alloc=24, ch_off=3)
     y = t.to_nchw(3, 11)
     rel = 2.0 ** -21 if prec == X3 else 2.0 ** -10
-    assert float(((y - x).abs() / x.abs().clamp_min(1e-3)).max()) <= rel
+    floor = 2.0 ** -34 if prec == X3 else 2.0 ** -24   # fp16 subnormal floor of lo (x 2^-11) / hi
+    assert bool(((y - x).abs() <= rel * x.abs() + floor).all())
     assert not t.hi[:, :, 0].any() and not t.hi[:, :, :, :8].any() and not t.hi[:, :, 24:].any()
 
 

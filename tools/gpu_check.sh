@@ -16,7 +16,7 @@ run() {  # name limit cmd...
   return 0
 }
 STEPS=${STEPS:-tests,smoke,bench,prof}
-[[ $STEPS == *tests* ]] && run tests 900 python -m pytest tests -m gpu -x -q
+[[ $STEPS == *tests* ]] && run tests 900 python -m pytest tests -m gpu -q
 [[ $STEPS == *smoke* ]] && run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 [[ $STEPS == *bench* ]] && run bench 600 python bench.py --steps 5 --warmup 2
 [[ $STEPS == *bsplit* ]] && run bench_split 600 python bench.py --steps 5 --warmup 2 --precision fp32_split16
