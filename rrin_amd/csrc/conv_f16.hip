@@ -494,12 +494,16 @@ __global__ void __launch_bounds__(256) head_h8_kernel(HeadH8Args a) {
     for (int co = 0; co < COUT; ++co) wr(co, acc[co]);
   } else if constexpr (MODE == RRIN_HEAD_FLOW) {
 #pragma clang fp contract(off)
-    if (a.fr_hi) {
-      for (int k = 0; k < 4; ++k) {
+    // round the raw flow to its stored form first, so that a later t-blend of the
+    // kept raw flow (skip_flow) reproduces these Ft bit for bit
+    for (int k = 0; k < 4; ++k) {
+      const _Float16 vh = (_Float16)acc[k];
+      const _Float16 vl = lo_of(acc[k], vh);
+      acc[k] = PLANES == 2 ? join(vh, vl) : (float)vh;
+      if (a.fr_hi) {
         const int64_t kk = h8_half_index(a.fr_img, a.fr_gp, a.fr_wp, img, k, y, x);
-        const _Float16 vh = (_Float16)acc[k];
         a.fr_hi[kk] = vh;
-        if constexpr (PLANES == 2) a.fr_lo[kk] = lo_of(acc[k], vh);
+        if constexpr (PLANES == 2) a.fr_lo[kk] = vl;
       }
     }
     for (int k = 0; k < 2; ++k) {
@@ -627,10 +631,11 @@ static float h2f(uint16_t h) {
 struct CfgH8 {
   int bm, th;
   size_t lds1, lds2;
+  bool pool_ok;
 };
 static const CfgH8 kCfgH8[] = {
 #define X(id, nw, wm, wn) {TileH8<nw, wm, wn, 1>::BM, TileH8<nw, wm, wn, 1>::TH, TileH8<nw, wm, wn, 1>::LDS, \
-                           TileH8<nw, wm, wn, 2>::LDS},
+                           TileH8<nw, wm, wn, 2>::LDS, (wn % 2) == 0},
     RRIN_H8_CFGS(X)
 #undef X
 };
@@ -710,6 +715,7 @@ extern "C" int rrin_conv3x3_h8_fwd(const rrin_conv_h8_desc* d, void* stream) {
   if (d->src.g.h != h || d->src.g.w != w) return RRIN_E_SHAPE;
   if (d->cin > 8 * d->src.groups || d->cout > 8 * d->dst.groups) return RRIN_E_ARG;
   if (d->epi_mode == RRIN_EPI_LEAKY_POOL) {
+    if (!kCfgH8[d->cfg].pool_ok) return RRIN_E_CONFIG;  // a wave must own both rows of a pool pair
     if (!h8_ok(d->pool, d->prec) || (h & 1) || (w & 1) || d->pool.g.h * 2 != h || d->pool.g.w * 2 != w ||
         d->cout > 8 * d->pool.groups)
       return RRIN_E_SHAPE;

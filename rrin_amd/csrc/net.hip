@@ -51,7 +51,9 @@ struct Plan {
   Buf T[kMaxDepth];       // first conv of a block: C_L ch
   Buf CAT[kMaxDepth - 1]; // [up | bridge]: 2 C_L ch  (levels 0..3)
   Buf BOT;                // Flow bottom (level 4) conv-b output: 512 ch
-  Buf UPT;                // F16*: upsampled input of an up.1 conv (64 ch at level 0, reused per level)
+  Buf UPT[kMaxDepth - 1]; // F16*: upsampled input of an up.1 conv, one per level (2 C_L ch).  Not
+                          // shared across levels: another level's interior writes would land in
+                          // this level's zero padding (the conv halo).
   Buf FLOWRAW;            // raw 4-ch Flow output, kept for reuse across t (skip_flow)
   int64_t bytes;
 };
@@ -87,7 +89,8 @@ void make_plan(int n, int h, int w, int prec, char* base, Plan& p) {
     if (L < kMaxDepth - 1) p.CAT[L] = take(2 * chans(L), p.g[L]);
   }
   p.BOT = take(chans(kMaxDepth - 1), p.g[kMaxDepth - 1]);
-  p.UPT = f32 ? Buf{nullptr, nullptr, 0, p.g[0]} : take(2 * chans(0), p.g[0]);
+  for (int L = 0; L < kMaxDepth - 1; ++L)
+    p.UPT[L] = f32 ? Buf{nullptr, nullptr, 0, p.g[L]} : take(2 * chans(L), p.g[L]);
   p.FLOWRAW = take(f32 ? 4 : 8, p.g[0]);
   p.bytes = off;
 }
@@ -263,7 +266,7 @@ int run_unet_h8(const Plan& p, const UNetSpec& u, const rrin_conv_weights* cw, c
   rrin_h8 x = hview(p.T[D - 1], 0, chans(D - 1));
   for (int L = D - 2; L >= 0; --L) {
     const int C = chans(L);
-    const rrin_h8 upin = hview(p.UPT, 0, 2 * C, p.g[L]);
+    const rrin_h8 upin = hview(p.UPT[L], 0, 2 * C);
     {
       ProfScope ps(g_prof, st, RRIN_KIND_LAYOUT, 0.0);
       RRIN_TRY(rrin_upsample2x_h8(&x, &upin, p.n, p.prec, st));

@@ -114,6 +114,8 @@ def test_h8_conv_pool(gpu, prec, n, cin, cout, h, w):
     ref = ref_conv(x, wt, b, 0.1)
     refp = F.avg_pool2d(ref, 2)
     for cfg in cfgs(prec, cout):
+        if _lib.lib().rrin_conv_h8_cfg_th(cfg) // 8 < 2 and cfg == 4:
+            continue  # WN == 1: no pool epilogue (rejected with RRIN_E_CONFIG, see test below)
         dst, pool = conv_h8(H8Tensor.from_nchw(x, prec), wt, b, cfg, prec, epi=_lib.EPI_LEAKY_POOL, dst_off=cout,
                             dst=H8Tensor(n, 2 * cout, h, w, gpu, prec))
         np.testing.assert_allclose(dst.to_nchw(cout, cout).cpu().double().numpy(), ref.numpy(), **TOL[prec])
@@ -146,3 +148,10 @@ def test_h8_upsample(gpu, prec, n, c, h, w):
     ref = F.interpolate(x.double().cpu(), scale_factor=2, mode="bilinear", align_corners=False)
     tol = 1e-6 if prec == X3 else 2e-3
     np.testing.assert_allclose(dst.to_nchw().cpu().double().numpy(), ref.numpy(), rtol=0, atol=tol)
+
+
+def test_h8_pool_rejected_for_single_row_waves(gpu):
+    x = torch.rand(1, 32, 16, 32, device=gpu)
+    wt, b = keyed_conv(32, 32)
+    with pytest.raises(_lib.RRINError, match="config"):
+        conv_h8(H8Tensor.from_nchw(x, X3), wt, b, 4, X3, epi=_lib.EPI_LEAKY_POOL)

@@ -22,6 +22,7 @@ STEPS=${STEPS:-tests,smoke,bench,prof}
 [[ $STEPS == *bsplit* ]] && run bench_split 600 python bench.py --steps 5 --warmup 2 --precision fp32_split16
 [[ $STEPS == *bf16* ]] && run bench_fp16 600 python bench.py --steps 5 --warmup 2 --precision fp16 --cpu-baseline off
 [[ $STEPS == *breakdown* ]] && run breakdown 300 python tools/conv_lab.py breakdown --out gpurun_out/breakdown.json
+[[ $STEPS == *probe* ]] && run probe 300 python tools/precision_probe.py
 [[ $STEPS == *tune* ]] && run tune 600 python tools/conv_lab.py tune --out gpurun_out/tune.json
 [[ $STEPS == *prof* ]] && run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --cpu-baseline off
 if [[ $STEPS == *pmc* ]]; then
