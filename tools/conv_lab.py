@@ -26,8 +26,9 @@ from rrin_amd.synthetic import keyed_state_dict, synthetic_batch  # noqa: E402
 UNETS = [("Flow", 6, 5), ("refine_flow", 10, 4), ("Mask", 16, 4), ("final", 9, 4)]
 
 
-def schedule(h, w):
-    """(unet, tag, cin, cout, level, src_mode, epi) in rrin_net_fwd launch order."""
+def schedule(h, w, h8=False):
+    """(unet, tag, cin, cout, level, src_mode, epi) in rrin_net_fwd launch order
+    (h8: the split/fp16 path launches an upsample pass before every up.1 conv)."""
     out = [("-", "pack", 0, 0, 0, -1, -1)]
     for name, cin0, D in UNETS:
         for L in range(D):
@@ -41,7 +42,9 @@ def schedule(h, w):
                 out.append((name, "mid", C_, C_, L, 0, 1))
         for L in range(D - 2, -1, -1):
             C_ = 32 << L
-            out.append((name, f"up{L}.up", 2 * C_, C_, L, 1, 0))
+            if h8:
+                out.append((name, f"up{L}.ups", 0, 0, L, -1, -1))
+            out.append((name, f"up{L}.up", 2 * C_, C_, L, 0 if h8 else 1, 0))
             out.append((name, f"up{L}.a", 2 * C_, C_, L, 0, 1))
             out.append((name, f"up{L}.b", C_, C_, L, 0, 1))
         out.append((name, "head", 32, 0, 0, -2, -2))
@@ -53,6 +56,7 @@ def breakdown(args):
     net = Net()
     net.load_state_dict(keyed_state_dict(net.state_dict()))
     net = net.to(dev).eval()
+    net.precision = args.precision
     eng = net.engine()
     lib = _lib.lib()
     i0, i1 = synthetic_batch(args.batch, args.height, args.width)
@@ -79,8 +83,7 @@ def breakdown(args):
         for i in range(cnt.value):
             tot.setdefault(i, []).append((kinds[i], ms[i], fl[i]))
     lib.rrin_prof_destroy(h)
-    sch = schedule(args.height, args.width)
-    cfgs = [None] + list(eng.cfgs)
+    sch = schedule(args.height, args.width, args.precision != "fp32")
     rows = []
     conv_i = 0
     for i, entry in enumerate(sch):
@@ -110,7 +113,58 @@ def breakdown(args):
         json.dump(rows, open(args.out, "w"), indent=1)
 
 
+def tune_h8(args):
+    from rrin_amd.pp import H8Tensor
+    from tests.test_gpu_h8 import pack_h8
+    dev = torch.device("cuda:0")
+    lib = _lib.lib()
+    prec = _lib.PRECISIONS[args.precision]
+    shapes = sorted({(e[2], e[3], e[4], e[5], e[6]) for e in schedule(args.height, args.width, True) if e[5] >= 0})
+    n = args.batch
+    results = []
+    for cin, cout, L, src, epi in shapes:
+        h, w = args.height >> L, args.width >> L
+        x = H8Tensor.from_nchw(torch.rand(n, cin, h, w, device=dev) * 2 - 1, prec)
+        dst = H8Tensor(n, cout, h, w, dev, prec)
+        pool = H8Tensor(n, cout, h // 2, w // 2, dev, prec) if epi == 2 else None
+        wt = torch.randn(cout, cin, 3, 3) / (3 * cin ** 0.5)
+        b = torch.zeros(cout)
+        best, line = None, []
+        for cfg in range(lib.rrin_conv_h8_cfg_count()):
+            if not lib.rrin_conv_h8_cfg_ok(cfg, prec) or lib.rrin_conv_h8_cfg_bm(cfg) > max(32, 2 * cout):
+                continue
+            whi, wlo, bp, inv = pack_h8(wt, b, cfg, prec, dev)
+            d = _lib.ConvH8Desc()
+            d.n, d.cin, d.cout, d.cfg, d.prec, d.epi_mode, d.slope, d.inv_wscale = n, cin, cout, cfg, prec, epi, 0.1, inv
+            d.src, d.dst = x.view(0, cin), dst.view(0, cout)
+            if pool is not None:
+                d.pool = pool.view(0, cout)
+            d.whi, d.wlo, d.bias = whi.data_ptr(), wlo.data_ptr(), bp.data_ptr()
+            st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+            if lib.rrin_conv3x3_h8_fwd(C.byref(d), st) != 0:
+                continue
+            ts = []
+            for _ in range(args.reps):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                _lib.check(lib.rrin_conv3x3_h8_fwd(C.byref(d), st))
+                e1.record()
+                e1.synchronize()
+                ts.append(e0.elapsed_time(e1))
+            ms = sorted(ts)[len(ts) // 2]
+            tf = 2 * 9 * cin * cout * h * w * n / (ms * 1e-3) / 1e12
+            line.append(f"cfg{cfg}:{ms:.3f}ms/{tf:.0f}TF")
+            results.append(dict(cin=cin, cout=cout, level=L, src=src, epi=epi, cfg=cfg, ms=ms, tflops=tf))
+            if best is None or ms < best[1]:
+                best = (cfg, ms, tf)
+        print(f"{cin:4d}->{cout:4d} L{L} epi{epi}: best cfg{best[0]} {best[2]:.0f} TF | " + " ".join(line), flush=True)
+    if args.out:
+        json.dump(results, open(args.out, "w"), indent=1)
+
+
 def tune(args):
+    if args.precision != "fp32":
+        return tune_h8(args)
     dev = torch.device("cuda:0")
     lib = _lib.lib()
     ncfg = lib.rrin_conv_cfg_count()
@@ -171,6 +225,7 @@ def main():
     ap.add_argument("--width", type=int, default=1280)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "fp32_split16", "fp16"])
     args = ap.parse_args()
     breakdown(args) if args.mode == "breakdown" else tune(args)
 

@@ -24,6 +24,9 @@ STEPS=${STEPS:-tests,smoke,bench,prof}
 [[ $STEPS == *breakdown* ]] && run breakdown 300 python tools/conv_lab.py breakdown --out gpurun_out/breakdown.json
 [[ $STEPS == *probe* ]] && run probe 300 python tools/precision_probe.py
 [[ $STEPS == *tune* ]] && run tune 600 python tools/conv_lab.py tune --out gpurun_out/tune.json
+[[ $STEPS == *tsplit* ]] && run tune_split 600 python tools/conv_lab.py tune --precision fp32_split16 --out gpurun_out/tune_split.json
+[[ $STEPS == *tfp16* ]] && run tune_fp16 600 python tools/conv_lab.py tune --precision fp16 --out gpurun_out/tune_fp16.json
+[[ $STEPS == *dsplit* ]] && run breakdown_split 300 python tools/conv_lab.py breakdown --precision fp32_split16 --out gpurun_out/breakdown_split.json
 [[ $STEPS == *prof* ]] && run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --cpu-baseline off
 if [[ $STEPS == *pmc* ]]; then
   run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 2 --warmup 1 --cpu-baseline off --no-prof
