@@ -88,7 +88,17 @@ __device__ inline uint4 mask_halves(uint4 v, int nvalid) {
   return v;
 }
 
-template <int NW, int WM, int WN, int PLANES, int EPI>
+// LDS-DMA: one 16-byte record per lane straight from global memory into the
+// lane-linear LDS image (global_load_lds_dwordx4; LDS address = wave-uniform
+// base + lane*16), no VGPRs and no LDS store pass.
+__device__ inline void dma16(const uint4* src, uint4* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+// DMA = true: stage with LDS-DMA (requires cin % 8 == 0: no partial channel
+// group to mask); false: register staging with masking (first convs, cin 6/9/10).
+template <int NW, int WM, int WN, int PLANES, int EPI, bool DMA>
 __global__ void __launch_bounds__(64 * NW) conv3x3_h8_kernel(ConvH8Args a) {
   using T = TileH8<NW, WM, WN, PLANES>;
   constexpr int NT = T::NT, BM = T::BM, TH = T::TH, ROWS = T::ROWS;
@@ -123,8 +133,40 @@ __global__ void __launch_bounds__(64 * NW) conv3x3_h8_kernel(ConvH8Args a) {
   const uint4* wsrc[2] = {a.w_hi + (int64_t)cob * a.nchunks * W_REC,
                           PLANES == 2 ? a.w_lo + (int64_t)cob * a.nchunks * W_REC : nullptr};
 
-  uint4 rin[PLANES][T::IN_IT];
-  uint4 rw[PLANES][T::W_IT];
+  uint4 rin[PLANES][DMA ? 1 : T::IN_IT];
+  uint4 rw[PLANES][DMA ? 1 : T::W_IT];
+  const int wave = tid >> 6;
+
+  // DMA staging of chunk c into buffer buf (input tile + weight slab, both planes)
+  auto issue = [&](int c, int buf) {
+#pragma unroll
+    for (int it = 0; it < T::IN_IT; ++it) {
+      const int idx = tid + NT * it;
+      if (idx < IN_REC) {
+        const int g = idx / (ROWS * H8_LC);
+        const int rem = idx - g * (ROWS * H8_LC);
+        const int r = rem / H8_LC;
+        const int col = rem - r * H8_LC;
+        const int gg = c * 2 + g;
+        // groups past cin read the zero top-padding row of group 0 instead
+        const int64_t off = gg * 8 < a.cin
+                                ? (int64_t)gg * a.src_gp + (int64_t)(y0 + r) * a.src_wp + x0 + (kH8PadLeft - 1) + col
+                                : (int64_t)(x0 + (kH8PadLeft - 1) + col);
+#pragma unroll
+        for (int p = 0; p < PLANES; ++p)
+          dma16(src[p] + off, s_in + (buf * PLANES + p) * IN_REC + NT * it + wave * 64);
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < T::W_IT; ++it) {
+      const int idx = tid + NT * it;
+      if (idx < W_REC) {
+#pragma unroll
+        for (int p = 0; p < PLANES; ++p)
+          dma16(wsrc[p] + (int64_t)c * W_REC + idx, s_w + (buf * PLANES + p) * W_REC + NT * it + wave * 64);
+      }
+    }
+  };
 
   auto load_in = [&](int c) {
 #pragma unroll
@@ -230,24 +272,38 @@ __global__ void __launch_bounds__(64 * NW) conv3x3_h8_kernel(ConvH8Args a) {
     }
   };
 
-  load_w(0);
-  load_in(0);
-  store_in(0);
-  store_w(0);
-  __syncthreads();
-  for (int c = 0; c < a.nchunks; ++c) {
-    const int buf = c & 1;
-    const bool more = (c + 1) < a.nchunks;
-    if (more) {
-      load_w(c + 1);
-      load_in(c + 1);
-    }
-    compute(buf);
-    if (more) {
-      store_in(buf ^ 1);
-      store_w(buf ^ 1);
-    }
+  if constexpr (DMA) {
+    issue(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    for (int c = 0; c < a.nchunks; ++c) {
+      const int buf = c & 1;
+      // buf^1 was last read in chunk c-1, before the barrier that ended it
+      if ((c + 1) < a.nchunks) issue(c + 1, buf ^ 1);
+      compute(buf);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  } else {
+    load_w(0);
+    load_in(0);
+    store_in(0);
+    store_w(0);
+    __syncthreads();
+    for (int c = 0; c < a.nchunks; ++c) {
+      const int buf = c & 1;
+      const bool more = (c + 1) < a.nchunks;
+      if (more) {
+        load_w(c + 1);
+        load_in(c + 1);
+      }
+      compute(buf);
+      if (more) {
+        store_in(buf ^ 1);
+        store_w(buf ^ 1);
+      }
+      __syncthreads();
+    }
   }
 
   // ---- epilogue: scale, bias, leaky, split, 8-B half-record stores (+ pool)
@@ -642,21 +698,28 @@ static const CfgH8 kCfgH8[] = {
 static constexpr int kNumCfgH8 = sizeof(kCfgH8) / sizeof(kCfgH8[0]);
 static constexpr size_t kMaxLds = 160 * 1024;
 
+template <int NW, int WM, int WN, int PLANES, int EPI, bool DMA>
+static int launch_h8_k(const ConvH8Args& args, int grid, hipStream_t st) {
+  using T = TileH8<NW, WM, WN, PLANES>;
+  auto k = conv3x3_h8_kernel<NW, WM, WN, PLANES, EPI, DMA>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)T::LDS);
+    if (e != hipSuccess) return (int)e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(k, dim3(grid), dim3(T::NT), T::LDS, st, args);
+  return hip_code(hipGetLastError());
+}
+
 template <int NW, int WM, int WN, int PLANES, int EPI>
 static int launch_h8_t(const ConvH8Args& args, int grid, hipStream_t st) {
   using T = TileH8<NW, WM, WN, PLANES>;
   if constexpr (T::LDS > kMaxLds) {
     return RRIN_E_CONFIG;
   } else {
-    auto k = conv3x3_h8_kernel<NW, WM, WN, PLANES, EPI>;
-    static bool attr_set = false;
-    if (!attr_set) {
-      hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)T::LDS);
-      if (e != hipSuccess) return (int)e;
-      attr_set = true;
-    }
-    hipLaunchKernelGGL(k, dim3(grid), dim3(T::NT), T::LDS, st, args);
-    return hip_code(hipGetLastError());
+    if (args.cin % 8 == 0) return launch_h8_k<NW, WM, WN, PLANES, EPI, true>(args, grid, st);
+    return launch_h8_k<NW, WM, WN, PLANES, EPI, false>(args, grid, st);
   }
 }
 
