@@ -14,7 +14,9 @@
 // K in chunks of 8 input channels x 9 taps.  Per chunk it stages into LDS
 //   input  [8 ch][TH+2 rows][40 cols]  (cols x0-4 .. x0+35, 16-B vector loads)
 //   weight [8 ch][9 taps][BM]          (pre-packed, one contiguous slab)
-// double-buffered with register prefetch of chunk c+1 during the MFMAs of c.
+// double-buffered: chunk c+1 is staged by LDS-DMA (global_load_lds_dwordx4)
+// while the MFMAs run on chunk c (UPSAMPLE2X: register prefetch of the low-res
+// tile + expansion in LDS).
 // One 32x32x2 MFMA covers a channel PAIR at one tap: lanes 0-31 carry channel
 // 2p, lanes 32-63 channel 2p+1, so every operand read is one conflict-free
 // ds_read_b32 with a compile-time immediate offset.
@@ -107,8 +109,38 @@ __global__ void __launch_bounds__(256) conv3x3_mfma_kernel(ConvArgs a) {
   const float* src_img = a.src + img * a.src_img;
   const float* wsrc = a.wpack + (int64_t)cob * a.nchunks * W_F;
 
-  float4 rin[T::IN_IT];
-  float4 rw[T::W_IT];
+  float4 rw[SRC == RRIN_SRC_DIRECT ? 1 : T::W_IT];
+
+  // DIRECT: LDS-DMA staging (global_load_lds_dwordx4, lane-linear LDS image,
+  // no staging VGPRs, no LDS store pass).  Channels past cin source the zero
+  // top-padding row.
+  auto dma16 = [&](const float* g, float* lds_wave_base) {
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                     (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+  };
+  auto issue = [&](int c, int buf) {
+#pragma unroll
+    for (int it = 0; it < T::IN_IT; ++it) {
+      const int idx = tid + 256 * it;
+      if (idx < T::IN_V4) {
+        const int ci = idx / (ROWS * 10);
+        const int rem = idx - ci * (ROWS * 10);
+        const int r = rem / 10;
+        const int q = rem - r * 10;
+        const int ch = c * CK + ci;
+        const int64_t off = ch < a.cin ? (int64_t)ch * a.src_plane + (int64_t)(y0 + r) * a.src_wp + x0 +
+                                             (kPadLeft - 4) + 4 * q
+                                       : (int64_t)(x0 + (kPadLeft - 4) + 4 * q);
+        dma16(src_img + off, s_in + buf * IN_F + 4 * (256 * it + wave * 64));
+      }
+    }
+    const float* g = wsrc + (int64_t)c * W_F;
+#pragma unroll
+    for (int it = 0; it < T::W_IT; ++it) {
+      const int idx = tid + 256 * it;
+      if (idx < T::W_V4) dma16(g + 4 * idx, s_w + buf * W_F + 4 * (256 * it + wave * 64));
+    }
+  };
 
   auto load_w = [&](int c) {
     const float4* g = reinterpret_cast<const float4*>(wsrc + (int64_t)c * W_F);
@@ -124,33 +156,6 @@ __global__ void __launch_bounds__(256) conv3x3_mfma_kernel(ConvArgs a) {
     for (int it = 0; it < T::W_IT; ++it) {
       const int idx = tid + 256 * it;
       if (idx < T::W_V4) s[idx] = rw[it];
-    }
-  };
-  // DIRECT: rectangular copy of padded rows y0..y0+ROWS-1, cols x0..x0+39.
-  auto load_in = [&](int c) {
-#pragma unroll
-    for (int it = 0; it < T::IN_IT; ++it) {
-      const int idx = tid + 256 * it;
-      if (idx < T::IN_V4) {
-        const int ci = idx / (ROWS * 10);
-        const int rem = idx - ci * (ROWS * 10);
-        const int r = rem / 10;
-        const int q = rem - r * 10;
-        const int ch = c * CK + ci;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (ch < a.cin)
-          v = *reinterpret_cast<const float4*>(src_img + (int64_t)ch * a.src_plane +
-                                               (int64_t)(y0 + r) * a.src_wp + x0 + (kPadLeft - 4) + 4 * q);
-        rin[it] = v;
-      }
-    }
-  };
-  auto store_in = [&](int buf) {
-    float4* s = reinterpret_cast<float4*>(s_in + buf * IN_F);
-#pragma unroll
-    for (int it = 0; it < T::IN_IT; ++it) {
-      const int idx = tid + 256 * it;
-      if (idx < T::IN_V4) s[idx] = rin[it];
     }
   };
   // UPSAMPLE2X (unet.py:77, bilinear x2, align_corners=False).  The low-res
@@ -251,38 +256,39 @@ __global__ void __launch_bounds__(256) conv3x3_mfma_kernel(ConvArgs a) {
     }
   };
 
-  // ---- prologue: chunk 0 into buffer 0
-  load_w(0);
   if constexpr (SRC == RRIN_SRC_DIRECT) {
-    load_in(0);
-    store_in(0);
+    // ---- DMA pipeline: chunk c+1 lands in buf^1 while the MFMAs run on c
+    issue(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int c = 0; c < a.nchunks; ++c) {
+      const int buf = c & 1;
+      if ((c + 1) < a.nchunks) issue(c + 1, buf ^ 1);  // buf^1 last read before the previous barrier
+      compute(buf);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
   } else {
+    // ---- UPSAMPLE2X: register prefetch of weights + low-res tile, LDS expansion
+    load_w(0);
     load_lr(0);
     expand_up(0);
-  }
-  store_w(0);
-  __syncthreads();
-
-  // ---- main K loop: prefetch c+1 into registers while the MFMAs run on c
-  for (int c = 0; c < a.nchunks; ++c) {
-    const int buf = c & 1;
-    const bool more = (c + 1) < a.nchunks;
-    if (more) {
-      load_w(c + 1);
-      if constexpr (SRC == RRIN_SRC_DIRECT)
-        load_in(c + 1);
-      else
-        load_lr(c + 1);
-    }
-    compute(buf);
-    if (more) {
-      if constexpr (SRC == RRIN_SRC_DIRECT)
-        store_in(buf ^ 1);
-      else
-        expand_up(buf ^ 1);  // contains one extra barrier (s_lr hand-off)
-      store_w(buf ^ 1);
-    }
+    store_w(0);
     __syncthreads();
+    for (int c = 0; c < a.nchunks; ++c) {
+      const int buf = c & 1;
+      const bool more = (c + 1) < a.nchunks;
+      if (more) {
+        load_w(c + 1);
+        load_lr(c + 1);
+      }
+      compute(buf);
+      if (more) {
+        expand_up(buf ^ 1);  // contains one extra barrier (s_lr hand-off)
+        store_w(buf ^ 1);
+      }
+      __syncthreads();
+    }
   }
 
   // ---- epilogue: bias, leaky, store (+ 2x2 average pool)
