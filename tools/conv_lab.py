@@ -217,9 +217,43 @@ def tune(args):
         json.dump(results, open(args.out, "w"), indent=1)
 
 
+def single(args):
+    """Run one conv shape/config --reps times (for rocprofv3 --pmc)."""
+    from rrin_amd.pp import H8Tensor
+    from tests.test_gpu_h8 import pack_h8
+    dev = torch.device("cuda:0")
+    lib = _lib.lib()
+    prec = _lib.PRECISIONS[args.precision]
+    cin, cout, L, epi, cfg = args.shape
+    n, h, w = args.batch, args.height >> L, args.width >> L
+    x = H8Tensor.from_nchw(torch.rand(n, cin, h, w, device=dev) * 2 - 1, prec)
+    dst = H8Tensor(n, cout, h, w, dev, prec)
+    pool = H8Tensor(n, cout, h // 2, w // 2, dev, prec) if epi == 2 else None
+    wt = torch.randn(cout, cin, 3, 3) / (3 * cin ** 0.5)
+    whi, wlo, bp, inv = pack_h8(wt, torch.zeros(cout), cfg, prec, dev)
+    d = _lib.ConvH8Desc()
+    d.n, d.cin, d.cout, d.cfg, d.prec, d.epi_mode, d.slope, d.inv_wscale = n, cin, cout, cfg, prec, epi, 0.1, inv
+    d.src, d.dst = x.view(0, cin), dst.view(0, cout)
+    if pool is not None:
+        d.pool = pool.view(0, cout)
+    d.whi, d.wlo, d.bias = whi.data_ptr(), wlo.data_ptr(), bp.data_ptr()
+    st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(args.reps):
+        _lib.check(lib.rrin_conv3x3_h8_fwd(C.byref(d), st))
+    e1.record()
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / args.reps
+    print(f"{cin}->{cout} L{L} epi{epi} cfg{cfg} {args.precision}: {ms:.4f} ms "
+          f"{2 * 9 * cin * cout * h * w * n / (ms * 1e-3) / 1e12:.1f} TF")
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("mode", choices=["breakdown", "tune"])
+    ap.add_argument("mode", choices=["breakdown", "tune", "single"])
+    ap.add_argument("--shape", type=int, nargs=5, default=[512, 256, 3, 1, 0],
+                    help="single: cin cout level epi cfg")
     ap.add_argument("--batch", type=int, default=4)
     ap.add_argument("--height", type=int, default=720)
     ap.add_argument("--width", type=int, default=1280)
@@ -227,7 +261,7 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--precision", default="fp32", choices=["fp32", "fp32_split16", "fp16"])
     args = ap.parse_args()
-    breakdown(args) if args.mode == "breakdown" else tune(args)
+    {"breakdown": breakdown, "tune": tune, "single": single}[args.mode](args)
 
 
 if __name__ == "__main__":

@@ -28,6 +28,12 @@ STEPS=${STEPS:-tests,smoke,bench,prof}
 [[ $STEPS == *tfp16* ]] && run tune_fp16 600 python tools/conv_lab.py tune --precision fp16 --out gpurun_out/tune_fp16.json
 [[ $STEPS == *dsplit* ]] && run breakdown_split 300 python tools/conv_lab.py breakdown --precision fp32_split16 --out gpurun_out/breakdown_split.json
 [[ $STEPS == *prof* ]] && run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --cpu-baseline off
+if [[ $STEPS == *sqc* ]]; then
+  for shp in "512 256 3 1 0" "32 32 0 1 1" "128 128 2 1 0"; do
+    tag=$(echo $shp | tr ' ' '_')
+    run sq_$tag 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/sq_$tag -o run -- python3 tools/conv_lab.py single --precision ${SQPREC:-fp32_split16} --reps 20 --shape $shp
+  done
+fi
 if [[ $STEPS == *pmc* ]]; then
   run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 2 --warmup 1 --cpu-baseline off --no-prof
   run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --steps 2 --warmup 1 --cpu-baseline off --no-prof
