@@ -54,16 +54,18 @@ def parse():
     ap.add_argument("--height", type=int, default=720)
     ap.add_argument("--width", type=int, default=1280)
     ap.add_argument("--t", type=float, default=0.5)
-    ap.add_argument("--precision", default="fp32", choices=["fp32", "fp32_split16", "fp16"],
+    ap.add_argument("--precision", default="fp32_split16", choices=["fp32", "fp32_split16", "fp16"],
                     help="fp32: exact fp32 MFMA; fp32_split16: fp32 values as fp16 hi+lo, 3 fp16 "
                          "products per fp32 product, fp32 accumulate; fp16: fp16 storage/products")
     ap.add_argument("--no-prof", action="store_true", help="skip the per-launch event profiler")
+    ap.add_argument("--no-alt", action="store_true",
+                    help="N=1: skip the secondary measurement of the exact-fp32 MFMA path")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-pairs", type=int, default=2, help="pairs timed on the CPU baseline")
     return ap.parse_args()
 
 
-def cpu_baseline(sd, h, w, pairs, t, gpu_out0):
+def cpu_baseline(sd, h, w, pairs, t, gpu_out0, alt_out0=None):
     """Time the CPU oracle on pair 0 and compare its output with the GPU's."""
     from oracle.ref_net import net_forward  # checker / baseline only
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
@@ -75,13 +77,40 @@ def cpu_baseline(sd, h, w, pairs, t, gpu_out0):
         for _ in range(pairs):
             ref = net_forward(sd, i0, i1, t)
         dt = time.perf_counter() - t0
-    d = (gpu_out0.double() - ref.double())
-    mse = float((d * d).mean())
-    parity = {"pair": 0, "max_abs": float(d.abs().max()),
-              "psnr_db": (10 * math.log10(1.0 / mse)) if mse > 0 else float("inf"), "gate_max_abs": 1e-3}
+    def compare(o):
+        d = (o.double() - ref.double())
+        mse = float((d * d).mean())
+        return {"pair": 0, "max_abs": float(d.abs().max()),
+                "psnr_db": (10 * math.log10(1.0 / mse)) if mse > 0 else float("inf"), "gate_max_abs": 1e-3}
+    parity = compare(gpu_out0)
+    if alt_out0 is not None:
+        parity["alt"] = compare(alt_out0)
     return ({"value": pairs / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
              "sample": f"{pairs} x Net.forward {w}x{h} N=1 fp32 on PyTorch-CPU (oracle/ref_net.py), "
                        f"{dt:.1f} s"}, parity)
+
+
+def time_steps(eng, i0, i1, t, steps, dev, prof=None):
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    out = None
+    with torch.no_grad():
+        for _ in range(steps):
+            out = eng.forward(i0, i1, t, prof=prof)
+    torch.cuda.synchronize(dev)
+    return time.perf_counter() - t0, out
+
+
+def read_prof(lib, prof, cap):
+    kinds = (C.c_int32 * cap)()
+    ms = (C.c_float * cap)()
+    fl = (C.c_double * cap)()
+    cnt = C.c_int32()
+    _lib.check(lib.rrin_prof_read(prof, kinds, ms, fl, cap, C.byref(cnt)), "rrin_prof_read")
+    n = cnt.value
+    conv = [(ms[i], fl[i]) for i in range(n) if kinds[i] == 0]
+    return (sum(m for m, _ in conv), sum(f for _, f in conv), len(conv),
+            sum(ms[i] for i in range(n) if kinds[i] == 1), sum(ms[i] for i in range(n) if kinds[i] == 2))
 
 
 def main():
@@ -200,9 +229,33 @@ def main():
         "cpu_baseline": None,
         "parity": None,
     }
+    alt_out = None
+    if world == 1 and not args.no_alt and args.precision != "fp32":
+        # the exact-fp32 MFMA path on the same inputs, for comparison in the same line
+        net.precision = "fp32"
+        eng32 = net.engine()
+        with torch.no_grad():
+            for _ in range(max(1, args.warmup)):
+                eng32.forward(i0, i1, args.t)
+        cap32 = 100 * args.steps
+        h32 = C.c_void_p()
+        _lib.check(lib.rrin_prof_create(cap32, C.byref(h32)), "rrin_prof_create")
+        el32, o32 = time_steps(eng32, i0, i1, args.t, args.steps, dev, h32.value)
+        cms, cfl, _, _, _ = read_prof(lib, h32.value, cap32)
+        lib.rrin_prof_destroy(h32.value)
+        alt_out = o32[0:1].cpu()
+        res["fp32_exact"] = {"value": round(B * args.steps / el32, 3), "ms_per_step": round(1e3 * el32 / args.steps, 3),
+                             "conv_tflops": round(cfl / (cms * 1e-3) / 1e12, 2),
+                             "conv_frac_of_fp32_peak": round(cfl / (cms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS, 4),
+                             "kernel": "conv3x3_mfma_kernel (v_mfma_f32_32x32x2_f32)"}
+        del eng32
+        net.precision = args.precision
     if rank == 0 and world == 1 and args.cpu_baseline == "auto":
         res["cpu_baseline"], res["parity"] = cpu_baseline({k: v.detach().cpu() for k, v in sd.items()}, H, W,
-                                                          args.cpu_pairs, args.t, last[0][0:1].cpu())
+                                                          args.cpu_pairs, args.t, last[0][0:1].cpu(),
+                                                          alt_out)
+        if "fp32_exact" in res:
+            res["fp32_exact"]["parity"] = res["parity"].pop("alt")
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:
