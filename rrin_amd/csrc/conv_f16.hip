@@ -682,7 +682,9 @@ static float h2f(uint16_t h) {
   X(2, 4, 2, 2)         \
   X(3, 4, 1, 4)         \
   X(4, 4, 2, 1)         \
-  X(5, 8, 4, 2)
+  X(5, 8, 4, 2)         \
+  X(6, 4, 1, 2)         \
+  X(7, 2, 1, 4)
 
 struct CfgH8 {
   int bm, th;
