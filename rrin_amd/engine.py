@@ -48,10 +48,13 @@ def choose_cfg(cin: int, cout: int, level: int) -> int:
 
 
 def choose_cfg_h8(cin: int, cout: int, prec: int) -> int:
-    """Tile config of the split-fp16 / fp16 conv (conv_f16.hip table)."""
-    if cout <= 32:
-        return 1        # BM 32 x TH 16, 512 threads
-    return 0            # BM 64 x TH 16, 512 threads
+    """Tile config of the split-fp16 / fp16 conv (conv_f16.hip table), from the
+    per-shape sweeps of tools/conv_lab.py tune (profiles/r01_v6_tune_*.txt)."""
+    if cin % 8:
+        return 1        # register-staged first convs (cin 6/9/10): BM 32 x TH 16, 8 waves
+    if cout == 32 or cout >= 512 or (cin == 32 and cout == 64):
+        return 6        # BM 32 x TH 8, 4 waves, 2 blocks/CU: small-K full-res and 80x45 layers
+    return 0            # BM 64 x TH 16, 8 waves
 
 
 def t_coefficients(t, n: int) -> torch.Tensor:
