@@ -52,6 +52,12 @@ def choose_cfg_h8(cin: int, cout: int, prec: int) -> int:
     per-shape sweeps of tools/conv_lab.py tune (profiles/r01_v6_tune_*.txt)."""
     if cin % 8:
         return 1        # register-staged first convs (cin 6/9/10): BM 32 x TH 16, 8 waves
+    if prec == _lib.PREC_F16:  # fp16 (one MFMA per product): LDS allows the BM 128 tile
+        if cout == 32 or cout >= 512:
+            return 1
+        if cin >= 256 and cout >= 128:
+            return 5    # BM 128 x TH 16, 8 waves
+        return 0
     if cout == 32 or cout >= 512 or (cin == 32 and cout == 64):
         return 6        # BM 32 x TH 8, 4 waves, 2 blocks/CU: small-K full-res and 80x45 layers
     return 0            # BM 64 x TH 16, 8 waves
