@@ -1,0 +1,244 @@
+"""Frame interpolation of an image folder / video — the reference's convert entry
+point (`/root/reference/convert.py:22-169`) on the HIP Net.
+
+Kept from the reference (so outputs and resume behave the same):
+* t schedule ``t = i / (sf + 1)`` for i = 1..sf (`convert.py:127-130`);
+* output naming ``{n:09d}{ext}``: first frame copied as 1, then per pair the sf
+  interpolated frames and the copied second frame (`convert.py:118-144`);
+* resume: ``resume_index = (len(dest) - 1) // (sf + 1)`` when more than 5
+  outputs exist (`convert.py:50-56`), restart at pair ``resume_index - 1`` with
+  ``img_count = resume_index + resume_index*sf - sf`` (`convert.py:95,118`);
+* frames: RGB, /255 (`ToTensor`), edge-padded on top to a multiple of 16
+  (`dataloader.py:91-108`); outputs cropped back and quantised with
+  ``mul(255).byte()`` truncation as ``to_pil_image`` does (`utils.py:51-58`).
+
+Different (documented in DESIGN.md):
+* frames are read in sorted order (the reference uses raw ``os.listdir`` order);
+* a width that is not a multiple of 16 is edge-padded on the right (the
+  reference pads the bottom by the width deficit and then fails in the U-Net);
+* paths use ``os.path.join`` (the reference hard-codes Windows ``\\\\``);
+* the pipeline is batched: ``batch`` pairs per call, the t-independent Flow
+  U-Net once per pair for all sf values of t (``Net.interpolate``), frames
+  decoded by a reader thread, outputs copied to pinned host memory
+  asynchronously and written by a thread pool (the reference decodes on the
+  main thread, recomputes Flow per t, syncs per frame and polls its writer
+  queue every 0.1 s: `convert.py:97,130,133`, `utils.py:61-62`).
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+import threading
+import time
+from concurrent.futures import ThreadPoolExecutor
+from queue import Queue
+
+import numpy as np
+import torch
+
+IMG_EXT = (".png", ".jpg", ".jpeg", ".bmp", ".tif", ".tiff", ".webp")
+
+
+def list_frames(folder):
+    return sorted(f for f in os.listdir(folder) if f.lower().endswith(IMG_EXT))
+
+
+def pad_amounts(width, height):
+    """(top_pad, right_pad) to the next multiple of 16 (dataloader.py:91-101)."""
+    right = (-width) % 16
+    top = (-height) % 16
+    return top, right
+
+
+def load_frame(path):
+    """PIL RGB -> float32 [3,H',W'] in [0,1], edge-padded (top / right) to /16."""
+    from PIL import Image
+    with Image.open(path) as im:
+        arr = np.asarray(im.convert("RGB"), dtype=np.uint8)
+    h, w = arr.shape[:2]
+    top, right = pad_amounts(w, h)
+    if top or right:
+        arr = np.pad(arr, ((top, 0), (0, right), (0, 0)), mode="edge")
+    t = torch.from_numpy(arr.copy()).permute(2, 0, 1).float().div_(255.0)
+    return t, {"width": w, "height": h, "top": top, "filetype": os.path.splitext(path)[1], "path": path}
+
+
+def to_uint8_image(t: torch.Tensor, meta) -> np.ndarray:
+    """[3,H',W'] float -> cropped HxWx3 uint8 with to_pil_image's mul(255).byte() truncation."""
+    a = t.mul(255).to(torch.uint8)  # truncation toward zero, as torchvision's to_pil_image
+    a = a[:, meta["top"]:meta["top"] + meta["height"], :meta["width"]]
+    return a.permute(1, 2, 0).contiguous().numpy()
+
+
+def save_image(arr, path):
+    from PIL import Image
+    Image.fromarray(arr).save(path)
+
+
+def resume_state(dest, sf):
+    """(resume_index, img_count) of convert.py:50-56,118."""
+    resume_index = 1
+    if os.path.exists(dest) and len(os.listdir(dest)) > 5:
+        resume_index = (len(os.listdir(dest)) - 1) // (sf + 1)
+    return resume_index, resume_index + resume_index * sf - sf
+
+
+def interpolate_folder(model, src, dest, sf, batch=4, resume=False, device=None, writers=4, log=print):
+    """Interpolate every consecutive pair of frames in ``src`` into ``dest``.
+
+    ``model`` is an ``rrin_amd.Net`` (anything with ``interpolate(i0, i1, ts)``
+    returning a list of ``[N,3,H,W]`` tensors works).  Returns frames written."""
+    frames = list_frames(src)
+    if len(frames) < 2:
+        raise ValueError(f"need at least two frames in {src}")
+    os.makedirs(dest, exist_ok=True)
+    resume_index, img_count = resume_state(dest, sf) if resume else (1, 1)
+    first_pair = resume_index - 1
+    ts = [i / (sf + 1) for i in range(1, sf + 1)]
+    pool = ThreadPoolExecutor(max_workers=writers)
+    futures = []
+    written = [0]
+
+    def put(fn, *a):
+        futures.append(pool.submit(fn, *a))
+        written[0] += 1
+
+    # reader thread: decodes frames ahead of the GPU (bounded queue)
+    q: Queue = Queue(maxsize=2 * batch + 2)
+
+    def reader():
+        for k in range(first_pair, len(frames)):
+            q.put((k, *load_frame(os.path.join(src, frames[k]))))
+        q.put(None)
+
+    threading.Thread(target=reader, daemon=True).start()
+    if img_count == 1:
+        put(shutil.copy, os.path.join(src, frames[first_pair]),
+            os.path.join(dest, f"{img_count:09d}{os.path.splitext(frames[first_pair])[1]}"))
+    prev = q.get()
+    done = False
+    t0 = time.time()
+    pending = []  # (host tensors [n,3,H,W] per t, metas of the pairs, img_count of the pair) awaiting D2H
+    while not done:
+        group = [prev]
+        while len(group) < batch + 1:
+            item = q.get()
+            if item is None:
+                done = True
+                break
+            group.append(item)
+        if len(group) < 2:
+            break
+        prev = group[-1]
+        i0 = torch.stack([g[1] for g in group[:-1]])
+        i1 = torch.stack([g[1] for g in group[1:]])
+        if device is not None:
+            i0 = i0.pin_memory().to(device, non_blocking=True)
+            i1 = i1.pin_memory().to(device, non_blocking=True)
+        with torch.no_grad():
+            outs = model.interpolate(i0, i1, ts) if hasattr(model, "interpolate") else [model(i0, i1, t) for t in ts]
+        host = []
+        for o in outs:
+            h = torch.empty(o.shape, dtype=o.dtype, pin_memory=device is not None)
+            h.copy_(o, non_blocking=device is not None)
+            host.append(h)
+        ev = None
+        if device is not None:
+            ev = torch.cuda.Event()
+            ev.record()
+        pending.append((ev, host, [g[2] for g in group[:-1]], [g[2] for g in group[1:]], img_count))
+        img_count += (sf + 1) * (len(group) - 1)
+        # retire the previous batch while this one computes
+        while len(pending) > 1:
+            _retire(pending.pop(0), sf, dest, put)
+    while pending:
+        _retire(pending.pop(0), sf, dest, put)
+    for f in futures:
+        f.result()
+    pool.shutdown(wait=True)
+    log(f"interpolated {len(frames) - first_pair - 1} pairs x {sf} frames in {time.time() - t0:.2f} s")
+    return written[0]
+
+
+def _retire(item, sf, dest, put):
+    ev, host, metas0, metas1, count = item
+    if ev is not None:
+        ev.synchronize()
+    for p, (m0, m1) in enumerate(zip(metas0, metas1)):
+        base = count + p * (sf + 1)
+        for i in range(sf):
+            put(lambda t, m, path: save_image(to_uint8_image(t, m), path), host[i][p], m0,
+                os.path.join(dest, f"{base + i + 1:09d}{m0['filetype']}"))
+        put(shutil.copy, m1["path"], os.path.join(dest, f"{base + sf + 1:09d}{m1['filetype']}"))
+
+
+def find_checkpoint(model_name, models_dir="models"):
+    """Last checkpoint whose name starts with model_name (convert.py:100-108);
+    sorted order, so Model0150.pth wins over Model0001.pth."""
+    if not os.path.isdir(models_dir):
+        raise TypeError(f"No model found with the name: {model_name}")
+    names = [n for n in sorted(os.listdir(models_dir)) if n.lower().startswith(model_name.lower())]
+    if not names:
+        raise TypeError(f"No model found with the name: {model_name}")
+    return os.path.join(models_dir, names[-1])
+
+
+def load_net(model_name, device, precision="fp32_split16", models_dir="models"):
+    """Net with the checkpoint's {'model','optim','epoch'} state (train.py:158-161),
+    loaded with torch.load(weights_only=True) — nothing in the file is executed."""
+    from .model import Net
+    net = Net()
+    path = find_checkpoint(model_name, models_dir)
+    state = torch.load(path, map_location="cpu", weights_only=True)
+    net.load_state_dict(state["model"] if "model" in state else state, strict=True)
+    print(f"Using model {path}.")
+    net.precision = precision
+    return net.to(device).eval()
+
+
+def _ffmpeg(cmd):
+    if shutil.which("ffmpeg") is None:
+        raise RuntimeError("ffmpeg is not installed: use --image_folder (video I/O needs ffmpeg, "
+                           "as in the reference convert.py:78,153-160)")
+    return subprocess.call(cmd)
+
+
+def convert(args):
+    """CLI entry (same flags as the reference __main__.py:47-63)."""
+    if args.input_video is not None:
+        temp = "temp_" + os.path.basename(args.input_video)
+        if args.resume and not os.path.exists(temp):
+            raise Exception("Did not find temp folder to resume!")
+    elif args.image_folder is not None:
+        temp = "temp"
+    else:
+        raise Exception("Missing arguments! Video or folder needs to be specified")
+    inp, dest = os.path.join(temp, "input"), os.path.join(temp, "output")
+    if not args.resume:
+        if os.path.exists(dest) and os.listdir(dest):
+            raise Exception("Folder is already in use! Did you intend to resume the progress? Use the --resume flag")
+        if args.input_video is not None:
+            shutil.rmtree(temp, ignore_errors=True)
+            os.makedirs(inp)
+            if _ffmpeg(["ffmpeg", "-i", args.input_video, "-vsync", "0", os.path.join(inp, "%9d.png")]):
+                print("Failed to convert video to images.")
+                sys.exit(1)
+    src = inp if args.input_video is not None else args.image_folder
+    if args.no_cuda or not torch.cuda.is_available():
+        raise RuntimeError("rrin_amd runs on ROCm GPUs only (the reference also moves the model to .cuda() "
+                           "unconditionally, convert.py:110)")
+    dev = torch.device("cuda", torch.cuda.current_device())
+    net = load_net(args.model_name, dev, getattr(args, "precision", "fp32_split16"))
+    t = time.time()
+    interpolate_folder(net, src, dest, args.sf, batch=getattr(args, "batch", 4), resume=args.resume, device=dev)
+    print("end=", time.time() - t)
+    if args.input_video is not None and args.output_video:
+        if _ffmpeg(["ffmpeg", "-r", str(args.fps), "-y", "-i", os.path.join(dest, "%9d.png"), "-c:v", "libvpx-vp9",
+                    "-crf", "30", "-b:v", "20M", "-pix_fmt", "yuv420p", args.output_video]):
+            print("Failed to convert interpolated images to video.")
+            sys.exit(1)
+    if args.rm:
+        shutil.rmtree(temp, ignore_errors=True)
+    print("Finished conversion")
