@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define RRIN_ABI_VERSION 2
+#define RRIN_ABI_VERSION 3
 
 #define RRIN_OK 0
 #define RRIN_E_SHAPE (-1)     /* H or W not a multiple of 16, or N < 1          */
@@ -153,6 +153,10 @@ typedef struct rrin_conv_h8_desc {
   int32_t epi_mode;            /* rrin_epi_mode */
   float slope;
   float inv_wscale;            /* from rrin_pack_conv3x3_h8: weights were scaled by 1/inv_wscale */
+  int32_t tail_finite;         /* 1: the channels [cin, 8*ceil(cin/8)) of src are finite (they meet
+                                  zero weights), so the LDS-DMA kernel may stage whole records;
+                                  0: cin % 8 != 0 uses the masking register-staged kernel */
+  int32_t pad_;
   rrin_h8 src, dst, pool;      /* pool: EPI_LEAKY_POOL only */
   const void* whi;             /* packed halves (rrin_pack_conv3x3_h8) */
   const void* wlo;             /* NULL for F16 */
@@ -175,6 +179,9 @@ int rrin_pack_conv3x3_h8(const float* w, const float* b, int32_t cout, int32_t c
 
 /* nn.Upsample(bilinear, x2) (unet.py:77) of an H8 view into another H8 view. */
 int rrin_upsample2x_h8(const rrin_h8* src, const rrin_h8* dst, int32_t n, int32_t prec, void* stream);
+/* x = cat(x0, x1) (model.py:33) into the 16-channel H8 Net buffer: channels
+ * 0-5 from the two NCHW frames, channels 6-15 zeroed (whole-record stores). */
+int rrin_pack_g16_h8(const float* i0, const float* i1, int32_t n, const rrin_h8* g16, int32_t prec, void* stream);
 /* NCHW fp32 <-> H8 view (c channels starting at channel ch_off of the view). */
 int rrin_nchw_to_h8(const float* src, int32_t n, int32_t c, int32_t ch_off, const rrin_h8* dst,
                     int32_t prec, void* stream);

@@ -9,7 +9,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "librrin_hip.so")
 
 # enums (rrin_hip.h)
@@ -55,7 +55,7 @@ class H8(C.Structure):
 class ConvH8Desc(C.Structure):
     _fields_ = [("n", C.c_int32), ("cin", C.c_int32), ("cout", C.c_int32), ("cfg", C.c_int32),
                 ("prec", C.c_int32), ("epi_mode", C.c_int32), ("slope", C.c_float), ("inv_wscale", C.c_float),
-                ("src", H8), ("dst", H8), ("pool", H8), ("whi", C.c_void_p), ("wlo", C.c_void_p),
+                ("tail_finite", C.c_int32), ("pad_", C.c_int32), ("src", H8), ("dst", H8), ("pool", H8), ("whi", C.c_void_p), ("wlo", C.c_void_p),
                 ("bias", C.c_void_p)]
 
 
@@ -105,6 +105,7 @@ SIGNATURES = {
     "rrin_pack_conv3x3_h8": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p,
                                        C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(C.c_float)]),
     "rrin_upsample2x_h8": (C.c_int, [C.POINTER(H8), C.POINTER(H8), C.c_int32, C.c_int32, C.c_void_p]),
+    "rrin_pack_g16_h8": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(H8), C.c_int32, C.c_void_p]),
     "rrin_nchw_to_h8": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.POINTER(H8), C.c_int32,
                                   C.c_void_p]),
     "rrin_h8_to_nchw": (C.c_int, [C.POINTER(H8), C.c_int32, C.c_int32, C.c_int32, C.c_void_p, C.c_int32,

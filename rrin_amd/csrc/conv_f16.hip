@@ -59,6 +59,7 @@ struct ConvH8Args {
   const float* bias;
   float inv_wscale, slope;
   int h, w, co_blocks, tiles_x, tiles_y, n;
+  int tail_finite;
 };
 
 template <int NW, int WM, int WN, int PLANES>
@@ -450,6 +451,36 @@ __global__ void nchw_to_h8_kernel(const float* __restrict__ src, _Float16* hi, _
   if (lo) lo[k] = lo_of(v, vh);
 }
 
+template <int PLANES>
+__global__ void pack_g16_h8_kernel(const float* __restrict__ i0, const float* __restrict__ i1, uint4* ghi,
+                                   uint4* glo, int64_t img_stride, int64_t gp, int wp, int h, int w,
+                                   int64_t total) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int x = (int)(i % w);
+  const int64_t t = i / w;
+  const int y = (int)(t % h);
+  const int img = (int)(t / h);
+  const int64_t hw = (int64_t)h * w;
+  const int64_t px = (int64_t)img * 3 * hw + (int64_t)y * w + x;
+  half8 hi = {}, lo = {};
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const float a = i0[px + c * hw], b = i1[px + c * hw];
+    hi[c] = (_Float16)a;
+    hi[3 + c] = (_Float16)b;
+    lo[c] = lo_of(a, hi[c]);
+    lo[3 + c] = lo_of(b, hi[3 + c]);
+  }
+  const int64_t rec = (int64_t)img * img_stride + (int64_t)(y + 1) * wp + x + kH8PadLeft;
+  ghi[rec] = __builtin_bit_cast(uint4, hi);
+  ghi[rec + gp] = make_uint4(0u, 0u, 0u, 0u);
+  if constexpr (PLANES == 2) {
+    glo[rec] = __builtin_bit_cast(uint4, lo);
+    glo[rec + gp] = make_uint4(0u, 0u, 0u, 0u);
+  }
+}
+
 __global__ void h8_to_nchw_kernel(const _Float16* __restrict__ hi, const _Float16* __restrict__ lo, int64_t img_stride,
                                   int64_t gp, int wp, int ch_off, float* dst, int c, int h, int w, int64_t total) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -720,7 +751,7 @@ static int launch_h8_t(const ConvH8Args& args, int grid, hipStream_t st) {
   if constexpr (T::LDS > kMaxLds) {
     return RRIN_E_CONFIG;
   } else {
-    if (args.cin % 8 == 0) return launch_h8_k<NW, WM, WN, PLANES, EPI, true>(args, grid, st);
+    if (args.cin % 8 == 0 || args.tail_finite) return launch_h8_k<NW, WM, WN, PLANES, EPI, true>(args, grid, st);
     return launch_h8_k<NW, WM, WN, PLANES, EPI, false>(args, grid, st);
   }
 }
@@ -817,6 +848,7 @@ extern "C" int rrin_conv3x3_h8_fwd(const rrin_conv_h8_desc* d, void* stream) {
   a.bias = d->bias;
   a.inv_wscale = d->inv_wscale;
   a.slope = d->slope;
+  a.tail_finite = d->tail_finite;
   a.h = h;
   a.w = w;
   a.co_blocks = (d->cout + ci.bm - 1) / ci.bm;
@@ -1029,5 +1061,22 @@ extern "C" int rrin_flow_tblend_h8(const rrin_h8* fr, const rrin_h8* g16, const 
     hipLaunchKernelGGL(flow_tblend_h8_kernel<1>, dim3(grid), dim3(256), 0, st, fhi, (const _Float16*)nullptr,
                        fr->img_stride, fr->g.plane, fr->g.wp, static_cast<_Float16*>(g16->hi), (_Float16*)nullptr,
                        g16->img_stride, g16->g.plane, g16->g.wp, coef, h, w, total);
+  return hip_code(hipGetLastError());
+}
+
+extern "C" int rrin_pack_g16_h8(const float* i0, const float* i1, int32_t n, const rrin_h8* g16, int32_t prec,
+                                void* stream) {
+  if (!i0 || !i1 || !g16 || n < 1 || (prec != RRIN_PREC_F16X3 && prec != RRIN_PREC_F16)) return RRIN_E_ARG;
+  if (!h8_ok(*g16, prec) || g16->g_off != 0 || g16->groups < 2) return RRIN_E_SHAPE;
+  const int64_t total = (int64_t)n * g16->g.h * g16->g.w;
+  const int grid = (int)((total + 255) / 256);
+  hipStream_t st = (hipStream_t)stream;
+  if (planes_of(prec) == 2)
+    hipLaunchKernelGGL(pack_g16_h8_kernel<2>, dim3(grid), dim3(256), 0, st, i0, i1, static_cast<uint4*>(g16->hi),
+                       static_cast<uint4*>(g16->lo), g16->img_stride, g16->g.plane, g16->g.wp, g16->g.h, g16->g.w,
+                       total);
+  else
+    hipLaunchKernelGGL(pack_g16_h8_kernel<1>, dim3(grid), dim3(256), 0, st, i0, i1, static_cast<uint4*>(g16->hi),
+                       (uint4*)nullptr, g16->img_stride, g16->g.plane, g16->g.wp, g16->g.h, g16->g.w, total);
   return hip_code(hipGetLastError());
 }

@@ -232,6 +232,7 @@ int conv_h8(const Plan& p, const rrin_conv_weights& cw, int cin, int cout, int e
   d.epi_mode = epi;
   d.slope = 0.1f;
   d.inv_wscale = cw.inv_wscale;
+  d.tail_finite = 1;  // every src of the schedule: cin % 8 == 0, or g16 whose tail channels are finite
   d.src = src;
   d.dst = dst;
   if (pool) d.pool = *pool;
@@ -334,8 +335,9 @@ extern "C" int rrin_net_fwd(const rrin_net_desc* d, void* stream) {
     int rc = 0;
     {
       ProfScope ps(g_prof, st, RRIN_KIND_LAYOUT, 0.0);
-      rc = rrin_nchw_to_h8(d->i0, d->n, 3, 0, &gall, d->prec, st);
-      if (!rc) rc = rrin_nchw_to_h8(d->i1, d->n, 3, 3, &gall, d->prec, st);
+      // x0, x1 into channels 0-5; channels 6-15 zeroed, so the first convs (cin 6/9/10)
+      // can stage whole records (their tail channels are finite and meet zero weights)
+      rc = rrin_pack_g16_h8(d->i0, d->i1, d->n, &gall, d->prec, st);
       if (!rc && d->skip_flow) {
         const rrin_h8 fr = hview(p.FLOWRAW, 0, 4);
         rc = rrin_flow_tblend_h8(&fr, &gall, d->coef, d->n, d->prec, st);

@@ -50,8 +50,6 @@ def choose_cfg(cin: int, cout: int, level: int) -> int:
 def choose_cfg_h8(cin: int, cout: int, prec: int) -> int:
     """Tile config of the split-fp16 / fp16 conv (conv_f16.hip table), from the
     per-shape sweeps of tools/conv_lab.py tune (profiles/r01_v6_tune_*.txt)."""
-    if cin % 8:
-        return 1        # register-staged first convs (cin 6/9/10): BM 32 x TH 16, 8 waves
     if prec == _lib.PREC_F16:  # fp16 (one MFMA per product): LDS allows the BM 128 tile
         if cout == 32 or cout >= 512:
             return 1

@@ -58,7 +58,7 @@ def pack_h8(w, b, cfg, prec, dev, perm=None):
 
 
 def conv_h8(src: H8Tensor, w, b, cfg, prec, epi=_lib.EPI_LINEAR, dst=None, dst_off=0, pool=None, perm=None,
-            cin=None):
+            cin=None, tail_finite=0):
     dev = src.hi.device
     cout, cin_w = w.shape[:2]
     cin = cin or cin_w
@@ -69,6 +69,7 @@ def conv_h8(src: H8Tensor, w, b, cfg, prec, epi=_lib.EPI_LINEAR, dst=None, dst_o
     whi, wlo, bp, inv = pack_h8(w, b, cfg, prec, dev, perm)
     d = _lib.ConvH8Desc()
     d.n, d.cin, d.cout, d.cfg, d.prec, d.epi_mode, d.slope, d.inv_wscale = src.n, cin, cout, cfg, prec, epi, 0.1, inv
+    d.tail_finite = tail_finite
     d.src = src.view(0, cin)
     d.dst = dst.view(dst_off, cout)
     if pool is not None:
@@ -155,3 +156,33 @@ def test_h8_pool_rejected_for_single_row_waves(gpu):
     wt, b = keyed_conv(32, 32)
     with pytest.raises(_lib.RRINError, match="config"):
         conv_h8(H8Tensor.from_nchw(x, X3), wt, b, 4, X3, epi=_lib.EPI_LEAKY_POOL)
+
+
+@pytest.mark.parametrize("prec", [X3, F16])
+@pytest.mark.parametrize("cin", [6, 9, 10])
+def test_h8_conv_dma_finite_tail(gpu, prec, cin):
+    """tail_finite=1: whole records staged by LDS-DMA; the finite tail channels
+    meet zero-padded weights (the first convs of the Net)."""
+    x = torch.rand(2, 16, 32, 48, device=gpu) * 2 - 1
+    wt, b = keyed_conv(cin, 32, "tail")
+    ref = ref_conv(x[:, :cin], wt, b)
+    for cfg in (1, 6):
+        dst, _ = conv_h8(H8Tensor.from_nchw(x, prec), wt, b, cfg, prec, cin=cin, tail_finite=1)
+        np.testing.assert_allclose(dst.to_nchw().cpu().double().numpy(), ref.numpy(), **TOL[prec])
+
+
+@pytest.mark.parametrize("prec", [X3, F16])
+def test_pack_g16(gpu, prec):
+    i0 = torch.rand(2, 3, 32, 48, device=gpu)
+    i1 = torch.rand(2, 3, 32, 48, device=gpu)
+    g = H8Tensor(2, 16, 32, 48, gpu, prec)
+    g.hi.fill_(7.0)
+    if g.lo is not None:
+        g.lo.fill_(7.0)
+    v = g.view(0, 16)
+    _lib.check(_lib.lib().rrin_pack_g16_h8(i0.data_ptr(), i1.data_ptr(), 2, C.byref(v), prec, H.stream(gpu)))
+    torch.cuda.synchronize()
+    out = g.to_nchw()
+    tol = 2.0 ** -20 if prec == X3 else 2.0 ** -10
+    assert float((out[:, :3] - i0).abs().max()) <= tol and float((out[:, 3:6] - i1).abs().max()) <= tol
+    assert not out[:, 6:].any()
