@@ -61,6 +61,8 @@ def parse():
     ap.add_argument("--no-alt", action="store_true",
                     help="N=1: skip the secondary measurement of the exact-fp32 MFMA path")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl = RCCL over xGMI (production); gloo only to rehearse N ranks on fewer GPUs")
     ap.add_argument("--cpu-pairs", type=int, default=2, help="pairs timed on the CPU baseline")
     return ap.parse_args()
 
@@ -120,10 +122,14 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    local = local % max(torch.cuda.device_count(), 1)  # rehearsal: several ranks may share a GPU
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     net = Net()
     sd = keyed_state_dict(net.state_dict())

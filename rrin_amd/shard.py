@@ -33,10 +33,11 @@ def gather_frames(local: torch.Tensor, group=None, out: torch.Tensor | None = No
         out = torch.empty((world * local.shape[0],) + tuple(local.shape[1:]),
                           dtype=local.dtype, device=local.device)
     if dist.get_backend(group) == "gloo":
-        parts = list(out.chunk(world))
-        dist.all_gather(parts, local, group=group)
-        if not all(p.data_ptr() == q.data_ptr() for p, q in zip(parts, out.chunk(world))):
-            out.copy_(torch.cat(parts))
+        # gloo (CPU tests / single-GPU rehearsal): gather through host memory
+        host = local.cpu()
+        parts = [torch.empty_like(host) for _ in range(world)]
+        dist.all_gather(parts, host, group=group)
+        out.copy_(torch.cat(parts))
     else:
         dist.all_gather_into_tensor(out, local, group=group)
     return out

@@ -21,6 +21,7 @@ STEPS=${STEPS:-tests,smoke,bench,prof}
 [[ $STEPS == *bench* ]] && run bench 600 python bench.py --steps 5 --warmup 2
 [[ $STEPS == *bsplit* ]] && run bench_split 600 python bench.py --steps 5 --warmup 2 --precision fp32_split16
 [[ $STEPS == *bf16* ]] && run bench_fp16 600 python bench.py --steps 5 --warmup 2 --precision fp16 --cpu-baseline off
+[[ $STEPS == *mgpu* ]] && run mgpu 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 3 --warmup 1 --batch 2 --dist-backend gloo
 [[ $STEPS == *breakdown* ]] && run breakdown 300 python tools/conv_lab.py breakdown --out gpurun_out/breakdown.json
 [[ $STEPS == *probe* ]] && run probe 300 python tools/precision_probe.py
 [[ $STEPS == *tune* ]] && run tune 600 python tools/conv_lab.py tune --out gpurun_out/tune.json
