@@ -34,7 +34,7 @@ sys.path.insert(0, REPO)
 from rrin_amd import Net, _lib  # noqa: E402
 from rrin_amd.shard import gather_frames  # noqa: E402
 from rrin_amd.synthetic import keyed_state_dict, synthetic_batch  # noqa: E402
-from rrin_amd.unet import conv_flops  # noqa: E402
+from rrin_amd.unet import conv_bytes, conv_flops  # noqa: E402
 
 FP32_PEAK_TFLOPS = 157.3   # MI355X dense fp32 (MFMA 32x32x2 f32 = VALU rate), MI355X_MICROARCH.md
 F16_PEAK_TFLOPS = 2500.0   # dense f16 MFMA (v_mfma_f32_32x32x16_f16), no sparsity
@@ -191,6 +191,7 @@ def main():
         conv_fl = sum(fl[i] for i in range(n) if kinds[i] == 0)
         head_ms = sum(ms[i] for i in range(n) if kinds[i] == 1)
         other_ms = sum(ms[i] for i in range(n) if kinds[i] == 2)
+        edge_ms = sum(ms[i] for i in range(n) if kinds[i] == 3)
         conv_launches = sum(1 for i in range(n) if kinds[i] == 0)
         lib.rrin_prof_destroy(prof)
         conv_ms_step = conv_ms / args.steps
@@ -207,7 +208,26 @@ def main():
                     "avg_launch_ms": conv_ms / max(conv_launches, 1),
                     "conv_ms_per_step": round(conv_ms_step, 3),
                     "head_ms_per_step": round(head_ms_step, 3),
-                    "layout_upsample_ms_per_step": round(other_ms / args.steps, 3)}
+                    "layout_upsample_ms_per_step": round(other_ms / args.steps, 3),
+                    "subpixel_ring_fix_ms_per_step": round(edge_ms / args.steps, 3)}
+
+    if roofline is not None:
+        # HBM bytes per conv launch from the PMC passes of the same command
+        # (tools/gpu_check.sh pmc -> tools/pmc_summary.py; rocprofv3 cannot
+        # collect counters inside this process's timed region)
+        tab = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_traffic.json")
+        key = f"{args.precision}@{W}x{H}x{B}"
+        if os.path.exists(tab):
+            ent = json.load(open(tab)).get(key)
+            if ent is not None:
+                roofline["traffic"] = round(ent["hbm_bytes_per_launch"])
+                roofline["traffic_unit"] = "bytes/launch"
+                roofline["traffic_per_step_gb"] = round(ent["hbm_bytes_per_step"] / 1e9, 2)
+                bpv = 2 if args.precision == "fp16" else 4  # split16 stores hi+lo halves
+                alg = sum(sum(conv_bytes(getattr(net, u), H, W, bpv))
+                          for u in ("Flow", "refine_flow", "Mask", "final"))
+                roofline["algorithmic_bytes_per_step_gb"] = round(B * alg / 1e9, 2)
+                roofline["traffic_source"] = "profiles/pmc_traffic.json[" + key + "]"
 
     pairs = world * B * args.steps
     value = pairs / elapsed

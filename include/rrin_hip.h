@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define RRIN_ABI_VERSION 3
+#define RRIN_ABI_VERSION 4
 
 #define RRIN_OK 0
 #define RRIN_E_SHAPE (-1)     /* H or W not a multiple of 16, or N < 1          */
@@ -58,7 +58,20 @@ typedef struct rrin_pp {
  * nn.Upsample(bilinear,x2) (unet.py:77, fused into the input staging) and
  * torch.cat(up,bridge) (unet.py:93, by channel-offset addressing). */
 enum rrin_src_mode { RRIN_SRC_DIRECT = 0, RRIN_SRC_UPSAMPLE2X = 1 };
-enum rrin_epi_mode { RRIN_EPI_LINEAR = 0, RRIN_EPI_LEAKY = 1, RRIN_EPI_LEAKY_POOL = 2 };
+enum rrin_epi_mode {
+  RRIN_EPI_LINEAR = 0,
+  RRIN_EPI_LEAKY = 1,
+  RRIN_EPI_LEAKY_POOL = 2,
+  /* H8 only.  LEAKY_REP: leaky, and the image border is also written into the
+   * 1-pixel padding ring (edge replicate) -- for a tensor whose only reader is
+   * a sub-pixel up conv.  SUBPIXEL: the conv is the phase-combined form of
+   * conv3x3(upsample_x2(src)) (rrin_subpixel_weights, cout = 4 x real cout):
+   * linear, outputs pixel-shuffled into dst (2x the size of src); the outermost
+   * ring of dst is not written but its pre-bias value goes to `edge` for
+   * rrin_subpixel_edge_fix_h8. */
+  RRIN_EPI_LEAKY_REP = 3,
+  RRIN_EPI_SUBPIXEL = 4
+};
 
 typedef struct rrin_conv_desc {
   int32_t n;            /* images                                              */
@@ -161,6 +174,7 @@ typedef struct rrin_conv_h8_desc {
   const void* whi;             /* packed halves (rrin_pack_conv3x3_h8) */
   const void* wlo;             /* NULL for F16 */
   const float* bias;           /* padded fp32 bias */
+  float* edge;                 /* EPI_SUBPIXEL: [n][cout/4][rrin_ring_pixels(H,W)] fp32 */
 } rrin_conv_h8_desc;
 
 int rrin_conv_h8_cfg_count(void);
@@ -176,6 +190,31 @@ int64_t rrin_pack_conv3x3_h8_halves(int32_t cout, int32_t cin, int32_t bm);
 int rrin_pack_conv3x3_h8(const float* w, const float* b, int32_t cout, int32_t cin, int32_t bm,
                          const int32_t* perm, int32_t prec, uint16_t* whi, uint16_t* wlo,
                          float* bpack, float* inv_wscale);
+
+/* ---- Sub-pixel form of the up block's upsample + conv (unet.py:77-78) ------
+ * conv3x3(upsample_bilinear_x2(x)) at output pixel (2m+py, 2n+px) equals a 3x3
+ * conv of x around (m, n) with phase-combined weights W'_(py,px), provided x is
+ * edge-replicated by one pixel; it then equals the conv over the replicate-padded
+ * upsampled image, so only the outermost output ring differs from the reference
+ * (zero padding) -- by the outside taps, which rrin_subpixel_edge_fix_h8 removes.
+ * rrin_subpixel_weights: w [cout][cin][3][3], b [cout] -> wsub [4*cout][cin][3][3],
+ * bsub [4*cout] with row co' = (co/8)*32 + (2*py+px)*8 + co%8 (cout % 8 == 0),
+ * computed in double. */
+int rrin_subpixel_weights(const float* w, const float* b, int32_t cout, int32_t cin, float* wsub, float* bsub);
+/* pixels on the outermost ring of an H x W image: top row, bottom row, then the
+ * left and right columns without the corners (ring index order). */
+int64_t rrin_ring_pixels(int32_t h, int32_t w);
+typedef struct rrin_edge_fix_desc {
+  int32_t n, cin, cout, prec;  /* cout: real output channels (<= 8*dst.groups), cin <= 256 */
+  int32_t epi_mode;            /* LINEAR or LEAKY */
+  float slope;
+  rrin_h8 src;                 /* low-res input of the sub-pixel conv (h x w)   */
+  rrin_h8 dst;                 /* its output (2h x 2w): ring pixels are written */
+  const float* edge;           /* pre-bias ring values from the EPI_SUBPIXEL conv */
+  const float* wedge;          /* original weights as [cin][9][cout] fp32       */
+  const float* bias;           /* original bias [cout]                          */
+} rrin_edge_fix_desc;
+int rrin_subpixel_edge_fix_h8(const rrin_edge_fix_desc* d, void* stream);
 
 /* nn.Upsample(bilinear, x2) (unet.py:77) of an H8 view into another H8 view. */
 int rrin_upsample2x_h8(const rrin_h8* src, const rrin_h8* dst, int32_t n, int32_t prec, void* stream);
@@ -217,6 +256,11 @@ typedef struct rrin_conv_weights {
   float inv_wscale;     /* F16*: from rrin_pack_conv3x3_h8                    */
   const void* whi;      /* F16*: packed halves                                */
   const void* wlo;      /* F16X3: packed lo halves                            */
+  int32_t subpixel;     /* F16*, up convs: 1 = whi/wlo/bias hold the sub-pixel
+                           weights (4*cout rows) and the upsample pass is skipped */
+  int32_t pad_;
+  const float* wedge;   /* subpixel: original weights [cin][9][cout] fp32      */
+  const float* bias_raw;/* subpixel: original bias [cout]                      */
 } rrin_conv_weights;
 
 typedef struct rrin_head_weights {
@@ -228,7 +272,7 @@ typedef struct rrin_head_weights {
  * schedule enqueues (bench.py uses it to time the MFMA conv kernels inside the
  * timed region).  Opaque; created/destroyed by the caller. */
 typedef struct rrin_prof rrin_prof;
-enum rrin_launch_kind { RRIN_KIND_CONV = 0, RRIN_KIND_HEAD = 1, RRIN_KIND_LAYOUT = 2 };
+enum rrin_launch_kind { RRIN_KIND_CONV = 0, RRIN_KIND_HEAD = 1, RRIN_KIND_LAYOUT = 2, RRIN_KIND_EDGE = 3 };
 
 int rrin_prof_create(int32_t capacity, rrin_prof** out);
 int rrin_prof_destroy(rrin_prof* p);

@@ -9,12 +9,13 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "librrin_hip.so")
 
 # enums (rrin_hip.h)
 SRC_DIRECT, SRC_UPSAMPLE2X = 0, 1
-EPI_LINEAR, EPI_LEAKY, EPI_LEAKY_POOL = 0, 1, 2
+EPI_LINEAR, EPI_LEAKY, EPI_LEAKY_POOL, EPI_LEAKY_REP, EPI_SUBPIXEL = 0, 1, 2, 3, 4
+KIND_CONV, KIND_HEAD, KIND_LAYOUT, KIND_EDGE = 0, 1, 2, 3
 HEAD_PLAIN, HEAD_FLOW, HEAD_REFINE, HEAD_MASK, HEAD_FINAL = 0, 1, 2, 3, 4
 PREC_F32, PREC_F16X3, PREC_F16 = 0, 1, 2
 PRECISIONS = {"fp32": PREC_F32, "fp32_split16": PREC_F16X3, "fp16": PREC_F16}
@@ -44,7 +45,8 @@ class HeadDesc(C.Structure):
 
 class ConvWeights(C.Structure):
     _fields_ = [("wpack", C.c_void_p), ("bias", C.c_void_p), ("cfg", C.c_int32), ("inv_wscale", C.c_float),
-                ("whi", C.c_void_p), ("wlo", C.c_void_p)]
+                ("whi", C.c_void_p), ("wlo", C.c_void_p), ("subpixel", C.c_int32), ("pad_", C.c_int32),
+                ("wedge", C.c_void_p), ("bias_raw", C.c_void_p)]
 
 
 class H8(C.Structure):
@@ -56,7 +58,13 @@ class ConvH8Desc(C.Structure):
     _fields_ = [("n", C.c_int32), ("cin", C.c_int32), ("cout", C.c_int32), ("cfg", C.c_int32),
                 ("prec", C.c_int32), ("epi_mode", C.c_int32), ("slope", C.c_float), ("inv_wscale", C.c_float),
                 ("tail_finite", C.c_int32), ("pad_", C.c_int32), ("src", H8), ("dst", H8), ("pool", H8), ("whi", C.c_void_p), ("wlo", C.c_void_p),
-                ("bias", C.c_void_p)]
+                ("bias", C.c_void_p), ("edge", C.c_void_p)]
+
+
+class EdgeFixDesc(C.Structure):
+    _fields_ = [("n", C.c_int32), ("cin", C.c_int32), ("cout", C.c_int32), ("prec", C.c_int32),
+                ("epi_mode", C.c_int32), ("slope", C.c_float), ("src", H8), ("dst", H8),
+                ("edge", C.c_void_p), ("wedge", C.c_void_p), ("bias", C.c_void_p)]
 
 
 class HeadH8Desc(C.Structure):
@@ -104,6 +112,10 @@ SIGNATURES = {
     "rrin_pack_conv3x3_h8_halves": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32]),
     "rrin_pack_conv3x3_h8": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p,
                                        C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(C.c_float)]),
+    "rrin_subpixel_weights": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p,
+                                        C.c_void_p]),
+    "rrin_ring_pixels": (C.c_int64, [C.c_int32, C.c_int32]),
+    "rrin_subpixel_edge_fix_h8": (C.c_int, [C.POINTER(EdgeFixDesc), C.c_void_p]),
     "rrin_upsample2x_h8": (C.c_int, [C.POINTER(H8), C.POINTER(H8), C.c_int32, C.c_int32, C.c_void_p]),
     "rrin_pack_g16_h8": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(H8), C.c_int32, C.c_void_p]),
     "rrin_nchw_to_h8": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.POINTER(H8), C.c_int32,

@@ -60,7 +60,19 @@ struct ConvH8Args {
   float inv_wscale, slope;
   int h, w, co_blocks, tiles_x, tiles_y, n;
   int tail_finite;
+  float* edge;  // EPI_SUBPIXEL: [n][cout/4][ring] pre-bias values of the 2h x 2w ring
+  int64_t ring;
 };
+
+// Ring index of pixel (y, x) of an H x W image (rrin_ring_pixels order: top
+// row, bottom row, left column, right column; corners in the rows), -1 inside.
+__device__ inline int64_t ring_index(int y, int x, int H, int W) {
+  if (y == 0) return x;
+  if (y == H - 1) return (int64_t)W + x;
+  if (x == 0) return 2 * (int64_t)W + (y - 1);
+  if (x == W - 1) return 2 * (int64_t)W + (H - 2) + (y - 1);
+  return -1;
+}
 
 template <int NW, int WM, int WN, int PLANES>
 struct TileH8 {
@@ -311,6 +323,55 @@ __global__ void __launch_bounds__(64 * NW) conv3x3_h8_kernel(ConvH8Args a) {
   const int yb = y0 + wn * WN;
   const int x = x0 + j;
   uint4* dst[2] = {a.dst_hi + img * a.dst_img, PLANES == 2 ? a.dst_lo + img * a.dst_img : nullptr};
+  if constexpr (EPI == RRIN_EPI_SUBPIXEL) {
+    // rows co' = (co/8)*32 + phase*8 + co%8: an MFMA row block (mt) is one
+    // 8-channel group, q its phase (py, px); LR pixel (y, x) -> HR (2y+py, 2x+px)
+    const int HH = 2 * a.h, WW = 2 * a.w, creal = a.cout >> 2;
+#pragma unroll
+    for (int mt = 0; mt < WM; ++mt) {
+      const int grp = (cob * BM + mt * 32) >> 5;
+      if (grp * 32 >= a.cout) continue;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int py = q >> 1, px = q & 1;
+        const int co0 = cob * BM + mt * 32 + 8 * q;
+        float bs[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bs[e] = a.bias[co0 + 4 * hh + e];
+#pragma unroll
+        for (int nt = 0; nt < WN; ++nt) {
+          const int y = yb + nt;
+          if (y >= a.h || x >= a.w) continue;
+          const int Y = 2 * y + py, X = 2 * x + px;
+          float t[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float u = acc[mt][nt][4 * q + e];
+            if constexpr (PLANES == 2) u = fmaf(accx[mt][nt][4 * q + e], kLoUnscale, u);
+            t[e] = u * a.inv_wscale;
+          }
+          const int64_t ri = ring_index(Y, X, HH, WW);
+          if (ri >= 0) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              a.edge[((int64_t)img * creal + grp * 8 + 4 * hh + e) * a.ring + ri] = t[e];
+          } else {
+            const int64_t rec = (int64_t)grp * a.dst_gp + (int64_t)(Y + 1) * a.dst_wp + X + kH8PadLeft;
+            _Float16 hi[4], lo[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float v = t[e] + bs[e];
+              hi[e] = (_Float16)v;
+              lo[e] = lo_of(v, hi[e]);
+            }
+            reinterpret_cast<uint2*>(dst[0] + rec)[hh] = __builtin_bit_cast(uint2, hi);
+            if constexpr (PLANES == 2) reinterpret_cast<uint2*>(dst[1] + rec)[hh] = __builtin_bit_cast(uint2, lo);
+          }
+        }
+      }
+    }
+    return;
+  }
   uint4* pdst[2] = {nullptr, nullptr};
   if constexpr (EPI == RRIN_EPI_LEAKY_POOL) {
     pdst[0] = a.pool_hi + img * a.pool_img;
@@ -345,8 +406,21 @@ __global__ void __launch_bounds__(64 * NW) conv3x3_h8_kernel(ConvH8Args a) {
             hi[e] = (_Float16)v[nt][e];
             lo[e] = lo_of(v[nt][e], hi[e]);
           }
-          reinterpret_cast<uint2*>(dst[0] + rec)[hh] = __builtin_bit_cast(uint2, hi);
-          if constexpr (PLANES == 2) reinterpret_cast<uint2*>(dst[1] + rec)[hh] = __builtin_bit_cast(uint2, lo);
+          const uint2 hv = __builtin_bit_cast(uint2, hi), lv = __builtin_bit_cast(uint2, lo);
+          reinterpret_cast<uint2*>(dst[0] + rec)[hh] = hv;
+          if constexpr (PLANES == 2) reinterpret_cast<uint2*>(dst[1] + rec)[hh] = lv;
+          if constexpr (EPI == RRIN_EPI_LEAKY_REP) {
+            // edge replicate into the padding ring (read only by a sub-pixel up conv)
+            const int dy0 = y == 0 ? -1 : 0, dy1 = y == a.h - 1 ? 1 : 0;
+            const int dx0 = x == 0 ? -1 : 0, dx1 = x == a.w - 1 ? 1 : 0;
+            for (int dy = dy0; dy <= dy1; ++dy)
+              for (int dx = dx0; dx <= dx1; ++dx)
+                if (dy | dx) {
+                  const int64_t r2 = rec + (int64_t)dy * a.dst_wp + dx;
+                  reinterpret_cast<uint2*>(dst[0] + r2)[hh] = hv;
+                  if constexpr (PLANES == 2) reinterpret_cast<uint2*>(dst[1] + r2)[hh] = lv;
+                }
+          }
         }
       }
       if constexpr (EPI == RRIN_EPI_LEAKY_POOL) {
@@ -426,6 +500,199 @@ __global__ void up2x_h8_kernel(const uint4* __restrict__ s_hi, const uint4* __re
   const int64_t drec = img * d_img + g * d_gp + (int64_t)(y + 1) * d_wp + x + kH8PadLeft;
   d_hi[drec] = __builtin_bit_cast(uint4, ohi);
   if constexpr (PLANES == 2) d_lo[drec] = __builtin_bit_cast(uint4, olo);
+}
+
+// ---- sub-pixel up conv: ring fix-up -------------------------------------------
+// The EPI_SUBPIXEL conv equals conv3x3 over the upsampled image U with edge-
+// replicate padding; the reference pads with zeros, so a ring pixel (Y, X) gets
+//   out = pre - sum_{outside taps} W[co][ci][ky][kx] * U(clamp(Y+ky-1), clamp(X+kx-1)) + bias.
+// Along each boundary line the outside taps of a pixel are the 3 taps of one
+// kernel row (top/bottom line) or column (left/right line) applied to U on that
+// line: a 1-D conv, done here as a small GEMM per tile of 64 line pixels x 32
+// output channels with U (recomputed from the low-res source exactly as
+// up2x_h8_kernel does) and the weights staged in LDS.  A corner also has the
+// two other taps of its outside column ("extra" slots).  Lines: top row and
+// bottom row (corners included), left and right columns without the corners.
+constexpr int kFixPx = 32, kFixCo = 32, kFixCi = 32;
+
+struct EdgeFixArgs {
+  const uint4* s_hi;
+  const uint4* s_lo;
+  int64_t s_img, s_gp;  // records
+  int s_wp, sh, sw, cin;
+  _Float16* d_hi;
+  _Float16* d_lo;
+  int64_t d_img, d_gp;
+  int d_wp, cout;
+  const float* edge;
+  const float* wedge;  // [cin][9][cout]
+  const float* bias;
+  int64_t ring;
+  float slope;
+  int leaky;
+  int tiles_row, tiles_col;  // tiles per row line / per column line
+};
+
+// The 4 low-res records (8 channels, both planes) that bilinear x2 (align_corners
+// = False, edge clamp) blends into U(Y, X), and the blend weights.
+template <int PLANES>
+struct Up8 {
+  uint4 q[4][PLANES];
+  float wa, wc;
+  __device__ void fetch(const EdgeFixArgs& a, const uint4* hi, const uint4* lo, int g, int Y, int X) {
+    int ra, rb, ca, cb;
+    if (Y & 1) { ra = Y >> 1; rb = min(ra + 1, a.sh - 1); wa = 0.75f; }
+    else { rb = Y >> 1; ra = max(rb - 1, 0); wa = 0.25f; }
+    if (X & 1) { ca = X >> 1; cb = min(ca + 1, a.sw - 1); wc = 0.75f; }
+    else { cb = X >> 1; ca = max(cb - 1, 0); wc = 0.25f; }
+    const int64_t base = (int64_t)g * a.s_gp + kH8PadLeft;
+    const int64_t r[4] = {base + (int64_t)(ra + 1) * a.s_wp + ca, base + (int64_t)(ra + 1) * a.s_wp + cb,
+                          base + (int64_t)(rb + 1) * a.s_wp + ca, base + (int64_t)(rb + 1) * a.s_wp + cb};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      q[k][0] = hi[r[k]];
+      if constexpr (PLANES == 2) q[k][1] = lo[r[k]];
+    }
+  }
+  __device__ void zero() {
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int p = 0; p < PLANES; ++p) q[k][p] = make_uint4(0u, 0u, 0u, 0u);
+    wa = wc = 0.5f;
+  }
+  __device__ float value(int e) const {  // horizontal then vertical, as upsample_bilinear2d
+    float v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const half8 h = __builtin_bit_cast(half8, q[k][0]);
+      v[k] = (float)h[e];
+      if constexpr (PLANES == 2) v[k] = join(h[e], __builtin_bit_cast(half8, q[k][PLANES - 1])[e]);
+    }
+    const float wb = 1.0f - wa, wd = 1.0f - wc;
+    const float top = wc * v[0] + wd * v[1];
+    const float bot = wc * v[2] + wd * v[3];
+    return wa * top + wb * bot;
+  }
+};
+
+template <int PLANES>
+__global__ void __launch_bounds__(256) edge_fix_h8_kernel(EdgeFixArgs a) {
+  __shared__ float s_u[kFixCi][kFixPx + 2];
+  __shared__ float s_ux[kFixCi][4];         // corner extras: [left ky_a, left ky_b, right ky_a, right ky_b]
+  __shared__ float s_w[7][kFixCi][kFixCo];  // slots 0-2 line taps, 3-6 corner extras
+  const int tid = threadIdx.x, px = tid & (kFixPx - 1), cg = tid / kFixPx;  // 8 groups of 4 channels
+  const int img = blockIdx.z, co0 = blockIdx.y * kFixCo;
+  const int H = 2 * a.sh, W = 2 * a.sw;
+  // line of this tile: 0 top, 1 bottom, 2 left, 3 right
+  int t = blockIdx.x, line;
+  if (t < 2 * a.tiles_row) { line = t / a.tiles_row; t -= line * a.tiles_row; }
+  else { t -= 2 * a.tiles_row; line = 2 + t / a.tiles_col; t -= (line - 2) * a.tiles_col; }
+  const bool row = line < 2;
+  const int full = row ? W : H;                 // U positions along the line
+  const int first = row ? 0 : 1, count = row ? W : H - 2;
+  const int pos0 = first + t * kFixPx;          // line coordinate of pixel px = 0
+  const int fixed = row ? (line == 0 ? 0 : H - 1) : (line == 2 ? 0 : W - 1);  // the other coordinate
+  const int out_k = (line == 0 || line == 2) ? 0 : 2;                          // outside row/col of the kernel
+  // corner extras (row lines only): corner at X = 0 and/or X = W-1 inside this tile
+  const bool has_l = row && pos0 == 0, has_r = row && pos0 <= W - 1 && W - 1 < pos0 + kFixPx;
+  const bool corners = has_l || has_r;
+  const int nslot = corners ? 7 : 3;
+  // extra slot s (0-1 left corner, 2-3 right): kernel row ky = the (s&1)-th of {0,1,2} minus out_k,
+  // column 0 (left) or 2 (right); its U sits at row fixed + ky - 1 of that image column
+  auto xky = [&](int sl) { return (sl & 1) + (out_k == 0 ? 1 : 0); };
+  const uint4* rhi = a.s_hi + (int64_t)img * a.s_img;
+  const uint4* rlo = PLANES == 2 ? a.s_lo + (int64_t)img * a.s_img : nullptr;
+
+  // per-thread staging work of one ci chunk, fetched one chunk ahead
+  constexpr int kItems = (kFixCi / 8) * (kFixPx + 2);  // U: record groups x line positions
+  static_assert(kItems <= 256, "one U item per thread");
+  Up8<PLANES> ru, rx;
+  float4 rw[7];
+  const int u_gl = tid / (kFixPx + 2), u_j = tid - u_gl * (kFixPx + 2);
+  const int w_ci = tid >> 3, w_cq = (tid & 7) * 4;
+  auto fetch = [&](int c0) {
+    if (tid < kItems) {
+      const int q = min(max(pos0 - 1 + u_j, 0), full - 1);
+      if (c0 + u_gl * 8 < a.cin) ru.fetch(a, rhi, rlo, (c0 >> 3) + u_gl, row ? fixed : q, row ? q : fixed);
+      else ru.zero();
+    }
+    if (corners && tid < 16) {  // 4 extra slots x 4 record groups
+      const int sl = tid >> 2, gl = tid & 3;
+      if (c0 + gl * 8 < a.cin) rx.fetch(a, rhi, rlo, (c0 >> 3) + gl, fixed + xky(sl) - 1, sl < 2 ? 0 : W - 1);
+      else rx.zero();
+    }
+    const bool ok = c0 + w_ci < a.cin && co0 + w_cq < a.cout;
+#pragma unroll
+    for (int sl = 0; sl < 7; ++sl) {
+      rw[sl] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (sl < nslot && ok) {
+        const int tap = sl < 3 ? (row ? out_k * 3 + sl : sl * 3 + out_k) : xky(sl - 3) * 3 + (sl < 5 ? 0 : 2);
+        rw[sl] = *reinterpret_cast<const float4*>(a.wedge + ((int64_t)(c0 + w_ci) * 9 + tap) * a.cout + co0 + w_cq);
+      }
+    }
+  };
+  auto stage = [&]() {
+    if (tid < kItems)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s_u[u_gl * 8 + e][u_j] = ru.value(e);
+    if (corners && tid < 16)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s_ux[(tid & 3) * 8 + e][tid >> 2] = rx.value(e);
+#pragma unroll
+    for (int sl = 0; sl < 7; ++sl)
+      if (sl < nslot) *reinterpret_cast<float4*>(&s_w[sl][w_ci][w_cq]) = rw[sl];
+  };
+
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  const int pos = pos0 + px;
+  const bool cl = has_l && pos == 0, cr = has_r && pos == W - 1;
+  fetch(0);
+  for (int c0 = 0; c0 < a.cin; c0 += kFixCi) {
+    stage();
+    __syncthreads();
+    if (c0 + kFixCi < a.cin) fetch(c0 + kFixCi);  // in flight during the FMAs below
+#pragma unroll 4
+    for (int ci = 0; ci < kFixCi; ++ci) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const float u = s_u[ci][px + k];
+        const float4 w = *reinterpret_cast<const float4*>(&s_w[k][ci][cg * 4]);
+        acc[0] = fmaf(w.x, u, acc[0]);
+        acc[1] = fmaf(w.y, u, acc[1]);
+        acc[2] = fmaf(w.z, u, acc[2]);
+        acc[3] = fmaf(w.w, u, acc[3]);
+      }
+      if (cl || cr) {
+        const int sb = cl ? 0 : 2;
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+          const float u = s_ux[ci][sb + m];
+          const float4 w = *reinterpret_cast<const float4*>(&s_w[3 + sb + m][ci][cg * 4]);
+          acc[0] = fmaf(w.x, u, acc[0]);
+          acc[1] = fmaf(w.y, u, acc[1]);
+          acc[2] = fmaf(w.z, u, acc[2]);
+          acc[3] = fmaf(w.w, u, acc[3]);
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (pos - first >= count) return;
+  const int Y = row ? fixed : pos, X = row ? pos : fixed;
+  const int64_t e = ring_index(Y, X, H, W);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int co = co0 + cg * 4 + i;
+    if (co >= a.cout) break;
+    float v = (a.edge[((int64_t)img * a.cout + co) * a.ring + e] - acc[i]) + a.bias[co];
+    if (a.leaky) v = v > 0.f ? v : v * a.slope;
+    const int64_t k = (((int64_t)img * a.d_img + (int64_t)(co >> 3) * a.d_gp + (int64_t)(Y + 1) * a.d_wp + X +
+                        kH8PadLeft) * 8) + (co & 7);
+    const _Float16 vh = (_Float16)v;
+    a.d_hi[k] = vh;
+    if constexpr (PLANES == 2) a.d_lo[k] = lo_of(v, vh);
+  }
 }
 
 // ---- layout kernels ------------------------------------------------------------
@@ -752,26 +1019,42 @@ static int launch_h8_t(const ConvH8Args& args, int grid, hipStream_t st) {
     return RRIN_E_CONFIG;
   } else {
     if (args.cin % 8 == 0 || args.tail_finite) return launch_h8_k<NW, WM, WN, PLANES, EPI, true>(args, grid, st);
-    return launch_h8_k<NW, WM, WN, PLANES, EPI, false>(args, grid, st);
+    if constexpr (EPI == RRIN_EPI_LEAKY_REP || EPI == RRIN_EPI_SUBPIXEL) {
+      return RRIN_E_CONFIG;  // decoder-side modes: always whole channel groups
+    } else {
+      return launch_h8_k<NW, WM, WN, PLANES, EPI, false>(args, grid, st);
+    }
   }
 }
 
 template <int NW, int WM, int WN>
 static int launch_h8_cfg(const ConvH8Args& args, int planes, int epi, int grid, hipStream_t st) {
   if (planes == 2) {
-    if (epi == RRIN_EPI_LINEAR) return launch_h8_t<NW, WM, WN, 2, RRIN_EPI_LINEAR>(args, grid, st);
-    if (epi == RRIN_EPI_LEAKY) return launch_h8_t<NW, WM, WN, 2, RRIN_EPI_LEAKY>(args, grid, st);
-    return launch_h8_t<NW, WM, WN, 2, RRIN_EPI_LEAKY_POOL>(args, grid, st);
+    switch (epi) {
+      case RRIN_EPI_LINEAR: return launch_h8_t<NW, WM, WN, 2, RRIN_EPI_LINEAR>(args, grid, st);
+      case RRIN_EPI_LEAKY: return launch_h8_t<NW, WM, WN, 2, RRIN_EPI_LEAKY>(args, grid, st);
+      case RRIN_EPI_LEAKY_POOL: return launch_h8_t<NW, WM, WN, 2, RRIN_EPI_LEAKY_POOL>(args, grid, st);
+      case RRIN_EPI_LEAKY_REP: return launch_h8_t<NW, WM, WN, 2, RRIN_EPI_LEAKY_REP>(args, grid, st);
+      default: return launch_h8_t<NW, WM, WN, 2, RRIN_EPI_SUBPIXEL>(args, grid, st);
+    }
   }
-  if (epi == RRIN_EPI_LINEAR) return launch_h8_t<NW, WM, WN, 1, RRIN_EPI_LINEAR>(args, grid, st);
-  if (epi == RRIN_EPI_LEAKY) return launch_h8_t<NW, WM, WN, 1, RRIN_EPI_LEAKY>(args, grid, st);
-  return launch_h8_t<NW, WM, WN, 1, RRIN_EPI_LEAKY_POOL>(args, grid, st);
+  switch (epi) {
+    case RRIN_EPI_LINEAR: return launch_h8_t<NW, WM, WN, 1, RRIN_EPI_LINEAR>(args, grid, st);
+    case RRIN_EPI_LEAKY: return launch_h8_t<NW, WM, WN, 1, RRIN_EPI_LEAKY>(args, grid, st);
+    case RRIN_EPI_LEAKY_POOL: return launch_h8_t<NW, WM, WN, 1, RRIN_EPI_LEAKY_POOL>(args, grid, st);
+    case RRIN_EPI_LEAKY_REP: return launch_h8_t<NW, WM, WN, 1, RRIN_EPI_LEAKY_REP>(args, grid, st);
+    default: return launch_h8_t<NW, WM, WN, 1, RRIN_EPI_SUBPIXEL>(args, grid, st);
+  }
 }
 
 static bool h8_ok(const rrin_h8& v, int prec) {
   if (!v.hi || (prec == RRIN_PREC_F16X3 && !v.lo)) return false;
   const rrin_geom g = make_geom_h8(v.g.h, v.g.w);
   return g.hp == v.g.hp && g.wp == v.g.wp && g.plane == v.g.plane;
+}
+
+static inline int64_t ring_pixels(int h, int w) {
+  return h < 2 ? (int64_t)w : 2 * (int64_t)w + 2 * (int64_t)(h - 2);
 }
 
 static inline int planes_of(int prec) { return prec == RRIN_PREC_F16X3 ? 2 : 1; }
@@ -805,11 +1088,13 @@ extern "C" int rrin_conv3x3_h8_fwd(const rrin_conv_h8_desc* d, void* stream) {
   if (d->prec == RRIN_PREC_F16X3 && !d->wlo) return RRIN_E_ARG;
   if (!rrin_conv_h8_cfg_ok(d->cfg, d->prec)) return RRIN_E_CONFIG;
   if (d->n < 1 || d->cin < 1 || d->cout < 8 || (d->cout & 7)) return RRIN_E_ARG;
-  if (d->epi_mode < RRIN_EPI_LINEAR || d->epi_mode > RRIN_EPI_LEAKY_POOL) return RRIN_E_ARG;
+  if (d->epi_mode < RRIN_EPI_LINEAR || d->epi_mode > RRIN_EPI_SUBPIXEL) return RRIN_E_ARG;
   if (!h8_ok(d->src, d->prec) || !h8_ok(d->dst, d->prec)) return RRIN_E_SHAPE;
-  const int h = d->dst.g.h, w = d->dst.g.w;
-  if (d->src.g.h != h || d->src.g.w != w) return RRIN_E_SHAPE;
-  if (d->cin > 8 * d->src.groups || d->cout > 8 * d->dst.groups) return RRIN_E_ARG;
+  const bool sub = d->epi_mode == RRIN_EPI_SUBPIXEL;
+  const int h = d->src.g.h, w = d->src.g.w;  // the grid the conv runs on
+  if (d->dst.g.h != (sub ? 2 * h : h) || d->dst.g.w != (sub ? 2 * w : w)) return RRIN_E_SHAPE;
+  if (d->cin > 8 * d->src.groups || (sub ? d->cout / 4 : d->cout) > 8 * d->dst.groups) return RRIN_E_ARG;
+  if (sub && ((d->cout & 31) || !d->edge)) return RRIN_E_ARG;
   if (d->epi_mode == RRIN_EPI_LEAKY_POOL) {
     if (!kCfgH8[d->cfg].pool_ok) return RRIN_E_CONFIG;  // a wave must own both rows of a pool pair
     if (!h8_ok(d->pool, d->prec) || (h & 1) || (w & 1) || d->pool.g.h * 2 != h || d->pool.g.w * 2 != w ||
@@ -851,6 +1136,10 @@ extern "C" int rrin_conv3x3_h8_fwd(const rrin_conv_h8_desc* d, void* stream) {
   a.tail_finite = d->tail_finite;
   a.h = h;
   a.w = w;
+  if (sub) {
+    a.edge = d->edge;
+    a.ring = ring_pixels(2 * h, 2 * w);
+  }
   a.co_blocks = (d->cout + ci.bm - 1) / ci.bm;
   a.tiles_x = (w + 31) / 32;
   a.tiles_y = (h + ci.th - 1) / ci.th;
@@ -913,6 +1202,83 @@ extern "C" int rrin_pack_conv3x3_h8(const float* w, const float* b, int32_t cout
             }
   for (int co = 0; co < cob_n * bm; ++co) bpack[co] = co < cout ? b[co] : 0.f;
   return 0;
+}
+
+extern "C" int64_t rrin_ring_pixels(int32_t h, int32_t w) {
+  if (h < 1 || w < 1) return RRIN_E_ARG;
+  return ring_pixels(h, w);
+}
+
+// Phase-combined weights of conv3x3 o upsample_x2 (see rrin_hip.h).  kR[p][a][k]:
+// coefficient of low-res row m+a-1 in upsampled row 2m+p+k-1 (align_corners=False).
+extern "C" int rrin_subpixel_weights(const float* w, const float* b, int32_t cout, int32_t cin, float* wsub,
+                                     float* bsub) {
+  if (!w || !b || !wsub || !bsub || cout < 8 || (cout & 7) || cin < 1) return RRIN_E_ARG;
+  static const double kR[2][3][3] = {{{0.75, 0.25, 0.0}, {0.25, 0.75, 0.75}, {0.0, 0.0, 0.25}},
+                                     {{0.25, 0.0, 0.0}, {0.75, 0.75, 0.25}, {0.0, 0.25, 0.75}}};
+  for (int co = 0; co < cout; ++co)
+    for (int ph = 0; ph < 4; ++ph) {
+      const int py = ph >> 1, px = ph & 1;
+      const int64_t row = (int64_t)(co >> 3) * 32 + ph * 8 + (co & 7);
+      bsub[row] = b[co];
+      for (int ci = 0; ci < cin; ++ci) {
+        const float* src = w + ((int64_t)co * cin + ci) * 9;
+        float* dst = wsub + (row * cin + ci) * 9;
+        for (int ay = 0; ay < 3; ++ay)
+          for (int ax = 0; ax < 3; ++ax) {
+            double acc = 0.0;
+            for (int ky = 0; ky < 3; ++ky)
+              for (int kx = 0; kx < 3; ++kx) acc += kR[py][ay][ky] * kR[px][ax][kx] * (double)src[ky * 3 + kx];
+            dst[ay * 3 + ax] = (float)acc;
+          }
+      }
+    }
+  return 0;
+}
+
+extern "C" int rrin_subpixel_edge_fix_h8(const rrin_edge_fix_desc* d, void* stream) {
+  if (!d || !d->edge || !d->wedge || !d->bias) return RRIN_E_ARG;
+  if (d->prec != RRIN_PREC_F16X3 && d->prec != RRIN_PREC_F16) return RRIN_E_ARG;
+  if (d->n < 1 || d->cin < 8 || (d->cin & 7) || d->cout < 8 || (d->cout & 7)) return RRIN_E_ARG;
+  if (d->epi_mode != RRIN_EPI_LINEAR && d->epi_mode != RRIN_EPI_LEAKY) return RRIN_E_ARG;
+  if (!h8_ok(d->src, d->prec) || !h8_ok(d->dst, d->prec)) return RRIN_E_SHAPE;
+  if (d->dst.g.h != 2 * d->src.g.h || d->dst.g.w != 2 * d->src.g.w) return RRIN_E_SHAPE;
+  if (d->cin > 8 * d->src.groups || d->cout > 8 * d->dst.groups) return RRIN_E_ARG;
+  const int planes = planes_of(d->prec);
+  EdgeFixArgs a;
+  memset(&a, 0, sizeof(a));
+  const int64_t sg = (int64_t)d->src.g_off * d->src.g.plane, dg = (int64_t)d->dst.g_off * d->dst.g.plane;
+  a.s_hi = static_cast<const uint4*>(d->src.hi) + sg;
+  a.s_lo = planes == 2 ? static_cast<const uint4*>(d->src.lo) + sg : nullptr;
+  a.s_img = d->src.img_stride;
+  a.s_gp = d->src.g.plane;
+  a.s_wp = d->src.g.wp;
+  a.sh = d->src.g.h;
+  a.sw = d->src.g.w;
+  a.cin = d->cin;
+  a.d_hi = static_cast<_Float16*>(d->dst.hi) + dg * 8;
+  a.d_lo = planes == 2 ? static_cast<_Float16*>(d->dst.lo) + dg * 8 : nullptr;
+  a.d_img = d->dst.img_stride;
+  a.d_gp = d->dst.g.plane;
+  a.d_wp = d->dst.g.wp;
+  a.cout = d->cout;
+  a.edge = d->edge;
+  a.wedge = d->wedge;
+  a.bias = d->bias;
+  a.ring = ring_pixels(d->dst.g.h, d->dst.g.w);
+  a.slope = d->slope;
+  a.leaky = d->epi_mode == RRIN_EPI_LEAKY;
+  const int H = d->dst.g.h, W = d->dst.g.w;
+  a.tiles_row = (W + kFixPx - 1) / kFixPx;
+  a.tiles_col = (H - 2 + kFixPx - 1) / kFixPx;
+  const dim3 grid((unsigned)(2 * a.tiles_row + 2 * a.tiles_col), (unsigned)((d->cout + kFixCo - 1) / kFixCo),
+                  (unsigned)d->n);
+  hipStream_t st = (hipStream_t)stream;
+  if (planes == 2)
+    hipLaunchKernelGGL(edge_fix_h8_kernel<2>, grid, dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL(edge_fix_h8_kernel<1>, grid, dim3(256), 0, st, a);
+  return hip_code(hipGetLastError());
 }
 
 extern "C" int rrin_upsample2x_h8(const rrin_h8* src, const rrin_h8* dst, int32_t n, int32_t prec, void* stream) {

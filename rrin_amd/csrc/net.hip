@@ -54,6 +54,9 @@ struct Plan {
   Buf UPT[kMaxDepth - 1]; // F16*: upsampled input of an up.1 conv, one per level (2 C_L ch).  Not
                           // shared across levels: another level's interior writes would land in
                           // this level's zero padding (the conv halo).
+  Buf LRB[kMaxDepth];     // F16*, L >= 1: low-res input of a sub-pixel up conv (C_L ch), written with
+                          // edge-replicate padding by its producer (EPI_LEAKY_REP)
+  float* EDGE;            // F16*: pre-bias ring values of the current sub-pixel up conv
   Buf FLOWRAW;            // raw 4-ch Flow output, kept for reuse across t (skip_flow)
   int64_t bytes;
 };
@@ -91,6 +94,20 @@ void make_plan(int n, int h, int w, int prec, char* base, Plan& p) {
   p.BOT = take(chans(kMaxDepth - 1), p.g[kMaxDepth - 1]);
   for (int L = 0; L < kMaxDepth - 1; ++L)
     p.UPT[L] = f32 ? Buf{nullptr, nullptr, 0, p.g[L]} : take(2 * chans(L), p.g[L]);
+  int64_t edge_floats = 0;
+  for (int L = 0; L < kMaxDepth; ++L) {
+    p.LRB[L] = (f32 || L == 0) ? Buf{nullptr, nullptr, 0, p.g[L]} : take(chans(L), p.g[L]);
+    if (L < kMaxDepth - 1) {
+      const int64_t hh = h >> L, ww = w >> L;
+      const int64_t e = (int64_t)n * chans(L) * (2 * ww + 2 * (hh - 2));
+      edge_floats = e > edge_floats ? e : edge_floats;
+    }
+  }
+  p.EDGE = nullptr;
+  if (!f32) {
+    p.EDGE = base ? reinterpret_cast<float*>(base + off) : nullptr;
+    off += align256(edge_floats * 4);
+  }
   p.FLOWRAW = take(f32 ? 4 : 8, p.g[0]);
   p.bytes = off;
 }
@@ -220,8 +237,10 @@ int run_unet(const Plan& p, const UNetSpec& u, const rrin_conv_weights* cw, cons
 }
 
 int conv_h8(const Plan& p, const rrin_conv_weights& cw, int cin, int cout, int epi, const rrin_h8& src,
-            const rrin_h8& dst, const rrin_h8* pool, hipStream_t st) {
-  ProfScope ps(g_prof, st, RRIN_KIND_CONV, 2.0 * 9 * cin * cout * (double)dst.g.h * dst.g.w * p.n);
+            const rrin_h8& dst, const rrin_h8* pool, hipStream_t st, float* edge = nullptr) {
+  // algorithmic FLOPs of the reference conv (a sub-pixel conv has 4 phase rows per real channel)
+  const int creal = epi == RRIN_EPI_SUBPIXEL ? cout / 4 : cout;
+  ProfScope ps(g_prof, st, RRIN_KIND_CONV, 2.0 * 9 * cin * creal * (double)dst.g.h * dst.g.w * p.n);
   rrin_conv_h8_desc d;
   memset(&d, 0, sizeof(d));
   d.n = p.n;
@@ -239,15 +258,40 @@ int conv_h8(const Plan& p, const rrin_conv_weights& cw, int cin, int cout, int e
   d.whi = cw.whi;
   d.wlo = cw.wlo;
   d.bias = cw.bias;
+  d.edge = edge;
   return rrin_conv3x3_h8_fwd(&d, st);
 }
 
-// One U-Net on the split-fp16 path: same dataflow as run_unet, plus an explicit
-// upsample pass (UPT) in front of every up.1 conv.
+// up.1 conv of the up block at level L on the sub-pixel path: low-res x (2C ch,
+// edge-replicated) -> CAT[L][0, C), then the ring fix-up.
+int upconv_subpixel(const Plan& p, const rrin_conv_weights& cw, int C, const rrin_h8& x, const rrin_h8& up,
+                    hipStream_t st) {
+  RRIN_TRY(conv_h8(p, cw, 2 * C, 4 * C, RRIN_EPI_SUBPIXEL, x, up, nullptr, st, p.EDGE));
+  rrin_edge_fix_desc e;
+  memset(&e, 0, sizeof(e));
+  e.n = p.n;
+  e.cin = 2 * C;
+  e.cout = C;
+  e.prec = p.prec;
+  e.epi_mode = RRIN_EPI_LINEAR;
+  e.src = x;
+  e.dst = up;
+  e.edge = p.EDGE;
+  e.wedge = cw.wedge;
+  e.bias = cw.bias_raw;
+  ProfScope ps(g_prof, st, RRIN_KIND_EDGE, 0.0);
+  return rrin_subpixel_edge_fix_h8(&e, st);
+}
+
+// One U-Net on the split-fp16 path: same dataflow as run_unet.  An up conv
+// either has sub-pixel weights (upsample folded into the conv; its producer then
+// writes the low-res tensor into LRB with edge-replicate padding) or runs after
+// an explicit upsample pass into UPT.
 int run_unet_h8(const Plan& p, const UNetSpec& u, const rrin_conv_weights* cw, const rrin_head_weights& hw,
                 const rrin_net_desc* nd, hipStream_t st) {
   const int D = u.depth;
   int k = 0;
+  rrin_h8 x;
   for (int L = 0; L < D; ++L) {
     const int C = chans(L);
     const int cin = L ? chans(L - 1) : u.in_ch;
@@ -261,24 +305,35 @@ int run_unet_h8(const Plan& p, const UNetSpec& u, const rrin_conv_weights* cw, c
     } else {
       const Buf& bot = (L == kMaxDepth - 1) ? p.BOT : p.CAT[L];
       RRIN_TRY(conv_h8(p, cw[k++], C, C, RRIN_EPI_LEAKY, t, hview(bot, 0, C), nullptr, st));
-      RRIN_TRY(conv_h8(p, cw[k++], C, C, RRIN_EPI_LEAKY, hview(bot, 0, C), t, nullptr, st));
+      // midconv; cw[k + 1] is the first up conv
+      const bool sub = D >= 2 && cw[k + 1].subpixel;
+      x = sub ? hview(p.LRB[L], 0, C) : t;
+      RRIN_TRY(conv_h8(p, cw[k++], C, C, sub ? RRIN_EPI_LEAKY_REP : RRIN_EPI_LEAKY, hview(bot, 0, C), x, nullptr,
+                       st));
     }
   }
-  rrin_h8 x = hview(p.T[D - 1], 0, chans(D - 1));
   for (int L = D - 2; L >= 0; --L) {
     const int C = chans(L);
-    const rrin_h8 upin = hview(p.UPT[L], 0, 2 * C);
-    {
-      ProfScope ps(g_prof, st, RRIN_KIND_LAYOUT, 0.0);
-      RRIN_TRY(rrin_upsample2x_h8(&x, &upin, p.n, p.prec, st));
-    }
     const rrin_h8 up = hview(p.CAT[L], 0, C);
-    RRIN_TRY(conv_h8(p, cw[k++], 2 * C, C, RRIN_EPI_LINEAR, upin, up, nullptr, st));
+    const rrin_conv_weights& cu = cw[k++];
+    if (cu.subpixel) {
+      RRIN_TRY(upconv_subpixel(p, cu, C, x, up, st));
+    } else {
+      const rrin_h8 upin = hview(p.UPT[L], 0, 2 * C);
+      {
+        ProfScope ps(g_prof, st, RRIN_KIND_LAYOUT, 0.0);
+        RRIN_TRY(rrin_upsample2x_h8(&x, &upin, p.n, p.prec, st));
+      }
+      RRIN_TRY(conv_h8(p, cu, 2 * C, C, RRIN_EPI_LINEAR, upin, up, nullptr, st));
+    }
     const rrin_h8 cat = hview(p.CAT[L], 0, 2 * C);
     const rrin_h8 t = hview(p.T[L], 0, C);
     RRIN_TRY(conv_h8(p, cw[k++], 2 * C, C, RRIN_EPI_LEAKY, cat, t, nullptr, st));
-    RRIN_TRY(conv_h8(p, cw[k++], C, C, RRIN_EPI_LEAKY, t, up, nullptr, st));
-    x = up;
+    // conv b; cw[k + 1] is the next level's up conv
+    const bool sub = L > 0 && cw[k + 1].subpixel;
+    const rrin_h8 out = sub ? hview(p.LRB[L], 0, C) : up;
+    RRIN_TRY(conv_h8(p, cw[k++], C, C, sub ? RRIN_EPI_LEAKY_REP : RRIN_EPI_LEAKY, t, out, nullptr, st));
+    x = out;
   }
   rrin_head_h8_desc hd;
   memset(&hd, 0, sizeof(hd));

@@ -21,6 +21,7 @@ import numpy as np
 import torch
 
 from . import _lib
+from .unet import _level_of
 
 UNET_ORDER = ("Flow", "refine_flow", "Mask", "final")
 
@@ -47,18 +48,19 @@ def choose_cfg(cin: int, cout: int, level: int) -> int:
     return 1            # BM 64 x TH 8
 
 
-def choose_cfg_h8(cin: int, cout: int, prec: int) -> int:
-    """Tile config of the split-fp16 / fp16 conv (conv_f16.hip table), from the
-    per-shape sweeps of tools/conv_lab.py tune (profiles/r01_v6_tune_*.txt)."""
-    if prec == _lib.PREC_F16:  # fp16 (one MFMA per product): LDS allows the BM 128 tile
-        if cout == 32 or cout >= 512:
-            return 1
+def choose_cfg_h8(cin: int, cout: int, prec: int, level: int = 0) -> int:
+    """Tile config of the split-fp16 / fp16 conv (conv_f16.hip table) for a conv
+    running on the grid of U-Net level ``level`` (a sub-pixel up conv runs on the
+    low-res grid with 4x the output rows), from the per-shape sweeps of
+    tools/conv_lab.py tune (profiles/r01_v8_tune_*.txt)."""
+    small = cout == 32 or level >= 4   # full-res 32-channel layers; the 45x80 bottom at 720p
+    if prec == _lib.PREC_F16:          # one MFMA per product: LDS allows the BM 128 tile
+        if small:
+            return 1    # BM 32 x TH 16, 8 waves
         if cin >= 256 and cout >= 128:
             return 5    # BM 128 x TH 16, 8 waves
         return 0
-    if cout == 32 or cout >= 512 or (cin == 32 and cout == 64):
-        return 6        # BM 32 x TH 8, 4 waves, 2 blocks/CU: small-K full-res and 80x45 layers
-    return 0            # BM 64 x TH 16, 8 waves
+    return 6 if small else 0  # BM 32 x TH 8 (4 waves, 2 blocks/CU) | BM 64 x TH 16 (8 waves)
 
 
 def t_coefficients(t, n: int) -> torch.Tensor:
@@ -87,8 +89,9 @@ def t_coefficients(t, n: int) -> torch.Tensor:
 class RRINEngine:
     MAX_WORKSPACES = 2
 
-    def __init__(self, net, precision: str = "fp32"):
+    def __init__(self, net, precision: str = "fp32", subpixel_max_level: int = 2):
         self.lib = _lib.lib()
+        self.subpixel_max_level = subpixel_max_level
         params = list(net.parameters())
         self.device = params[0].device
         if self.device.type != "cuda":
@@ -158,8 +161,10 @@ class RRINEngine:
         L = self.lib
         halves, biases, meta = [], [], []
         hoff = boff = 0
+        self.edge_t = []  # device tensors referenced by the table (sub-pixel convs)
         for name in UNET_ORDER:
-            for idx, (tag, conv) in enumerate(getattr(net, name).conv_list()):
+            unet = getattr(net, name)
+            for idx, (tag, conv) in enumerate(unet.conv_list()):
                 w = conv.weight.detach().to("cpu", torch.float32).contiguous().numpy()
                 b = conv.bias.detach().to("cpu", torch.float32).contiguous().numpy()
                 cout, cin = w.shape[0], w.shape[1]
@@ -167,7 +172,20 @@ class RRINEngine:
                     self.heads_t.append((torch.from_numpy(w.copy()).to(self.device),
                                          torch.from_numpy(b.copy()).to(self.device)))
                     continue
-                cfg = choose_cfg_h8(cin, cout, self.prec)
+                edge = None
+                level = _level_of(unet, tag)
+                if tag.endswith(".up") and level <= self.subpixel_max_level:
+                    level += 1  # runs on the low-res grid
+                    # upsample folded into phase-combined weights (rrin_subpixel_weights)
+                    ws = np.empty((4 * cout, cin, 3, 3), np.float32)
+                    bs = np.empty(4 * cout, np.float32)
+                    _lib.check(L.rrin_subpixel_weights(w.ctypes.data, b.ctypes.data, cout, cin, ws.ctypes.data,
+                                                       bs.ctypes.data), "rrin_subpixel_weights")
+                    edge = (torch.from_numpy(np.ascontiguousarray(w.transpose(1, 2, 3, 0))).to(self.device),
+                            torch.from_numpy(b.copy()).to(self.device))
+                    self.edge_t.append(edge)
+                    w, b, cout = ws, bs, 4 * cout
+                cfg = choose_cfg_h8(cin, cout, self.prec, level)
                 bm = L.rrin_conv_h8_cfg_bm(cfg)
                 nh = L.rrin_pack_conv3x3_h8_halves(cout, cin, bm)
                 whi = np.empty(nh, np.uint16)
@@ -181,7 +199,7 @@ class RRINEngine:
                     perm_arr.ctypes.data if perm_arr is not None else None, self.prec, whi.ctypes.data,
                     wlo.ctypes.data if wlo is not None else None, bp.ctypes.data, C.byref(inv)),
                     "rrin_pack_conv3x3_h8")
-                meta.append((hoff, hoff + nh if wlo is not None else None, boff, cfg, inv.value))
+                meta.append((hoff, hoff + nh if wlo is not None else None, boff, cfg, inv.value, edge))
                 halves.append(whi)
                 hoff += nh
                 if wlo is not None:
@@ -195,13 +213,17 @@ class RRINEngine:
         self.bias_blob = torch.from_numpy(np.concatenate(biases)).to(self.device)
         hb, bb = self.blob.data_ptr(), self.bias_blob.data_ptr()
         self.conv_table = (_lib.ConvWeights * len(meta))()
-        for i, (ho, lo, bo, cfg, inv) in enumerate(meta):
+        for i, (ho, lo, bo, cfg, inv, edge) in enumerate(meta):
             e = self.conv_table[i]
             e.whi = hb + 2 * ho
             e.wlo = hb + 2 * lo if lo is not None else None
             e.bias = bb + 4 * bo
             e.cfg = cfg
             e.inv_wscale = inv
+            if edge is not None:
+                e.subpixel = 1
+                e.wedge = edge[0].data_ptr()
+                e.bias_raw = edge[1].data_ptr()
         self.head_table = (_lib.HeadWeights * 4)()
         for i, (w, b) in enumerate(self.heads_t):
             self.head_table[i].w = w.data_ptr()

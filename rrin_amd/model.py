@@ -39,6 +39,10 @@ class Net(nn.Module):
         #   "fp32_split16" fp32 values as fp16 hi+lo pairs, 3 f16 MFMA products, fp32 accumulate
         #   "fp16"         fp16 storage and products, fp32 accumulate (BASELINE fp16 configs)
         self.precision = "fp32"
+        # fp32_split16 / fp16: up convs whose output level is <= this run as
+        # sub-pixel convs on the low-res input (upsample folded into the weights,
+        # no upsample pass); -1 = always an explicit upsample pass
+        self.subpixel_max_level = 2
         self.register_load_state_dict_post_hook(Net._on_load)
 
     # Packed weights are rebuilt after load_state_dict / .to() / param edits.
@@ -57,9 +61,10 @@ class Net(nn.Module):
     def engine(self):
         from .engine import RRINEngine
         if (self._engine is None or self._engine_version != self._weights_version
-                or self._engine.precision != self.precision):
+                or self._engine.precision != self.precision
+                or self._engine.subpixel_max_level != self.subpixel_max_level):
             self._engine = None  # free the previous packed weights first
-            self._engine = RRINEngine(self, self.precision)
+            self._engine = RRINEngine(self, self.precision, self.subpixel_max_level)
             self._engine_version = self._weights_version
         return self._engine
 

@@ -113,3 +113,21 @@ def _level_of(unet: UNet, tag: str) -> int:
         j = int(tag[2:tag.index(".")])
         return unet.depth - 2 - j
     return 0  # last
+
+
+def conv_bytes(unet: UNet, h: int, w: int, bytes_per_value: int = 4) -> tuple[int, int]:
+    """Algorithmic HBM bytes (read, written) of the 3x3 body convs of one UNet
+    forward (head excluded): each conv reads its input once and writes its
+    output once; a down block's second conv also writes the 2x2-pooled copy; an
+    up conv reads its input at low resolution (the x2 upsample is recomputable)."""
+    rd = wr = 0
+    for tag, conv in unet.conv_list():
+        if tag == "last":
+            continue
+        lvl = _level_of(unet, tag)
+        px = (h >> lvl) * (w >> lvl)
+        rd += conv.in_channels * (px // 4 if tag.endswith(".up") else px)
+        wr += conv.out_channels * px
+        if tag.startswith("down") and tag.endswith(".b") and lvl < unet.depth - 1:
+            wr += conv.out_channels * px // 4
+    return rd * bytes_per_value, wr * bytes_per_value

@@ -5,6 +5,7 @@ three exact fp16 products with fp32 accumulation (error ~2^-21 relative per
 product), so it is held to the fp32 tolerances.  fp16 is held to the SURVEY
 §8d fp16 gate: max-abs <= 1e-2 and PSNR >= 45 dB vs the fp32 CPU reference."""
 import ctypes as C
+from types import SimpleNamespace
 
 import numpy as np
 import pytest
@@ -186,3 +187,92 @@ def test_pack_g16(gpu, prec):
     tol = 2.0 ** -20 if prec == X3 else 2.0 ** -10
     assert float((out[:, :3] - i0).abs().max()) <= tol and float((out[:, 3:6] - i1).abs().max()) <= tol
     assert not out[:, 6:].any()
+
+
+def replicate_ring(t: H8Tensor):
+    """Edge-replicate an H8 tensor's interior into its 1-pixel padding ring (what
+    EPI_LEAKY_REP writes)."""
+    h, w = t.h, t.w
+    for a in (t.hi, t.lo):
+        if a is None:
+            continue
+        a[:, :, 0, 8:8 + w] = a[:, :, 1, 8:8 + w]
+        a[:, :, h + 1, 8:8 + w] = a[:, :, h, 8:8 + w]
+        a[:, :, 0:h + 2, 7] = a[:, :, 0:h + 2, 8]
+        a[:, :, 0:h + 2, 8 + w] = a[:, :, 0:h + 2, 7 + w]
+
+
+@pytest.mark.parametrize("prec", [X3, F16])
+def test_h8_leaky_rep_writes_replicated_ring(gpu, prec):
+    x = torch.rand(2, 32, 13, 45, device=gpu) * 2 - 1
+    wt, b = keyed_conv(32, 64, "rep")
+    ref = ref_conv(x, wt, b, 0.1)
+    for cfg in (0, 6):
+        dst, _ = conv_h8(H8Tensor.from_nchw(x, prec), wt, b, cfg, prec, epi=_lib.EPI_LEAKY_REP)
+        np.testing.assert_allclose(dst.to_nchw().cpu().double().numpy(), ref.numpy(), **TOL[prec])
+        # the ring must equal the replicated border; everything else in the padding stays zero
+        want = SimpleNamespace(h=dst.h, w=dst.w, hi=dst.hi.clone(), lo=dst.lo.clone() if dst.lo is not None else None)
+        for a in (want.hi, want.lo):
+            if a is not None:
+                a[:, :, 0] = 0
+                a[:, :, dst.h + 1:] = 0
+                a[:, :, :, :8] = 0
+                a[:, :, :, 8 + dst.w:] = 0
+        replicate_ring(want)
+        assert torch.equal(dst.hi, want.hi), f"cfg {cfg}"
+        if prec == X3:
+            assert torch.equal(dst.lo, want.lo)
+        assert dst.hi[:, :, 0, 7:9 + dst.w].any() and dst.hi[:, :, 1:dst.h + 1, 7].any()
+
+
+def subpixel_upconv(src: H8Tensor, w, b, cfg, prec, dst=None):
+    """EPI_SUBPIXEL conv + ring fix-up through the C ABI (the Net's up.1 conv)."""
+    lib = _lib.lib()
+    dev = src.hi.device
+    cout, cin = w.shape[:2]
+    wn = w.detach().cpu().float().contiguous().numpy()
+    bn = b.detach().cpu().float().contiguous().numpy()
+    ws = np.empty((4 * cout, cin, 3, 3), np.float32)
+    bs = np.empty(4 * cout, np.float32)
+    _lib.check(lib.rrin_subpixel_weights(wn.ctypes.data, bn.ctypes.data, cout, cin, ws.ctypes.data, bs.ctypes.data))
+    whi, wlo, bp, inv = pack_h8(torch.from_numpy(ws), torch.from_numpy(bs), cfg, prec, dev)
+    H_, W_ = 2 * src.h, 2 * src.w
+    if dst is None:
+        dst = H8Tensor(src.n, cout, H_, W_, dev, prec)
+    edge = torch.full((src.n, cout, lib.rrin_ring_pixels(H_, W_)), float("nan"), device=dev)
+    d = _lib.ConvH8Desc()
+    d.n, d.cin, d.cout, d.cfg, d.prec, d.epi_mode, d.slope, d.inv_wscale = (src.n, cin, 4 * cout, cfg, prec,
+                                                                            _lib.EPI_SUBPIXEL, 0.1, inv)
+    d.src, d.dst = src.view(0, cin), dst.view(0, cout)
+    d.whi, d.wlo, d.bias = whi.data_ptr(), wlo.data_ptr() if prec == X3 else None, bp.data_ptr()
+    d.edge = edge.data_ptr()
+    _lib.check(lib.rrin_conv3x3_h8_fwd(C.byref(d), H.stream(dev)), "rrin_conv3x3_h8_fwd(subpixel)")
+    wedge = torch.from_numpy(np.ascontiguousarray(wn.transpose(1, 2, 3, 0))).to(dev)
+    braw = torch.from_numpy(bn.copy()).to(dev)
+    e = _lib.EdgeFixDesc()
+    e.n, e.cin, e.cout, e.prec, e.epi_mode, e.slope = src.n, cin, cout, prec, _lib.EPI_LINEAR, 0.1
+    e.src, e.dst = src.view(0, cin), dst.view(0, cout)
+    e.edge, e.wedge, e.bias = edge.data_ptr(), wedge.data_ptr(), braw.data_ptr()
+    _lib.check(lib.rrin_subpixel_edge_fix_h8(C.byref(e), H.stream(dev)), "rrin_subpixel_edge_fix_h8")
+    torch.cuda.synchronize(dev)
+    return dst
+
+
+@pytest.mark.parametrize("prec", [X3, F16])
+@pytest.mark.parametrize("n,cin,cout,sh,sw", [(2, 64, 32, 20, 36), (1, 128, 64, 23, 40), (1, 256, 128, 5, 7),
+                                              (2, 512, 256, 3, 5), (1, 64, 32, 1, 1)])
+def test_h8_subpixel_upconv(gpu, prec, n, cin, cout, sh, sw):
+    """conv3x3(upsample_x2(x)) of the up block (unet.py:77-78) as one low-res
+    sub-pixel conv + ring fix-up, against upsample-then-conv in float64."""
+    x = torch.rand(n, cin, sh, sw, device=gpu) * 2 - 1
+    wt, b = keyed_conv(cin, cout, "sub")
+    up = F.interpolate(x.double().cpu(), scale_factor=2, mode="bilinear", align_corners=False)
+    ref = F.conv2d(up, wt.double().cpu(), b.double().cpu(), padding=1)
+    src = H8Tensor.from_nchw(x, prec)
+    replicate_ring(src)
+    for cfg in cfgs(prec, 4 * cout):
+        dst = subpixel_upconv(src, wt, b, cfg, prec, dst=H8Tensor(n, 2 * cout, 2 * sh, 2 * sw, gpu, prec))
+        np.testing.assert_allclose(dst.to_nchw(0, cout).cpu().double().numpy(), ref.numpy(), **TOL[prec],
+                                   err_msg=f"cfg {cfg}")
+        assert not dst.to_nchw(cout, cout).any()           # the bridge half of CAT is untouched
+        assert not dst.hi[:, :, 0].any() and not dst.hi[:, :, :, :8].any()  # zero padding kept

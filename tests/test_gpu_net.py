@@ -152,3 +152,19 @@ def test_interpolate_reuses_flow(gpu, precision):
         single = [net(i0, i1, t) for t in ts]
     for a, b in zip(many, single):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("precision", ["fp32_split16", "fp16"])
+@pytest.mark.parametrize("level", [-1, 0, 3])
+def test_subpixel_levels_agree(gpu, golden, precision, level):
+    """Folding the upsample into the up convs (sub-pixel levels 0..level) gives the
+    reference result at every setting; -1 = explicit upsample pass everywhere.
+    The 80x112 golden has odd low-res sizes (5x7 bottom)."""
+    g = golden("net_odd")
+    net = make_net(gpu, stress=False)
+    net.precision = precision
+    net.subpixel_max_level = level
+    i0, i1 = torch.from_numpy(g["i0"]).to(gpu), torch.from_numpy(g["i1"]).to(gpu)
+    with torch.no_grad():
+        err = maxabs(net(i0, i1, 0.5).cpu(), g["out_t050"])
+    assert err <= (1e-4 if precision == "fp32_split16" else 1e-2), f"level {level}: {err:.3e}"

@@ -26,11 +26,15 @@ from rrin_amd.synthetic import keyed_state_dict, synthetic_batch  # noqa: E402
 UNETS = [("Flow", 6, 5), ("refine_flow", 10, 4), ("Mask", 16, 4), ("final", 9, 4)]
 
 
-def schedule(h, w, h8=False):
-    """(unet, tag, cin, cout, level, src_mode, epi) in rrin_net_fwd launch order
-    (h8: the split/fp16 path launches an upsample pass before every up.1 conv)."""
+def schedule(h, w, h8=False, sub_max_level=2):
+    """(unet, tag, cin, cout, level, src_mode, epi) in rrin_net_fwd launch order.
+    h8 (split/fp16 path): an up conv at level <= sub_max_level is a sub-pixel
+    conv on the low-res input (src 2, epi 4, cout = real channels) followed by
+    its ring fix-up, and its producer writes edge-replicated (epi 3); other up
+    convs follow an explicit upsample pass."""
     out = [("-", "pack", 0, 0, 0, -1, -1)]
     for name, cin0, D in UNETS:
+        sub = [h8 and L <= sub_max_level for L in range(D)]
         for L in range(D):
             C_ = 32 << L
             cin = (32 << (L - 1)) if L else cin0
@@ -39,14 +43,18 @@ def schedule(h, w, h8=False):
                 out.append((name, f"down{L}.b", C_, C_, L, 0, 2))
             else:
                 out.append((name, f"down{L}.b", C_, C_, L, 0, 1))
-                out.append((name, "mid", C_, C_, L, 0, 1))
+                out.append((name, "mid", C_, C_, L, 0, 3 if sub[D - 2] else 1))
         for L in range(D - 2, -1, -1):
             C_ = 32 << L
-            if h8:
-                out.append((name, f"up{L}.ups", 0, 0, L, -1, -1))
-            out.append((name, f"up{L}.up", 2 * C_, C_, L, 0 if h8 else 1, 0))
+            if sub[L]:
+                out.append((name, f"up{L}.sub", 2 * C_, C_, L, 2, 4))
+                out.append((name, f"up{L}.ring", 0, 0, L, -3, -3))
+            else:
+                if h8:
+                    out.append((name, f"up{L}.ups", 0, 0, L, -1, -1))
+                out.append((name, f"up{L}.up", 2 * C_, C_, L, 0 if h8 else 1, 0))
             out.append((name, f"up{L}.a", 2 * C_, C_, L, 0, 1))
-            out.append((name, f"up{L}.b", C_, C_, L, 0, 1))
+            out.append((name, f"up{L}.b", C_, C_, L, 0, 3 if (L > 0 and sub[L - 1]) else 1))
         out.append((name, "head", 32, 0, 0, -2, -2))
     return out
 
@@ -83,7 +91,7 @@ def breakdown(args):
         for i in range(cnt.value):
             tot.setdefault(i, []).append((kinds[i], ms[i], fl[i]))
     lib.rrin_prof_destroy(h)
-    sch = schedule(args.height, args.width, args.precision != "fp32")
+    sch = schedule(args.height, args.width, args.precision != "fp32", net.subpixel_max_level)
     rows = []
     conv_i = 0
     for i, entry in enumerate(sch):
@@ -124,19 +132,24 @@ def tune_h8(args):
     results = []
     for cin, cout, L, src, epi in shapes:
         h, w = args.height >> L, args.width >> L
-        x = H8Tensor.from_nchw(torch.rand(n, cin, h, w, device=dev) * 2 - 1, prec)
+        kout = 4 * cout if epi == 4 else cout          # sub-pixel: 4 phase rows per channel, low-res grid
+        hs, ws_ = (h // 2, w // 2) if epi == 4 else (h, w)
+        x = H8Tensor.from_nchw(torch.rand(n, cin, hs, ws_, device=dev) * 2 - 1, prec)
         dst = H8Tensor(n, cout, h, w, dev, prec)
         pool = H8Tensor(n, cout, h // 2, w // 2, dev, prec) if epi == 2 else None
-        wt = torch.randn(cout, cin, 3, 3) / (3 * cin ** 0.5)
-        b = torch.zeros(cout)
+        edge = torch.zeros(n, cout, lib.rrin_ring_pixels(h, w), device=dev) if epi == 4 else None
+        wt = torch.randn(kout, cin, 3, 3) / (3 * cin ** 0.5)
+        b = torch.zeros(kout)
         best, line = None, []
         for cfg in range(lib.rrin_conv_h8_cfg_count()):
-            if not lib.rrin_conv_h8_cfg_ok(cfg, prec) or lib.rrin_conv_h8_cfg_bm(cfg) > max(32, 2 * cout):
+            if not lib.rrin_conv_h8_cfg_ok(cfg, prec) or lib.rrin_conv_h8_cfg_bm(cfg) > max(32, 2 * kout):
                 continue
             whi, wlo, bp, inv = pack_h8(wt, b, cfg, prec, dev)
             d = _lib.ConvH8Desc()
-            d.n, d.cin, d.cout, d.cfg, d.prec, d.epi_mode, d.slope, d.inv_wscale = n, cin, cout, cfg, prec, epi, 0.1, inv
+            d.n, d.cin, d.cout, d.cfg, d.prec, d.epi_mode, d.slope, d.inv_wscale = n, cin, kout, cfg, prec, epi, 0.1, inv
             d.src, d.dst = x.view(0, cin), dst.view(0, cout)
+            if edge is not None:
+                d.edge = edge.data_ptr()
             if pool is not None:
                 d.pool = pool.view(0, cout)
             d.whi, d.wlo, d.bias = whi.data_ptr(), wlo.data_ptr(), bp.data_ptr()

@@ -28,7 +28,7 @@ STEPS=${STEPS:-tests,smoke,bench,prof}
 [[ $STEPS == *tsplit* ]] && run tune_split 600 python tools/conv_lab.py tune --precision fp32_split16 --out gpurun_out/tune_split.json
 [[ $STEPS == *tfp16* ]] && run tune_fp16 600 python tools/conv_lab.py tune --precision fp16 --out gpurun_out/tune_fp16.json
 [[ $STEPS == *dsplit* ]] && run breakdown_split 300 python tools/conv_lab.py breakdown --precision fp32_split16 --out gpurun_out/breakdown_split.json
-[[ $STEPS == *prof* ]] && run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --cpu-baseline off
+[[ $STEPS == *prof* ]] && run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --cpu-baseline off --no-alt
 if [[ $STEPS == *sqc* ]]; then
   for shp in "512 256 3 1 0" "32 32 0 1 1" "128 128 2 1 0"; do
     tag=$(echo $shp | tr ' ' '_')
@@ -36,8 +36,10 @@ if [[ $STEPS == *sqc* ]]; then
   done
 fi
 if [[ $STEPS == *pmc* ]]; then
-  run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 2 --warmup 1 --cpu-baseline off --no-prof
-  run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --steps 2 --warmup 1 --cpu-baseline off --no-prof
-  python tools/pmc_summary.py --fetch gpurun_out/pmc_fetch --write gpurun_out/pmc_write --steps 3 --out gpurun_out/traffic.json > gpurun_out/pmc_summary.log 2>&1; cat gpurun_out/pmc_summary.log
+  for prec in ${PMCPREC:-fp32_split16 fp32 fp16}; do
+    run pmc_fetch_$prec 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch_$prec -o run -- python3 bench.py --steps 2 --warmup 1 --cpu-baseline off --no-prof --no-alt --precision $prec
+    run pmc_write_$prec 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write_$prec -o run -- python3 bench.py --steps 2 --warmup 1 --cpu-baseline off --no-prof --no-alt --precision $prec
+    python tools/pmc_summary.py --fetch gpurun_out/pmc_fetch_$prec --write gpurun_out/pmc_write_$prec --steps 3 --out gpurun_out/traffic_$prec.json --table gpurun_out/pmc_traffic.json --precision $prec > gpurun_out/pmc_summary_$prec.log 2>&1; cat gpurun_out/pmc_summary_$prec.log
+  done
 fi
 exit 0

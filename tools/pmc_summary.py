@@ -42,6 +42,10 @@ def main():
     ap.add_argument("--write", required=True)
     ap.add_argument("--steps", type=int, required=True, help="Net.forward calls in the profiled run")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--table", default=None,
+                    help="merge the conv family's per-launch bytes into this table (read by bench.py)")
+    ap.add_argument("--precision", default="fp32_split16")
+    ap.add_argument("--config", default="1280x720x4", help="WxHxB of the profiled bench run")
     a = ap.parse_args()
     fetch = load(a.fetch, "FETCH_SIZE")
     write = load(a.write, "WRITE_SIZE")
@@ -63,6 +67,16 @@ def main():
     if a.out:
         json.dump({"correction": "hbm = (2*FETCH_SIZE + WRITE_SIZE) KiB (gfx950 FETCH_SIZE = 1/2 of wide reads)",
                    "steps": a.steps, "kernels": res}, open(a.out, "w"), indent=1)
+    if a.table:
+        fam_name = "conv3x3_mfma_kernel" if a.precision == "fp32" else "conv3x3_h8_kernel"
+        tab = json.load(open(a.table)) if os.path.exists(a.table) else {}
+        r = res[fam_name]
+        tab[f"{a.precision}@{a.config}"] = {
+            "kernel_family": fam_name, "hbm_bytes_per_launch": r["hbm_bytes_per_dispatch"],
+            "hbm_bytes_per_step": r["hbm_bytes_per_step"], "launches_per_step": r["dispatches_per_step"],
+            "correction": "hbm = (2*FETCH_SIZE + WRITE_SIZE) KiB, separate --pmc passes",
+            "source": os.path.basename(os.path.normpath(a.fetch)) + " + " + os.path.basename(os.path.normpath(a.write))}
+        json.dump(tab, open(a.table, "w"), indent=1, sort_keys=True)
 
 
 if __name__ == "__main__":
