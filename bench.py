@@ -34,7 +34,7 @@ sys.path.insert(0, REPO)
 from rrin_amd import Net, _lib  # noqa: E402
 from rrin_amd.shard import gather_frames  # noqa: E402
 from rrin_amd.synthetic import keyed_state_dict, synthetic_batch  # noqa: E402
-from rrin_amd.unet import conv_bytes, conv_flops  # noqa: E402
+from rrin_amd.unet import conv_bytes, conv_flops, roofline_bound_s  # noqa: E402
 
 FP32_PEAK_TFLOPS = 157.3   # MI355X dense fp32 (MFMA 32x32x2 f32 = VALU rate), MI355X_MICROARCH.md
 F16_PEAK_TFLOPS = 2500.0   # dense f16 MFMA (v_mfma_f32_32x32x16_f16), no sparsity
@@ -210,6 +210,12 @@ def main():
                     "head_ms_per_step": round(head_ms_step, 3),
                     "layout_upsample_ms_per_step": round(other_ms / args.steps, 3),
                     "subpixel_ring_fix_ms_per_step": round(edge_ms / args.steps, 3)}
+        # SURVEY §8d per-layer bound: sum_l max(FLOP_l / peak, bytes_l / 8 TB/s) over the body convs
+        bpv = 2 if args.precision == "fp16" else 4
+        tlb = B * sum(roofline_bound_s(getattr(net, u), H, W, bpv, peak * 1e12, HBM_PEAK_GBS * 1e9)
+                      for u in ("Flow", "refine_flow", "Mask", "final"))
+        roofline["t_lb_conv_ms_per_step"] = round(1e3 * tlb, 3)
+        roofline["t_lb_frac_of_conv_time"] = round(1e3 * tlb / conv_ms_step, 4)
 
     if roofline is not None:
         # HBM bytes per conv launch from the PMC passes of the same command

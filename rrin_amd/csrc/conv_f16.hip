@@ -29,6 +29,7 @@ namespace rrin {
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float float2v __attribute__((ext_vector_type(2)));
 
 constexpr int H8_LC = 34;  // staged input row: records of pixels x0-1 .. x0+32
 
@@ -785,7 +786,8 @@ struct HeadH8Args {
 
 template <int COUT, int MODE, int PLANES>
 __global__ void __launch_bounds__(256) head_h8_kernel(HeadH8Args a) {
-  constexpr int CIN = 32, HROWS = 10, HLC = 40;
+  // tile 16 rows x 32 cols; thread = 2 vertically adjacent pixels (packed fp32 FMA)
+  constexpr int CIN = 32, HROWS = 18, HLC = 40;
   __shared__ __attribute__((aligned(16))) float s_in[8 * HROWS * HLC];
   const int tid = threadIdx.x;
   int bid = blockIdx.x;
@@ -793,111 +795,200 @@ __global__ void __launch_bounds__(256) head_h8_kernel(HeadH8Args a) {
   bid /= a.tiles_x;
   const int ty = bid % a.tiles_y;
   const int img = bid / a.tiles_y;
-  const int x0 = tx * 32, y0 = ty * 8;
-  const int r = tid >> 5, xl = tid & 31;
+  const int x0 = tx * 32, y0 = ty * 16;
+  const int r2 = 2 * (tid >> 5), xl = tid & 31;
 
-  float acc[COUT];
+  // weights are wave-uniform: scalar loads, no LDS traffic
+  float2v acc2[COUT];
 #pragma unroll
-  for (int co = 0; co < COUT; ++co) acc[co] = a.bias[co];
-
+  for (int co = 0; co < COUT; ++co) acc2[co] = float2v{a.bias[co], a.bias[co]};
+  // records of rows y0-1..y0+16, cols x0-1..x0+32 of one channel group, fetched
+  // one group ahead into registers, then converted to fp32 planar LDS
+  constexpr int kRec = HROWS * H8_LC, kIt = (kRec + 255) / 256;
+  uint4 pre[kIt][PLANES];
+  auto fetch = [&](int g) {
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) {
+      const int idx = tid + 256 * it;
+      if (idx < kRec) {
+        const int rr = idx / H8_LC, col = idx - rr * H8_LC;
+        const int64_t rec = img * a.src_img + (int64_t)g * a.src_gp + (int64_t)(y0 + rr) * a.src_wp + x0 +
+                            (kH8PadLeft - 1) + col;
+        pre[it][0] = a.src_hi[rec];
+        if constexpr (PLANES == 2) pre[it][1] = a.src_lo[rec];
+      }
+    }
+  };
+  fetch(0);
   for (int g = 0; g < CIN / 8; ++g) {
-    // stage records of rows y0-1..y0+8, cols x0-1..x0+32 -> fp32 planar LDS
-    for (int idx = tid; idx < HROWS * H8_LC; idx += 256) {
-      const int rr = idx / H8_LC, col = idx - rr * H8_LC;
-      const int64_t rec = img * a.src_img + (int64_t)g * a.src_gp + (int64_t)(y0 + rr) * a.src_wp + x0 +
-                          (kH8PadLeft - 1) + col;
-      const half8 vh = __builtin_bit_cast(half8, a.src_hi[rec]);
-      half8 vl = {};
-      if constexpr (PLANES == 2) vl = __builtin_bit_cast(half8, a.src_lo[rec]);
 #pragma unroll
-      for (int e = 0; e < 8; ++e)
-        s_in[(e * HROWS + rr) * HLC + col + 3] = PLANES == 2 ? join(vh[e], vl[e]) : (float)vh[e];
+    for (int it = 0; it < kIt; ++it) {
+      const int idx = tid + 256 * it;
+      if (idx < kRec) {
+        const int rr = idx / H8_LC, col = idx - rr * H8_LC;
+        const half8 vh = __builtin_bit_cast(half8, pre[it][0]);
+        half8 vl = {};
+        if constexpr (PLANES == 2) vl = __builtin_bit_cast(half8, pre[it][PLANES - 1]);
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          s_in[(e * HROWS + rr) * HLC + col + 3] = PLANES == 2 ? join(vh[e], vl[e]) : (float)vh[e];
+      }
     }
     __syncthreads();
+    if (g + 1 < CIN / 8) fetch(g + 1);
 #pragma unroll
-    for (int ci = 0; ci < 8; ++ci)
+    for (int ci = 0; ci < 8; ++ci) {
+      float rows[4][3];  // input rows r2-1 .. r2+2 (staged rows r2 .. r2+3), cols xl-1 .. xl+1
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) rows[k][kx] = s_in[(ci * HROWS + r2 + k) * HLC + xl + 3 + kx];
 #pragma unroll
       for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
         for (int kx = 0; kx < 3; ++kx) {
-          const float v = s_in[(ci * HROWS + r + ky) * HLC + xl + 3 + kx];
+          const float2v v = {rows[ky][kx], rows[ky + 1][kx]};
 #pragma unroll
-          for (int co = 0; co < COUT; ++co)
-            acc[co] = fmaf(a.w[((co * CIN) + g * 8 + ci) * 9 + ky * 3 + kx], v, acc[co]);
+          for (int co = 0; co < COUT; ++co) {
+            const float w = a.w[((co * CIN) + g * 8 + ci) * 9 + ky * 3 + kx];
+            acc2[co] = __builtin_elementwise_fma(float2v{w, w}, v, acc2[co]);
+          }
         }
+    }
     __syncthreads();
   }
 
-  const int y = y0 + r, x = x0 + xl;
-  if (y >= a.h || x >= a.w_) return;
-  auto idx_of = [&](int ch, int yy, int xx) { return h8_half_index(a.g_img, a.g_gp, a.g_wp, img, ch, yy, xx); };
-  auto rd = [&](int ch, int yy, int xx) -> float {
-    const int64_t k = idx_of(ch, yy, xx);
-    return PLANES == 2 ? join(a.g_hi[k], a.g_lo[k]) : (float)a.g_hi[k];
+  for (int p = 0; p < 2; ++p) {
+  float acc[COUT];
+#pragma unroll
+  for (int co = 0; co < COUT; ++co) acc[co] = acc2[co][p];
+  const int y = y0 + r2 + p, x = x0 + xl;
+  if (y >= a.h || x >= a.w_) continue;
+  // Net buffer records of this pixel: group 0 = ch 0-7, group 1 = ch 8-15
+  const int64_t rec0 = img * a.g_img + (int64_t)(y + 1) * a.g_wp + x + kH8PadLeft, rec1 = rec0 + a.g_gp;
+  uint4* ghi = reinterpret_cast<uint4*>(a.g_hi);
+  uint4* glo = reinterpret_cast<uint4*>(a.g_lo);
+  auto load8 = [&](int64_t rec, float* v) {
+    const half8 h = __builtin_bit_cast(half8, ghi[rec]);
+    half8 l = {};
+    if constexpr (PLANES == 2) l = __builtin_bit_cast(half8, glo[rec]);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = PLANES == 2 ? join(h[e], l[e]) : (float)h[e];
   };
-  auto wr = [&](int ch, float v) {
-    const int64_t k = idx_of(ch, y, x);
-    const _Float16 vh = (_Float16)v;
-    a.g_hi[k] = vh;
-    if constexpr (PLANES == 2) a.g_lo[k] = lo_of(v, vh);
+  // n consecutive channels starting at half `e0` of record `rec` (one 2/4/8/16-B store per plane)
+  auto store = [&](int64_t rec, int e0, const float* v, int n) {
+    _Float16 hv[8], lv[8];
+    for (int e = 0; e < n; ++e) {
+      hv[e] = (_Float16)v[e];
+      lv[e] = lo_of(v[e], hv[e]);
+    }
+    _Float16* ph = reinterpret_cast<_Float16*>(ghi + rec) + e0;
+    _Float16* pl = reinterpret_cast<_Float16*>(glo + rec) + e0;
+    if (n == 8) {
+      *reinterpret_cast<uint4*>(ph) = __builtin_bit_cast(uint4, hv);
+      if constexpr (PLANES == 2) *reinterpret_cast<uint4*>(pl) = __builtin_bit_cast(uint4, lv);
+    } else if (n == 2) {
+      *reinterpret_cast<uint32_t*>(ph) = (uint32_t)__builtin_bit_cast(uint16_t, hv[0]) |
+                                         ((uint32_t)__builtin_bit_cast(uint16_t, hv[1]) << 16);
+      if constexpr (PLANES == 2)
+        *reinterpret_cast<uint32_t*>(pl) = (uint32_t)__builtin_bit_cast(uint16_t, lv[0]) |
+                                           ((uint32_t)__builtin_bit_cast(uint16_t, lv[1]) << 16);
+    } else {
+      for (int e = 0; e < n; ++e) {
+        ph[e] = hv[e];
+        if constexpr (PLANES == 2) pl[e] = lv[e];
+      }
+    }
   };
   const float* cf = a.coef + img * 8;
 
   if constexpr (MODE == RRIN_HEAD_PLAIN) {
-#pragma unroll
-    for (int co = 0; co < COUT; ++co) wr(co, acc[co]);
+    for (int co = 0; co < COUT; ++co) {
+      const int64_t k = h8_half_index(a.g_img, a.g_gp, a.g_wp, img, co, y, x);
+      const _Float16 vh = (_Float16)acc[co];
+      a.g_hi[k] = vh;
+      if constexpr (PLANES == 2) a.g_lo[k] = lo_of(acc[co], vh);
+    }
   } else if constexpr (MODE == RRIN_HEAD_FLOW) {
 #pragma clang fp contract(off)
     // round the raw flow to its stored form first, so that a later t-blend of the
     // kept raw flow (skip_flow) reproduces these Ft bit for bit
+    _Float16 rh[4], rl[4];
     for (int k = 0; k < 4; ++k) {
-      const _Float16 vh = (_Float16)acc[k];
-      const _Float16 vl = lo_of(acc[k], vh);
-      acc[k] = PLANES == 2 ? join(vh, vl) : (float)vh;
-      if (a.fr_hi) {
-        const int64_t kk = h8_half_index(a.fr_img, a.fr_gp, a.fr_wp, img, k, y, x);
-        a.fr_hi[kk] = vh;
-        if constexpr (PLANES == 2) a.fr_lo[kk] = vl;
-      }
+      rh[k] = (_Float16)acc[k];
+      rl[k] = lo_of(acc[k], rh[k]);
+      acc[k] = PLANES == 2 ? join(rh[k], rl[k]) : (float)rh[k];
     }
+    if (a.fr_hi) {
+      const int64_t kk = h8_half_index(a.fr_img, a.fr_gp, a.fr_wp, img, 0, y, x);
+      *reinterpret_cast<uint2*>(a.fr_hi + kk) = __builtin_bit_cast(uint2, rh);
+      if constexpr (PLANES == 2) *reinterpret_cast<uint2*>(a.fr_lo + kk) = __builtin_bit_cast(uint2, rl);
+    }
+    float f0[2], f1[2];
     for (int k = 0; k < 2; ++k) {
-      wr(6 + k, cf[0] * acc[k] + cf[1] * acc[2 + k]);
-      wr(8 + k, cf[2] * acc[k] - cf[3] * acc[2 + k]);
+      f0[k] = cf[0] * acc[k] + cf[1] * acc[2 + k];
+      f1[k] = cf[2] * acc[k] - cf[3] * acc[2 + k];
     }
+    store(rec0, 6, f0, 2);
+    store(rec1, 0, f1, 2);
   } else if constexpr (MODE == RRIN_HEAD_REFINE) {
 #pragma clang fp contract(off)
-    const float f0u = rd(6, y, x) + acc[0], f0v = rd(7, y, x) + acc[1];
-    const float f1u = rd(8, y, x) + acc[2], f1v = rd(9, y, x) + acc[3];
-    wr(6, f0u);
-    wr(7, f0v);
-    wr(8, f1u);
-    wr(9, f1v);
-    const WarpTaps t0 = warp_taps(x, y, f0u, f0v, a.h, a.w_);
-    const WarpTaps t1 = warp_taps(x, y, f1u, f1v, a.h, a.w_);
+    float g0[8], g1[8];
+    load8(rec0, g0);
+    load8(rec1, g1);
+    const float f0[2] = {g0[6] + acc[0], g0[7] + acc[1]};
+    float o1[8];
+    o1[0] = g1[0] + acc[2];
+    o1[1] = g1[1] + acc[3];
+    const WarpTaps t0 = warp_taps(x, y, f0[0], f0[1], a.h, a.w_);
+    const WarpTaps t1 = warp_taps(x, y, o1[0], o1[1], a.h, a.w_);
+    // backwarp x0 (ch 0-2) with Ft0 and x1 (ch 3-5) with Ft1: one record load per tap and plane
+    auto warp3 = [&](const WarpTaps& t, int c0, float* o) {
+      float q[4][8];
+      const bool ok[4] = {t.vy0 && t.vx0, t.vy0 && t.vx1, t.vy1 && t.vx0, t.vy1 && t.vx1};
 #pragma unroll
-    for (int ch = 0; ch < 3; ++ch) {
-      wr(10 + ch, warp_apply_f(t0, [&](int yy, int xx) { return rd(ch, yy, xx); }));
-      wr(13 + ch, warp_apply_f(t1, [&](int yy, int xx) { return rd(3 + ch, yy, xx); }));
-    }
+      for (int k = 0; k < 4; ++k) {
+        if (ok[k]) {
+          load8(img * a.g_img + (int64_t)(t.y0 + (k >> 1) + 1) * a.g_wp + t.x0 + (k & 1) + kH8PadLeft, q[k]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) q[k][e] = 0.0f;
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+        o[c] = q[0][c0 + c] * t.nw + q[1][c0 + c] * t.ne + q[2][c0 + c] * t.sw + q[3][c0 + c] * t.se;
+    };
+    warp3(t0, 0, o1 + 2);
+    warp3(t1, 3, o1 + 5);
+    store(rec0, 6, f0, 2);
+    store(rec1, 0, o1, 8);
   } else if constexpr (MODE == RRIN_HEAD_MASK) {
 #pragma clang fp contract(off)
+    float g1[8];
+    load8(rec1, g1);
     const float m0 = 1.0f / (1.0f + expf(-acc[0]));
     const float m1 = 1.0f / (1.0f + expf(-acc[1]));
     const float w1 = cf[4] * m0, w2 = cf[5] * m1;
     const float den = w1 + w2 + 1e-8f;
     float o[3];
 #pragma unroll
-    for (int ch = 0; ch < 3; ++ch) o[ch] = (w1 * rd(10 + ch, y, x) + w2 * rd(13 + ch, y, x)) / den;
-#pragma unroll
-    for (int ch = 0; ch < 3; ++ch) wr(6 + ch, o[ch]);
+    for (int ch = 0; ch < 3; ++ch) o[ch] = (w1 * g1[2 + ch] + w2 * g1[5 + ch]) / den;
+    store(rec0, 6, o, 2);
+    store(rec1, 0, o + 2, 1);
   } else {  // FINAL
 #pragma clang fp contract(off)
+    float g0[8], g1[8];
+    load8(rec0, g0);
+    load8(rec1, g1);
+    const float base[3] = {g0[6], g0[7], g1[0]};
     float* o = a.out + ((int64_t)img * 3) * a.h * a.w_ + (int64_t)y * a.w_ + x;
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch) {
-      const float v = acc[ch] + rd(6 + ch, y, x);
+      const float v = acc[ch] + base[ch];
       o[(int64_t)ch * a.h * a.w_] = v < 0.0f ? 0.0f : (v > 1.0f ? 1.0f : v);
     }
+  }
   }
 }
 
@@ -1386,7 +1477,7 @@ extern "C" int rrin_head_h8_fwd(const rrin_head_h8_desc* d, void* stream) {
   a.h = h;
   a.w_ = w;
   a.tiles_x = (w + 31) / 32;
-  a.tiles_y = (h + 7) / 8;
+  a.tiles_y = (h + 15) / 16;
   const int grid = a.tiles_x * a.tiles_y * d->n;
   hipStream_t st = (hipStream_t)stream;
   switch (d->mode) {

@@ -115,19 +115,33 @@ def _level_of(unet: UNet, tag: str) -> int:
     return 0  # last
 
 
-def conv_bytes(unet: UNet, h: int, w: int, bytes_per_value: int = 4) -> tuple[int, int]:
-    """Algorithmic HBM bytes (read, written) of the 3x3 body convs of one UNet
-    forward (head excluded): each conv reads its input once and writes its
-    output once; a down block's second conv also writes the 2x2-pooled copy; an
-    up conv reads its input at low resolution (the x2 upsample is recomputable)."""
-    rd = wr = 0
+def conv_work(unet: UNet, h: int, w: int, bytes_per_value: int = 4):
+    """Per body conv (head excluded): (tag, algorithmic FLOPs, bytes read, bytes
+    written).  Each conv reads its input once and writes its output once; a down
+    block's second conv also writes the 2x2-pooled copy; an up conv reads its
+    input at low resolution (the x2 upsample is recomputable)."""
+    out = []
     for tag, conv in unet.conv_list():
         if tag == "last":
             continue
         lvl = _level_of(unet, tag)
         px = (h >> lvl) * (w >> lvl)
-        rd += conv.in_channels * (px // 4 if tag.endswith(".up") else px)
-        wr += conv.out_channels * px
+        rd = conv.in_channels * (px // 4 if tag.endswith(".up") else px)
+        wr = conv.out_channels * px
         if tag.startswith("down") and tag.endswith(".b") and lvl < unet.depth - 1:
             wr += conv.out_channels * px // 4
-    return rd * bytes_per_value, wr * bytes_per_value
+        fl = 2 * conv.out_channels * conv.in_channels * 9 * px
+        out.append((tag, fl, rd * bytes_per_value, wr * bytes_per_value))
+    return out
+
+
+def conv_bytes(unet: UNet, h: int, w: int, bytes_per_value: int = 4) -> tuple[int, int]:
+    """Algorithmic HBM bytes (read, written) of the body convs of one UNet forward."""
+    work = conv_work(unet, h, w, bytes_per_value)
+    return sum(r for _, _, r, _ in work), sum(wb for _, _, _, wb in work)
+
+
+def roofline_bound_s(unet: UNet, h: int, w: int, bytes_per_value: int, peak_flops: float, bw: float) -> float:
+    """Per-layer roofline bound T_LB = sum over body convs of max(FLOP/peak, bytes/BW)
+    (SURVEY §8d), in seconds for one image."""
+    return sum(max(fl / peak_flops, (r + wb) / bw) for _, fl, r, wb in conv_work(unet, h, w, bytes_per_value))

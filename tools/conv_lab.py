@@ -66,6 +66,16 @@ def breakdown(args):
     net = net.to(dev).eval()
     net.precision = args.precision
     eng = net.engine()
+    if args.first_cfg is not None:
+        # the first conv of each U-Net is entry 0 of its block of the table; a config
+        # with the same BM shares the weight packing, so it can be swapped in place
+        k = 0
+        for name, _, D in UNETS:
+            e = eng.conv_table[k]
+            if _lib.lib().rrin_conv_h8_cfg_bm(e.cfg) == _lib.lib().rrin_conv_h8_cfg_bm(args.first_cfg):
+                e.cfg = args.first_cfg
+                eng.cfgs[k] = args.first_cfg
+            k += 2 * D + 1 + 3 * (D - 1)
     lib = _lib.lib()
     i0, i1 = synthetic_batch(args.batch, args.height, args.width)
     i0, i1 = i0.to(dev), i1.to(dev)
@@ -272,6 +282,8 @@ def main():
     ap.add_argument("--width", type=int, default=1280)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--first-cfg", type=int, default=None,
+                    help="breakdown: run the first conv of every U-Net with this H8 config (same BM only)")
     ap.add_argument("--precision", default="fp32", choices=["fp32", "fp32_split16", "fp16"])
     args = ap.parse_args()
     {"breakdown": breakdown, "tune": tune, "single": single}[args.mode](args)

@@ -28,6 +28,7 @@ STEPS=${STEPS:-tests,smoke,bench,prof}
 [[ $STEPS == *tsplit* ]] && run tune_split 600 python tools/conv_lab.py tune --precision fp32_split16 --out gpurun_out/tune_split.json
 [[ $STEPS == *tfp16* ]] && run tune_fp16 600 python tools/conv_lab.py tune --precision fp16 --out gpurun_out/tune_fp16.json
 [[ $STEPS == *dsplit* ]] && run breakdown_split 300 python tools/conv_lab.py breakdown --precision fp32_split16 --out gpurun_out/breakdown_split.json
+[[ $STEPS == *dfirst* ]] && run breakdown_first1 300 python tools/conv_lab.py breakdown --precision fp32_split16 --first-cfg 1
 [[ $STEPS == *prof* ]] && run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --cpu-baseline off --no-alt
 if [[ $STEPS == *sqc* ]]; then
   for shp in "512 256 3 1 0" "32 32 0 1 1" "128 128 2 1 0"; do
