@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define RRIN_ABI_VERSION 4
+#define RRIN_ABI_VERSION 5
 
 #define RRIN_OK 0
 #define RRIN_E_SHAPE (-1)     /* H or W not a multiple of 16, or N < 1          */
@@ -181,6 +181,9 @@ int rrin_conv_h8_cfg_count(void);
 int rrin_conv_h8_cfg_bm(int32_t cfg);
 int rrin_conv_h8_cfg_th(int32_t cfg);
 int rrin_conv_h8_cfg_ok(int32_t cfg, int32_t prec); /* 1 if the config fits LDS at prec */
+/* 1 if the config can run a conv with cin input channels (a config that keeps
+ * every weight chunk resident in LDS needs them to fit) */
+int rrin_conv_h8_cfg_fits(int32_t cfg, int32_t prec, int32_t cin);
 int rrin_conv3x3_h8_fwd(const rrin_conv_h8_desc* d, void* stream);
 
 /* Host packing: [co_block][chunk of 16 ci][tap][half][bm][8] halves, weights

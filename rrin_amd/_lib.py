@@ -9,7 +9,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "librrin_hip.so")
 
 # enums (rrin_hip.h)
@@ -108,6 +108,7 @@ SIGNATURES = {
     "rrin_conv_h8_cfg_bm": (C.c_int, [C.c_int32]),
     "rrin_conv_h8_cfg_th": (C.c_int, [C.c_int32]),
     "rrin_conv_h8_cfg_ok": (C.c_int, [C.c_int32, C.c_int32]),
+    "rrin_conv_h8_cfg_fits": (C.c_int, [C.c_int32, C.c_int32, C.c_int32]),
     "rrin_conv3x3_h8_fwd": (C.c_int, [C.POINTER(ConvH8Desc), C.c_void_p]),
     "rrin_pack_conv3x3_h8_halves": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32]),
     "rrin_pack_conv3x3_h8": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p,

@@ -110,17 +110,47 @@ __device__ inline void dma16(const uint4* src, uint4* lds_wave_base) {
                                    (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
 }
 
+// Schedule knobs of the kernel (template SCHED; the cfg table picks them per
+// layer, tools/conv_lab.py ablate times them).  SPREAD issues the next chunk's
+// DMA pieces between the first kSpreadTaps taps of the current chunk instead
+// of in one burst before it; STAGGER lets waves NW/2.. issue theirs after tap
+// kStaggerTap instead (the two wave halves of a SIMD then load at different
+// times); WRES keeps every weight chunk of the block's channel block resident
+// in LDS, staged once per block.  Lab-only ablations (wrong outputs, they time
+// what is left): NO_WDMA / NO_IDMA keep reading the chunk-0 weight slab /
+// input tile instead of staging later chunks, NO_MFMA keeps the LDS operand
+// reads but drops the MFMAs, NO_EPI drops the epilogue.
+enum : int {
+  SCHED_NO_WDMA = 1, SCHED_NO_IDMA = 2, SCHED_NO_MFMA = 4, SCHED_NO_EPI = 8,
+  SCHED_SPREAD = 16, SCHED_WRES = 32, SCHED_STAGGER = 64
+};
+constexpr int kSpreadTaps = 6, kStaggerTap = 3;
+
 // DMA = true: stage with LDS-DMA (requires cin % 8 == 0: no partial channel
 // group to mask); false: register staging with masking (first convs, cin 6/9/10).
-template <int NW, int WM, int WN, int PLANES, int EPI, bool DMA>
+//
+// A block computes the output tiles (BM channels x TH rows x 32 columns of one
+// image, channel block fastest) bid, bid + gridDim.x, ...  With a grid of every
+// tile that is one tile per block; with a persistent grid (a few blocks per
+// CU) chunk 0 of a block's next tile is staged while the last chunk of the
+// current one computes, so only its first tile waits for staging.  WRES needs
+// every tile of a block in one channel block (gridDim.x % co_blocks == 0).
+template <int NW, int WM, int WN, int PLANES, int EPI, bool DMA, int SCHED = 0>
 __global__ void __launch_bounds__(64 * NW) conv3x3_h8_kernel(ConvH8Args a) {
   using T = TileH8<NW, WM, WN, PLANES>;
   constexpr int NT = T::NT, BM = T::BM, TH = T::TH, ROWS = T::ROWS;
   constexpr int IN_REC = T::IN_REC, W_REC = T::W_REC;
+  constexpr bool kNoW = (SCHED & SCHED_NO_WDMA) != 0, kNoIn = (SCHED & SCHED_NO_IDMA) != 0;
+  constexpr bool kNoMfma = (SCHED & SCHED_NO_MFMA) != 0, kNoEpi = (SCHED & SCHED_NO_EPI) != 0;
+  constexpr bool kSpread = DMA && (SCHED & SCHED_SPREAD) != 0;
+  constexpr bool kStagger = DMA && !kSpread && (SCHED & SCHED_STAGGER) != 0 && NW >= 2;
+  constexpr bool kWRes = DMA && (SCHED & SCHED_WRES) != 0;
+  // DMA pieces (one 16-B record per thread and plane) of one chunk: input tile, then weight slab
+  constexpr int NPIECE = T::IN_IT + (kWRes ? 0 : T::W_IT);
 
   extern __shared__ __attribute__((aligned(16))) uint4 smem4[];
   uint4* s_in = smem4;                          // [buf][plane][IN_REC]
-  uint4* s_w = smem4 + 2 * PLANES * IN_REC;     // [buf][plane][W_REC]
+  uint4* s_w = smem4 + 2 * PLANES * IN_REC;     // [buf][plane][W_REC]; WRES: [chunk][plane][W_REC]
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -134,55 +164,62 @@ __global__ void __launch_bounds__(64 * NW) conv3x3_h8_kernel(ConvH8Args a) {
     const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
     bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
   }
-  const int cob = bid % a.co_blocks;
-  bid /= a.co_blocks;
-  const int tx = bid % a.tiles_x;
-  bid /= a.tiles_x;
-  const int ty = bid % a.tiles_y;
-  const int img = bid / a.tiles_y;
-  const int x0 = tx * 32;
-  const int y0 = ty * TH;
-
-  const uint4* src[2] = {a.src_hi + img * a.src_img, PLANES == 2 ? a.src_lo + img * a.src_img : nullptr};
-  const uint4* wsrc[2] = {a.w_hi + (int64_t)cob * a.nchunks * W_REC,
-                          PLANES == 2 ? a.w_lo + (int64_t)cob * a.nchunks * W_REC : nullptr};
+  const int ntiles = a.co_blocks * a.tiles_x * a.tiles_y * a.n;
+  struct TileId {
+    int cob, x0, y0, img;
+  };
+  auto tile_id = [&](int t) {
+    TileId o;
+    o.cob = t % a.co_blocks;
+    t /= a.co_blocks;
+    o.x0 = (t % a.tiles_x) * 32;
+    t /= a.tiles_x;
+    o.y0 = (t % a.tiles_y) * TH;
+    o.img = t / a.tiles_y;
+    return o;
+  };
 
   uint4 rin[PLANES][DMA ? 1 : T::IN_IT];
   uint4 rw[PLANES][DMA ? 1 : T::W_IT];
-  const int wave = tid >> 6;
 
-  // DMA staging of chunk c into buffer buf (input tile + weight slab, both planes)
-  auto issue = [&](int c, int buf) {
-#pragma unroll
-    for (int it = 0; it < T::IN_IT; ++it) {
-      const int idx = tid + NT * it;
-      if (idx < IN_REC) {
-        const int g = idx / (ROWS * H8_LC);
-        const int rem = idx - g * (ROWS * H8_LC);
-        const int r = rem / H8_LC;
-        const int col = rem - r * H8_LC;
-        const int gg = c * 2 + g;
-        // groups past cin read the zero top-padding row of group 0 instead
-        const int64_t off = gg * 8 < a.cin
-                                ? (int64_t)gg * a.src_gp + (int64_t)(y0 + r) * a.src_wp + x0 + (kH8PadLeft - 1) + col
-                                : (int64_t)(x0 + (kH8PadLeft - 1) + col);
-#pragma unroll
-        for (int p = 0; p < PLANES; ++p)
-          dma16(src[p] + off, s_in + (buf * PLANES + p) * IN_REC + NT * it + wave * 64);
-      }
+  // LDS-DMA staging of chunk c of tile tl: input piece `it` into buffer buf,
+  // weight piece `it` into weight slot `slot` (both planes)
+  auto issue_in = [&](const TileId& tl, int c, int buf, int it) {
+    const int idx = tid + NT * it;
+    if (idx < IN_REC) {
+      const int g = idx / (ROWS * H8_LC);
+      const int rem = idx - g * (ROWS * H8_LC);
+      const int r = rem / H8_LC;
+      const int col = rem - r * H8_LC;
+      const int gg = c * 2 + g;
+      // groups past cin read the zero top-padding row of group 0 instead
+      const int64_t off = (int64_t)tl.img * a.src_img +
+                          (gg * 8 < a.cin ? (int64_t)gg * a.src_gp + (int64_t)(tl.y0 + r) * a.src_wp : 0) +
+                          tl.x0 + (kH8PadLeft - 1) + col;
+      uint4* d = s_in + buf * PLANES * IN_REC + NT * it + (tid & ~63);
+      dma16(a.src_hi + off, d);
+      if constexpr (PLANES == 2) dma16(a.src_lo + off, d + IN_REC);
     }
-#pragma unroll
-    for (int it = 0; it < T::W_IT; ++it) {
-      const int idx = tid + NT * it;
-      if (idx < W_REC) {
-#pragma unroll
-        for (int p = 0; p < PLANES; ++p)
-          dma16(wsrc[p] + (int64_t)c * W_REC + idx, s_w + (buf * PLANES + p) * W_REC + NT * it + wave * 64);
-      }
+  };
+  auto issue_w = [&](const TileId& tl, int c, int slot, int it) {
+    const int idx = tid + NT * it;
+    if (idx < W_REC) {
+      const int64_t off = ((int64_t)tl.cob * a.nchunks + c) * W_REC + idx;
+      uint4* d = s_w + slot * PLANES * W_REC + NT * it + (tid & ~63);
+      dma16(a.w_hi + off, d);
+      if constexpr (PLANES == 2) dma16(a.w_lo + off, d + W_REC);
+    }
+  };
+  auto issue_piece = [&](const TileId& tl, int c, int buf, int k) {
+    if (k < T::IN_IT) {
+      if constexpr (!kNoIn) issue_in(tl, c, buf, k);
+    } else {
+      if constexpr (!kNoW) issue_w(tl, c, buf, k - T::IN_IT);
     }
   };
 
-  auto load_in = [&](int c) {
+  auto load_in = [&](const TileId& tl, int c) {
+    const uint4* src[2] = {a.src_hi, a.src_lo};
 #pragma unroll
     for (int it = 0; it < T::IN_IT; ++it) {
       const int idx = tid + NT * it;
@@ -193,7 +230,8 @@ __global__ void __launch_bounds__(64 * NW) conv3x3_h8_kernel(ConvH8Args a) {
         const int col = rem - r * H8_LC;
         const int gg = c * 2 + g;
         const int nval = a.cin - gg * 8;
-        const int64_t off = (int64_t)gg * a.src_gp + (int64_t)(y0 + r) * a.src_wp + x0 + (kH8PadLeft - 1) + col;
+        const int64_t off = (int64_t)tl.img * a.src_img + (int64_t)gg * a.src_gp + (int64_t)(tl.y0 + r) * a.src_wp +
+                            tl.x0 + (kH8PadLeft - 1) + col;
 #pragma unroll
         for (int p = 0; p < PLANES; ++p) {
           uint4 v = make_uint4(0u, 0u, 0u, 0u);
@@ -215,13 +253,14 @@ __global__ void __launch_bounds__(64 * NW) conv3x3_h8_kernel(ConvH8Args a) {
         if (idx < IN_REC) s_in[(buf * PLANES + p) * IN_REC + idx] = rin[p][it];
       }
   };
-  auto load_w = [&](int c) {
+  auto load_w = [&](const TileId& tl, int c) {
+    const uint4* wsrc[2] = {a.w_hi, a.w_lo};
 #pragma unroll
     for (int p = 0; p < PLANES; ++p)
 #pragma unroll
       for (int it = 0; it < T::W_IT; ++it) {
         const int idx = tid + NT * it;
-        if (idx < W_REC) rw[p][it] = wsrc[p][(int64_t)c * W_REC + idx];
+        if (idx < W_REC) rw[p][it] = wsrc[p][((int64_t)tl.cob * a.nchunks + c) * W_REC + idx];
       }
   };
   auto store_w = [&](int buf) {
@@ -236,26 +275,18 @@ __global__ void __launch_bounds__(64 * NW) conv3x3_h8_kernel(ConvH8Args a) {
 
   // acc: hi*hi products; accx (F16X3): hi*lo' + lo'*hi, 2^11 too large
   floatx16 acc[WM][WN], accx[WM][WN];
-#pragma unroll
-  for (int mt = 0; mt < WM; ++mt)
-#pragma unroll
-    for (int nt = 0; nt < WN; ++nt)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        acc[mt][nt][i] = 0.f;
-        accx[mt][nt][i] = 0.f;
-      }
 
   // 9 taps per chunk; one K16 block = 16 input channels at one tap (lanes
   // 0-31 carry channels 0-7 of the chunk, lanes 32-63 channels 8-15).
-  // Operands of tap t+1 are read before the MFMAs of tap t issue.
-  auto compute = [&](int buf) {
+  // Operands of tap t+1 are read before the MFMAs of tap t issue; after_tap(t)
+  // runs behind tap t's MFMAs (SPREAD / STAGGER: DMA pieces of the next chunk).
+  auto compute = [&](int buf, int wslot, auto&& after_tap) {
     const uint4* si[PLANES];
     const uint4* sw[PLANES];
 #pragma unroll
     for (int p = 0; p < PLANES; ++p) {
-      si[p] = s_in + (buf * PLANES + p) * IN_REC + (hh * ROWS + wn * WN) * H8_LC + j;
-      sw[p] = s_w + (buf * PLANES + p) * W_REC + hh * BM + j;
+      si[p] = s_in + ((kNoIn ? 0 : buf) * PLANES + p) * IN_REC + (hh * ROWS + wn * WN) * H8_LC + j;
+      sw[p] = s_w + ((kNoW ? 0 : wslot) * PLANES + p) * W_REC + hh * BM + j;
     }
     half8 av[2][PLANES][WM], bv[2][PLANES][WN];
     auto ld = [&](int t, int slot) {
@@ -277,177 +308,247 @@ __global__ void __launch_bounds__(64 * NW) conv3x3_h8_kernel(ConvH8Args a) {
       for (int mt = 0; mt < WM; ++mt)
 #pragma unroll
         for (int nt = 0; nt < WN; ++nt) {
-          if constexpr (PLANES == 2) {
-            accx[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[s][1][mt], bv[s][0][nt], accx[mt][nt], 0, 0, 0);
-            accx[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[s][0][mt], bv[s][1][nt], accx[mt][nt], 0, 0, 0);
+          if constexpr (kNoMfma) {
+            asm volatile("" ::"v"(av[s][0][mt]), "v"(bv[s][0][nt]));
+            if constexpr (PLANES == 2) asm volatile("" ::"v"(av[s][1][mt]), "v"(bv[s][1][nt]));
+          } else {
+            if constexpr (PLANES == 2) {
+              accx[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[s][1][mt], bv[s][0][nt], accx[mt][nt], 0, 0, 0);
+              accx[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[s][0][mt], bv[s][1][nt], accx[mt][nt], 0, 0, 0);
+            }
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[s][0][mt], bv[s][0][nt], acc[mt][nt], 0, 0, 0);
           }
-          acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[s][0][mt], bv[s][0][nt], acc[mt][nt], 0, 0, 0);
         }
+      after_tap(t);
     }
   };
 
+  int tile = bid;
+  if (tile >= ntiles) return;
+  TileId cur = tile_id(tile);
+  // prologue: chunk 0 of the block's first tile (WRES: and every weight chunk)
   if constexpr (DMA) {
-    issue(0, 0);
+#pragma unroll
+    for (int it = 0; it < T::IN_IT; ++it) issue_in(cur, 0, 0, it);
+    for (int c = 0; c < (kWRes ? a.nchunks : 1); ++c)
+#pragma unroll
+      for (int it = 0; it < T::W_IT; ++it) issue_w(cur, c, c, it);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    for (int c = 0; c < a.nchunks; ++c) {
-      const int buf = c & 1;
-      // buf^1 was last read in chunk c-1, before the barrier that ended it
-      if ((c + 1) < a.nchunks) issue(c + 1, buf ^ 1);
-      compute(buf);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    }
   } else {
-    load_w(0);
-    load_in(0);
+    load_w(cur, 0);
+    load_in(cur, 0);
     store_in(0);
     store_w(0);
-    __syncthreads();
+  }
+  __syncthreads();
+  int buf = 0;
+  for (;;) {
+    const int ntile = tile + (int)gridDim.x;
+    const bool more = ntile < ntiles;
+    const TileId nxt = tile_id(more ? ntile : tile);
+#pragma unroll
+    for (int mt = 0; mt < WM; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < WN; ++nt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          acc[mt][nt][i] = 0.f;
+          accx[mt][nt][i] = 0.f;
+        }
     for (int c = 0; c < a.nchunks; ++c) {
-      const int buf = c & 1;
-      const bool more = (c + 1) < a.nchunks;
-      if (more) {
-        load_w(c + 1);
-        load_in(c + 1);
+      // staged during this chunk: chunk c+1 of this tile, or chunk 0 of the next tile
+      const bool last = c + 1 == a.nchunks;
+      const bool pre = !last || more;
+      const TileId& pt = last ? nxt : cur;
+      const int pc = last ? 0 : c + 1;
+      const int wslot = kWRes ? c : buf;
+      if constexpr (DMA) {
+        // buf^1 was last read in the previous chunk, before the barrier that ended it
+        if constexpr (kSpread) {
+          compute(buf, wslot, [&](int t) {
+            if (t < kSpreadTaps && pre) {
+#pragma unroll
+              for (int k = t * NPIECE / kSpreadTaps; k < (t + 1) * NPIECE / kSpreadTaps; ++k)
+                issue_piece(pt, pc, buf ^ 1, k);
+            }
+          });
+        } else if constexpr (kStagger) {
+          const bool late = __builtin_amdgcn_readfirstlane(tid) >= NT / 2;
+          if (pre && !late) {
+#pragma unroll
+            for (int k = 0; k < NPIECE; ++k) issue_piece(pt, pc, buf ^ 1, k);
+          }
+          compute(buf, wslot, [&](int t) {
+            if (t == kStaggerTap && pre && late) {
+#pragma unroll
+              for (int k = 0; k < NPIECE; ++k) issue_piece(pt, pc, buf ^ 1, k);
+            }
+          });
+        } else {
+          if (pre) {
+#pragma unroll
+            for (int k = 0; k < NPIECE; ++k) issue_piece(pt, pc, buf ^ 1, k);
+          }
+          compute(buf, wslot, [](int) {});
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      } else {
+        if (pre) {
+          load_w(pt, pc);
+          load_in(pt, pc);
+        }
+        compute(buf, buf, [](int) {});
+        if (pre) {
+          store_in(buf ^ 1);
+          store_w(buf ^ 1);
+        }
+        __syncthreads();
       }
-      compute(buf);
-      if (more) {
-        store_in(buf ^ 1);
-        store_w(buf ^ 1);
-      }
-      __syncthreads();
+      buf ^= 1;
     }
-  }
 
-  // ---- epilogue: scale, bias, leaky, split, 8-B half-record stores (+ pool)
-  const int yb = y0 + wn * WN;
-  const int x = x0 + j;
-  uint4* dst[2] = {a.dst_hi + img * a.dst_img, PLANES == 2 ? a.dst_lo + img * a.dst_img : nullptr};
-  if constexpr (EPI == RRIN_EPI_SUBPIXEL) {
-    // rows co' = (co/8)*32 + phase*8 + co%8: an MFMA row block (mt) is one
-    // 8-channel group, q its phase (py, px); LR pixel (y, x) -> HR (2y+py, 2x+px)
-    const int HH = 2 * a.h, WW = 2 * a.w, creal = a.cout >> 2;
+    // ---- epilogue: scale, bias, leaky, split, 8-B half-record stores (+ pool)
+    const int cob = cur.cob, x0 = cur.x0, img = cur.img;
+    const int yb = cur.y0 + wn * WN;
+    const int x = x0 + j;
+    uint4* dst[2] = {a.dst_hi + img * a.dst_img, PLANES == 2 ? a.dst_lo + img * a.dst_img : nullptr};
+    if constexpr (kNoEpi) {
 #pragma unroll
-    for (int mt = 0; mt < WM; ++mt) {
-      const int grp = (cob * BM + mt * 32) >> 5;
-      if (grp * 32 >= a.cout) continue;
+      for (int mt = 0; mt < WM; ++mt)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int py = q >> 1, px = q & 1;
-        const int co0 = cob * BM + mt * 32 + 8 * q;
-        float bs[4];
+        for (int nt = 0; nt < WN; ++nt)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) bs[e] = a.bias[co0 + 4 * hh + e];
+          for (int i = 0; i < 16; ++i) asm volatile("" ::"v"(acc[mt][nt][i]), "v"(accx[mt][nt][i]));
+      (void)cob, (void)yb, (void)x, (void)dst;
+    } else if constexpr (EPI == RRIN_EPI_SUBPIXEL) {
+      // rows co' = (co/8)*32 + phase*8 + co%8: an MFMA row block (mt) is one
+      // 8-channel group, q its phase (py, px); LR pixel (y, x) -> HR (2y+py, 2x+px)
+      const int HH = 2 * a.h, WW = 2 * a.w, creal = a.cout >> 2;
 #pragma unroll
-        for (int nt = 0; nt < WN; ++nt) {
-          const int y = yb + nt;
-          if (y >= a.h || x >= a.w) continue;
-          const int Y = 2 * y + py, X = 2 * x + px;
-          float t[4];
+      for (int mt = 0; mt < WM; ++mt) {
+        const int grp = (cob * BM + mt * 32) >> 5;
+        if (grp * 32 >= a.cout) continue;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            float u = acc[mt][nt][4 * q + e];
-            if constexpr (PLANES == 2) u = fmaf(accx[mt][nt][4 * q + e], kLoUnscale, u);
-            t[e] = u * a.inv_wscale;
-          }
-          const int64_t ri = ring_index(Y, X, HH, WW);
-          if (ri >= 0) {
+        for (int q = 0; q < 4; ++q) {
+          const int py = q >> 1, px = q & 1;
+          const int co0 = cob * BM + mt * 32 + 8 * q;
+          float bs[4];
 #pragma unroll
-            for (int e = 0; e < 4; ++e)
-              a.edge[((int64_t)img * creal + grp * 8 + 4 * hh + e) * a.ring + ri] = t[e];
-          } else {
-            const int64_t rec = (int64_t)grp * a.dst_gp + (int64_t)(Y + 1) * a.dst_wp + X + kH8PadLeft;
-            _Float16 hi[4], lo[4];
+          for (int e = 0; e < 4; ++e) bs[e] = a.bias[co0 + 4 * hh + e];
+#pragma unroll
+          for (int nt = 0; nt < WN; ++nt) {
+            const int y = yb + nt;
+            if (y >= a.h || x >= a.w) continue;
+            const int Y = 2 * y + py, X = 2 * x + px;
+            float t[4];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              const float v = t[e] + bs[e];
-              hi[e] = (_Float16)v;
-              lo[e] = lo_of(v, hi[e]);
+              float u = acc[mt][nt][4 * q + e];
+              if constexpr (PLANES == 2) u = fmaf(accx[mt][nt][4 * q + e], kLoUnscale, u);
+              t[e] = u * a.inv_wscale;
             }
-            reinterpret_cast<uint2*>(dst[0] + rec)[hh] = __builtin_bit_cast(uint2, hi);
-            if constexpr (PLANES == 2) reinterpret_cast<uint2*>(dst[1] + rec)[hh] = __builtin_bit_cast(uint2, lo);
+            const int64_t ri = ring_index(Y, X, HH, WW);
+            if (ri >= 0) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e)
+                a.edge[((int64_t)img * creal + grp * 8 + 4 * hh + e) * a.ring + ri] = t[e];
+            } else {
+              const int64_t rec = (int64_t)grp * a.dst_gp + (int64_t)(Y + 1) * a.dst_wp + X + kH8PadLeft;
+              _Float16 hi[4], lo[4];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const float v = t[e] + bs[e];
+                hi[e] = (_Float16)v;
+                lo[e] = lo_of(v, hi[e]);
+              }
+              reinterpret_cast<uint2*>(dst[0] + rec)[hh] = __builtin_bit_cast(uint2, hi);
+              if constexpr (PLANES == 2) reinterpret_cast<uint2*>(dst[1] + rec)[hh] = __builtin_bit_cast(uint2, lo);
+            }
           }
         }
       }
-    }
-    return;
-  }
-  uint4* pdst[2] = {nullptr, nullptr};
-  if constexpr (EPI == RRIN_EPI_LEAKY_POOL) {
-    pdst[0] = a.pool_hi + img * a.pool_img;
-    if (PLANES == 2) pdst[1] = a.pool_lo + img * a.pool_img;
-  }
-#pragma unroll
-  for (int mt = 0; mt < WM; ++mt) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int co0 = cob * BM + mt * 32 + 8 * q;  // first channel of the record
-      const int grp = co0 >> 3;
-      float bs[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) bs[e] = a.bias[co0 + 4 * hh + e];
-      float v[WN][4];
-#pragma unroll
-      for (int nt = 0; nt < WN; ++nt) {
-        const int y = yb + nt;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float t = acc[mt][nt][4 * q + e];
-          if constexpr (PLANES == 2) t = fmaf(accx[mt][nt][4 * q + e], kLoUnscale, t);
-          t = t * a.inv_wscale + bs[e];
-          if constexpr (EPI != RRIN_EPI_LINEAR) t = t > 0.f ? t : t * a.slope;
-          v[nt][e] = t;
-        }
-        if (co0 < a.cout && y < a.h && x < a.w) {
-          const int64_t rec = (int64_t)grp * a.dst_gp + (int64_t)(y + 1) * a.dst_wp + x + kH8PadLeft;
-          _Float16 hi[4], lo[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            hi[e] = (_Float16)v[nt][e];
-            lo[e] = lo_of(v[nt][e], hi[e]);
-          }
-          const uint2 hv = __builtin_bit_cast(uint2, hi), lv = __builtin_bit_cast(uint2, lo);
-          reinterpret_cast<uint2*>(dst[0] + rec)[hh] = hv;
-          if constexpr (PLANES == 2) reinterpret_cast<uint2*>(dst[1] + rec)[hh] = lv;
-          if constexpr (EPI == RRIN_EPI_LEAKY_REP) {
-            // edge replicate into the padding ring (read only by a sub-pixel up conv)
-            const int dy0 = y == 0 ? -1 : 0, dy1 = y == a.h - 1 ? 1 : 0;
-            const int dx0 = x == 0 ? -1 : 0, dx1 = x == a.w - 1 ? 1 : 0;
-            for (int dy = dy0; dy <= dy1; ++dy)
-              for (int dx = dx0; dx <= dx1; ++dx)
-                if (dy | dx) {
-                  const int64_t r2 = rec + (int64_t)dy * a.dst_wp + dx;
-                  reinterpret_cast<uint2*>(dst[0] + r2)[hh] = hv;
-                  if constexpr (PLANES == 2) reinterpret_cast<uint2*>(dst[1] + r2)[hh] = lv;
-                }
-          }
-        }
-      }
+    } else {
+      uint4* pdst[2] = {nullptr, nullptr};
       if constexpr (EPI == RRIN_EPI_LEAKY_POOL) {
+        pdst[0] = a.pool_hi + img * a.pool_img;
+        if (PLANES == 2) pdst[1] = a.pool_lo + img * a.pool_img;
+      }
 #pragma unroll
-        for (int p2 = 0; p2 < WN / 2; ++p2) {
-          float s4[4];
+      for (int mt = 0; mt < WM; ++mt) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            float s = v[2 * p2][e] + v[2 * p2 + 1][e];
-            s4[e] = 0.25f * (s + __shfl_xor(s, 1));
-          }
-          const int y = yb + 2 * p2;
-          if (!(j & 1) && co0 < a.cout && y < a.h && x < a.w) {
-            const int64_t rec = (int64_t)grp * a.pool_gp + (int64_t)(y / 2 + 1) * a.pool_wp + x / 2 + kH8PadLeft;
-            _Float16 hi[4], lo[4];
+        for (int q = 0; q < 4; ++q) {
+          const int co0 = cob * BM + mt * 32 + 8 * q;  // first channel of the record
+          const int grp = co0 >> 3;
+          float bs[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) bs[e] = a.bias[co0 + 4 * hh + e];
+          float v[WN][4];
+#pragma unroll
+          for (int nt = 0; nt < WN; ++nt) {
+            const int y = yb + nt;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              hi[e] = (_Float16)s4[e];
-              lo[e] = lo_of(s4[e], hi[e]);
+              float t = acc[mt][nt][4 * q + e];
+              if constexpr (PLANES == 2) t = fmaf(accx[mt][nt][4 * q + e], kLoUnscale, t);
+              t = t * a.inv_wscale + bs[e];
+              if constexpr (EPI != RRIN_EPI_LINEAR) t = t > 0.f ? t : t * a.slope;
+              v[nt][e] = t;
             }
-            reinterpret_cast<uint2*>(pdst[0] + rec)[hh] = __builtin_bit_cast(uint2, hi);
-            if constexpr (PLANES == 2) reinterpret_cast<uint2*>(pdst[1] + rec)[hh] = __builtin_bit_cast(uint2, lo);
+            if (co0 < a.cout && y < a.h && x < a.w) {
+              const int64_t rec = (int64_t)grp * a.dst_gp + (int64_t)(y + 1) * a.dst_wp + x + kH8PadLeft;
+              _Float16 hi[4], lo[4];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                hi[e] = (_Float16)v[nt][e];
+                lo[e] = lo_of(v[nt][e], hi[e]);
+              }
+              const uint2 hv = __builtin_bit_cast(uint2, hi), lv = __builtin_bit_cast(uint2, lo);
+              reinterpret_cast<uint2*>(dst[0] + rec)[hh] = hv;
+              if constexpr (PLANES == 2) reinterpret_cast<uint2*>(dst[1] + rec)[hh] = lv;
+              if constexpr (EPI == RRIN_EPI_LEAKY_REP) {
+                // edge replicate into the padding ring (read only by a sub-pixel up conv)
+                const int dy0 = y == 0 ? -1 : 0, dy1 = y == a.h - 1 ? 1 : 0;
+                const int dx0 = x == 0 ? -1 : 0, dx1 = x == a.w - 1 ? 1 : 0;
+                for (int dy = dy0; dy <= dy1; ++dy)
+                  for (int dx = dx0; dx <= dx1; ++dx)
+                    if (dy | dx) {
+                      const int64_t r2 = rec + (int64_t)dy * a.dst_wp + dx;
+                      reinterpret_cast<uint2*>(dst[0] + r2)[hh] = hv;
+                      if constexpr (PLANES == 2) reinterpret_cast<uint2*>(dst[1] + r2)[hh] = lv;
+                    }
+              }
+            }
+          }
+          if constexpr (EPI == RRIN_EPI_LEAKY_POOL) {
+#pragma unroll
+            for (int p2 = 0; p2 < WN / 2; ++p2) {
+              float s4[4];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                float s = v[2 * p2][e] + v[2 * p2 + 1][e];
+                s4[e] = 0.25f * (s + __shfl_xor(s, 1));
+              }
+              const int y = yb + 2 * p2;
+              if (!(j & 1) && co0 < a.cout && y < a.h && x < a.w) {
+                const int64_t rec = (int64_t)grp * a.pool_gp + (int64_t)(y / 2 + 1) * a.pool_wp + x / 2 + kH8PadLeft;
+                _Float16 hi[4], lo[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                  hi[e] = (_Float16)s4[e];
+                  lo[e] = lo_of(s4[e], hi[e]);
+                }
+                reinterpret_cast<uint2*>(pdst[0] + rec)[hh] = __builtin_bit_cast(uint2, hi);
+                if constexpr (PLANES == 2) reinterpret_cast<uint2*>(pdst[1] + rec)[hh] = __builtin_bit_cast(uint2, lo);
+              }
+            }
           }
         }
       }
-    }
+    }  // epilogue
+    if (!more) break;
+    tile = ntile;
+    cur = nxt;
   }
 }
 
@@ -1064,77 +1165,126 @@ static float h2f(uint16_t h) {
   return sign ? -f : f;
 }
 
-// Config table: cfg -> (NW waves along rows, WM co-tiles, WN rows per wave)
-#define RRIN_H8_CFGS(X) \
-  X(0, 8, 2, 2)         \
-  X(1, 8, 1, 2)         \
-  X(2, 4, 2, 2)         \
-  X(3, 4, 1, 4)         \
-  X(4, 4, 2, 1)         \
-  X(5, 8, 4, 2)         \
-  X(6, 4, 1, 2)         \
-  X(7, 2, 1, 4)
+// Config table: cfg -> (NW waves along rows, WM co-tiles, WN rows per wave,
+// SC schedule knobs SCHED_*, PE grid: 0 = one tile per block, k = k x the
+// blocks a CU holds at once, persistent)
+#define RRIN_H8_CFGS(X)  \
+  X(0, 8, 2, 2, 0, 0)    \
+  X(1, 8, 1, 2, 0, 0)    \
+  X(2, 4, 2, 2, 0, 0)    \
+  X(3, 4, 1, 4, 0, 0)    \
+  X(4, 4, 2, 1, 0, 0)    \
+  X(5, 8, 4, 2, 0, 0)    \
+  X(6, 4, 1, 2, 0, 0)    \
+  X(7, 2, 1, 4, 0, 0)    \
+  X(8, 4, 1, 2, 32, 1)   \
+  X(9, 8, 1, 2, 32, 1)   \
+  X(10, 8, 2, 2, 16, 1)  \
+  X(11, 8, 2, 2, 16, 0)  \
+  X(12, 4, 1, 2, 16, 1)  \
+  X(13, 8, 1, 2, 16, 1)  \
+  X(14, 4, 1, 2, 48, 1)  \
+  X(15, 8, 1, 2, 48, 1)
+
+// Shared memory of one block: double-buffered input tile and weight slab, or
+// with WRES every chunk's weight slab resident.
+template <int NW, int WM, int WN, int PLANES>
+constexpr size_t h8_lds_bytes(bool wres, int nchunks) {
+  using T = TileH8<NW, WM, WN, PLANES>;
+  return ((size_t)2 * T::IN_REC + (size_t)(wres && nchunks > 2 ? nchunks : 2) * T::W_REC) * PLANES * 16;
+}
 
 struct CfgH8 {
   int bm, th;
-  size_t lds1, lds2;
+  size_t lds1, lds2;  // at two weight slabs (WRES: at <= 2 chunks)
+  size_t wslab;       // bytes of one weight slab per plane (WRES: one more per chunk past 2)
   bool pool_ok;
+  int sched, persist;
 };
 static const CfgH8 kCfgH8[] = {
-#define X(id, nw, wm, wn) {TileH8<nw, wm, wn, 1>::BM, TileH8<nw, wm, wn, 1>::TH, TileH8<nw, wm, wn, 1>::LDS, \
-                           TileH8<nw, wm, wn, 2>::LDS, (wn % 2) == 0},
+#define X(id, nw, wm, wn, sc, pe)                                                                               \
+  {TileH8<nw, wm, wn, 1>::BM, TileH8<nw, wm, wn, 1>::TH, h8_lds_bytes<nw, wm, wn, 1>((sc & SCHED_WRES) != 0, 2), \
+   h8_lds_bytes<nw, wm, wn, 2>((sc & SCHED_WRES) != 0, 2), (size_t)TileH8<nw, wm, wn, 1>::W_REC * 16,     \
+   (wn % 2) == 0, sc, pe},
     RRIN_H8_CFGS(X)
 #undef X
 };
 static constexpr int kNumCfgH8 = sizeof(kCfgH8) / sizeof(kCfgH8[0]);
 static constexpr size_t kMaxLds = 160 * 1024;
 
-template <int NW, int WM, int WN, int PLANES, int EPI, bool DMA>
-static int launch_h8_k(const ConvH8Args& args, int grid, hipStream_t st) {
+static int num_cus() {
+  static int n[16] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return 256;
+  if (!n[dev] && hipDeviceGetAttribute(&n[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) n[dev] = 256;
+  return n[dev];
+}
+
+template <int NW, int WM, int WN, int PLANES, int EPI, bool DMA, int SCHED>
+static int launch_h8_k(const ConvH8Args& args, int persist, hipStream_t st) {
   using T = TileH8<NW, WM, WN, PLANES>;
-  auto k = conv3x3_h8_kernel<NW, WM, WN, PLANES, EPI, DMA>;
+  auto k = conv3x3_h8_kernel<NW, WM, WN, PLANES, EPI, DMA, SCHED>;
+  constexpr bool wres = DMA && (SCHED & SCHED_WRES) != 0;
+  const size_t lds = h8_lds_bytes<NW, WM, WN, PLANES>(wres, args.nchunks);
+  if (lds > kMaxLds) return RRIN_E_CONFIG;
   static bool attr_set = false;
+  static int per_cu[40] = {0};  // resident blocks per CU, by LDS footprint (WRES: chunk count)
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)T::LDS);
+    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds);
     if (e != hipSuccess) return (int)e;
     attr_set = true;
   }
-  hipLaunchKernelGGL(k, dim3(grid), dim3(T::NT), T::LDS, st, args);
+  const int64_t ntiles = (int64_t)args.co_blocks * args.tiles_x * args.tiles_y * args.n;
+  int64_t grid = ntiles;
+  if (persist > 0) {
+    int& pc = per_cu[wres ? (args.nchunks < 40 ? args.nchunks : 39) : 0];
+    if (!pc) {
+      hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, (const void*)k, T::NT, lds);
+      if (e != hipSuccess) return (int)e;
+      if (pc < 1) pc = 1;
+    }
+    int64_t g = (int64_t)persist * pc * num_cus();
+    g -= g % args.co_blocks;  // WRES: every tile of a block in the block's channel block
+    if (g < args.co_blocks) g = args.co_blocks;
+    if (g < grid) grid = g;
+  }
+  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(T::NT), lds, st, args);
   return hip_code(hipGetLastError());
 }
 
-template <int NW, int WM, int WN, int PLANES, int EPI>
-static int launch_h8_t(const ConvH8Args& args, int grid, hipStream_t st) {
+template <int NW, int WM, int WN, int PLANES, int EPI, int SCHED>
+static int launch_h8_t(const ConvH8Args& args, int persist, hipStream_t st) {
   using T = TileH8<NW, WM, WN, PLANES>;
   if constexpr (T::LDS > kMaxLds) {
     return RRIN_E_CONFIG;
   } else {
-    if (args.cin % 8 == 0 || args.tail_finite) return launch_h8_k<NW, WM, WN, PLANES, EPI, true>(args, grid, st);
+    if (args.cin % 8 == 0 || args.tail_finite)
+      return launch_h8_k<NW, WM, WN, PLANES, EPI, true, SCHED>(args, persist, st);
     if constexpr (EPI == RRIN_EPI_LEAKY_REP || EPI == RRIN_EPI_SUBPIXEL) {
       return RRIN_E_CONFIG;  // decoder-side modes: always whole channel groups
     } else {
-      return launch_h8_k<NW, WM, WN, PLANES, EPI, false>(args, grid, st);
+      return launch_h8_k<NW, WM, WN, PLANES, EPI, false, 0>(args, persist, st);  // knobs need DMA
     }
   }
 }
 
-template <int NW, int WM, int WN>
-static int launch_h8_cfg(const ConvH8Args& args, int planes, int epi, int grid, hipStream_t st) {
+template <int NW, int WM, int WN, int SCHED>
+static int launch_h8_cfg(const ConvH8Args& args, int planes, int epi, int persist, hipStream_t st) {
   if (planes == 2) {
     switch (epi) {
-      case RRIN_EPI_LINEAR: return launch_h8_t<NW, WM, WN, 2, RRIN_EPI_LINEAR>(args, grid, st);
-      case RRIN_EPI_LEAKY: return launch_h8_t<NW, WM, WN, 2, RRIN_EPI_LEAKY>(args, grid, st);
-      case RRIN_EPI_LEAKY_POOL: return launch_h8_t<NW, WM, WN, 2, RRIN_EPI_LEAKY_POOL>(args, grid, st);
-      case RRIN_EPI_LEAKY_REP: return launch_h8_t<NW, WM, WN, 2, RRIN_EPI_LEAKY_REP>(args, grid, st);
-      default: return launch_h8_t<NW, WM, WN, 2, RRIN_EPI_SUBPIXEL>(args, grid, st);
+      case RRIN_EPI_LINEAR: return launch_h8_t<NW, WM, WN, 2, RRIN_EPI_LINEAR, SCHED>(args, persist, st);
+      case RRIN_EPI_LEAKY: return launch_h8_t<NW, WM, WN, 2, RRIN_EPI_LEAKY, SCHED>(args, persist, st);
+      case RRIN_EPI_LEAKY_POOL: return launch_h8_t<NW, WM, WN, 2, RRIN_EPI_LEAKY_POOL, SCHED>(args, persist, st);
+      case RRIN_EPI_LEAKY_REP: return launch_h8_t<NW, WM, WN, 2, RRIN_EPI_LEAKY_REP, SCHED>(args, persist, st);
+      default: return launch_h8_t<NW, WM, WN, 2, RRIN_EPI_SUBPIXEL, SCHED>(args, persist, st);
     }
   }
   switch (epi) {
-    case RRIN_EPI_LINEAR: return launch_h8_t<NW, WM, WN, 1, RRIN_EPI_LINEAR>(args, grid, st);
-    case RRIN_EPI_LEAKY: return launch_h8_t<NW, WM, WN, 1, RRIN_EPI_LEAKY>(args, grid, st);
-    case RRIN_EPI_LEAKY_POOL: return launch_h8_t<NW, WM, WN, 1, RRIN_EPI_LEAKY_POOL>(args, grid, st);
-    case RRIN_EPI_LEAKY_REP: return launch_h8_t<NW, WM, WN, 1, RRIN_EPI_LEAKY_REP>(args, grid, st);
-    default: return launch_h8_t<NW, WM, WN, 1, RRIN_EPI_SUBPIXEL>(args, grid, st);
+    case RRIN_EPI_LINEAR: return launch_h8_t<NW, WM, WN, 1, RRIN_EPI_LINEAR, SCHED>(args, persist, st);
+    case RRIN_EPI_LEAKY: return launch_h8_t<NW, WM, WN, 1, RRIN_EPI_LEAKY, SCHED>(args, persist, st);
+    case RRIN_EPI_LEAKY_POOL: return launch_h8_t<NW, WM, WN, 1, RRIN_EPI_LEAKY_POOL, SCHED>(args, persist, st);
+    case RRIN_EPI_LEAKY_REP: return launch_h8_t<NW, WM, WN, 1, RRIN_EPI_LEAKY_REP, SCHED>(args, persist, st);
+    default: return launch_h8_t<NW, WM, WN, 1, RRIN_EPI_SUBPIXEL, SCHED>(args, persist, st);
   }
 }
 
@@ -1150,34 +1300,14 @@ static inline int64_t ring_pixels(int h, int w) {
 
 static inline int planes_of(int prec) { return prec == RRIN_PREC_F16X3 ? 2 : 1; }
 
-}  // namespace rrin
-
-using namespace rrin;
-
-extern "C" int rrin_make_geom_h8(int32_t h, int32_t w, rrin_geom* g) {
-  if (!g || h < 1 || w < 1) return RRIN_E_ARG;
-  *g = make_geom_h8(h, w);
-  return 0;
-}
-
-extern "C" int rrin_conv_h8_cfg_count(void) { return kNumCfgH8; }
-extern "C" int rrin_conv_h8_cfg_bm(int32_t cfg) {
-  return (cfg >= 0 && cfg < kNumCfgH8) ? kCfgH8[cfg].bm : RRIN_E_CONFIG;
-}
-extern "C" int rrin_conv_h8_cfg_th(int32_t cfg) {
-  return (cfg >= 0 && cfg < kNumCfgH8) ? kCfgH8[cfg].th : RRIN_E_CONFIG;
-}
-extern "C" int rrin_conv_h8_cfg_ok(int32_t cfg, int32_t prec) {
-  if (cfg < 0 || cfg >= kNumCfgH8) return 0;
-  if (prec != RRIN_PREC_F16X3 && prec != RRIN_PREC_F16) return 0;
-  return (planes_of(prec) == 2 ? kCfgH8[cfg].lds2 : kCfgH8[cfg].lds1) <= kMaxLds ? 1 : 0;
-}
-
-extern "C" int rrin_conv3x3_h8_fwd(const rrin_conv_h8_desc* d, void* stream) {
+// Validate a conv descriptor and turn it into kernel arguments.
+static int h8_prepare(const rrin_conv_h8_desc* d, ConvH8Args& a) {
   if (!d || !d->whi || !d->bias) return RRIN_E_ARG;
   if (d->prec != RRIN_PREC_F16X3 && d->prec != RRIN_PREC_F16) return RRIN_E_ARG;
   if (d->prec == RRIN_PREC_F16X3 && !d->wlo) return RRIN_E_ARG;
-  if (!rrin_conv_h8_cfg_ok(d->cfg, d->prec)) return RRIN_E_CONFIG;
+  if (d->cfg < 0 || d->cfg >= kNumCfgH8 ||
+      (planes_of(d->prec) == 2 ? kCfgH8[d->cfg].lds2 : kCfgH8[d->cfg].lds1) > kMaxLds)
+    return RRIN_E_CONFIG;
   if (d->n < 1 || d->cin < 1 || d->cout < 8 || (d->cout & 7)) return RRIN_E_ARG;
   if (d->epi_mode < RRIN_EPI_LINEAR || d->epi_mode > RRIN_EPI_SUBPIXEL) return RRIN_E_ARG;
   if (!h8_ok(d->src, d->prec) || !h8_ok(d->dst, d->prec)) return RRIN_E_SHAPE;
@@ -1194,7 +1324,6 @@ extern "C" int rrin_conv3x3_h8_fwd(const rrin_conv_h8_desc* d, void* stream) {
   }
   const int planes = planes_of(d->prec);
   const CfgH8& ci = kCfgH8[d->cfg];
-  ConvH8Args a;
   memset(&a, 0, sizeof(a));
   const int64_t sg = (int64_t)d->src.g_off * d->src.g.plane;
   a.src_hi = static_cast<const uint4*>(d->src.hi) + sg;
@@ -1235,18 +1364,89 @@ extern "C" int rrin_conv3x3_h8_fwd(const rrin_conv_h8_desc* d, void* stream) {
   a.tiles_x = (w + 31) / 32;
   a.tiles_y = (h + ci.th - 1) / ci.th;
   a.n = d->n;
-  const int64_t grid = (int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n;
-  if (grid > 0x7fffffff) return RRIN_E_SHAPE;
+  if ((int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n > 0x7fffffff) return RRIN_E_SHAPE;
+  return 0;
+}
+
+}  // namespace rrin
+
+using namespace rrin;
+
+extern "C" int rrin_make_geom_h8(int32_t h, int32_t w, rrin_geom* g) {
+  if (!g || h < 1 || w < 1) return RRIN_E_ARG;
+  *g = make_geom_h8(h, w);
+  return 0;
+}
+
+extern "C" int rrin_conv_h8_cfg_count(void) { return kNumCfgH8; }
+extern "C" int rrin_conv_h8_cfg_bm(int32_t cfg) {
+  return (cfg >= 0 && cfg < kNumCfgH8) ? kCfgH8[cfg].bm : RRIN_E_CONFIG;
+}
+extern "C" int rrin_conv_h8_cfg_th(int32_t cfg) {
+  return (cfg >= 0 && cfg < kNumCfgH8) ? kCfgH8[cfg].th : RRIN_E_CONFIG;
+}
+extern "C" int rrin_conv_h8_cfg_ok(int32_t cfg, int32_t prec) {
+  if (cfg < 0 || cfg >= kNumCfgH8) return 0;
+  if (prec != RRIN_PREC_F16X3 && prec != RRIN_PREC_F16) return 0;
+  return (planes_of(prec) == 2 ? kCfgH8[cfg].lds2 : kCfgH8[cfg].lds1) <= kMaxLds ? 1 : 0;
+}
+
+extern "C" int rrin_conv_h8_cfg_fits(int32_t cfg, int32_t prec, int32_t cin) {
+  if (!rrin_conv_h8_cfg_ok(cfg, prec) || cin < 1) return 0;
+  const CfgH8& c = kCfgH8[cfg];
+  const int nch = (cin + 15) / 16;
+  if (!(c.sched & SCHED_WRES) || nch <= 2) return 1;
+  const int planes = planes_of(prec);
+  const size_t lds = (planes == 2 ? c.lds2 : c.lds1) + (size_t)(nch - 2) * c.wslab * planes;
+  return lds <= kMaxLds ? 1 : 0;
+}
+
+extern "C" int rrin_conv3x3_h8_fwd(const rrin_conv_h8_desc* d, void* stream) {
+  ConvH8Args a;
+  const int rc = h8_prepare(d, a);
+  if (rc) return rc;
+  const int planes = planes_of(d->prec);
   hipStream_t st = (hipStream_t)stream;
   switch (d->cfg) {
-#define X(id, nw, wm, wn) \
-  case id:                \
-    return launch_h8_cfg<nw, wm, wn>(a, planes, d->epi_mode, (int)grid, st);
+#define X(id, nw, wm, wn, sc, pe) \
+  case id:                        \
+    return launch_h8_cfg<nw, wm, wn, sc>(a, planes, d->epi_mode, pe, st);
     RRIN_H8_CFGS(X)
 #undef X
   }
   return RRIN_E_CONFIG;
 }
+
+#ifdef RRIN_LAB
+// Kernel lab (tools/conv_lab.py ablate; built only into librrin_lab.so, `make
+// lab`): one F16X3 LEAKY conv of tile config cfg 0, 1 or 6 with the schedule
+// knobs `sched` (SCHED_*, ablations included) and grid `persist` (as PE).
+template <int NW, int WM, int WN>
+static int lab_cfg(const ConvH8Args& a, int sched, int persist, hipStream_t st) {
+  switch (sched) {
+#define L(v) \
+  case v:    \
+    return launch_h8_k<NW, WM, WN, 2, RRIN_EPI_LEAKY, true, v>(a, persist, st);
+    L(0) L(1) L(2) L(3) L(4) L(7) L(8) L(16) L(32) L(48) L(64) L(96)
+#undef L
+  }
+  return RRIN_E_CONFIG;
+}
+
+extern "C" int rrin_conv3x3_h8_lab(const rrin_conv_h8_desc* d, int32_t sched, int32_t persist, void* stream) {
+  if (!d || d->prec != RRIN_PREC_F16X3 || d->epi_mode != RRIN_EPI_LEAKY || (d->cin % 8)) return RRIN_E_ARG;
+  ConvH8Args a;
+  const int rc = h8_prepare(d, a);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  switch (d->cfg) {
+    case 0: return lab_cfg<8, 2, 2>(a, sched, persist, st);
+    case 1: return lab_cfg<8, 1, 2>(a, sched, persist, st);
+    case 6: return lab_cfg<4, 1, 2>(a, sched, persist, st);
+  }
+  return RRIN_E_CONFIG;
+}
+#endif
 
 extern "C" int64_t rrin_pack_conv3x3_h8_halves(int32_t cout, int32_t cin, int32_t bm) {
   if (cout < 1 || cin < 1 || bm < 32 || bm % 32) return RRIN_E_ARG;

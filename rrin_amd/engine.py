@@ -48,19 +48,39 @@ def choose_cfg(cin: int, cout: int, level: int) -> int:
     return 1            # BM 64 x TH 8
 
 
+# Tile config per conv shape (cin, output rows, level of the grid it runs on)
+# of the split-fp16 / fp16 convs: fastest in the sweep of every config on every
+# conv of the Net (tools/conv_lab.py tune, 1280x720, 4 pairs;
+# profiles/r01_v10/tune_*.txt).  The shapes are fixed by the architecture
+# (channels and levels), so the keys hold at every resolution.  Sub-pixel up
+# convs run on the low-res grid with 4x the output rows.
+H8_TUNED = {
+    _lib.PREC_F16X3: {(6, 32, 0): 13, (9, 32, 0): 13, (10, 32, 0): 15, (16, 32, 0): 9, (32, 32, 0): 15,
+                      (32, 64, 1): 8, (64, 32, 0): 9, (64, 64, 1): 10, (64, 128, 1): 10, (64, 128, 2): 11,
+                      (128, 64, 1): 10, (128, 128, 2): 11, (128, 256, 2): 10, (128, 256, 3): 11,
+                      (256, 128, 2): 11, (256, 256, 3): 11, (256, 512, 3): 11, (256, 512, 4): 1,
+                      (512, 256, 3): 11, (512, 512, 4): 1},
+    _lib.PREC_F16: {(6, 32, 0): 15, (9, 32, 0): 13, (10, 32, 0): 15, (16, 32, 0): 9, (32, 32, 0): 9,
+                    (32, 64, 1): 10, (64, 32, 0): 9, (64, 64, 1): 9, (64, 128, 1): 10, (64, 128, 2): 11,
+                    (128, 64, 1): 0, (128, 128, 2): 11, (128, 256, 2): 11, (128, 256, 3): 10,
+                    (256, 128, 2): 11, (256, 256, 3): 10, (256, 512, 3): 11, (256, 512, 4): 4,
+                    (512, 256, 3): 5, (512, 512, 4): 4},
+}
+
+
 def choose_cfg_h8(cin: int, cout: int, prec: int, level: int = 0) -> int:
     """Tile config of the split-fp16 / fp16 conv (conv_f16.hip table) for a conv
     running on the grid of U-Net level ``level`` (a sub-pixel up conv runs on the
-    low-res grid with 4x the output rows), from the per-shape sweeps of
-    tools/conv_lab.py tune (profiles/r01_v8_tune_*.txt)."""
-    small = cout == 32 or level >= 4   # full-res 32-channel layers; the 45x80 bottom at 720p
-    if prec == _lib.PREC_F16:          # one MFMA per product: LDS allows the BM 128 tile
-        if small:
-            return 1    # BM 32 x TH 16, 8 waves
-        if cin >= 256 and cout >= 128:
-            return 5    # BM 128 x TH 16, 8 waves
-        return 0
-    return 6 if small else 0  # BM 32 x TH 8 (4 waves, 2 blocks/CU) | BM 64 x TH 16 (8 waves)
+    low-res grid with 4x the output rows): the swept choice (H8_TUNED), else a
+    level rule from the same sweep."""
+    cfg = H8_TUNED.get(prec, {}).get((cin, cout, level))
+    if cfg is not None and _lib.lib().rrin_conv_h8_cfg_fits(cfg, prec, cin):
+        return cfg
+    if level == 0 or cout <= 32:
+        return 9 if _lib.lib().rrin_conv_h8_cfg_fits(9, prec, cin) else 13  # BM 32 x TH 16, persistent
+    if level >= 4:
+        return 1    # BM 32 x TH 16, 8 waves: the 45x80 bottom at 720p
+    return 10 if level == 1 else 11  # BM 64 x TH 16, spread DMA issue (persistent at level 1)
 
 
 def t_coefficients(t, n: int) -> torch.Tensor:

@@ -137,3 +137,8 @@ def test_h8_geometry_and_cfgs():
     assert all(lib.rrin_conv_h8_cfg_ok(c, 2) for c in range(lib.rrin_conv_h8_cfg_count()))
     for prec in (0, 1, 2):
         assert lib.rrin_net_workspace_bytes(2, 64, 96, prec) > 0
+    # weight-resident configs (all weight chunks in LDS) fit small cin only
+    for c in range(lib.rrin_conv_h8_cfg_count()):
+        assert lib.rrin_conv_h8_cfg_fits(c, 1, 16) == ok[c]
+    assert lib.rrin_conv_h8_cfg_fits(9, 1, 64) == 1 and lib.rrin_conv_h8_cfg_fits(9, 1, 128) == 0
+    assert lib.rrin_conv_h8_cfg_fits(8, 1, 512) == 0 and lib.rrin_conv_h8_cfg_fits(0, 1, 512) == 1

@@ -33,10 +33,10 @@ def keyed_conv(cin, cout, key="h8"):
             keyed_tensor(f"{key}.{cin}.{cout}.b", (cout,), cin * 9))
 
 
-def cfgs(prec, cout):
+def cfgs(prec, cout, cin):
     lib = _lib.lib()
     return [c for c in range(lib.rrin_conv_h8_cfg_count())
-            if lib.rrin_conv_h8_cfg_ok(c, prec) and lib.rrin_conv_h8_cfg_bm(c) <= max(32, 2 * cout)]
+            if lib.rrin_conv_h8_cfg_fits(c, prec, cin) and lib.rrin_conv_h8_cfg_bm(c) <= max(32, 2 * cout)]
 
 
 def pack_h8(w, b, cfg, prec, dev, perm=None):
@@ -101,7 +101,7 @@ def test_h8_conv_golden(gpu, golden, prec, cin, cout):
     w = keyed_tensor(f"golden.conv.{cin}.{cout}.weight", (cout, cin, 3, 3), cin * 9)
     b = keyed_tensor(f"golden.conv.{cin}.{cout}.bias", (cout,), cin * 9)
     x = torch.from_numpy(g[f"conv_{cin}_{cout}_in"]).to(gpu)
-    for cfg in cfgs(prec, cout):
+    for cfg in cfgs(prec, cout, cin):
         dst, _ = conv_h8(H8Tensor.from_nchw(x, prec), w, b, cfg, prec)
         np.testing.assert_allclose(dst.to_nchw().cpu().numpy(), g[f"conv_{cin}_{cout}_out"], **TOL[prec],
                                    err_msg=f"cfg {cfg}")
@@ -115,7 +115,7 @@ def test_h8_conv_pool(gpu, prec, n, cin, cout, h, w):
     wt, b = keyed_conv(cin, cout)
     ref = ref_conv(x, wt, b, 0.1)
     refp = F.avg_pool2d(ref, 2)
-    for cfg in cfgs(prec, cout):
+    for cfg in cfgs(prec, cout, cin):
         if _lib.lib().rrin_conv_h8_cfg_th(cfg) // 8 < 2 and cfg == 4:
             continue  # WN == 1: no pool epilogue (rejected with RRIN_E_CONFIG, see test below)
         dst, pool = conv_h8(H8Tensor.from_nchw(x, prec), wt, b, cfg, prec, epi=_lib.EPI_LEAKY_POOL, dst_off=cout,
@@ -270,7 +270,7 @@ def test_h8_subpixel_upconv(gpu, prec, n, cin, cout, sh, sw):
     ref = F.conv2d(up, wt.double().cpu(), b.double().cpu(), padding=1)
     src = H8Tensor.from_nchw(x, prec)
     replicate_ring(src)
-    for cfg in cfgs(prec, 4 * cout):
+    for cfg in cfgs(prec, 4 * cout, cin):
         dst = subpixel_upconv(src, wt, b, cfg, prec, dst=H8Tensor(n, 2 * cout, 2 * sh, 2 * sw, gpu, prec))
         np.testing.assert_allclose(dst.to_nchw(0, cout).cpu().double().numpy(), ref.numpy(), **TOL[prec],
                                    err_msg=f"cfg {cfg}")

@@ -5,6 +5,10 @@
       per-launch time / TFLOP/s of one Net.forward in schedule order (HIP events)
   python tools/conv_lab.py tune [--batch 4 ...] [--out gpurun_out/tune.json]
       every tile config on every distinct conv shape of the Net; best per shape
+  python tools/conv_lab.py ablate [--reps 7]
+      split16 conv schedule variants and ablations (librrin_lab.so, `make lab`):
+      interleaved rounds in one process, median per variant; the schedule
+      variants are checked bitwise against the product kernel
 """
 from __future__ import annotations
 
@@ -152,7 +156,7 @@ def tune_h8(args):
         b = torch.zeros(kout)
         best, line = None, []
         for cfg in range(lib.rrin_conv_h8_cfg_count()):
-            if not lib.rrin_conv_h8_cfg_ok(cfg, prec) or lib.rrin_conv_h8_cfg_bm(cfg) > max(32, 2 * kout):
+            if not lib.rrin_conv_h8_cfg_fits(cfg, prec, cin) or lib.rrin_conv_h8_cfg_bm(cfg) > max(32, 2 * kout):
                 continue
             whi, wlo, bp, inv = pack_h8(wt, b, cfg, prec, dev)
             d = _lib.ConvH8Desc()
@@ -272,9 +276,87 @@ def single(args):
           f"{2 * 9 * cin * cout * h * w * n / (ms * 1e-3) / 1e12:.1f} TF")
 
 
+# (name, SCHED_* knobs of conv_f16.hip, persistent grid) -- the lab build's variants
+LAB_VARIANTS = [("base", 0, 0), ("persist", 0, 1), ("spread", 16, 0), ("persist+spread", 16, 1),
+                ("stagger", 64, 0), ("persist+stagger", 64, 1), ("wres", 32, 0), ("persist+wres", 32, 1),
+                ("persist+wres+spread", 48, 1), ("persist+wres+stagger", 96, 1),
+                ("noW", 1, 0), ("noIn", 2, 0), ("noLoads", 3, 0), ("noMfma", 4, 0), ("ldsOnly", 7, 0),
+                ("noEpi", 8, 0)]
+LAB_SHAPES = [(32, 32, 0, 6), (64, 32, 0, 6), (64, 32, 0, 1), (64, 64, 1, 0), (128, 64, 1, 0), (128, 128, 2, 0),
+              (256, 128, 2, 0), (256, 256, 3, 0), (512, 256, 3, 0), (512, 512, 4, 0)]
+
+
+def ablate(args):
+    from rrin_amd.pp import H8Tensor
+    from tests.test_gpu_h8 import pack_h8
+    lab = C.CDLL(os.path.join(REPO, "rrin_amd", "librrin_lab.so"))
+    fn = lab.rrin_conv3x3_h8_lab
+    fn.restype = C.c_int
+    fn.argtypes = [C.POINTER(_lib.ConvH8Desc), C.c_int32, C.c_int32, C.c_void_p]
+    lib = _lib.lib()
+    dev = torch.device("cuda:0")
+    prec = _lib.PREC_F16X3
+    st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    results = []
+    for cin, cout, L, cfg in LAB_SHAPES:
+        n, h, w = args.batch, args.height >> L, args.width >> L
+        torch.manual_seed(cin * 1000 + cout)
+        x = H8Tensor.from_nchw(torch.rand(n, cin, h, w, device=dev) * 2 - 1, prec)
+        dst = H8Tensor(n, cout, h, w, dev, prec)
+        wt = torch.randn(cout, cin, 3, 3) / (3 * cin ** 0.5)
+        whi, wlo, bp, inv = pack_h8(wt, torch.randn(cout) * 0.1, cfg, prec, dev)
+        d = _lib.ConvH8Desc()
+        d.n, d.cin, d.cout, d.cfg, d.prec, d.epi_mode, d.slope, d.inv_wscale = (n, cin, cout, cfg, prec,
+                                                                                _lib.EPI_LEAKY, 0.1, inv)
+        d.src, d.dst = x.view(0, cin), dst.view(0, cout)
+        d.whi, d.wlo, d.bias = whi.data_ptr(), wlo.data_ptr(), bp.data_ptr()
+        _lib.check(lib.rrin_conv3x3_h8_fwd(C.byref(d), st))
+        torch.cuda.synchronize()
+        ref = (dst.hi.clone(), dst.lo.clone())
+        fl = 2 * 9 * cin * cout * h * w * n
+        ok, times = {}, {}
+        for name, sched, pers in LAB_VARIANTS:
+            dst.hi.zero_()
+            dst.lo.zero_()
+            rc = fn(C.byref(d), sched, pers, st)
+            torch.cuda.synchronize()
+            if rc != 0:
+                ok[name] = f"rc{rc}"
+                continue
+            if sched & 15 == 0:
+                ok[name] = "ok" if torch.equal(dst.hi, ref[0]) and torch.equal(dst.lo, ref[1]) else "MISMATCH"
+            times[name] = []
+        for _ in range(args.reps):  # interleaved rounds (guide rule 24)
+            for name, sched, pers in LAB_VARIANTS:
+                if name not in times:
+                    continue
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(3):
+                    fn(C.byref(d), sched, pers, st)
+                e1.record()
+                e1.synchronize()
+                times[name].append(e0.elapsed_time(e1) / 3)
+        base = sorted(times["base"])[len(times["base"]) // 2]
+        line = []
+        for name, sched, pers in LAB_VARIANTS:
+            if name not in times:
+                line.append(f"{name}:{ok.get(name)}")
+                continue
+            ms = sorted(times[name])[len(times[name]) // 2]
+            results.append(dict(cin=cin, cout=cout, level=L, cfg=cfg, variant=name, sched=sched, persist=pers, ms=ms,
+                                tflops=fl / (ms * 1e-3) / 1e12, check=ok.get(name, "-")))
+            tag = "" if ok.get(name, "ok") == "ok" else "(" + ok[name] + ")"
+            line.append(f"{name}:{ms:.3f}({ms / base:.2f}){tag}")
+        print(f"{cin:4d}->{cout:4d} L{L} cfg{cfg} base {base:.3f} ms {fl / (base * 1e-3) / 1e12:.0f} TF | "
+              + " ".join(line), flush=True)
+    if args.out:
+        json.dump(results, open(args.out, "w"), indent=1)
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("mode", choices=["breakdown", "tune", "single"])
+    ap.add_argument("mode", choices=["breakdown", "tune", "single", "ablate"])
     ap.add_argument("--shape", type=int, nargs=5, default=[512, 256, 3, 1, 0],
                     help="single: cin cout level epi cfg")
     ap.add_argument("--batch", type=int, default=4)
@@ -286,7 +368,7 @@ def main():
                     help="breakdown: run the first conv of every U-Net with this H8 config (same BM only)")
     ap.add_argument("--precision", default="fp32", choices=["fp32", "fp32_split16", "fp16"])
     args = ap.parse_args()
-    {"breakdown": breakdown, "tune": tune, "single": single}[args.mode](args)
+    {"breakdown": breakdown, "tune": tune, "single": single, "ablate": ablate}[args.mode](args)
 
 
 if __name__ == "__main__":
