@@ -29,6 +29,7 @@ namespace rrin {
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef float float2v __attribute__((ext_vector_type(2)));
 
 constexpr int H8_LC = 34;  // staged input row: records of pixels x0-1 .. x0+32
@@ -119,10 +120,12 @@ __device__ inline void dma16(const uint4* src, uint4* lds_wave_base) {
 // in LDS, staged once per block.  Lab-only ablations (wrong outputs, they time
 // what is left): NO_WDMA / NO_IDMA keep reading the chunk-0 weight slab /
 // input tile instead of staging later chunks, NO_MFMA keeps the LDS operand
-// reads but drops the MFMAs, NO_EPI drops the epilogue.
+// reads but drops the MFMAs, NO_EPI drops the epilogue; MFMA16 issues every
+// 32x32x16 product as two v_mfma_f32_16x16x32_f16 of the same FLOPs on the
+// same operands (a clock/throughput probe of the other MFMA shape).
 enum : int {
   SCHED_NO_WDMA = 1, SCHED_NO_IDMA = 2, SCHED_NO_MFMA = 4, SCHED_NO_EPI = 8,
-  SCHED_SPREAD = 16, SCHED_WRES = 32, SCHED_STAGGER = 64
+  SCHED_SPREAD = 16, SCHED_WRES = 32, SCHED_STAGGER = 64, SCHED_MFMA16 = 128
 };
 constexpr int kSpreadTaps = 6, kStaggerTap = 3;
 
@@ -145,6 +148,7 @@ __global__ void __launch_bounds__(64 * NW) conv3x3_h8_kernel(ConvH8Args a) {
   constexpr bool kSpread = DMA && (SCHED & SCHED_SPREAD) != 0;
   constexpr bool kStagger = DMA && !kSpread && (SCHED & SCHED_STAGGER) != 0 && NW >= 2;
   constexpr bool kWRes = DMA && (SCHED & SCHED_WRES) != 0;
+  constexpr bool kMfma16 = (SCHED & SCHED_MFMA16) != 0;
   // DMA pieces (one 16-B record per thread and plane) of one chunk: input tile, then weight slab
   constexpr int NPIECE = T::IN_IT + (kWRes ? 0 : T::W_IT);
 
@@ -275,6 +279,7 @@ __global__ void __launch_bounds__(64 * NW) conv3x3_h8_kernel(ConvH8Args a) {
 
   // acc: hi*hi products; accx (F16X3): hi*lo' + lo'*hi, 2^11 too large
   floatx16 acc[WM][WN], accx[WM][WN];
+  floatx4 p16[kMfma16 ? WM : 1][kMfma16 ? WN : 1][2][PLANES];  // MFMA16 probe accumulators
 
   // 9 taps per chunk; one K16 block = 16 input channels at one tap (lanes
   // 0-31 carry channels 0-7 of the chunk, lanes 32-63 channels 8-15).
@@ -311,6 +316,18 @@ __global__ void __launch_bounds__(64 * NW) conv3x3_h8_kernel(ConvH8Args a) {
           if constexpr (kNoMfma) {
             asm volatile("" ::"v"(av[s][0][mt]), "v"(bv[s][0][nt]));
             if constexpr (PLANES == 2) asm volatile("" ::"v"(av[s][1][mt]), "v"(bv[s][1][nt]));
+          } else if constexpr (kMfma16) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+              if constexpr (PLANES == 2) {
+                p16[mt][nt][u][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[s][1][mt], bv[s][0][nt],
+                                                                           p16[mt][nt][u][1], 0, 0, 0);
+                p16[mt][nt][u][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[s][0][mt], bv[s][1][nt],
+                                                                           p16[mt][nt][u][1], 0, 0, 0);
+              }
+              p16[mt][nt][u][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[s][0][mt], bv[s][0][nt],
+                                                                         p16[mt][nt][u][0], 0, 0, 0);
+            }
           } else {
             if constexpr (PLANES == 2) {
               accx[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[s][1][mt], bv[s][0][nt], accx[mt][nt], 0, 0, 0);
@@ -354,6 +371,7 @@ __global__ void __launch_bounds__(64 * NW) conv3x3_h8_kernel(ConvH8Args a) {
         for (int i = 0; i < 16; ++i) {
           acc[mt][nt][i] = 0.f;
           accx[mt][nt][i] = 0.f;
+          if constexpr (kMfma16) p16[mt][nt][i >> 3][(i >> 2) & (PLANES - 1)][i & 3] = 0.f;
         }
     for (int c = 0; c < a.nchunks; ++c) {
       // staged during this chunk: chunk c+1 of this tile, or chunk 0 of the next tile
@@ -406,6 +424,18 @@ __global__ void __launch_bounds__(64 * NW) conv3x3_h8_kernel(ConvH8Args a) {
         __syncthreads();
       }
       buf ^= 1;
+    }
+
+    if constexpr (kMfma16) {  // probe: keep the results live (values are not the conv)
+#pragma unroll
+      for (int mt = 0; mt < WM; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < WN; ++nt)
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            acc[mt][nt][i] = p16[mt][nt][i >> 2][0][i & 3];
+            accx[mt][nt][i] = p16[mt][nt][i >> 2][PLANES - 1][i & 3];
+          }
     }
 
     // ---- epilogue: scale, bias, leaky, split, 8-B half-record stores (+ pool)
@@ -1427,7 +1457,7 @@ static int lab_cfg(const ConvH8Args& a, int sched, int persist, hipStream_t st) 
 #define L(v) \
   case v:    \
     return launch_h8_k<NW, WM, WN, 2, RRIN_EPI_LEAKY, true, v>(a, persist, st);
-    L(0) L(1) L(2) L(3) L(4) L(7) L(8) L(16) L(32) L(48) L(64) L(96)
+    L(0) L(1) L(2) L(3) L(4) L(7) L(8) L(16) L(32) L(48) L(64) L(96) L(128) L(144)
 #undef L
   }
   return RRIN_E_CONFIG;

@@ -280,6 +280,7 @@ def single(args):
 LAB_VARIANTS = [("base", 0, 0), ("persist", 0, 1), ("spread", 16, 0), ("persist+spread", 16, 1),
                 ("stagger", 64, 0), ("persist+stagger", 64, 1), ("wres", 32, 0), ("persist+wres", 32, 1),
                 ("persist+wres+spread", 48, 1), ("persist+wres+stagger", 96, 1),
+                ("mfma16", 128, 0), ("spread+mfma16", 144, 0), ("persist+spread+mfma16", 144, 1),
                 ("noW", 1, 0), ("noIn", 2, 0), ("noLoads", 3, 0), ("noMfma", 4, 0), ("ldsOnly", 7, 0),
                 ("noEpi", 8, 0)]
 LAB_SHAPES = [(32, 32, 0, 6), (64, 32, 0, 6), (64, 32, 0, 1), (64, 64, 1, 0), (128, 64, 1, 0), (128, 128, 2, 0),
@@ -323,7 +324,7 @@ def ablate(args):
             if rc != 0:
                 ok[name] = f"rc{rc}"
                 continue
-            if sched & 15 == 0:
+            if sched & 143 == 0:
                 ok[name] = "ok" if torch.equal(dst.hi, ref[0]) and torch.equal(dst.lo, ref[1]) else "MISMATCH"
             times[name] = []
         for _ in range(args.reps):  # interleaved rounds (guide rule 24)
