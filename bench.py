@@ -3,8 +3,10 @@
 
 One step = one ``Net.forward`` over this rank's batch of synthetic 1280x720
 fp32 frame pairs (inputs already resident in HBM) + the RCCL all-gather that
-reassembles the interpolated frames of all ranks (rrin_amd.shard).  Weak
-scaling: every rank owns ``--batch`` pairs per step.
+reassembles the interpolated frames of all ranks (rrin_amd.shard); the gather
+of step k runs on RCCL's stream while step k+1 computes, and every gather has
+completed before the clock stops.  Weak scaling: every rank owns ``--batch``
+pairs per step.
 
   python bench.py [--gpus N --steps K --warmup W --batch B --height H --width W]
   torchrun --nproc-per-node N bench.py --gpus N ...   (driver, N > 1)
@@ -32,7 +34,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 from rrin_amd import Net, _lib  # noqa: E402
-from rrin_amd.shard import gather_frames  # noqa: E402
+from rrin_amd.shard import GatherPipeline  # noqa: E402
 from rrin_amd.synthetic import keyed_state_dict, synthetic_batch  # noqa: E402
 from rrin_amd.unet import conv_bytes, conv_flops, roofline_bound_s  # noqa: E402
 
@@ -139,19 +141,22 @@ def main():
     B, H, W = args.batch, args.height, args.width
     i0, i1 = synthetic_batch(B, H, W, first_index=rank * B)
     i0, i1 = i0.to(dev), i1.to(dev)
-    gathered = torch.empty((world * B, 3, H, W), device=dev) if world > 1 else None
+    # the all-gather of step k overlaps the compute of step k+1 (double-buffered outputs)
+    gather = GatherPipeline((world * B, 3, H, W), torch.float32, dev) if world > 1 else None
     eng = net.engine()
     lib = _lib.lib()
 
     def step(prof=None):
         with torch.no_grad():
             out = eng.forward(i0, i1, args.t, prof=prof)
-            if world > 1:
-                gather_frames(out, out=gathered)
+            if gather is not None:
+                gather.submit(out)
         return out
 
     for _ in range(args.warmup):
         step()
+    if gather is not None:
+        gather.drain()
     torch.cuda.synchronize(dev)
     last = [None]
 
@@ -169,6 +174,8 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         last[0] = step(prof)
+    if gather is not None:
+        gather.drain()  # every step's gather is inside the timed region
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()

@@ -23,24 +23,59 @@ def shard_bounds(global_batch: int, rank: int, world: int):
     return rank * per, (rank + 1) * per
 
 
-def gather_frames(local: torch.Tensor, group=None, out: torch.Tensor | None = None) -> torch.Tensor:
-    """All-gather equal shards ``local`` [b,...] into ``[world*b, ...]`` (rank order)."""
+def gather_frames(local: torch.Tensor, group=None, out: torch.Tensor | None = None, async_op: bool = False):
+    """All-gather equal shards ``local`` [b,...] into ``[world*b, ...]`` (rank order).
+    ``async_op=True`` returns ``(out, work)``: on RCCL the gather runs on the
+    communicator's stream and ``work.wait()`` orders the caller's stream after
+    it; gloo (CPU tests / single-GPU rehearsal) completes before returning."""
     world = dist.get_world_size(group)
+    work = None
     if world == 1:
-        return local if out is None else out.copy_(local)
+        out = local if out is None else out.copy_(local)
+        return (out, work) if async_op else out
     local = local.contiguous()
     if out is None:
         out = torch.empty((world * local.shape[0],) + tuple(local.shape[1:]),
                           dtype=local.dtype, device=local.device)
     if dist.get_backend(group) == "gloo":
-        # gloo (CPU tests / single-GPU rehearsal): gather through host memory
+        # gather through host memory
         host = local.cpu()
         parts = [torch.empty_like(host) for _ in range(world)]
         dist.all_gather(parts, host, group=group)
         out.copy_(torch.cat(parts))
     else:
-        dist.all_gather_into_tensor(out, local, group=group)
-    return out
+        work = dist.all_gather_into_tensor(out, local, group=group, async_op=async_op)
+    return (out, work) if async_op else out
+
+
+class GatherPipeline:
+    """Overlap the all-gather of step k with the compute of step k+1 (SURVEY
+    §8e: the gather is issued on a side stream while the next batch computes).
+    ``depth`` output buffers are cycled; a buffer's previous gather is waited
+    for before it is reused, and ``drain()`` waits for every gather in flight."""
+
+    def __init__(self, shape, dtype, device, group=None, depth: int = 2):
+        self.group = group
+        self.bufs = [torch.empty(shape, dtype=dtype, device=device) for _ in range(depth)]
+        self.inflight = [None] * depth  # (work, local) per buffer
+        self.k = 0
+
+    def submit(self, local: torch.Tensor) -> torch.Tensor:
+        i = self.k % len(self.bufs)
+        self.k += 1
+        if self.inflight[i] is not None:
+            work, _ = self.inflight[i]
+            if work is not None:
+                work.wait()
+        out, work = gather_frames(local, group=self.group, out=self.bufs[i], async_op=True)
+        self.inflight[i] = (work, local)  # keep the shard alive until its gather is done
+        return out
+
+    def drain(self):
+        for i, f in enumerate(self.inflight):
+            if f is not None and f[0] is not None:
+                f[0].wait()
+            self.inflight[i] = None
 
 
 def interpolate_sharded(net, i0_local: torch.Tensor, i1_local: torch.Tensor, t=0.5, group=None,

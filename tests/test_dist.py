@@ -80,3 +80,32 @@ def test_sharded_equals_unsharded(tmp_path):
         ref = net_forward(sd, i0, i1, 0.5)
     assert got.shape == (4, 3, 32, 48)
     assert torch.allclose(got, ref, atol=1e-6, rtol=0)
+
+
+def _pipeline_worker(rank, world, port, result_path):
+    """GatherPipeline: three steps through two cycled buffers; every gather
+    returns the rank-ordered concatenation of that step's shards."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from rrin_amd.shard import GatherPipeline
+    pipe = GatherPipeline((world * 2, 3, 4, 5), torch.float32, "cpu")
+    outs = []
+    for k in range(3):
+        local = torch.full((2, 3, 4, 5), float(10 * k + rank))
+        outs.append(pipe.submit(local).clone())
+    pipe.drain()
+    if rank == 0:
+        torch.save(torch.stack(outs), result_path)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gather_pipeline_gloo(tmp_path):
+    world = 2
+    path = str(tmp_path / "pipe.pt")
+    mp.start_processes(_pipeline_worker, args=(world, _free_port(), path), nprocs=world, join=True,
+                       start_method="spawn")
+    got = torch.load(path, weights_only=True)
+    for k in range(3):
+        ref = torch.cat([torch.full((2, 3, 4, 5), float(10 * k + r)) for r in range(world)])
+        assert torch.equal(got[k], ref)
