@@ -1664,7 +1664,8 @@ static int head_h8_launch(const HeadH8Args& a, int planes, int grid, hipStream_t
   return hip_code(hipGetLastError());
 }
 
-extern "C" int rrin_head_h8_fwd(const rrin_head_h8_desc* d, void* stream) {
+// Validate a head descriptor and turn it into kernel arguments (grid: blocks).
+static int head_prepare(const rrin_head_h8_desc* d, HeadH8Args& a, int& grid) {
   if (!d || !d->w || !d->bias || d->cin != 32 || d->n < 1) return RRIN_E_ARG;
   if (d->prec != RRIN_PREC_F16X3 && d->prec != RRIN_PREC_F16) return RRIN_E_ARG;
   if (!h8_ok(d->src, d->prec) || !h8_ok(d->g16, d->prec)) return RRIN_E_SHAPE;
@@ -1677,7 +1678,6 @@ extern "C" int rrin_head_h8_fwd(const rrin_head_h8_desc* d, void* stream) {
   }
   if (d->mode == RRIN_HEAD_FINAL && !d->out) return RRIN_E_ARG;
   const int planes = planes_of(d->prec);
-  HeadH8Args a;
   memset(&a, 0, sizeof(a));
   const int64_t sg = (int64_t)d->src.g_off * d->src.g.plane;
   a.src_hi = static_cast<const uint4*>(d->src.hi) + sg;
@@ -1708,7 +1708,16 @@ extern "C" int rrin_head_h8_fwd(const rrin_head_h8_desc* d, void* stream) {
   a.w_ = w;
   a.tiles_x = (w + 31) / 32;
   a.tiles_y = (h + 15) / 16;
-  const int grid = a.tiles_x * a.tiles_y * d->n;
+  grid = a.tiles_x * a.tiles_y * d->n;
+  return 0;
+}
+
+extern "C" int rrin_head_h8_fwd(const rrin_head_h8_desc* d, void* stream) {
+  HeadH8Args a;
+  int grid = 0;
+  const int rc = head_prepare(d, a, grid);
+  if (rc) return rc;
+  const int planes = planes_of(d->prec);
   hipStream_t st = (hipStream_t)stream;
   switch (d->mode) {
     case RRIN_HEAD_PLAIN:
