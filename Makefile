@@ -1,7 +1,13 @@
 # Builds rrin_amd/librrin_hip.so for gfx950 (MI355X).  `make -j16`
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH  ?= gfx950
-CXXFLAGS := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function -Iinclude
+# No packed FP32 VALU ops (v_pk_fma/mul/add_f32) in any kernel: measured on MI355X,
+# the low element of a v_pk_fma_f32 in lanes 48-63 of a wave came out perturbed
+# when a co-resident workgroup of another kernel on the CU ran LDS-DMA + MFMA
+# (DESIGN.md §9).  The flag also reaches the host compile, which ignores it
+# (one "not a recognized feature" line per file).
+NOPK := -Xclang -target-feature -Xclang -packed-fp32-ops
+CXXFLAGS := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function -Iinclude $(NOPK)
 SRC_DIR := rrin_amd/csrc
 OBJ_DIR := build/obj
 SRCS := $(wildcard $(SRC_DIR)/*.hip)

@@ -66,6 +66,8 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (production); gloo only to rehearse N ranks on fewer GPUs")
     ap.add_argument("--cpu-pairs", type=int, default=2, help="pairs timed on the CPU baseline")
+    ap.add_argument("--streams", type=int, default=1,
+                    help="HIP streams the rank's pairs are split over (their kernels overlap)")
     return ap.parse_args()
 
 
@@ -148,7 +150,7 @@ def main():
 
     def step(prof=None):
         with torch.no_grad():
-            out = eng.forward(i0, i1, args.t, prof=prof)
+            out = eng.forward(i0, i1, args.t, prof=prof, streams=args.streams)
             if gather is not None:
                 gather.submit(out)
         return out
@@ -163,7 +165,7 @@ def main():
     prof = None
     cap = 0
     if not args.no_prof:
-        cap = 100 * args.steps
+        cap = 100 * args.steps * max(1, args.streams)
         h = C.c_void_p()
         _lib.check(lib.rrin_prof_create(cap, C.byref(h)), "rrin_prof_create")
         prof = h.value

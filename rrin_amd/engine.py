@@ -107,7 +107,7 @@ def t_coefficients(t, n: int) -> torch.Tensor:
 
 
 class RRINEngine:
-    MAX_WORKSPACES = 2
+    MAX_WORKSPACES = 4
 
     def __init__(self, net, precision: str = "fp32", subpixel_max_level: int = 2):
         self.lib = _lib.lib()
@@ -174,6 +174,7 @@ class RRINEngine:
         self.cfgs = [m[2] for m in meta]
         self._ws = OrderedDict()
         self._flow_valid = {}
+        self._sides = []
 
     def _init_h8(self, net):
         """Pack for the split-fp16 (F16X3) or fp16 (F16) path: [cob][16-ch chunk][tap][half][bm][8]
@@ -251,9 +252,10 @@ class RRINEngine:
         self.cfgs = [m[3] for m in meta]
         self._ws = OrderedDict()
         self._flow_valid = {}
+        self._sides = []
 
-    def workspace(self, n: int, h: int, w: int) -> torch.Tensor:
-        key = (n, h, w)
+    def workspace(self, n: int, h: int, w: int, slot: int = 0) -> torch.Tensor:
+        key = (n, h, w, slot)
         ws = self._ws.get(key)
         if ws is None:
             nbytes = self.lib.rrin_net_workspace_bytes(n, h, w, self.prec)
@@ -269,11 +271,21 @@ class RRINEngine:
             self._ws.move_to_end(key)
         return ws
 
-    def forward(self, i0: torch.Tensor, i1: torch.Tensor, t=0.5, prof=None, reuse_flow: bool = False) -> torch.Tensor:
+    def _side_streams(self, k: int):
+        if len(self._sides) < k:
+            self._sides += [torch.cuda.Stream(self.device) for _ in range(k - len(self._sides))]
+        return self._sides[:k]
+
+    def forward(self, i0: torch.Tensor, i1: torch.Tensor, t=0.5, prof=None, reuse_flow: bool = False,
+                streams: int = 1) -> torch.Tensor:
         """One Net.forward.  ``reuse_flow=True`` promises that (i0, i1) is the pair
         of the previous call with the same shape: the Flow U-Net (t-independent,
         model.py:35, 30 % of the FLOPs) is skipped and its kept raw output is
-        re-blended for this t."""
+        re-blended for this t.  ``streams > 1`` splits the batch
+        into that many contiguous parts, each with its own workspace, enqueued
+        on its own HIP stream: the parts' kernels overlap, filling each other's
+        launch gaps and last-wave tails (pairs are independent, so the output is
+        bitwise the same)."""
         if i0.device != self.device or i1.device != self.device:
             raise RuntimeError(f"inputs on {i0.device}/{i1.device}, model on {self.device}")
         if i0.dtype != torch.float32 or i1.dtype != torch.float32:
@@ -288,20 +300,35 @@ class RRINEngine:
         i1 = i1.contiguous()
         out = torch.empty_like(i0)
         coef = t_coefficients(t, n).to(self.device, non_blocking=True)
+        k = max(1, min(int(streams), n))
+        bounds = [(n * j // k, n * (j + 1) // k) for j in range(k)]
         with torch.cuda.device(self.device):
-            ws = self.workspace(n, h, w)
-            skip = bool(reuse_flow) and self._flow_valid.get((n, h, w), False)
-            d = _lib.NetDesc()
-            d.n, d.h, d.w = n, h, w
-            d.i0, d.i1, d.out, d.coef = i0.data_ptr(), i1.data_ptr(), out.data_ptr(), coef.data_ptr()
-            d.convs = self.conv_table
-            d.heads = self.head_table
-            d.workspace = ws.data_ptr()
-            d.workspace_bytes = ws.numel()
-            d.skip_flow = 1 if skip else 0
-            d.prec = self.prec
-            d.prof = prof
-            stream = torch.cuda.current_stream(self.device).cuda_stream
-            _lib.check(self.lib.rrin_net_fwd(C.byref(d), C.c_void_p(stream)), "rrin_net_fwd")
-            self._flow_valid[(n, h, w)] = True
+            main = torch.cuda.current_stream(self.device)
+            # workspaces first: a new one is zero-filled on the main stream, before the fork
+            wss = [self.workspace(hi - lo, h, w, j) for j, (lo, hi) in enumerate(bounds)]
+            sides = self._side_streams(k - 1)
+            for s in sides:
+                s.wait_stream(main)
+            for j, (lo, hi) in enumerate(bounds):
+                st = main if j == 0 else sides[j - 1]
+                self._forward_part(i0[lo:hi], i1[lo:hi], out[lo:hi], coef[lo:hi], j, wss[j], st, prof, reuse_flow)
+            for s in sides:
+                main.wait_stream(s)
         return out
+
+    def _forward_part(self, i0, i1, out, coef, slot, ws, stream, prof, reuse_flow):
+        n, _, h, w = i0.shape
+        key = (n, h, w, slot)
+        skip = bool(reuse_flow) and self._flow_valid.get(key, False)
+        d = _lib.NetDesc()
+        d.n, d.h, d.w = n, h, w
+        d.i0, d.i1, d.out, d.coef = i0.data_ptr(), i1.data_ptr(), out.data_ptr(), coef.data_ptr()
+        d.convs = self.conv_table
+        d.heads = self.head_table
+        d.workspace = ws.data_ptr()
+        d.workspace_bytes = ws.numel()
+        d.skip_flow = 1 if skip else 0
+        d.prec = self.prec
+        d.prof = prof
+        _lib.check(self.lib.rrin_net_fwd(C.byref(d), C.c_void_p(stream.cuda_stream)), "rrin_net_fwd")
+        self._flow_valid[key] = True

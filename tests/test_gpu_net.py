@@ -77,6 +77,22 @@ def test_batch_equals_per_sample_and_deterministic(gpu, nets):
     assert torch.equal(full, parts)
 
 
+@pytest.mark.parametrize("precision", ["fp32_split16", "fp16", "fp32"])
+def test_streams_split_is_bitwise(gpu, nets, precision):
+    """The batch split over several HIP streams (engine.forward(streams=k)) gives the
+    single-stream output bit for bit, also when k does not divide the batch."""
+    net = nets["stress"]
+    net.precision = precision
+    i0, i1 = synthetic_batch(5, 64, 96, first_index=21)
+    i0, i1 = i0.to(gpu), i1.to(gpu)
+    eng = net.engine()
+    with torch.no_grad():
+        one = eng.forward(i0, i1, 0.5)
+        for k in (2, 3):
+            assert torch.equal(eng.forward(i0, i1, 0.5, streams=k), one)
+    net.precision = "fp32"
+
+
 def test_weight_reload_repacks(gpu):
     net = make_net(gpu)
     i0, i1 = synthetic_batch(1, 64, 64)
