@@ -42,6 +42,23 @@ constexpr float kLoUnscale = 1.0f / 2048.0f;
 __device__ inline _Float16 lo_of(float v, _Float16 hi) { return (_Float16)((v - (float)hi) * kLoScale); }
 __device__ inline float join(_Float16 hi, _Float16 lo) { return fmaf((float)lo, kLoUnscale, (float)hi); }
 
+typedef _Float16 half2v __attribute__((ext_vector_type(2)));
+// hi/lo split of 4 consecutive channels into two 8-B record halves: hi = RNE fp16
+// of v (v_cvt_pk_f16_f32, two values per op), lo = fp16 of (v - hi) * 2^11 as one
+// v_fma_mix_f32 (hi read as f16) on v * 2^11 -- the exact difference, so the same
+// bits as lo_of (the kernels are built without packed FP32 ops).
+__device__ inline void split4(const float* v, uint2& hv, uint2& lv) {
+  const half2v h0 = __builtin_convertvector((float2v){v[0], v[1]}, half2v);
+  const half2v h1 = __builtin_convertvector((float2v){v[2], v[3]}, half2v);
+  const float l0 = fmaf((float)h0[0], -kLoScale, v[0] * kLoScale), l1 = fmaf((float)h0[1], -kLoScale, v[1] * kLoScale);
+  const float l2 = fmaf((float)h1[0], -kLoScale, v[2] * kLoScale), l3 = fmaf((float)h1[1], -kLoScale, v[3] * kLoScale);
+  hv = make_uint2(__builtin_bit_cast(unsigned, h0), __builtin_bit_cast(unsigned, h1));
+  lv = make_uint2(__builtin_bit_cast(unsigned, __builtin_convertvector((float2v){l0, l1}, half2v)),
+                  __builtin_bit_cast(unsigned, __builtin_convertvector((float2v){l2, l3}, half2v)));
+}
+// LeakyReLU for 0 <= slope <= 1 (h8_prepare checks): one mul + one max
+__device__ inline float leaky(float t, float slope) { return fmaxf(t, t * slope); }
+
 struct ConvH8Args {
   const uint4* src_hi;
   const uint4* src_lo;
@@ -485,15 +502,13 @@ __global__ void __launch_bounds__(64 * NW) conv3x3_h8_kernel(ConvH8Args a) {
                 a.edge[((int64_t)img * creal + grp * 8 + 4 * hh + e) * a.ring + ri] = t[e];
             } else {
               const int64_t rec = (int64_t)grp * a.dst_gp + (int64_t)(Y + 1) * a.dst_wp + X + kH8PadLeft;
-              _Float16 hi[4], lo[4];
+              float v[4];
 #pragma unroll
-              for (int e = 0; e < 4; ++e) {
-                const float v = t[e] + bs[e];
-                hi[e] = (_Float16)v;
-                lo[e] = lo_of(v, hi[e]);
-              }
-              reinterpret_cast<uint2*>(dst[0] + rec)[hh] = __builtin_bit_cast(uint2, hi);
-              if constexpr (PLANES == 2) reinterpret_cast<uint2*>(dst[1] + rec)[hh] = __builtin_bit_cast(uint2, lo);
+              for (int e = 0; e < 4; ++e) v[e] = t[e] + bs[e];
+              uint2 hv, lv;
+              split4(v, hv, lv);
+              reinterpret_cast<uint2*>(dst[0] + rec)[hh] = hv;
+              if constexpr (PLANES == 2) reinterpret_cast<uint2*>(dst[1] + rec)[hh] = lv;
             }
           }
         }
@@ -522,18 +537,13 @@ __global__ void __launch_bounds__(64 * NW) conv3x3_h8_kernel(ConvH8Args a) {
               float t = acc[mt][nt][4 * q + e];
               if constexpr (PLANES == 2) t = fmaf(accx[mt][nt][4 * q + e], kLoUnscale, t);
               t = t * a.inv_wscale + bs[e];
-              if constexpr (EPI != RRIN_EPI_LINEAR) t = t > 0.f ? t : t * a.slope;
+              if constexpr (EPI != RRIN_EPI_LINEAR) t = leaky(t, a.slope);
               v[nt][e] = t;
             }
             if (co0 < a.cout && y < a.h && x < a.w) {
               const int64_t rec = (int64_t)grp * a.dst_gp + (int64_t)(y + 1) * a.dst_wp + x + kH8PadLeft;
-              _Float16 hi[4], lo[4];
-#pragma unroll
-              for (int e = 0; e < 4; ++e) {
-                hi[e] = (_Float16)v[nt][e];
-                lo[e] = lo_of(v[nt][e], hi[e]);
-              }
-              const uint2 hv = __builtin_bit_cast(uint2, hi), lv = __builtin_bit_cast(uint2, lo);
+              uint2 hv, lv;
+              split4(v[nt], hv, lv);
               reinterpret_cast<uint2*>(dst[0] + rec)[hh] = hv;
               if constexpr (PLANES == 2) reinterpret_cast<uint2*>(dst[1] + rec)[hh] = lv;
               if constexpr (EPI == RRIN_EPI_LEAKY_REP) {
@@ -562,14 +572,10 @@ __global__ void __launch_bounds__(64 * NW) conv3x3_h8_kernel(ConvH8Args a) {
               const int y = yb + 2 * p2;
               if (!(j & 1) && co0 < a.cout && y < a.h && x < a.w) {
                 const int64_t rec = (int64_t)grp * a.pool_gp + (int64_t)(y / 2 + 1) * a.pool_wp + x / 2 + kH8PadLeft;
-                _Float16 hi[4], lo[4];
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                  hi[e] = (_Float16)s4[e];
-                  lo[e] = lo_of(s4[e], hi[e]);
-                }
-                reinterpret_cast<uint2*>(pdst[0] + rec)[hh] = __builtin_bit_cast(uint2, hi);
-                if constexpr (PLANES == 2) reinterpret_cast<uint2*>(pdst[1] + rec)[hh] = __builtin_bit_cast(uint2, lo);
+                uint2 hv, lv;
+                split4(s4, hv, lv);
+                reinterpret_cast<uint2*>(pdst[0] + rec)[hh] = hv;
+                if constexpr (PLANES == 2) reinterpret_cast<uint2*>(pdst[1] + rec)[hh] = lv;
               }
             }
           }
@@ -1346,6 +1352,7 @@ static int h8_prepare(const rrin_conv_h8_desc* d, ConvH8Args& a) {
   if (d->dst.g.h != (sub ? 2 * h : h) || d->dst.g.w != (sub ? 2 * w : w)) return RRIN_E_SHAPE;
   if (d->cin > 8 * d->src.groups || (sub ? d->cout / 4 : d->cout) > 8 * d->dst.groups) return RRIN_E_ARG;
   if (sub && ((d->cout & 31) || !d->edge)) return RRIN_E_ARG;
+  if (!(d->slope >= 0.f && d->slope <= 1.f)) return RRIN_E_ARG;  // leaky() as max(t, slope t)
   if (d->epi_mode == RRIN_EPI_LEAKY_POOL) {
     if (!kCfgH8[d->cfg].pool_ok) return RRIN_E_CONFIG;  // a wave must own both rows of a pool pair
     if (!h8_ok(d->pool, d->prec) || (h & 1) || (w & 1) || d->pool.g.h * 2 != h || d->pool.g.w * 2 != w ||
