@@ -357,6 +357,123 @@ __global__ void __launch_bounds__(64 * NW) conv3x3_h8_kernel(ConvH8Args a) {
     }
   };
 
+  // ---- epilogue piece (mt, q) of tile tl: V = the combined accumulators
+  // (acc + accx 2^-11, weight scale still applied): scale, bias, leaky, split,
+  // 8-B half-record stores (+ pool / edge-replicate / sub-pixel ring scratch).
+  auto epi_piece = [&](const TileId& tl, const auto& V, int mt, int q) {
+    const int cob = tl.cob, x0 = tl.x0, img = tl.img;
+    const int yb = tl.y0 + wn * WN;
+    const int x = x0 + j;
+    uint4* dst[2] = {a.dst_hi + img * a.dst_img, PLANES == 2 ? a.dst_lo + img * a.dst_img : nullptr};
+    if constexpr (EPI == RRIN_EPI_SUBPIXEL) {
+      // rows co' = (co/8)*32 + phase*8 + co%8: an MFMA row block (mt) is one
+      // 8-channel group, q its phase (py, px); LR pixel (y, x) -> HR (2y+py, 2x+px)
+      const int HH = 2 * a.h, WW = 2 * a.w, creal = a.cout >> 2;
+      const int grp = (cob * BM + mt * 32) >> 5;
+      if (grp * 32 >= a.cout) return;
+      const int py = q >> 1, px = q & 1;
+      const int co0 = cob * BM + mt * 32 + 8 * q;
+      float bs[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bs[e] = a.bias[co0 + 4 * hh + e];
+#pragma unroll
+      for (int nt = 0; nt < WN; ++nt) {
+        const int y = yb + nt;
+        if (y >= a.h || x >= a.w) continue;
+        const int Y = 2 * y + py, X = 2 * x + px;
+        float t[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) t[e] = V[mt][nt][4 * q + e] * a.inv_wscale;
+        const int64_t ri = ring_index(Y, X, HH, WW);
+        if (ri >= 0) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) a.edge[((int64_t)img * creal + grp * 8 + 4 * hh + e) * a.ring + ri] = t[e];
+        } else {
+          const int64_t rec = (int64_t)grp * a.dst_gp + (int64_t)(Y + 1) * a.dst_wp + X + kH8PadLeft;
+          float v[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = t[e] + bs[e];
+          uint2 hv, lv;
+          split4(v, hv, lv);
+          reinterpret_cast<uint2*>(dst[0] + rec)[hh] = hv;
+          if constexpr (PLANES == 2) reinterpret_cast<uint2*>(dst[1] + rec)[hh] = lv;
+        }
+      }
+    } else {
+      uint4* pdst[2] = {nullptr, nullptr};
+      if constexpr (EPI == RRIN_EPI_LEAKY_POOL) {
+        pdst[0] = a.pool_hi + img * a.pool_img;
+        if (PLANES == 2) pdst[1] = a.pool_lo + img * a.pool_img;
+      }
+      const int co0 = cob * BM + mt * 32 + 8 * q;  // first channel of the record
+      const int grp = co0 >> 3;
+      float bs[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bs[e] = a.bias[co0 + 4 * hh + e];
+      float v[WN][4];
+#pragma unroll
+      for (int nt = 0; nt < WN; ++nt) {
+        const int y = yb + nt;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float t = V[mt][nt][4 * q + e];
+          t = t * a.inv_wscale + bs[e];
+          if constexpr (EPI != RRIN_EPI_LINEAR) t = leaky(t, a.slope);
+          v[nt][e] = t;
+        }
+        if (co0 < a.cout && y < a.h && x < a.w) {
+          const int64_t rec = (int64_t)grp * a.dst_gp + (int64_t)(y + 1) * a.dst_wp + x + kH8PadLeft;
+          uint2 hv, lv;
+          split4(v[nt], hv, lv);
+          reinterpret_cast<uint2*>(dst[0] + rec)[hh] = hv;
+          if constexpr (PLANES == 2) reinterpret_cast<uint2*>(dst[1] + rec)[hh] = lv;
+          if constexpr (EPI == RRIN_EPI_LEAKY_REP) {
+            // edge replicate into the padding ring (read only by a sub-pixel up conv)
+            const int dy0 = y == 0 ? -1 : 0, dy1 = y == a.h - 1 ? 1 : 0;
+            const int dx0 = x == 0 ? -1 : 0, dx1 = x == a.w - 1 ? 1 : 0;
+            for (int dy = dy0; dy <= dy1; ++dy)
+              for (int dx = dx0; dx <= dx1; ++dx)
+                if (dy | dx) {
+                  const int64_t r2 = rec + (int64_t)dy * a.dst_wp + dx;
+                  reinterpret_cast<uint2*>(dst[0] + r2)[hh] = hv;
+                  if constexpr (PLANES == 2) reinterpret_cast<uint2*>(dst[1] + r2)[hh] = lv;
+                }
+          }
+        }
+      }
+      if constexpr (EPI == RRIN_EPI_LEAKY_POOL) {
+#pragma unroll
+        for (int p2 = 0; p2 < WN / 2; ++p2) {
+          float s4[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float s = v[2 * p2][e] + v[2 * p2 + 1][e];
+            s4[e] = 0.25f * (s + __shfl_xor(s, 1));
+          }
+          const int y = yb + 2 * p2;
+          if (!(j & 1) && co0 < a.cout && y < a.h && x < a.w) {
+            const int64_t rec = (int64_t)grp * a.pool_gp + (int64_t)(y / 2 + 1) * a.pool_wp + x / 2 + kH8PadLeft;
+            uint2 hv, lv;
+            split4(s4, hv, lv);
+            reinterpret_cast<uint2*>(pdst[0] + rec)[hh] = hv;
+            if constexpr (PLANES == 2) reinterpret_cast<uint2*>(pdst[1] + rec)[hh] = lv;
+          }
+        }
+      }
+    }
+  };
+  // combined accumulators: V = acc + accx 2^-11 (F16X3), V = acc (F16)
+  auto combine = [&](floatx16 (&V)[WM][WN]) {
+#pragma unroll
+    for (int mt = 0; mt < WM; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < WN; ++nt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          V[mt][nt][i] = PLANES == 2 ? fmaf(accx[mt][nt][i], kLoUnscale, acc[mt][nt][i]) : acc[mt][nt][i];
+  };
+  constexpr int NPIECE_EPI = WM * 4;
+
   int tile = bid;
   if (tile >= ntiles) return;
   TileId cur = tile_id(tile);
@@ -455,11 +572,6 @@ __global__ void __launch_bounds__(64 * NW) conv3x3_h8_kernel(ConvH8Args a) {
           }
     }
 
-    // ---- epilogue: scale, bias, leaky, split, 8-B half-record stores (+ pool)
-    const int cob = cur.cob, x0 = cur.x0, img = cur.img;
-    const int yb = cur.y0 + wn * WN;
-    const int x = x0 + j;
-    uint4* dst[2] = {a.dst_hi + img * a.dst_img, PLANES == 2 ? a.dst_lo + img * a.dst_img : nullptr};
     if constexpr (kNoEpi) {
 #pragma unroll
       for (int mt = 0; mt < WM; ++mt)
@@ -467,121 +579,12 @@ __global__ void __launch_bounds__(64 * NW) conv3x3_h8_kernel(ConvH8Args a) {
         for (int nt = 0; nt < WN; ++nt)
 #pragma unroll
           for (int i = 0; i < 16; ++i) asm volatile("" ::"v"(acc[mt][nt][i]), "v"(accx[mt][nt][i]));
-      (void)cob, (void)yb, (void)x, (void)dst;
-    } else if constexpr (EPI == RRIN_EPI_SUBPIXEL) {
-      // rows co' = (co/8)*32 + phase*8 + co%8: an MFMA row block (mt) is one
-      // 8-channel group, q its phase (py, px); LR pixel (y, x) -> HR (2y+py, 2x+px)
-      const int HH = 2 * a.h, WW = 2 * a.w, creal = a.cout >> 2;
-#pragma unroll
-      for (int mt = 0; mt < WM; ++mt) {
-        const int grp = (cob * BM + mt * 32) >> 5;
-        if (grp * 32 >= a.cout) continue;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int py = q >> 1, px = q & 1;
-          const int co0 = cob * BM + mt * 32 + 8 * q;
-          float bs[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) bs[e] = a.bias[co0 + 4 * hh + e];
-#pragma unroll
-          for (int nt = 0; nt < WN; ++nt) {
-            const int y = yb + nt;
-            if (y >= a.h || x >= a.w) continue;
-            const int Y = 2 * y + py, X = 2 * x + px;
-            float t[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              float u = acc[mt][nt][4 * q + e];
-              if constexpr (PLANES == 2) u = fmaf(accx[mt][nt][4 * q + e], kLoUnscale, u);
-              t[e] = u * a.inv_wscale;
-            }
-            const int64_t ri = ring_index(Y, X, HH, WW);
-            if (ri >= 0) {
-#pragma unroll
-              for (int e = 0; e < 4; ++e)
-                a.edge[((int64_t)img * creal + grp * 8 + 4 * hh + e) * a.ring + ri] = t[e];
-            } else {
-              const int64_t rec = (int64_t)grp * a.dst_gp + (int64_t)(Y + 1) * a.dst_wp + X + kH8PadLeft;
-              float v[4];
-#pragma unroll
-              for (int e = 0; e < 4; ++e) v[e] = t[e] + bs[e];
-              uint2 hv, lv;
-              split4(v, hv, lv);
-              reinterpret_cast<uint2*>(dst[0] + rec)[hh] = hv;
-              if constexpr (PLANES == 2) reinterpret_cast<uint2*>(dst[1] + rec)[hh] = lv;
-            }
-          }
-        }
-      }
     } else {
-      uint4* pdst[2] = {nullptr, nullptr};
-      if constexpr (EPI == RRIN_EPI_LEAKY_POOL) {
-        pdst[0] = a.pool_hi + img * a.pool_img;
-        if (PLANES == 2) pdst[1] = a.pool_lo + img * a.pool_img;
-      }
+      floatx16 V[WM][WN];
+      combine(V);
 #pragma unroll
-      for (int mt = 0; mt < WM; ++mt) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int co0 = cob * BM + mt * 32 + 8 * q;  // first channel of the record
-          const int grp = co0 >> 3;
-          float bs[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) bs[e] = a.bias[co0 + 4 * hh + e];
-          float v[WN][4];
-#pragma unroll
-          for (int nt = 0; nt < WN; ++nt) {
-            const int y = yb + nt;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              float t = acc[mt][nt][4 * q + e];
-              if constexpr (PLANES == 2) t = fmaf(accx[mt][nt][4 * q + e], kLoUnscale, t);
-              t = t * a.inv_wscale + bs[e];
-              if constexpr (EPI != RRIN_EPI_LINEAR) t = leaky(t, a.slope);
-              v[nt][e] = t;
-            }
-            if (co0 < a.cout && y < a.h && x < a.w) {
-              const int64_t rec = (int64_t)grp * a.dst_gp + (int64_t)(y + 1) * a.dst_wp + x + kH8PadLeft;
-              uint2 hv, lv;
-              split4(v[nt], hv, lv);
-              reinterpret_cast<uint2*>(dst[0] + rec)[hh] = hv;
-              if constexpr (PLANES == 2) reinterpret_cast<uint2*>(dst[1] + rec)[hh] = lv;
-              if constexpr (EPI == RRIN_EPI_LEAKY_REP) {
-                // edge replicate into the padding ring (read only by a sub-pixel up conv)
-                const int dy0 = y == 0 ? -1 : 0, dy1 = y == a.h - 1 ? 1 : 0;
-                const int dx0 = x == 0 ? -1 : 0, dx1 = x == a.w - 1 ? 1 : 0;
-                for (int dy = dy0; dy <= dy1; ++dy)
-                  for (int dx = dx0; dx <= dx1; ++dx)
-                    if (dy | dx) {
-                      const int64_t r2 = rec + (int64_t)dy * a.dst_wp + dx;
-                      reinterpret_cast<uint2*>(dst[0] + r2)[hh] = hv;
-                      if constexpr (PLANES == 2) reinterpret_cast<uint2*>(dst[1] + r2)[hh] = lv;
-                    }
-              }
-            }
-          }
-          if constexpr (EPI == RRIN_EPI_LEAKY_POOL) {
-#pragma unroll
-            for (int p2 = 0; p2 < WN / 2; ++p2) {
-              float s4[4];
-#pragma unroll
-              for (int e = 0; e < 4; ++e) {
-                float s = v[2 * p2][e] + v[2 * p2 + 1][e];
-                s4[e] = 0.25f * (s + __shfl_xor(s, 1));
-              }
-              const int y = yb + 2 * p2;
-              if (!(j & 1) && co0 < a.cout && y < a.h && x < a.w) {
-                const int64_t rec = (int64_t)grp * a.pool_gp + (int64_t)(y / 2 + 1) * a.pool_wp + x / 2 + kH8PadLeft;
-                uint2 hv, lv;
-                split4(s4, hv, lv);
-                reinterpret_cast<uint2*>(pdst[0] + rec)[hh] = hv;
-                if constexpr (PLANES == 2) reinterpret_cast<uint2*>(pdst[1] + rec)[hh] = lv;
-              }
-            }
-          }
-        }
-      }
-    }  // epilogue
+      for (int p = 0; p < NPIECE_EPI; ++p) epi_piece(cur, V, p / 4, p % 4);
+    }
     if (!more) break;
     tile = ntile;
     cur = nxt;

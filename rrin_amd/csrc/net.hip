@@ -437,8 +437,10 @@ extern "C" int rrin_prof_create(int32_t capacity, rrin_prof** out) {
   p->ev.resize(2 * (size_t)capacity);
   p->kind.resize(capacity);
   p->flops.resize(capacity);
+  // timing-only events: no system-scope fence (a default event record writes
+  // back and invalidates the caches, which the next launch then pays for)
   for (auto& e : p->ev) {
-    hipError_t r = hipEventCreate(&e);
+    hipError_t r = hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
     if (r != hipSuccess) {
       delete p;
       return (int)r;

@@ -276,3 +276,42 @@ def test_h8_subpixel_upconv(gpu, prec, n, cin, cout, sh, sw):
                                    err_msg=f"cfg {cfg}")
         assert not dst.to_nchw(cout, cout).any()           # the bridge half of CAT is untouched
         assert not dst.hi[:, :, 0].any() and not dst.hi[:, :, :, :8].any()  # zero padding kept
+
+
+@pytest.mark.parametrize("prec", [X3, F16])
+@pytest.mark.parametrize("cin,epi", [(32, _lib.EPI_LEAKY_POOL), (64, _lib.EPI_LEAKY), (32, _lib.EPI_LINEAR)])
+def test_h8_conv_many_tiles_per_block(gpu, prec, cin, epi):
+    """Shapes with more tiles than a persistent grid holds, so each block loops
+    over several tiles (chunk 0 of tile k+1 staged behind tile k's last chunk)."""
+    n, cout, h, w = 4, 32, 96, 640
+    x = torch.rand(n, cin, h, w, device=gpu) * 2 - 1
+    wt, b = keyed_conv(cin, cout, "many")
+    slope = None if epi == _lib.EPI_LINEAR else 0.1
+    ref = ref_conv(x, wt, b, slope)
+    refp = F.avg_pool2d(ref, 2)
+    for cfg in cfgs(prec, cout, cin):
+        if epi == _lib.EPI_LEAKY_POOL and cfg == 4:
+            continue
+        dst, pool = conv_h8(H8Tensor.from_nchw(x, prec), wt, b, cfg, prec, epi=epi)
+        np.testing.assert_allclose(dst.to_nchw().cpu().double().numpy(), ref.numpy(), **TOL[prec],
+                                   err_msg=f"cfg {cfg}")
+        if pool is not None:
+            np.testing.assert_allclose(pool.to_nchw().cpu().double().numpy(), refp.numpy(), **TOL[prec],
+                                       err_msg=f"cfg {cfg} pool")
+
+
+@pytest.mark.parametrize("prec", [X3, F16])
+def test_h8_subpixel_many_tiles_per_block(gpu, prec):
+    """Sub-pixel up conv (ring scratch + phase epilogue) on a grid with several
+    tiles per block, every config."""
+    n, cin, cout, sh, sw = 4, 64, 32, 48, 320
+    x = torch.rand(n, cin, sh, sw, device=gpu) * 2 - 1
+    wt, b = keyed_conv(cin, cout, "subm")
+    up = F.interpolate(x.double().cpu(), scale_factor=2, mode="bilinear", align_corners=False)
+    ref = F.conv2d(up, wt.double().cpu(), b.double().cpu(), padding=1)
+    src = H8Tensor.from_nchw(x, prec)
+    replicate_ring(src)
+    for cfg in cfgs(prec, 4 * cout, cin):
+        dst = subpixel_upconv(src, wt, b, cfg, prec, dst=H8Tensor(n, 2 * cout, 2 * sh, 2 * sw, gpu, prec))
+        np.testing.assert_allclose(dst.to_nchw(0, cout).cpu().double().numpy(), ref.numpy(), **TOL[prec],
+                                   err_msg=f"cfg {cfg}")
