@@ -66,8 +66,9 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (production); gloo only to rehearse N ranks on fewer GPUs")
     ap.add_argument("--cpu-pairs", type=int, default=2, help="pairs timed on the CPU baseline")
-    ap.add_argument("--streams", type=int, default=1,
-                    help="HIP streams the rank's pairs are split over (their kernels overlap)")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="HIP streams the rank's pairs are split over (their kernels overlap, filling each "
+                         "other's launch gaps and last-wave tails; outputs are bitwise those of one stream)")
     return ap.parse_args()
 
 
@@ -94,6 +95,19 @@ def cpu_baseline(sd, h, w, pairs, t, gpu_out0, alt_out0=None):
     return ({"value": pairs / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
              "sample": f"{pairs} x Net.forward {w}x{h} N=1 fp32 on PyTorch-CPU (oracle/ref_net.py), "
                        f"{dt:.1f} s"}, parity)
+
+
+def union_ms(spans):
+    """Length of the union of [t0, t1] intervals (ms)."""
+    tot, end = 0.0, None
+    for a, b in sorted(spans):
+        if end is None or a > end:
+            tot += b - a
+            end = b
+        elif b > end:
+            tot += b - end
+            end = b
+    return tot
 
 
 def time_steps(eng, i0, i1, t, steps, dev, prof=None):
@@ -202,10 +216,16 @@ def main():
         other_ms = sum(ms[i] for i in range(n) if kinds[i] == 2)
         edge_ms = sum(ms[i] for i in range(n) if kinds[i] == 3)
         conv_launches = sum(1 for i in range(n) if kinds[i] == 0)
+        # busy time of the conv family = union of its launch spans (launches of
+        # the --streams parts overlap; with one stream this is the sum)
+        t0s, t1s = (C.c_float * cap)(), (C.c_float * cap)()
+        cnt2 = C.c_int32()
+        _lib.check(lib.rrin_prof_read_spans(prof, t0s, t1s, cap, C.byref(cnt2)), "rrin_prof_read_spans")
+        conv_busy = union_ms([(t0s[i], t1s[i]) for i in range(cnt2.value) if kinds[i] == 0])
         lib.rrin_prof_destroy(prof)
         conv_ms_step = conv_ms / args.steps
         head_ms_step = head_ms / args.steps
-        achieved = conv_fl / (conv_ms * 1e-3) / 1e12
+        achieved = conv_fl / (conv_busy * 1e-3) / 1e12
         peak = PEAK[args.precision]
         roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1),
                     "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None,
@@ -215,6 +235,9 @@ def main():
                                "conv3x3_h8_kernel (77 body convs, v_mfma_f32_32x32x16_f16)"),
                     "flops_per_launch_avg": conv_fl / max(conv_launches, 1),
                     "avg_launch_ms": conv_ms / max(conv_launches, 1),
+                    "conv_busy_ms_per_step": round(conv_busy / args.steps, 3),
+                    "launch_overlap": round(conv_ms / conv_busy, 3),
+                    "streams": args.streams,
                     "conv_ms_per_step": round(conv_ms_step, 3),
                     "head_ms_per_step": round(head_ms_step, 3),
                     "layout_upsample_ms_per_step": round(other_ms / args.steps, 3),
@@ -224,14 +247,14 @@ def main():
         tlb = B * sum(roofline_bound_s(getattr(net, u), H, W, bpv, peak * 1e12, HBM_PEAK_GBS * 1e9)
                       for u in ("Flow", "refine_flow", "Mask", "final"))
         roofline["t_lb_conv_ms_per_step"] = round(1e3 * tlb, 3)
-        roofline["t_lb_frac_of_conv_time"] = round(1e3 * tlb / conv_ms_step, 4)
+        roofline["t_lb_frac_of_conv_time"] = round(1e3 * tlb / (conv_busy / args.steps), 4)
 
     if roofline is not None:
         # HBM bytes per conv launch from the PMC passes of the same command
         # (tools/gpu_check.sh pmc -> tools/pmc_summary.py; rocprofv3 cannot
         # collect counters inside this process's timed region)
         tab = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_traffic.json")
-        key = f"{args.precision}@{W}x{H}x{B}"
+        key = f"{args.precision}@{W}x{H}x{B}" + (f"s{args.streams}" if args.streams > 1 else "")
         if os.path.exists(tab):
             ent = json.load(open(tab)).get(key)
             if ent is not None:

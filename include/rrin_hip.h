@@ -283,6 +283,9 @@ int rrin_prof_reset(rrin_prof* p);
 /* After the stream has synchronised: per recorded launch its kind, elapsed
  * milliseconds and algorithmic FLOPs (2*MAC of the conv; 0 for layout). */
 int rrin_prof_read(rrin_prof* p, int32_t* kinds, float* ms, double* flops, int32_t cap, int32_t* count);
+/* Start / end of every recorded launch in ms after the first recorded event
+ * (launches on several streams: the union of their spans is the busy time). */
+int rrin_prof_read_spans(rrin_prof* p, float* t0_ms, float* t1_ms, int32_t cap, int32_t* count);
 
 typedef struct rrin_net_desc {
   int32_t n, h, w, pad_;

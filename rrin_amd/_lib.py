@@ -133,6 +133,8 @@ SIGNATURES = {
     "rrin_prof_reset": (C.c_int, [C.c_void_p]),
     "rrin_prof_read": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32,
                                  C.POINTER(C.c_int32)]),
+    "rrin_prof_read_spans": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32,
+                                       C.POINTER(C.c_int32)]),
     "rrin_abi_version": (C.c_int, []),
     "rrin_strerror": (C.c_char_p, [C.c_int]),
 }

@@ -480,6 +480,18 @@ extern "C" int rrin_prof_read(rrin_prof* p, int32_t* kinds, float* ms, double* f
   return 0;
 }
 
+extern "C" int rrin_prof_read_spans(rrin_prof* p, float* t0_ms, float* t1_ms, int32_t cap, int32_t* count) {
+  if (!p || !count || !t0_ms || !t1_ms) return RRIN_E_ARG;
+  const int n = p->count < cap ? p->count : cap;
+  for (int i = 0; i < n; ++i) {
+    hipError_t r = hipEventElapsedTime(&t0_ms[i], p->ev[0], p->ev[2 * i]);
+    if (r == hipSuccess) r = hipEventElapsedTime(&t1_ms[i], p->ev[0], p->ev[2 * i + 1]);
+    if (r != hipSuccess) return (int)r;
+  }
+  *count = n;
+  return 0;
+}
+
 // ---- weight packing (host) ------------------------------------------------
 // wpack[cob][chunk][ci8][tap][bm]: the slab a block stages per K chunk is
 // contiguous; zero rows/cols pad cin to 8 and cout to bm.

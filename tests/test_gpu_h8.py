@@ -315,3 +315,34 @@ def test_h8_subpixel_many_tiles_per_block(gpu, prec):
         dst = subpixel_upconv(src, wt, b, cfg, prec, dst=H8Tensor(n, 2 * cout, 2 * sh, 2 * sw, gpu, prec))
         np.testing.assert_allclose(dst.to_nchw(0, cout).cpu().double().numpy(), ref.numpy(), **TOL[prec],
                                    err_msg=f"cfg {cfg}")
+
+
+def head_h8(src: H8Tensor, dst: H8Tensor, w, b, mode, coef=None, out=None, prec=X3):
+    dev = src.hi.device
+    w_d = w.detach().float().contiguous().to(dev)
+    b_d = b.detach().float().contiguous().to(dev)
+    d = _lib.HeadH8Desc()
+    d.n, d.cin, d.cout, d.mode, d.prec = src.n, 32, w.shape[0], mode, prec
+    d.src, d.g16 = src.view(0, 32), dst.view(0, dst.c)
+    d.w, d.bias = w_d.data_ptr(), b_d.data_ptr()
+    d.coef = coef.data_ptr() if coef is not None else None
+    d.out = out.data_ptr() if out is not None else None
+    _lib.check(_lib.lib().rrin_head_h8_fwd(C.byref(d), H.stream(dev)), "rrin_head_h8_fwd")
+    torch.cuda.synchronize(dev)
+
+
+@pytest.mark.parametrize("prec", [X3, F16])
+@pytest.mark.parametrize("cout", [2, 3, 4])
+@pytest.mark.parametrize("n,h,w,scale", [(2, 40, 72, 1.0), (1, 20, 50, 1e-3), (3, 16, 32, 300.0)])
+def test_h8_head_plain(gpu, prec, cout, n, h, w, scale):
+    """MFMA head conv (32 -> cout) against float64: weights split in the kernel
+    with a per-channel power-of-two scale (tiny and large weights), ragged tiles."""
+    x = torch.rand(n, 32, h, w, device=gpu) * 2 - 1
+    wt, b = keyed_conv(32, cout, "headh8")
+    wt = wt * scale
+    dst = H8Tensor(n, 16, h, w, gpu, prec)
+    head_h8(H8Tensor.from_nchw(x, prec), dst, wt, b, _lib.HEAD_PLAIN, prec=prec)
+    ref = ref_conv(x, wt, b)
+    tol = dict(rtol=1e-4, atol=1e-4 * max(scale, 1.0)) if prec == X3 else dict(rtol=2e-2, atol=2e-2 * max(scale, 1.0))
+    np.testing.assert_allclose(dst.to_nchw(0, cout).cpu().double().numpy(), ref.numpy(), **tol)
+    assert not dst.to_nchw(cout, 16 - cout).any()

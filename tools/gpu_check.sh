@@ -40,7 +40,7 @@ if [[ $STEPS == *pmc* ]]; then
   for prec in ${PMCPREC:-fp32_split16 fp32 fp16}; do
     run pmc_fetch_$prec 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch_$prec -o run -- python3 bench.py --steps 2 --warmup 1 --cpu-baseline off --no-prof --no-alt --precision $prec
     run pmc_write_$prec 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write_$prec -o run -- python3 bench.py --steps 2 --warmup 1 --cpu-baseline off --no-prof --no-alt --precision $prec
-    python tools/pmc_summary.py --fetch gpurun_out/pmc_fetch_$prec --write gpurun_out/pmc_write_$prec --steps 3 --out gpurun_out/traffic_$prec.json --table gpurun_out/pmc_traffic.json --precision $prec > gpurun_out/pmc_summary_$prec.log 2>&1; cat gpurun_out/pmc_summary_$prec.log
+    python tools/pmc_summary.py --fetch gpurun_out/pmc_fetch_$prec --write gpurun_out/pmc_write_$prec --steps 3 --out gpurun_out/traffic_$prec.json --table gpurun_out/pmc_traffic.json --precision $prec --config ${PMCCFG:-1280x720x4s2} > gpurun_out/pmc_summary_$prec.log 2>&1; cat gpurun_out/pmc_summary_$prec.log
   done
 fi
 exit 0
