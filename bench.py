@@ -270,7 +270,9 @@ def main():
     pairs = world * B * args.steps
     value = pairs / elapsed
     res = {
-        "metric": "interpolated frames/sec at 1280x720 fp32 (Net.forward, frame pairs/s)",
+        "metric": ("interpolated frames/sec at 1280x720 fp32 (Net.forward, frame pairs/s)"
+                   if (W, H, args.precision) == (1280, 720, "fp32_split16") else
+                   f"interpolated frames/sec at {W}x{H} {args.precision} (Net.forward, frame pairs/s)"),
         "value": round(value, 3),
         "unit": "frames/s",
         "n_gpus": world,
