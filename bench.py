@@ -69,6 +69,8 @@ def parse():
     ap.add_argument("--streams", type=int, default=2,
                     help="HIP streams the rank's pairs are split over (their kernels overlap, filling each "
                          "other's launch gaps and last-wave tails; outputs are bitwise those of one stream)")
+    ap.add_argument("--split", default=None,
+                    help="explicit pairs per stream, e.g. 1,3 (overrides --streams' even split)")
     return ap.parse_args()
 
 
@@ -161,10 +163,13 @@ def main():
     gather = GatherPipeline((world * B, 3, H, W), torch.float32, dev) if world > 1 else None
     eng = net.engine()
     lib = _lib.lib()
+    split = [int(c) for c in args.split.split(",")] if args.split else None
+    if split:
+        args.streams = len(split)
 
     def step(prof=None):
         with torch.no_grad():
-            out = eng.forward(i0, i1, args.t, prof=prof, streams=args.streams)
+            out = eng.forward(i0, i1, args.t, prof=prof, streams=args.streams, split=split)
             if gather is not None:
                 gather.submit(out)
         return out

@@ -277,7 +277,7 @@ class RRINEngine:
         return self._sides[:k]
 
     def forward(self, i0: torch.Tensor, i1: torch.Tensor, t=0.5, prof=None, reuse_flow: bool = False,
-                streams: int = 1) -> torch.Tensor:
+                streams: int = 1, split=None) -> torch.Tensor:
         """One Net.forward.  ``reuse_flow=True`` promises that (i0, i1) is the pair
         of the previous call with the same shape: the Flow U-Net (t-independent,
         model.py:35, 30 % of the FLOPs) is skipped and its kept raw output is
@@ -285,7 +285,7 @@ class RRINEngine:
         into that many contiguous parts, each with its own workspace, enqueued
         on its own HIP stream: the parts' kernels overlap, filling each other's
         launch gaps and last-wave tails (pairs are independent, so the output is
-        bitwise the same)."""
+        bitwise the same).  ``split`` gives the part sizes explicitly."""
         if i0.device != self.device or i1.device != self.device:
             raise RuntimeError(f"inputs on {i0.device}/{i1.device}, model on {self.device}")
         if i0.dtype != torch.float32 or i1.dtype != torch.float32:
@@ -300,8 +300,18 @@ class RRINEngine:
         i1 = i1.contiguous()
         out = torch.empty_like(i0)
         coef = t_coefficients(t, n).to(self.device, non_blocking=True)
-        k = max(1, min(int(streams), n))
-        bounds = [(n * j // k, n * (j + 1) // k) for j in range(k)]
+        if split is not None:  # explicit part sizes (pairs per stream)
+            split = [int(c) for c in split]
+            if sum(split) != n or min(split) < 1:
+                raise ValueError(f"split {split} does not partition a batch of {n}")
+            cuts = [0]
+            for c in split:
+                cuts.append(cuts[-1] + c)
+            bounds = list(zip(cuts[:-1], cuts[1:]))
+            k = len(bounds)
+        else:
+            k = max(1, min(int(streams), n))
+            bounds = [(n * j // k, n * (j + 1) // k) for j in range(k)]
         with torch.cuda.device(self.device):
             main = torch.cuda.current_stream(self.device)
             # workspaces first: a new one is zero-filled on the main stream, before the fork

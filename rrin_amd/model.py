@@ -43,6 +43,10 @@ class Net(nn.Module):
         # sub-pixel convs on the low-res input (upsample folded into the weights,
         # no upsample pass); -1 = always an explicit upsample pass
         self.subpixel_max_level = 2
+        # HIP streams a batch of N >= 2 pairs is split over (pairs are
+        # independent: the output is bitwise that of one stream; the parts'
+        # kernels fill each other's launch gaps and tails)
+        self.streams = 2
         self.register_load_state_dict_post_hook(Net._on_load)
 
     # Packed weights are rebuilt after load_state_dict / .to() / param edits.
@@ -75,7 +79,8 @@ class Net(nn.Module):
         if torch.is_grad_enabled():
             raise RuntimeError("rrin_amd.Net.interpolate is inference-only: use torch.no_grad()")
         eng = self.engine()
-        return [eng.forward(input0, input1, t, reuse_flow=(k > 0)) for k, t in enumerate(ts)]
+        return [eng.forward(input0, input1, t, reuse_flow=(k > 0), streams=self.streams)
+                for k, t in enumerate(ts)]
 
     def forward(self, input0, input1, t=0.5):
         if torch.is_grad_enabled() and (input0.requires_grad or input1.requires_grad or
@@ -83,4 +88,4 @@ class Net(nn.Module):
             raise RuntimeError(
                 "rrin_amd.Net runs HIP inference kernels only (no backward): call it under "
                 "torch.no_grad() or torch.inference_mode(), as convert.py:117 does")
-        return self.engine().forward(input0, input1, t)
+        return self.engine().forward(input0, input1, t, streams=self.streams)
