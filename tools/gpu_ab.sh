@@ -1,9 +1,12 @@
+#!/bin/bash
+# A/B of tile tables in the default bench (unprofiled; interleaved rounds)
+# usage: A='{json}' B='{json}' bash tools/gpu_ab.sh
 mkdir -p gpurun_out
-N='{}'
-T='{"(32,32,0)": 8, "(32,64,1)": 10, "(64,32,0)": 15, "(128,256,2)": 13, "(256,128,2)": 10}'
-for i in 1 2; do
-timeout -k 10 300 python tools/bench_ab.py "$N" -- --steps 10 --warmup 3 --cpu-baseline off --no-alt > gpurun_out/ab_base_$i.log 2>&1 || exit 1
-timeout -k 10 300 python tools/bench_ab.py "$T" -- --steps 10 --warmup 3 --cpu-baseline off --no-alt > gpurun_out/ab_new_$i.log 2>&1 || exit 1
-timeout -k 10 300 python tools/bench_ab.py "$N" -- --steps 10 --warmup 3 --cpu-baseline off --no-alt --no-prof > gpurun_out/ab_base_noprof_$i.log 2>&1 || exit 1
+A=${A:-'{}'}
+run() { timeout -k 10 300 python tools/bench_ab.py "$1" -- --steps 10 --warmup 3 --cpu-baseline off --no-alt --no-prof 2>&1 | tail -1 | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(sys.argv[1], d['value'])" "$1"; }
+for i in 1 2 3; do
+run "$A" || exit 1
+run "$B" || exit 1
+[ -n "${C:-}" ] && { run "$C" || exit 1; }
 done
-for f in gpurun_out/ab_*.log; do echo $f $(grep -o '"value": [0-9.]*' $f) $(grep -o '"conv_ms_per_step": [0-9.]*' $f); done
+exit 0
