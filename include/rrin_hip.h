@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define RRIN_ABI_VERSION 5
+#define RRIN_ABI_VERSION 6
 
 #define RRIN_OK 0
 #define RRIN_E_SHAPE (-1)     /* H or W not a multiple of 16, or N < 1          */

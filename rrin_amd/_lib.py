@@ -9,7 +9,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "librrin_hip.so")
 
 # enums (rrin_hip.h)
