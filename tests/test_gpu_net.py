@@ -90,6 +90,11 @@ def test_streams_split_is_bitwise(gpu, nets, precision):
         one = eng.forward(i0, i1, 0.5)
         for k in (2, 3):
             assert torch.equal(eng.forward(i0, i1, 0.5, streams=k), one)
+        assert torch.equal(eng.forward(i0, i1, 0.5, split=[1, 4]), one)
+        net.streams = 1
+        assert torch.equal(net(i0, i1, 0.5), one)
+        net.streams = 2  # the module default
+        assert torch.equal(net(i0, i1, 0.5), one)
     net.precision = "fp32"
 
 
