@@ -12,10 +12,11 @@ pairs per step.
   torchrun --nproc-per-node N bench.py --gpus N ...   (driver, N > 1)
 
 Rank 0 prints one JSON line.  ``roofline`` is for the dominant kernel (the
-MFMA conv3x3 family): algorithmic conv FLOPs / summed conv launch time, both
-measured live with HIP events recorded around every launch of the timed
-steps; ``cpu_baseline`` times the CPU oracle (oracle/, a restatement of the
-reference op sequence) on a bounded sample on this host.
+MFMA conv3x3 family): algorithmic conv FLOPs / the family's busy time (union of
+its launch spans — the batch runs as ``--streams`` parts whose launches
+overlap), measured live with HIP events recorded around every launch of the
+timed steps; ``cpu_baseline`` times the CPU oracle (oracle/, a restatement of
+the reference op sequence) on a bounded sample on this host.
 """
 from __future__ import annotations
 
