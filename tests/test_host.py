@@ -82,3 +82,13 @@ def test_synthetic_pairs_deterministic():
     assert 0 <= a1.min() and a1.max() <= 1
     x0, _ = synthetic_batch(3, 32, 48, first_index=4)
     assert torch.equal(x0[1:2], a0)
+
+
+def test_bench_union_ms():
+    """bench.py's conv busy time: union of launch spans (overlapping streams)."""
+    import bench
+    assert bench.union_ms([]) == 0.0
+    assert bench.union_ms([(0.0, 1.0), (2.0, 3.0)]) == 2.0            # disjoint: the sum
+    assert bench.union_ms([(0.0, 2.0), (1.0, 3.0)]) == 3.0            # overlap counted once
+    assert bench.union_ms([(1.0, 4.0), (0.0, 5.0), (2.0, 3.0)]) == 5.0  # nested, unsorted
+    assert bench.union_ms([(0.0, 1.0), (1.0, 2.0)]) == 2.0            # touching
