@@ -113,13 +113,13 @@ def union_ms(spans):
     return tot
 
 
-def time_steps(eng, i0, i1, t, steps, dev, prof=None):
+def time_steps(eng, i0, i1, t, steps, dev, prof=None, streams=1):
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     out = None
     with torch.no_grad():
         for _ in range(steps):
-            out = eng.forward(i0, i1, t, prof=prof)
+            out = eng.forward(i0, i1, t, prof=prof, streams=streams)
     torch.cuda.synchronize(dev)
     return time.perf_counter() - t0, out
 
@@ -131,9 +131,11 @@ def read_prof(lib, prof, cap):
     cnt = C.c_int32()
     _lib.check(lib.rrin_prof_read(prof, kinds, ms, fl, cap, C.byref(cnt)), "rrin_prof_read")
     n = cnt.value
-    conv = [(ms[i], fl[i]) for i in range(n) if kinds[i] == 0]
-    return (sum(m for m, _ in conv), sum(f for _, f in conv), len(conv),
-            sum(ms[i] for i in range(n) if kinds[i] == 1), sum(ms[i] for i in range(n) if kinds[i] == 2))
+    t0s, t1s = (C.c_float * cap)(), (C.c_float * cap)()
+    _lib.check(lib.rrin_prof_read_spans(prof, t0s, t1s, cap, C.byref(cnt)), "rrin_prof_read_spans")
+    conv = [i for i in range(n) if kinds[i] == 0]
+    # conv busy time (union of spans), conv FLOPs, launches
+    return union_ms([(t0s[i], t1s[i]) for i in conv]), sum(fl[i] for i in conv), len(conv)
 
 
 def main():
@@ -308,18 +310,18 @@ def main():
         eng32 = net.engine()
         with torch.no_grad():
             for _ in range(max(1, args.warmup)):
-                eng32.forward(i0, i1, args.t)
-        cap32 = 100 * args.steps
+                eng32.forward(i0, i1, args.t, streams=args.streams)
+        cap32 = 100 * args.steps * max(1, args.streams)
         h32 = C.c_void_p()
         _lib.check(lib.rrin_prof_create(cap32, C.byref(h32)), "rrin_prof_create")
-        el32, o32 = time_steps(eng32, i0, i1, args.t, args.steps, dev, h32.value)
-        cms, cfl, _, _, _ = read_prof(lib, h32.value, cap32)
+        el32, o32 = time_steps(eng32, i0, i1, args.t, args.steps, dev, h32.value, args.streams)
+        cms, cfl, _ = read_prof(lib, h32.value, cap32)
         lib.rrin_prof_destroy(h32.value)
         alt_out = o32[0:1].cpu()
         res["fp32_exact"] = {"value": round(B * args.steps / el32, 3), "ms_per_step": round(1e3 * el32 / args.steps, 3),
                              "conv_tflops": round(cfl / (cms * 1e-3) / 1e12, 2),
                              "conv_frac_of_fp32_peak": round(cfl / (cms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS, 4),
-                             "kernel": "conv3x3_mfma_kernel (v_mfma_f32_32x32x2_f32)"}
+                             "kernel": "conv3x3_mfma_kernel (v_mfma_f32_32x32x2_f32)", "streams": args.streams}
         del eng32
         net.precision = args.precision
     if rank == 0 and world == 1 and args.cpu_baseline == "auto":
