@@ -67,13 +67,45 @@ H8_TUNED = {
                     (512, 256, 3): 5, (512, 512, 4): 4},
 }
 
+# Smaller work per forward part leaves the deep levels with a few dozen BM 64 x
+# TH 16 tiles for 256 CUs (the 640x368 L3 grid is 46x80 px: 36 blocks), so the
+# same sweep at the smaller workloads picks other tiles — mostly BM 32 x TH 8/16
+# persistent (cfg 12/13).  Size classes by pixels per forward part (n*h*w):
+# "small" <= SMALL_PX (sweep at 640x368 x 1 = BASELINE config C2, conv sum
+# 3.33 -> 2.20 ms), "medium" <= MEDIUM_PX (1280x720 x 1, 5.79 -> 5.34 ms), else
+# "large" (H8_TUNED).  profiles/r01_v13/tune_*.txt; split16 only (the fp16
+# path keeps H8_TUNED at every size).
+SMALL_PX = 500_000
+MEDIUM_PX = 1_200_000
+H8_TUNED_BY_SIZE = {
+    "small": {_lib.PREC_F16X3: {(6, 32, 0): 15, (9, 32, 0): 15, (10, 32, 0): 9, (16, 32, 0): 9, (32, 32, 0): 13,
+                                (32, 64, 1): 13, (64, 32, 0): 13, (64, 64, 1): 13, (64, 128, 1): 10,
+                                (64, 128, 2): 12, (128, 64, 1): 13, (128, 128, 2): 12, (128, 256, 2): 13,
+                                (128, 256, 3): 12, (256, 128, 2): 12, (256, 256, 3): 12, (256, 512, 3): 13,
+                                (256, 512, 4): 12, (512, 256, 3): 12, (512, 512, 4): 12}},
+    "medium": {_lib.PREC_F16X3: {(6, 32, 0): 9, (9, 32, 0): 13, (10, 32, 0): 15, (16, 32, 0): 8, (32, 32, 0): 8,
+                                 (32, 64, 1): 10, (64, 32, 0): 12, (64, 64, 1): 10, (64, 128, 1): 12,
+                                 (64, 128, 2): 11, (128, 64, 1): 11, (128, 128, 2): 10, (128, 256, 2): 11,
+                                 (128, 256, 3): 13, (256, 128, 2): 10, (256, 256, 3): 13, (256, 512, 3): 11,
+                                 (256, 512, 4): 13, (512, 256, 3): 13, (512, 512, 4): 13}},
+}
 
-def choose_cfg_h8(cin: int, cout: int, prec: int, level: int = 0) -> int:
+
+def size_class(pixels: int) -> str:
+    """Tile-table class of a forward part of ``pixels`` = n*h*w output pixels."""
+    if pixels <= SMALL_PX:
+        return "small"
+    return "medium" if pixels <= MEDIUM_PX else "large"
+
+
+def choose_cfg_h8(cin: int, cout: int, prec: int, level: int = 0, size: str = "large") -> int:
     """Tile config of the split-fp16 / fp16 conv (conv_f16.hip table) for a conv
     running on the grid of U-Net level ``level`` (a sub-pixel up conv runs on the
-    low-res grid with 4x the output rows): the swept choice (H8_TUNED), else a
-    level rule from the same sweep."""
-    cfg = H8_TUNED.get(prec, {}).get((cin, cout, level))
+    low-res grid with 4x the output rows) in a forward part of size class
+    ``size``: the swept choice (H8_TUNED_BY_SIZE, H8_TUNED), else a level rule
+    from the same sweep."""
+    table = H8_TUNED_BY_SIZE.get(size, {}).get(prec) or H8_TUNED.get(prec, {})
+    cfg = table.get((cin, cout, level))
     if cfg is not None and _lib.lib().rrin_conv_h8_cfg_fits(cfg, prec, cin):
         return cfg
     if level == 0 or cout <= 32:
@@ -178,11 +210,12 @@ class RRINEngine:
 
     def _init_h8(self, net):
         """Pack for the split-fp16 (F16X3) or fp16 (F16) path: [cob][16-ch chunk][tap][half][bm][8]
-        halves (rrin_pack_conv3x3_h8), one device blob of halves + one of fp32 biases."""
+        halves (rrin_pack_conv3x3_h8), one device blob of halves + one of fp32 biases per
+        tile-table size class (the block of output channels BM of a conv's tile config sets
+        its packing); the "large" class is packed here, the others on first use."""
         L = self.lib
-        halves, biases, meta = [], [], []
-        hoff = boff = 0
-        self.edge_t = []  # device tensors referenced by the table (sub-pixel convs)
+        self.edge_t = []  # device tensors referenced by the tables (sub-pixel convs)
+        self._h8_convs = []  # (w, b, cin, cout rows, grid level, first-conv perm, edge) per body conv
         for name in UNET_ORDER:
             unet = getattr(net, name)
             for idx, (tag, conv) in enumerate(unet.conv_list()):
@@ -206,36 +239,62 @@ class RRINEngine:
                             torch.from_numpy(b.copy()).to(self.device))
                     self.edge_t.append(edge)
                     w, b, cout = ws, bs, 4 * cout
-                cfg = choose_cfg_h8(cin, cout, self.prec, level)
-                bm = L.rrin_conv_h8_cfg_bm(cfg)
-                nh = L.rrin_pack_conv3x3_h8_halves(cout, cin, bm)
-                whi = np.empty(nh, np.uint16)
-                wlo = np.empty(nh, np.uint16) if self.prec == _lib.PREC_F16X3 else None
-                bp = np.empty(L.rrin_pack_bias_floats(cout, bm), np.float32)
-                inv = C.c_float()
                 perm = FIRST_CONV_PERM[name] if idx == 0 else None
                 perm_arr = np.asarray(perm, np.int32) if perm is not None else None
-                _lib.check(L.rrin_pack_conv3x3_h8(
-                    w.ctypes.data, b.ctypes.data, cout, cin, bm,
-                    perm_arr.ctypes.data if perm_arr is not None else None, self.prec, whi.ctypes.data,
-                    wlo.ctypes.data if wlo is not None else None, bp.ctypes.data, C.byref(inv)),
-                    "rrin_pack_conv3x3_h8")
-                meta.append((hoff, hoff + nh if wlo is not None else None, boff, cfg, inv.value, edge))
-                halves.append(whi)
+                self._h8_convs.append((w, b, cin, cout, level, perm_arr, edge))
+        if len(self._h8_convs) != L.rrin_net_conv_count():
+            raise RuntimeError(f"packed {len(self._h8_convs)} convs, library expects {L.rrin_net_conv_count()}")
+        self.head_table = (_lib.HeadWeights * 4)()
+        for i, (w, b) in enumerate(self.heads_t):
+            self.head_table[i].w = w.data_ptr()
+            self.head_table[i].bias = b.data_ptr()
+        self._packs = {}
+        _, _, self.conv_table, self.cfgs = self._pack_h8("large")
+        self._ws = OrderedDict()
+        self._flow_valid = {}
+        self._sides = []
+
+    def _pack_h8(self, size: str):
+        """(halves blob, bias blob, ConvWeights table, cfgs) of size class ``size``, cached;
+        classes whose tile configs agree share one packing."""
+        p = self._packs.get(size)
+        if p is not None:
+            return p
+        L = self.lib
+        cfgs = [choose_cfg_h8(cin, cout, self.prec, level, size) for (_, _, cin, cout, level, _, _) in self._h8_convs]
+        key = tuple(cfgs)
+        p = self._packs.get(key)
+        if p is not None:
+            self._packs[size] = p
+            return p
+        halves, biases, meta = [], [], []
+        hoff = boff = 0
+        for (w, b, cin, cout, level, perm_arr, edge), cfg in zip(self._h8_convs, cfgs):
+            bm = L.rrin_conv_h8_cfg_bm(cfg)
+            nh = L.rrin_pack_conv3x3_h8_halves(cout, cin, bm)
+            whi = np.empty(nh, np.uint16)
+            wlo = np.empty(nh, np.uint16) if self.prec == _lib.PREC_F16X3 else None
+            bp = np.empty(L.rrin_pack_bias_floats(cout, bm), np.float32)
+            inv = C.c_float()
+            _lib.check(L.rrin_pack_conv3x3_h8(
+                w.ctypes.data, b.ctypes.data, cout, cin, bm,
+                perm_arr.ctypes.data if perm_arr is not None else None, self.prec, whi.ctypes.data,
+                wlo.ctypes.data if wlo is not None else None, bp.ctypes.data, C.byref(inv)),
+                "rrin_pack_conv3x3_h8")
+            meta.append((hoff, hoff + nh if wlo is not None else None, boff, cfg, inv.value, edge))
+            halves.append(whi)
+            hoff += nh
+            if wlo is not None:
+                halves.append(wlo)
                 hoff += nh
-                if wlo is not None:
-                    halves.append(wlo)
-                    hoff += nh
-                biases.append(bp)
-                boff += bp.size
-        if len(meta) != L.rrin_net_conv_count():
-            raise RuntimeError(f"packed {len(meta)} convs, library expects {L.rrin_net_conv_count()}")
-        self.blob = torch.from_numpy(np.concatenate(halves).view(np.int16)).to(self.device)
-        self.bias_blob = torch.from_numpy(np.concatenate(biases)).to(self.device)
-        hb, bb = self.blob.data_ptr(), self.bias_blob.data_ptr()
-        self.conv_table = (_lib.ConvWeights * len(meta))()
+            biases.append(bp)
+            boff += bp.size
+        blob = torch.from_numpy(np.concatenate(halves).view(np.int16)).to(self.device)
+        bias_blob = torch.from_numpy(np.concatenate(biases)).to(self.device)
+        hb, bb = blob.data_ptr(), bias_blob.data_ptr()
+        table = (_lib.ConvWeights * len(meta))()
         for i, (ho, lo, bo, cfg, inv, edge) in enumerate(meta):
-            e = self.conv_table[i]
+            e = table[i]
             e.whi = hb + 2 * ho
             e.wlo = hb + 2 * lo if lo is not None else None
             e.bias = bb + 4 * bo
@@ -245,14 +304,16 @@ class RRINEngine:
                 e.subpixel = 1
                 e.wedge = edge[0].data_ptr()
                 e.bias_raw = edge[1].data_ptr()
-        self.head_table = (_lib.HeadWeights * 4)()
-        for i, (w, b) in enumerate(self.heads_t):
-            self.head_table[i].w = w.data_ptr()
-            self.head_table[i].bias = b.data_ptr()
-        self.cfgs = [m[3] for m in meta]
-        self._ws = OrderedDict()
-        self._flow_valid = {}
-        self._sides = []
+        p = (blob, bias_blob, table, cfgs)
+        self._packs[key] = p
+        self._packs[size] = p
+        return p
+
+    def conv_table_for(self, n: int, h: int, w: int):
+        """ConvWeights table of a forward part of n pairs at h x w (its tile-table size class)."""
+        if self.prec == _lib.PREC_F32:
+            return self.conv_table
+        return self._pack_h8(size_class(n * h * w))[2]
 
     def workspace(self, n: int, h: int, w: int, slot: int = 0) -> torch.Tensor:
         key = (n, h, w, slot)
@@ -333,7 +394,7 @@ class RRINEngine:
         d = _lib.NetDesc()
         d.n, d.h, d.w = n, h, w
         d.i0, d.i1, d.out, d.coef = i0.data_ptr(), i1.data_ptr(), out.data_ptr(), coef.data_ptr()
-        d.convs = self.conv_table
+        d.convs = self.conv_table_for(n, h, w)
         d.heads = self.head_table
         d.workspace = ws.data_ptr()
         d.workspace_bytes = ws.numel()
