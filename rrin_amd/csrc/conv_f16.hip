@@ -717,12 +717,25 @@ struct Up8 {
   }
 };
 
-template <int PLANES>
-__global__ void __launch_bounds__(256) edge_fix_h8_kernel(EdgeFixArgs a) {
-  __shared__ float s_u[kFixCi][kFixPx + 2];
-  __shared__ float s_ux[kFixCi][4];         // corner extras: [left ky_a, left ky_b, right ky_a, right ky_b]
-  __shared__ float s_w[7][kFixCi][kFixCo];  // slots 0-2 line taps, 3-6 corner extras
-  const int tid = threadIdx.x, px = tid & (kFixPx - 1), cg = tid / kFixPx;  // 8 groups of 4 channels
+// K split (template KS): the block is KS groups of 256 threads; group k stages
+// and accumulates chunks k, k + KS, ... of the input channels in its own LDS
+// region, and group 0 adds the other groups' sums in group order at the end
+// (one launch, fixed summation order).  KS > 1 shortens the serial chunk chain
+// of the few blocks a small ring has (the deep levels: cin 128-256, 16-64
+// blocks at 640x368) and gives each CU more waves to hide LDS latency.
+constexpr int kFixSubFloats = kFixCi * (kFixPx + 2) + kFixCi * 4 + 7 * kFixCi * kFixCo;
+
+template <int PLANES, int KS>
+__global__ void __launch_bounds__(256 * KS) edge_fix_h8_kernel(EdgeFixArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float s_fix[];
+  const int ks = threadIdx.x >> 8;  // K group (wave-uniform)
+  float* s_base = s_fix + ks * kFixSubFloats;
+  float(*s_u)[kFixPx + 2] = reinterpret_cast<float(*)[kFixPx + 2]>(s_base);
+  // corner extras: [left ky_a, left ky_b, right ky_a, right ky_b]
+  float(*s_ux)[4] = reinterpret_cast<float(*)[4]>(s_base + kFixCi * (kFixPx + 2));
+  // slots 0-2 line taps, 3-6 corner extras
+  float(*s_w)[kFixCi][kFixCo] = reinterpret_cast<float(*)[kFixCi][kFixCo]>(s_base + kFixCi * (kFixPx + 2) + kFixCi * 4);
+  const int tid = threadIdx.x & 255, px = tid & (kFixPx - 1), cg = tid / kFixPx;  // 8 groups of 4 channels
   const int img = blockIdx.z, co0 = blockIdx.y * kFixCo;
   const int H = 2 * a.sh, W = 2 * a.sw;
   // line of this tile: 0 top, 1 bottom, 2 left, 3 right
@@ -788,11 +801,12 @@ __global__ void __launch_bounds__(256) edge_fix_h8_kernel(EdgeFixArgs a) {
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
   const int pos = pos0 + px;
   const bool cl = has_l && pos == 0, cr = has_r && pos == W - 1;
-  fetch(0);
-  for (int c0 = 0; c0 < a.cin; c0 += kFixCi) {
+  // every K group runs the same number of chunks (launch: cin % (KS * kFixCi) == 0)
+  fetch(ks * kFixCi);
+  for (int c0 = ks * kFixCi; c0 < a.cin; c0 += KS * kFixCi) {
     stage();
     __syncthreads();
-    if (c0 + kFixCi < a.cin) fetch(c0 + kFixCi);  // in flight during the FMAs below
+    if (c0 + KS * kFixCi < a.cin) fetch(c0 + KS * kFixCi);  // in flight during the FMAs below
 #pragma unroll 4
     for (int ci = 0; ci < kFixCi; ++ci) {
 #pragma unroll
@@ -818,6 +832,19 @@ __global__ void __launch_bounds__(256) edge_fix_h8_kernel(EdgeFixArgs a) {
       }
     }
     __syncthreads();
+  }
+  if constexpr (KS > 1) {
+    // groups 1.. park their sums in their own (now idle) staging region
+    if (ks > 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) s_base[i * 256 + tid] = acc[i];
+    }
+    __syncthreads();
+    if (ks > 0) return;
+#pragma unroll
+    for (int k = 1; k < KS; ++k)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i] += s_fix[k * kFixSubFloats + i * 256 + tid];
   }
   if (pos - first >= count) return;
   const int Y = row ? fixed : pos, X = row ? pos : fixed;
@@ -1567,6 +1594,22 @@ extern "C" int rrin_subpixel_weights(const float* w, const float* b, int32_t cou
   return 0;
 }
 
+template <int PLANES, int KS>
+static int edge_fix_launch(const EdgeFixArgs& a, dim3 grid, hipStream_t st) {
+  constexpr size_t lds = (size_t)KS * kFixSubFloats * sizeof(float);
+  static_assert(lds <= 160 * 1024, "edge fix LDS");
+  static_assert(kFixSubFloats >= 4 * 256, "K-group sums fit a staging region");
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)edge_fix_h8_kernel<PLANES, KS>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return (int)e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((edge_fix_h8_kernel<PLANES, KS>), grid, dim3(256 * KS), lds, st, a);
+  return hip_code(hipGetLastError());
+}
+
 extern "C" int rrin_subpixel_edge_fix_h8(const rrin_edge_fix_desc* d, void* stream) {
   if (!d || !d->edge || !d->wedge || !d->bias) return RRIN_E_ARG;
   if (d->prec != RRIN_PREC_F16X3 && d->prec != RRIN_PREC_F16) return RRIN_E_ARG;
@@ -1604,12 +1647,19 @@ extern "C" int rrin_subpixel_edge_fix_h8(const rrin_edge_fix_desc* d, void* stre
   a.tiles_col = (H - 2 + kFixPx - 1) / kFixPx;
   const dim3 grid((unsigned)(2 * a.tiles_row + 2 * a.tiles_col), (unsigned)((d->cout + kFixCo - 1) / kFixCo),
                   (unsigned)d->n);
+  // K split by cin and precision only (the summation order never depends on
+  // batch or size); split16 stops at 2 groups (4 x 256 threads cap a thread at
+  // 128 VGPRs: the two-plane kernel spills there)
+  int ks = d->cin % (2 * kFixCi) == 0 && d->cin >= 4 * kFixCi ? 2 : 1;
+  if (planes == 1 && d->cin % (4 * kFixCi) == 0 && d->cin >= 8 * kFixCi) ks = 4;
   hipStream_t st = (hipStream_t)stream;
-  if (planes == 2)
-    hipLaunchKernelGGL(edge_fix_h8_kernel<2>, grid, dim3(256), 0, st, a);
-  else
-    hipLaunchKernelGGL(edge_fix_h8_kernel<1>, grid, dim3(256), 0, st, a);
-  return hip_code(hipGetLastError());
+  switch (planes * 8 + ks) {
+    case 2 * 8 + 2: return edge_fix_launch<2, 2>(a, grid, st);
+    case 2 * 8 + 1: return edge_fix_launch<2, 1>(a, grid, st);
+    case 1 * 8 + 4: return edge_fix_launch<1, 4>(a, grid, st);
+    case 1 * 8 + 2: return edge_fix_launch<1, 2>(a, grid, st);
+    default: return edge_fix_launch<1, 1>(a, grid, st);
+  }
 }
 
 extern "C" int rrin_upsample2x_h8(const rrin_h8* src, const rrin_h8* dst, int32_t n, int32_t prec, void* stream) {
