@@ -189,3 +189,27 @@ def test_subpixel_levels_agree(gpu, golden, precision, level):
     with torch.no_grad():
         err = maxabs(net(i0, i1, 0.5).cpu(), g["out_t050"])
     assert err <= (1e-4 if precision == "fp32_split16" else 1e-2), f"level {level}: {err:.3e}"
+
+
+@pytest.mark.parametrize("precision", ["fp32_split16", "fp16"])
+def test_size_class_tables_bitwise(gpu, nets, precision):
+    """The tile table follows the pixels per forward part (engine.size_class);
+    every config accumulates K in the same order, so the output must not depend
+    on which class's table (and packing) ran."""
+    net = nets["stress"]
+    net.precision = precision
+    try:
+        eng = net.engine()
+        i0, i1 = synthetic_batch(2, 128, 192)
+        i0, i1 = i0.to(gpu), i1.to(gpu)
+        outs = {}
+        for cls in ("small", "medium", "large"):
+            table = eng._pack_h8(cls)[2]
+            eng.conv_table_for = lambda n, h, w, t=table: t
+            with torch.no_grad():
+                outs[cls] = eng.forward(i0, i1, 0.5).cpu()
+            del eng.conv_table_for
+        assert torch.equal(outs["small"], outs["large"])
+        assert torch.equal(outs["medium"], outs["large"])
+    finally:
+        net.precision = "fp32"

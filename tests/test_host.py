@@ -92,3 +92,23 @@ def test_bench_union_ms():
     assert bench.union_ms([(0.0, 2.0), (1.0, 3.0)]) == 3.0            # overlap counted once
     assert bench.union_ms([(1.0, 4.0), (0.0, 5.0), (2.0, 3.0)]) == 5.0  # nested, unsorted
     assert bench.union_ms([(0.0, 1.0), (1.0, 2.0)]) == 2.0            # touching
+
+
+def test_size_class_tables():
+    """Every tuned tile table entry names a config that exists and fits its cin
+    (the library's own check), and the size classes split at the documented
+    pixel counts."""
+    from rrin_amd import _lib, engine
+    lib = _lib.lib()
+    ncfg = lib.rrin_conv_h8_cfg_count()
+    tables = [(p, t) for p, t in engine.H8_TUNED.items()]
+    tables += [(p, t) for cls in engine.H8_TUNED_BY_SIZE.values() for p, t in cls.items()]
+    for prec, table in tables:
+        for (cin, cout, level), cfg in table.items():
+            assert 0 <= cfg < ncfg
+            assert lib.rrin_conv_h8_cfg_fits(cfg, prec, cin) == 1, (cin, cout, level, cfg)
+        # the size-class tables cover the same conv shapes as the large one
+        assert set(table) == set(engine.H8_TUNED[prec]) or prec not in engine.H8_TUNED
+    assert engine.size_class(640 * 368) == "small"
+    assert engine.size_class(1280 * 720) == "medium"
+    assert engine.size_class(2 * 1280 * 720) == "large"
