@@ -1233,7 +1233,8 @@ static float h2f(uint16_t h) {
 
 // Config table: cfg -> (NW waves along rows, WM co-tiles, WN rows per wave,
 // SC schedule knobs SCHED_*, PE grid: 0 = one tile per block, k = k x the
-// blocks a CU holds at once, persistent)
+// blocks a CU holds at once, persistent).  16-17 (BM 32 x TH 4) are for the
+// few-tile deep levels of small workloads (engine size classes).
 #define RRIN_H8_CFGS(X)  \
   X(0, 8, 2, 2, 0, 0)    \
   X(1, 8, 1, 2, 0, 0)    \
@@ -1250,7 +1251,9 @@ static float h2f(uint16_t h) {
   X(12, 4, 1, 2, 16, 1)  \
   X(13, 8, 1, 2, 16, 1)  \
   X(14, 4, 1, 2, 48, 1)  \
-  X(15, 8, 1, 2, 48, 1)
+  X(15, 8, 1, 2, 48, 1)  \
+  X(16, 4, 1, 1, 16, 1)  \
+  X(17, 2, 1, 2, 16, 1)
 
 // Shared memory of one block: double-buffered input tile and weight slab, or
 // with WRES every chunk's weight slab resident.

@@ -72,17 +72,17 @@ H8_TUNED = {
 # same sweep at the smaller workloads picks other tiles — mostly BM 32 x TH 8/16
 # persistent (cfg 12/13).  Size classes by pixels per forward part (n*h*w):
 # "small" <= SMALL_PX (sweep at 640x368 x 1 = BASELINE config C2, conv sum
-# 3.33 -> 2.20 ms), "medium" <= MEDIUM_PX (1280x720 x 1, 5.79 -> 5.34 ms), else
-# "large" (H8_TUNED).  profiles/r01_v13/tune_*.txt; split16 only (the fp16
+# 3.30 -> 2.11 ms; BM 32 x TH 4 (cfg 16) at the deepest levels), "medium" <=
+# MEDIUM_PX (1280x720 x 1, 5.79 -> 5.34 ms), else "large" (H8_TUNED).  profiles/r01_v13/tune_*.txt; split16 only (the fp16
 # path keeps H8_TUNED at every size).
 SMALL_PX = 500_000
 MEDIUM_PX = 1_200_000
 H8_TUNED_BY_SIZE = {
-    "small": {_lib.PREC_F16X3: {(6, 32, 0): 15, (9, 32, 0): 15, (10, 32, 0): 9, (16, 32, 0): 9, (32, 32, 0): 13,
-                                (32, 64, 1): 13, (64, 32, 0): 13, (64, 64, 1): 13, (64, 128, 1): 10,
-                                (64, 128, 2): 12, (128, 64, 1): 13, (128, 128, 2): 12, (128, 256, 2): 13,
-                                (128, 256, 3): 12, (256, 128, 2): 12, (256, 256, 3): 12, (256, 512, 3): 13,
-                                (256, 512, 4): 12, (512, 256, 3): 12, (512, 512, 4): 12}},
+    "small": {_lib.PREC_F16X3: {(6, 32, 0): 15, (9, 32, 0): 13, (10, 32, 0): 15, (16, 32, 0): 13, (32, 32, 0): 13,
+                                (32, 64, 1): 13, (64, 32, 0): 13, (64, 64, 1): 13, (64, 128, 1): 11,
+                                (64, 128, 2): 16, (128, 64, 1): 13, (128, 128, 2): 12, (128, 256, 2): 13,
+                                (128, 256, 3): 16, (256, 128, 2): 16, (256, 256, 3): 12, (256, 512, 3): 13,
+                                (256, 512, 4): 16, (512, 256, 3): 16, (512, 512, 4): 16}},
     "medium": {_lib.PREC_F16X3: {(6, 32, 0): 9, (9, 32, 0): 13, (10, 32, 0): 15, (16, 32, 0): 8, (32, 32, 0): 8,
                                  (32, 64, 1): 10, (64, 32, 0): 12, (64, 64, 1): 10, (64, 128, 1): 12,
                                  (64, 128, 2): 11, (128, 64, 1): 11, (128, 128, 2): 10, (128, 256, 2): 11,
