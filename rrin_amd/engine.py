@@ -73,8 +73,9 @@ H8_TUNED = {
 # persistent (cfg 12/13).  Size classes by pixels per forward part (n*h*w):
 # "small" <= SMALL_PX (sweep at 640x368 x 1 = BASELINE config C2, conv sum
 # 3.30 -> 2.11 ms; BM 32 x TH 4 (cfg 16) at the deepest levels), "medium" <=
-# MEDIUM_PX (1280x720 x 1, 5.79 -> 5.34 ms), else "large" (H8_TUNED).  profiles/r01_v13/tune_*.txt; split16 only (the fp16
-# path keeps H8_TUNED at every size).
+# MEDIUM_PX (1280x720 x 1, 5.79 -> 5.34 ms), else "large" (H8_TUNED).
+# profiles/r01_v13/tune_*.txt; split16 only (the fp16 path keeps H8_TUNED at
+# every size).
 SMALL_PX = 500_000
 MEDIUM_PX = 1_200_000
 H8_TUNED_BY_SIZE = {
@@ -248,7 +249,8 @@ class RRINEngine:
         for i, (w, b) in enumerate(self.heads_t):
             self.head_table[i].w = w.data_ptr()
             self.head_table[i].bias = b.data_ptr()
-        self._packs = {}
+        self._packs = {}          # size class -> packing
+        self._packs_by_cfgs = {}  # tuple of per-conv configs -> packing (shared between classes)
         _, _, self.conv_table, self.cfgs = self._pack_h8("large")
         self._ws = OrderedDict()
         self._flow_valid = {}
@@ -263,7 +265,7 @@ class RRINEngine:
         L = self.lib
         cfgs = [choose_cfg_h8(cin, cout, self.prec, level, size) for (_, _, cin, cout, level, _, _) in self._h8_convs]
         key = tuple(cfgs)
-        p = self._packs.get(key)
+        p = self._packs_by_cfgs.get(key)
         if p is not None:
             self._packs[size] = p
             return p
@@ -305,7 +307,7 @@ class RRINEngine:
                 e.wedge = edge[0].data_ptr()
                 e.bias_raw = edge[1].data_ptr()
         p = (blob, bias_blob, table, cfgs)
-        self._packs[key] = p
+        self._packs_by_cfgs[key] = p
         self._packs[size] = p
         return p
 
