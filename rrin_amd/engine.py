@@ -161,6 +161,8 @@ class RRINEngine:
         if self.prec != _lib.PREC_F32:
             self._init_h8(net)
             return
+        self._levels32 = []         # grid level per body conv (fp32 path)
+        self._table32_small = None  # small size class: TH 4 tiles at levels >= 1
         for name in UNET_ORDER:
             unet = getattr(net, name)
             convs = unet.conv_list()
@@ -173,6 +175,7 @@ class RRINEngine:
                                          torch.from_numpy(b.copy()).to(self.device)))
                     continue
                 cfg = choose_cfg(cin, cout, 0)
+                self._levels32.append(_level_of(unet, tag))
                 bm = L.rrin_conv_cfg_bm(cfg)
                 nw = L.rrin_pack_conv3x3_floats(cout, cin, bm)
                 nb = L.rrin_pack_bias_floats(cout, bm)
@@ -314,7 +317,22 @@ class RRINEngine:
     def conv_table_for(self, n: int, h: int, w: int):
         """ConvWeights table of a forward part of n pairs at h x w (its tile-table size class)."""
         if self.prec == _lib.PREC_F32:
-            return self.conv_table
+            if size_class(n * h * w) != "small":
+                return self.conv_table
+            if self._table32_small is None:
+                # sweep at 640x368 x 1 (profiles/r01_v13/tune_fp32_640x368x1.txt): BM 64 x TH 4
+                # (cfg 4) beats BM 64 x TH 8 (cfg 1) on every level 1-3 conv, 2.18 -> 1.46 ms;
+                # same BM, so the same packed weights
+                L = self.lib
+                if L.rrin_conv_cfg_bm(4) != L.rrin_conv_cfg_bm(1):
+                    raise RuntimeError("fp32 small-class tiles need cfg 1 and 4 to share BM")
+                t = (_lib.ConvWeights * len(self.cfgs))()
+                C.memmove(t, self.conv_table, C.sizeof(self.conv_table))
+                for i, lvl in enumerate(self._levels32):
+                    if lvl >= 1 and t[i].cfg == 1:
+                        t[i].cfg = 4
+                self._table32_small = t
+            return self._table32_small
         return self._pack_h8(size_class(n * h * w))[2]
 
     def workspace(self, n: int, h: int, w: int, slot: int = 0) -> torch.Tensor:

@@ -213,3 +213,20 @@ def test_size_class_tables_bitwise(gpu, nets, precision):
         assert torch.equal(outs["medium"], outs["large"])
     finally:
         net.precision = "fp32"
+
+
+def test_size_class_tables_bitwise_fp32(gpu, nets):
+    """Exact-fp32 path: the small class swaps BM 64 x TH 8 tiles for BM 64 x TH 4
+    at levels >= 1 (same packing); the output must be bitwise the large class's."""
+    net = nets["stress"]
+    net.precision = "fp32"
+    eng = net.engine()
+    i0, i1 = synthetic_batch(2, 128, 192)
+    i0, i1 = i0.to(gpu), i1.to(gpu)
+    with torch.no_grad():
+        small = eng.forward(i0, i1, 0.5).cpu()
+        assert any(t.cfg == 4 for t in eng.conv_table_for(2, 128, 192))
+        eng.conv_table_for = lambda n, h, w: eng.conv_table
+        large = eng.forward(i0, i1, 0.5).cpu()
+        del eng.conv_table_for
+    assert torch.equal(small, large)
