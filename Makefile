@@ -15,10 +15,12 @@ OBJS := $(patsubst $(SRC_DIR)/%.hip,$(OBJ_DIR)/%.o,$(SRCS))
 LIB := rrin_amd/librrin_hip.so
 # kernel lab (tools/conv_lab.py ablate): the split16 conv with schedule knobs / ablations
 LAB := rrin_amd/librrin_lab.so
+# exact-fp32 conv with ablation knobs (tools/conv_lab.py ablate32)
+LAB32 := rrin_amd/librrin_lab32.so
 
 all: $(LIB)
 
-lab: $(LAB)
+lab: $(LAB) $(LAB32)
 
 $(OBJ_DIR)/%.o: $(SRC_DIR)/%.hip $(SRC_DIR)/common.hpp include/rrin_hip.h
 	@mkdir -p $(OBJ_DIR)
@@ -30,11 +32,14 @@ $(LIB): $(OBJS)
 $(LAB): $(SRC_DIR)/conv_f16.hip $(SRC_DIR)/common.hpp include/rrin_hip.h
 	$(HIPCC) $(CXXFLAGS) -DRRIN_LAB -shared -o $@ $<
 
+$(LAB32): $(SRC_DIR)/conv_mfma.hip $(SRC_DIR)/common.hpp include/rrin_hip.h
+	$(HIPCC) $(CXXFLAGS) -DRRIN_LAB -shared -o $@ $<
+
 # kernel register / LDS / occupancy report
 resource: $(SRCS)
 	$(HIPCC) $(CXXFLAGS) -Rpass-analysis=kernel-resource-usage -c $(SRC_DIR)/conv_mfma.hip -o /dev/null
 
 clean:
-	rm -rf build $(LIB) $(LAB)
+	rm -rf build $(LIB) $(LAB) $(LAB32)
 
 .PHONY: all lab clean resource

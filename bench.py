@@ -2,7 +2,9 @@
 """RRIN inference throughput on MI355X (BASELINE.json metric).
 
 One step = one ``Net.forward`` over this rank's batch of synthetic 1280x720
-fp32 frame pairs (inputs already resident in HBM) + the RCCL all-gather that
+fp32 frame pairs (inputs already resident in HBM) in exact fp32 arithmetic
+(``--precision fp32``, the default: fp32 storage, v_mfma_f32_32x32x2_f32
+products, fp32 accumulation) + the RCCL all-gather that
 reassembles the interpolated frames of all ranks (rrin_amd.shard); the gather
 of step k runs on RCCL's stream while step k+1 computes, and every gather has
 completed before the clock stops.  Weak scaling: every rank owns ``--batch``
@@ -48,6 +50,11 @@ HBM_PEAK_GBS = 8000.0
 # three f16 MFMA products on every fp32 product.
 PEAK = {"fp32": FP32_PEAK_TFLOPS, "fp32_split16": F16_PEAK_TFLOPS / 3, "fp16": F16_PEAK_TFLOPS}
 MFMA_PRODUCTS = {"fp32": 1, "fp32_split16": 3, "fp16": 1}
+# Only "fp32" is fp32 arithmetic (the BASELINE metric); split16 emulates fp32 with fp16 products.
+PREC_LABEL = {"fp32": "fp32", "fp32_split16": "fp32-emulated (fp16 hi+lo x3)", "fp16": "fp16"}
+DTYPE = {"fp32": "f32",
+         "fp32_split16": "f16x3 (fp32-emulated: fp16 hi+lo split, 3 f16 MFMA products, f32 accumulate)",
+         "fp16": "f16"}
 
 
 def parse():
@@ -59,12 +66,14 @@ def parse():
     ap.add_argument("--height", type=int, default=720)
     ap.add_argument("--width", type=int, default=1280)
     ap.add_argument("--t", type=float, default=0.5)
-    ap.add_argument("--precision", default="fp32_split16", choices=["fp32", "fp32_split16", "fp16"],
-                    help="fp32: exact fp32 MFMA; fp32_split16: fp32 values as fp16 hi+lo, 3 fp16 "
-                         "products per fp32 product, fp32 accumulate; fp16: fp16 storage/products")
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "fp32_split16", "fp16"],
+                    help="fp32: exact fp32 (v_mfma_f32_32x32x2_f32, fp32 storage) -- the BASELINE metric; "
+                         "fp32_split16: fp32-EMULATED (values as fp16 hi+lo, 3 fp16 products per fp32 "
+                         "product, fp32 accumulate); fp16: fp16 storage/products")
     ap.add_argument("--no-prof", action="store_true", help="skip the per-launch event profiler")
     ap.add_argument("--no-alt", action="store_true",
-                    help="N=1: skip the secondary measurement of the exact-fp32 MFMA path")
+                    help="N=1: skip the secondary line (fp32 run: the fp32-emulated split16 path; "
+                         "other precisions: the exact-fp32 path)")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (production); gloo only to rehearse N ranks on fewer GPUs")
@@ -77,10 +86,30 @@ def parse():
     return ap.parse_args()
 
 
+def host_cpu_share():
+    """(threads to use, description): the CPUs this process may run on -- the
+    cgroup CPU quota when one is set (a GPU box gives each 1-GPU job a share of
+    a larger host), else the affinity mask."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    threads = min(aff, quota) if quota else aff
+    env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if env:
+        threads = min(threads, env) if quota else env
+    return threads, {"host_cpus": os.cpu_count(), "affinity_cpus": aff, "cgroup_cpu_quota": quota,
+                     "omp_num_threads": env or None}
+
+
 def cpu_baseline(sd, h, w, pairs, t, gpu_out0, alt_out0=None):
     """Time the CPU oracle on pair 0 and compare its output with the GPU's."""
     from oracle.ref_net import net_forward  # checker / baseline only
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    threads, host = host_cpu_share()
     torch.set_num_threads(threads)
     i0, i1 = synthetic_batch(1, h, w, first_index=0)
     with torch.no_grad():
@@ -99,7 +128,9 @@ def cpu_baseline(sd, h, w, pairs, t, gpu_out0, alt_out0=None):
         parity["alt"] = compare(alt_out0)
     return ({"value": pairs / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
              "sample": f"{pairs} x Net.forward {w}x{h} N=1 fp32 on PyTorch-CPU (oracle/ref_net.py), "
-                       f"{dt:.1f} s"}, parity)
+                       f"{dt:.1f} s", "host": host,
+             "cores_note": "threads used = the CPUs this job may use (cgroup quota / affinity / OMP_NUM_THREADS); "
+                           "host_cpus = every CPU of the machine"}, parity)
 
 
 def union_ms(spans):
@@ -172,11 +203,13 @@ def main():
     if split:
         args.streams = len(split)
 
+    last_gather = [None]
+
     def step(prof=None):
         with torch.no_grad():
             out = eng.forward(i0, i1, args.t, prof=prof, streams=args.streams, split=split)
             if gather is not None:
-                gather.submit(out)
+                last_gather[0] = (out, gather.submit(out)[0])
         return out
 
     for _ in range(args.warmup):
@@ -270,6 +303,8 @@ def main():
                     "flops_per_launch_avg": conv_fl / max(conv_launches, 1),
                     "avg_launch_ms": conv_ms / max(conv_launches, 1),
                     "conv_busy_ms_per_step": round(conv_busy / args.steps, 3),
+                    "frac_basis": ("algorithmic conv FLOPs / conv busy time = union of the conv launch spans "
+                                   "(HIP events on each launch's own stream; the --streams parts overlap)"),
                     "launch_overlap": round(conv_ms / conv_busy, 3),
                     "streams": args.streams,
                     "conv_ms_per_step": round(conv_ms_step, 3),
@@ -301,12 +336,27 @@ def main():
                 roofline["algorithmic_bytes_per_step_gb"] = round(B * alg / 1e9, 2)
                 roofline["traffic_source"] = "profiles/pmc_traffic.json[" + key + "]"
 
+    gather_check = None
+    if world > 1:
+        # the gathered output of the last step equals every rank's own shard in
+        # rank order: per-rank checksums of the local output vs the gather's slices
+        gather.drain()
+        local = last_gather[0][0].double()
+        mine = torch.stack([local.sum(), (local * local).sum()])
+        allc = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allc, mine.cpu() if args.dist_backend == "gloo" else mine)
+        g = last_gather[0][1].double()
+        ok = all(torch.allclose(torch.stack([g[r * B:(r + 1) * B].sum(), (g[r * B:(r + 1) * B] ** 2).sum()]).cpu(),
+                                allc[r].cpu(), rtol=0, atol=0) for r in range(world))
+        gather_check = {"ok": bool(ok), "what": "sum and sum of squares of every rank's output shard == the "
+                                                "rank-order slice of the all-gathered output (last step)"}
+        if not ok:
+            raise RuntimeError("all-gathered output does not match the ranks' shards")
+
     pairs = world * B * args.steps
     value = pairs / elapsed
     res = {
-        "metric": ("interpolated frames/sec at 1280x720 fp32 (Net.forward, frame pairs/s)"
-                   if (W, H, args.precision) == (1280, 720, "fp32_split16") else
-                   f"interpolated frames/sec at {W}x{H} {args.precision} (Net.forward, frame pairs/s)"),
+        "metric": f"interpolated frames/sec at {W}x{H} {PREC_LABEL[args.precision]} (Net.forward, frame pairs/s)",
         "value": round(value, 3),
         "unit": "frames/s",
         "n_gpus": world,
@@ -316,47 +366,55 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": {"fp32": "f32", "fp32_split16": "f32 (fp16 hi+lo split, 3 MFMA products, f32 accumulate)",
-                  "fp16": "f16"}[args.precision],
+        "dtype": DTYPE[args.precision],
         "data": "synthetic (key-seeded weights, randint/255 frame pairs; SURVEY §8c-d)",
-        "config": {"workload": f"RRIN Net.forward {W}x{H} fp32, {B} pairs/GPU/step, t={args.t}, "
-                               f"+ all-gather of outputs",
+        "config": {"workload": f"RRIN Net.forward {W}x{H} {PREC_LABEL[args.precision]}, {B} pairs/GPU/step, "
+                               f"t={args.t}, + all-gather of outputs",
                    "global_batch": world * B, "height": H, "width": W,
                    "parallelism": f"frame-batch dp{world}",
                    "gflop_per_pair": round(sum(conv_flops(getattr(net, u), H, W)
                                                for u in ("Flow", "refine_flow", "Mask", "final")) / 1e9, 1)},
         "roofline": roofline,
         "unprofiled": unprofiled,
+        "gather_check": gather_check,
         "cpu_baseline": None,
         "parity": None,
     }
     alt_out = None
-    if world == 1 and not args.no_alt and args.precision != "fp32":
-        # the exact-fp32 MFMA path on the same inputs, for comparison in the same line
-        net.precision = "fp32"
-        eng32 = net.engine()
+    alt_key = None
+    if world == 1 and not args.no_alt and args.precision in ("fp32", "fp32_split16", "fp16"):
+        # secondary line on the same inputs: an fp32 run reports the fp32-emulated
+        # split16 path beside it; any other precision reports the exact-fp32 path
+        alt = "fp32_split16" if args.precision == "fp32" else "fp32"
+        alt_key = "fp32_emulated_split16" if alt == "fp32_split16" else "fp32_exact"
+        net.precision = alt
+        eng2 = net.engine()
         with torch.no_grad():
             for _ in range(max(1, args.warmup)):
-                eng32.forward(i0, i1, args.t, streams=args.streams)
-        cap32 = 100 * args.steps * max(1, args.streams)
-        h32 = C.c_void_p()
-        _lib.check(lib.rrin_prof_create(cap32, C.byref(h32)), "rrin_prof_create")
-        el32, o32 = time_steps(eng32, i0, i1, args.t, args.steps, dev, h32.value, args.streams)
-        cms, cfl, _ = read_prof(lib, h32.value, cap32)
-        lib.rrin_prof_destroy(h32.value)
-        alt_out = o32[0:1].cpu()
-        res["fp32_exact"] = {"value": round(B * args.steps / el32, 3), "ms_per_step": round(1e3 * el32 / args.steps, 3),
-                             "conv_tflops": round(cfl / (cms * 1e-3) / 1e12, 2),
-                             "conv_frac_of_fp32_peak": round(cfl / (cms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS, 4),
-                             "kernel": "conv3x3_mfma_kernel (v_mfma_f32_32x32x2_f32)", "streams": args.streams}
-        del eng32
+                eng2.forward(i0, i1, args.t, streams=args.streams)
+        cap2 = 100 * args.steps * max(1, args.streams)
+        h2 = C.c_void_p()
+        _lib.check(lib.rrin_prof_create(cap2, C.byref(h2)), "rrin_prof_create")
+        el2, o2 = time_steps(eng2, i0, i1, args.t, args.steps, dev, h2.value, args.streams)
+        cbusy, cfl, _ = read_prof(lib, h2.value, cap2)
+        lib.rrin_prof_destroy(h2.value)
+        alt_out = o2[0:1].cpu()
+        tf = cfl / (cbusy * 1e-3) / 1e12
+        res[alt_key] = {"value": round(B * args.steps / el2, 3), "ms_per_step": round(1e3 * el2 / args.steps, 3),
+                        "dtype": DTYPE[alt], "metric": f"interpolated frames/sec at {W}x{H} {PREC_LABEL[alt]}",
+                        "conv_tflops": round(tf, 2), "peak": round(PEAK[alt], 1),
+                        "conv_frac_of_peak": round(tf / PEAK[alt], 4),
+                        "kernel": ("conv3x3_h8_kernel (v_mfma_f32_32x32x16_f16 x3)" if alt == "fp32_split16"
+                                   else "exact-fp32 conv (v_mfma_f32_32x32x2_f32)"),
+                        "streams": args.streams}
+        del eng2
         net.precision = args.precision
     if rank == 0 and world == 1 and args.cpu_baseline == "auto":
         res["cpu_baseline"], res["parity"] = cpu_baseline({k: v.detach().cpu() for k, v in sd.items()}, H, W,
                                                           args.cpu_pairs, args.t, last[0][0:1].cpu(),
                                                           alt_out)
-        if "fp32_exact" in res:
-            res["fp32_exact"]["parity"] = res["parity"].pop("alt")
+        if alt_key in res:
+            res[alt_key]["parity"] = res["parity"].pop("alt")
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:

@@ -27,7 +27,8 @@ def build_parser():
     cv.add_argument("--resume", action="store_true", default=False)
     # rrin_amd additions
     cv.add_argument("--batch", type=int, default=4, help="frame pairs per GPU call")
-    cv.add_argument("--precision", default="fp32_split16", choices=["fp32", "fp32_split16", "fp16"])
+    cv.add_argument("--precision", default="fp32", choices=["fp32", "fp32_split16", "fp16"],
+                    help="fp32: exact fp32 (default); fp32_split16: fp32-emulated with fp16 hi+lo x3; fp16")
     return p
 
 

@@ -68,9 +68,17 @@ struct Tile {
   static_assert(16 % TH == 0, "TH must divide the 16-row plane padding");
 };
 
-template <int WAVES_M, int WAVES_N, int WM, int WN, int SRC, int EPI>
+// Lab-only ablations (template SCHED, librrin_lab32.so; wrong outputs, they
+// time what is left): NO_DMA skips staging later chunks (keeps computing on
+// chunk 0), NO_MFMA keeps the LDS operand reads but drops the MFMAs, NO_EPI
+// drops the epilogue stores, NO_SYNC drops the per-chunk wait + barrier.
+enum : int { S32_NO_DMA = 1, S32_NO_MFMA = 2, S32_NO_EPI = 4, S32_NO_SYNC = 8 };
+
+template <int WAVES_M, int WAVES_N, int WM, int WN, int SRC, int EPI, int SCHED = 0>
 __global__ void __launch_bounds__(256) conv3x3_mfma_kernel(ConvArgs a) {
   using T = Tile<WAVES_M, WAVES_N, WM, WN>;
+  constexpr bool kNoDma = (SCHED & S32_NO_DMA) != 0, kNoMfma = (SCHED & S32_NO_MFMA) != 0;
+  constexpr bool kNoEpi = (SCHED & S32_NO_EPI) != 0, kNoSync = (SCHED & S32_NO_SYNC) != 0;
   constexpr int BM = T::BM, TH = T::TH, ROWS = T::ROWS;
   constexpr int IN_F = T::IN_F, W_F = T::W_F;
 
@@ -251,8 +259,12 @@ __global__ void __launch_bounds__(256) conv3x3_mfma_kernel(ConvArgs a) {
 #pragma unroll
       for (int mt = 0; mt < WM; ++mt)
 #pragma unroll
-        for (int nt = 0; nt < WN; ++nt)
-          acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[st & 1][mt], bv[st & 1][nt], acc[mt][nt], 0, 0, 0);
+        for (int nt = 0; nt < WN; ++nt) {
+          if constexpr (kNoMfma)
+            asm volatile("" ::"v"(av[st & 1][mt]), "v"(bv[st & 1][nt]));
+          else
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[st & 1][mt], bv[st & 1][nt], acc[mt][nt], 0, 0, 0);
+        }
     }
   };
 
@@ -262,11 +274,13 @@ __global__ void __launch_bounds__(256) conv3x3_mfma_kernel(ConvArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     for (int c = 0; c < a.nchunks; ++c) {
-      const int buf = c & 1;
-      if ((c + 1) < a.nchunks) issue(c + 1, buf ^ 1);  // buf^1 last read before the previous barrier
+      const int buf = kNoDma ? 0 : c & 1;
+      if (!kNoDma && (c + 1) < a.nchunks) issue(c + 1, buf ^ 1);  // buf^1 last read before the previous barrier
       compute(buf);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
+      if constexpr (!kNoSync) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
     }
   } else {
     // ---- UPSAMPLE2X: register prefetch of weights + low-res tile, LDS expansion
@@ -292,6 +306,15 @@ __global__ void __launch_bounds__(256) conv3x3_mfma_kernel(ConvArgs a) {
   }
 
   // ---- epilogue: bias, leaky, store (+ 2x2 average pool)
+  if constexpr (kNoEpi) {
+#pragma unroll
+    for (int mt = 0; mt < WM; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < WN; ++nt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) asm volatile("" ::"v"(acc[mt][nt][i]));
+    return;
+  }
   const int yb = y0 + wn * WN;
   const int x = x0 + j;
 #pragma unroll
@@ -353,11 +376,11 @@ static const CfgInfo kCfg[] = {
 };
 static constexpr int kNumCfg = sizeof(kCfg) / sizeof(kCfg[0]);
 
-template <int A, int B, int C, int D, int SRC, int EPI>
+template <int A, int B, int C, int D, int SRC, int EPI, int SCHED = 0>
 static int launch_t(const ConvArgs& args, int grid, hipStream_t st) {
   using T = Tile<A, B, C, D>;
   constexpr size_t lds = SRC == RRIN_SRC_UPSAMPLE2X ? T::LDS_BYTES_UP : T::LDS_BYTES;
-  auto k = conv3x3_mfma_kernel<A, B, C, D, SRC, EPI>;
+  auto k = conv3x3_mfma_kernel<A, B, C, D, SRC, EPI, SCHED>;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -388,7 +411,8 @@ extern "C" int rrin_conv_cfg_count(void) { return kNumCfg; }
 extern "C" int rrin_conv_cfg_bm(int32_t cfg) { return (cfg >= 0 && cfg < kNumCfg) ? kCfg[cfg].bm : RRIN_E_CONFIG; }
 extern "C" int rrin_conv_cfg_th(int32_t cfg) { return (cfg >= 0 && cfg < kNumCfg) ? kCfg[cfg].th : RRIN_E_CONFIG; }
 
-extern "C" int rrin_conv3x3_fwd(const rrin_conv_desc* d, void* stream) {
+// Validate a descriptor and fill the kernel arguments; grid = one block per tile.
+static int conv_prepare(const rrin_conv_desc* d, ConvArgs& a, int& grid_out) {
   if (!d || !d->src.base || !d->dst.base || !d->wpack || !d->bias) return RRIN_E_ARG;
   if (d->cfg < 0 || d->cfg >= kNumCfg) return RRIN_E_CONFIG;
   if (d->n < 1 || d->cin < 1 || d->cout < 1) return RRIN_E_ARG;
@@ -413,7 +437,7 @@ extern "C" int rrin_conv3x3_fwd(const rrin_conv_desc* d, void* stream) {
   if (gs.wp != d->src.g.wp || gs.hp != d->src.g.hp || gd.wp != d->dst.g.wp || gd.hp != d->dst.g.hp)
     return RRIN_E_SHAPE;
 
-  ConvArgs a;
+  a = ConvArgs{};
   a.src = d->src.base + (int64_t)d->src.ch_off * d->src.g.plane;
   a.src_img = d->src.img_stride;
   a.src_plane = d->src.g.plane;
@@ -447,13 +471,55 @@ extern "C" int rrin_conv3x3_fwd(const rrin_conv_desc* d, void* stream) {
   a.slope = d->slope;
   const int64_t grid = (int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n;
   if (grid > 0x7fffffff) return RRIN_E_SHAPE;
+  grid_out = (int)grid;
+  return 0;
+}
+
+extern "C" int rrin_conv3x3_fwd(const rrin_conv_desc* d, void* stream) {
+  ConvArgs a;
+  int grid = 0;
+  const int rc = conv_prepare(d, a, grid);
+  if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;
   switch (d->cfg) {
 #define X(id, A, B, C, D) \
   case id:                \
-    return launch_cfg<A, B, C, D>(a, d->src_mode, d->epi_mode, (int)grid, st);
+    return launch_cfg<A, B, C, D>(a, d->src_mode, d->epi_mode, grid, st);
     RRIN_CONV_CFGS(X)
 #undef X
   }
   return RRIN_E_CONFIG;
 }
+
+#ifdef RRIN_LAB
+// Kernel lab (tools/conv_lab.py ablate32; librrin_lab32.so, `make lab`): one
+// direct LEAKY conv of any config with the ablation bits S32_* in `sched`.
+template <int A, int B, int C, int D>
+static int lab32_cfg(const ConvArgs& a, int sched, int grid, hipStream_t st) {
+  switch (sched) {
+#define L(v) \
+  case v:    \
+    return launch_t<A, B, C, D, RRIN_SRC_DIRECT, RRIN_EPI_LEAKY, v>(a, grid, st);
+    L(0) L(1) L(2) L(3) L(4) L(8) L(9) L(12) L(13)
+#undef L
+  }
+  return RRIN_E_CONFIG;
+}
+
+extern "C" int rrin_conv3x3_lab32(const rrin_conv_desc* d, int32_t sched, void* stream) {
+  if (!d || d->src_mode != RRIN_SRC_DIRECT || d->epi_mode != RRIN_EPI_LEAKY) return RRIN_E_ARG;
+  ConvArgs a;
+  int grid = 0;
+  const int rc = conv_prepare(d, a, grid);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  switch (d->cfg) {
+#define X(id, A, B, C, D) \
+  case id:                \
+    return lab32_cfg<A, B, C, D>(a, sched, grid, st);
+    RRIN_CONV_CFGS(X)
+#undef X
+  }
+  return RRIN_E_CONFIG;
+}
+#endif

@@ -12,12 +12,19 @@ is no PyTorch-operator path.  The HIP path requires:
 * inputs on a ROCm device, fp32 (the metric's dtype), NCHW, H % 16 == W % 16 == 0
   (the reference raises at `model.py:41` otherwise — we raise earlier);
 * autograd off (``torch.no_grad()`` / ``inference_mode``), as in the production
-  caller `convert.py:117`.  Training (`train.py`) needs backward kernels, which
-  are out of scope; we raise instead of silently detaching.
+  caller `convert.py:117`.
+
+With autograd on (the training caller `train.py:98`) ``forward``
+runs the reference math with PyTorch operators on the model's device instead
+(``_forward_autograd``, same op order as `model.py:32-65`), so that training
+keeps working through the drop-in; there are no HIP backward kernels.  That
+path is never taken for inference, and without autograd a missing or failing
+HIP library raises.
 """
 from __future__ import annotations
 
 import torch
+import torch.nn.functional as F
 from torch import nn
 
 from .unet import UNet
@@ -32,6 +39,7 @@ class Net(nn.Module):
         self.refine_flow = UNet(10, 4, 4)
         self.final = UNet(9, 3, 4)
         self._engine = None
+        self._engine_fp = None
         self._engine_version = -1
         self._weights_version = 0
         # Arithmetic of the HIP path (not part of the reference contract):
@@ -49,7 +57,10 @@ class Net(nn.Module):
         self.streams = 2
         self.register_load_state_dict_post_hook(Net._on_load)
 
-    # Packed weights are rebuilt after load_state_dict / .to() / param edits.
+    # Packed weights are rebuilt after load_state_dict / .to() (version bump) and
+    # after any in-place parameter edit (optimizer.step, p.copy_, nn.init, a
+    # sub-UNet's load_state_dict): engine() compares each parameter's storage
+    # pointer and autograd version counter with those the packing was built from.
     @staticmethod
     def _on_load(module, incompatible_keys):
         module._weights_version += 1
@@ -62,14 +73,20 @@ class Net(nn.Module):
         self._weights_version += 1
         return out
 
+    def _weights_fingerprint(self):
+        return tuple((p.data_ptr(), p._version) for p in self.parameters())
+
     def engine(self):
         from .engine import RRINEngine
+        fp = self._weights_fingerprint()
         if (self._engine is None or self._engine_version != self._weights_version
+                or self._engine_fp != fp
                 or self._engine.precision != self.precision
                 or self._engine.subpixel_max_level != self.subpixel_max_level):
             self._engine = None  # free the previous packed weights first
             self._engine = RRINEngine(self, self.precision, self.subpixel_max_level)
             self._engine_version = self._weights_version
+            self._engine_fp = fp
         return self._engine
 
     def interpolate(self, input0, input1, ts):
@@ -85,7 +102,34 @@ class Net(nn.Module):
     def forward(self, input0, input1, t=0.5):
         if torch.is_grad_enabled() and (input0.requires_grad or input1.requires_grad or
                                         any(p.requires_grad for p in self.parameters())):
-            raise RuntimeError(
-                "rrin_amd.Net runs HIP inference kernels only (no backward): call it under "
-                "torch.no_grad() or torch.inference_mode(), as convert.py:117 does")
+            return self._forward_autograd(input0, input1, t)
         return self.engine().forward(input0, input1, t, streams=self.streams)
+
+    @staticmethod
+    def _backwarp(img, flow):
+        """model.py:8-21 with the grid built on the image's device (the reference
+        hard-codes .cuda())."""
+        n, _, h, w = img.shape
+        gy, gx = torch.meshgrid(torch.arange(h, device=img.device), torch.arange(w, device=img.device),
+                                indexing="ij")
+        x = gx.unsqueeze(0).expand(n, h, w).float() + flow[:, 0]
+        y = gy.unsqueeze(0).expand(n, h, w).float() + flow[:, 1]
+        grid = torch.stack((2 * (x / w - 0.5), 2 * (y / h - 0.5)), dim=3)
+        return F.grid_sample(img, grid, mode="bilinear", padding_mode="zeros", align_corners=False)
+
+    def _forward_autograd(self, input0, input1, t=0.5):
+        """Training path (autograd on): model.py:32-65 with PyTorch operators."""
+        x = torch.cat((input0, input1), 1)
+        flow = self.Flow(x)
+        f01, f10 = flow[:, :2], flow[:, 2:4]
+        ft0 = -(1 - t) * t * f01 + t * t * f10
+        ft1 = (1 - t) * (1 - t) * f01 - t * (1 - t) * f10
+        r = self.refine_flow(torch.cat((ft0, ft1, x), 1))
+        ft0 = ft0 + r[:, :2]
+        ft1 = ft1 + r[:, 2:4]
+        xt1 = self._backwarp(input0, ft0)
+        xt2 = self._backwarp(input1, ft1)
+        m = torch.sigmoid(self.Mask(torch.cat((ft0, ft1, x, xt1, xt2), 1)))
+        w1, w2 = (1 - t) * m[:, 0:1], t * m[:, 1:2]
+        out = (w1 * xt1 + w2 * xt2) / (w1 + w2 + 1e-8)
+        return (self.final(torch.cat((input0, input1, out), 1)) + out).clamp(0, 1)

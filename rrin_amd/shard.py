@@ -60,7 +60,11 @@ class GatherPipeline:
         self.inflight = [None] * depth  # (work, local) per buffer
         self.k = 0
 
-    def submit(self, local: torch.Tensor) -> torch.Tensor:
+    def submit(self, local: torch.Tensor):
+        """Issue the gather of ``local``; returns ``(out, work)``.  ``out`` is only
+        valid after ``work.wait()`` (RCCL: orders the caller's stream after the
+        gather) or ``drain()``; ``work`` is None when the gather already completed
+        (gloo, one rank)."""
         i = self.k % len(self.bufs)
         self.k += 1
         if self.inflight[i] is not None:
@@ -69,7 +73,7 @@ class GatherPipeline:
                 work.wait()
         out, work = gather_frames(local, group=self.group, out=self.bufs[i], async_op=True)
         self.inflight[i] = (work, local)  # keep the shard alive until its gather is done
-        return out
+        return out, work
 
     def drain(self):
         for i, f in enumerate(self.inflight):

@@ -19,6 +19,7 @@ Channel plan (``wf=5``): level i has ``2**(5+i)`` channels (unet.py:26).
 from __future__ import annotations
 
 import torch
+import torch.nn.functional as F
 from torch import nn
 
 WF = 5                 # unet.py:15 default width factor
@@ -89,9 +90,24 @@ class UNet(nn.Module):
         out.append(("last", self.last))
         return out
 
-    def forward(self, x):  # pragma: no cover - guarded
-        raise RuntimeError("rrin_amd.UNet is a parameter container; run rrin_amd.Net "
-                           "(HIP engine) instead of calling a sub-UNet directly")
+    def forward(self, x):
+        """Autograd (training) path only: the reference U-Net math with PyTorch
+        operators (unet.py:40-51, 59-63, 76-94), so that ``train.py:98`` can
+        back-propagate through ``rrin_amd.Net``.  Inference never comes here:
+        without autograd this raises, and ``Net.forward`` runs the HIP kernels."""
+        if not torch.is_grad_enabled():
+            raise RuntimeError("rrin_amd.UNet.forward is the autograd (training) path; inference runs "
+                               "rrin_amd.Net's HIP engine (call the Net under torch.no_grad())")
+        bridges = []
+        for i, d in enumerate(self.down_path):
+            x = d.block(x)
+            if i < self.depth - 1:
+                bridges.append(x)
+                x = F.avg_pool2d(x, 2)
+        x = F.leaky_relu(self.midconv(x), LEAKY_SLOPE)
+        for j, u in enumerate(self.up_path):
+            x = u.conv_block.block(torch.cat((u.up(x), bridges[-j - 1]), 1))
+        return self.last(x)
 
 
 def conv_flops(unet: UNet, h: int, w: int) -> int:

@@ -124,3 +124,75 @@ def test_convert_on_gpu_matches_oracle(tmp_path, gpu):
         a = np.asarray(Image.open(os.path.join(dest, name))).astype(int)
         b = np.asarray(Image.open(os.path.join(str(tmp_path / "ref"), name))).astype(int)
         assert np.abs(a - b).max() <= 1 and (a != b).mean() < 0.01
+
+
+class BlendModel:
+    """Cheap deterministic stand-in (plumbing tests): (1-t) i0 + t i1."""
+
+    def interpolate(self, i0, i1, ts):
+        return [(1 - t) * i0 + t * i1 for t in ts]
+
+
+def test_reader_error_is_raised(tmp_path):
+    """A frame the reader thread cannot decode surfaces as an exception in the
+    caller instead of a hang (the thread hands the error over the queue)."""
+    src, dest = str(tmp_path / "in"), str(tmp_path / "out")
+    make_frames(src, 4, 32, 48)
+    with open(os.path.join(src, f"{3:09d}.png"), "wb") as f:
+        f.write(b"not a png")
+    with pytest.raises(RuntimeError, match="reading input frames failed"):
+        cv.interpolate_folder(BlendModel(), src, dest, sf=1, batch=2, log=lambda *a: None)
+
+
+def test_pair_shards_cover_pairs_with_one_frame_halo():
+    sh = cv.pair_shards(0, 11, 4)            # 10 pairs over 4 ranks
+    assert sh == [(0, 2), (2, 5), (5, 7), (7, 10)]
+    assert all(b == c for (_, b), (c, _) in zip(sh[:-1], sh[1:]))   # contiguous; rank r reads frame b = next lo
+    assert cv.pair_shards(3, 11, 2) == [(3, 6), (6, 10)]          # resume: pairs 3..9
+    assert cv.pair_shards(0, 3, 4) == [(0, 0), (0, 1), (1, 1), (1, 2)]  # fewer pairs than ranks
+
+
+def _convert_worker(rank, world, port, src, dest, gather, resume):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        cv.interpolate_folder(BlendModel(), src, dest, sf=2, batch=2, rank=rank, world=world, gather=gather,
+                              resume=resume, log=lambda *a: None)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("gather", [True, False])
+def test_sharded_convert_equals_single_process(tmp_path, gather):
+    """World-2 gloo: sharded pairs (+ all-gather to rank 0, or per-rank writes)
+    give byte-identical files to the one-process run, also when resuming."""
+    import socket
+    import torch.multiprocessing as mp
+
+    def port():
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        p = s.getsockname()[1]
+        s.close()
+        return p
+
+    src = str(tmp_path / "in")
+    make_frames(src, 8, 32, 48, seed=5)       # 7 pairs: ranks get 3 and 4
+    ref = str(tmp_path / "ref")
+    cv.interpolate_folder(BlendModel(), src, ref, sf=2, batch=2, log=lambda *a: None)
+    dest = str(tmp_path / "out")
+    mp.spawn(_convert_worker, args=(2, port(), src, dest, gather, False), nprocs=2, join=True)
+    assert sorted(os.listdir(dest)) == sorted(os.listdir(ref))
+    for name in os.listdir(ref):
+        assert open(os.path.join(dest, name), "rb").read() == open(os.path.join(ref, name), "rb").read(), name
+    # resume after 7 files: (7-1)//3 = 2 -> restart at pair 1 (convert.py:54,95,118)
+    dest2 = str(tmp_path / "out2")
+    os.makedirs(dest2)
+    for name in sorted(os.listdir(ref))[:7]:
+        os.link(os.path.join(ref, name), os.path.join(dest2, name))
+    mp.spawn(_convert_worker, args=(2, port(), src, dest2, gather, True), nprocs=2, join=True)
+    assert sorted(os.listdir(dest2)) == sorted(os.listdir(ref))
+    for name in os.listdir(ref):
+        assert open(os.path.join(dest2, name), "rb").read() == open(os.path.join(ref, name), "rb").read(), name

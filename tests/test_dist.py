@@ -92,7 +92,10 @@ def _pipeline_worker(rank, world, port, result_path):
     outs = []
     for k in range(3):
         local = torch.full((2, 3, 4, 5), float(10 * k + rank))
-        outs.append(pipe.submit(local).clone())
+        out, work = pipe.submit(local)
+        if work is not None:
+            work.wait()
+        outs.append(out.clone())
     pipe.drain()
     if rank == 0:
         torch.save(torch.stack(outs), result_path)

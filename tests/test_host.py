@@ -33,11 +33,40 @@ def test_conv_flops_match_survey():
     assert abs(total720 / 1e9 - 1600.0) < 0.1
 
 
-def test_forward_requires_no_grad():
+def test_autograd_path_matches_golden_and_trains():
+    """With autograd on (train.py:98) Net.forward runs the reference math with
+    PyTorch operators: equal to the reference's own output (golden,
+    written by the unmodified reference) and differentiable."""
+    g = np.load(os.path.join(GOLDEN, "net_default.npz"))
     net = Net()
-    x = torch.zeros(1, 3, 16, 16)
-    with pytest.raises(RuntimeError, match="no_grad"):
-        net(x, x)
+    net.load_state_dict(keyed_state_dict(net.state_dict()), strict=True)
+    i0, i1 = torch.from_numpy(g["i0"]), torch.from_numpy(g["i1"])
+    out = net(i0, i1, 0.5)
+    assert out.requires_grad
+    assert torch.allclose(out, torch.from_numpy(g["out_t050"]), atol=1e-6, rtol=0)
+    out.mean().backward()
+    assert net.Flow.down_path[0].block[0].weight.grad is not None
+    assert float(net.final.last.weight.grad.abs().sum()) > 0
+
+
+def test_unet_forward_is_autograd_only():
+    net = Net()
+    with torch.no_grad(), pytest.raises(RuntimeError, match="autograd"):
+        net.Flow(torch.zeros(1, 6, 16, 16))
+
+
+def test_packed_weights_follow_inplace_edits():
+    """The engine's packing is keyed by every parameter's (storage, version):
+    an in-place edit (optimizer step, p.copy_, a sub-UNet load_state_dict)
+    changes the fingerprint."""
+    net = Net()
+    fp0 = net._weights_fingerprint()
+    with torch.no_grad():
+        net.Mask.last.bias.add_(1.0)
+    fp1 = net._weights_fingerprint()
+    assert fp1 != fp0
+    net.Flow.load_state_dict(net.Flow.state_dict())
+    assert net._weights_fingerprint() != fp1
 
 
 def test_forward_requires_rocm_device():

@@ -253,6 +253,41 @@ def single(args):
     prec = _lib.PRECISIONS[args.precision]
     cin, cout, L, epi, cfg = args.shape
     n, h, w = args.batch, args.height >> L, args.width >> L
+    if args.precision == "fp32":  # exact-fp32 PP conv; --src 1 = fused upsample of a half-size input
+        from tests.hip_helpers import pack
+        src = args.src
+        hs, ws_ = (h // 2, w // 2) if src == 1 else (h, w)
+        x = PPTensor.from_nchw(torch.rand(n, cin, hs, ws_, device=dev) * 2 - 1)
+        dst = PPTensor(n, cout, h, w, dev)
+        pool = PPTensor(n, cout, h // 2, w // 2, dev) if epi == 2 else None
+        wp, bp = pack(torch.randn(cout, cin, 3, 3) / (3 * cin ** 0.5), torch.zeros(cout), cfg, dev=dev)
+        d = _lib.ConvDesc()
+        d.n, d.cin, d.cout, d.cfg, d.src_mode, d.epi_mode, d.slope = n, cin, cout, cfg, src, epi, 0.1
+        d.src, d.dst = x.view(0, cin), dst.view(0, cout)
+        if pool is not None:
+            d.pool = pool.view(0, cout)
+        d.wpack, d.bias = wp.data_ptr(), bp.data_ptr()
+        if args.sched is None:
+            fwd = lambda st: _lib.check(lib.rrin_conv3x3_fwd(C.byref(d), st))  # noqa: E731
+        else:  # lab build with ablation bits (librrin_lab32.so)
+            lab = C.CDLL(os.path.join(REPO, "rrin_amd", "librrin_lab32.so"))
+            lab.rrin_conv3x3_lab32.argtypes = [C.POINTER(_lib.ConvDesc), C.c_int32, C.c_void_p]
+            fwd = lambda st: _lib.check(lab.rrin_conv3x3_lab32(C.byref(d), args.sched, st))  # noqa: E731
+    else:
+        fwd = None
+    if fwd is not None:
+        st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+        fwd(st)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.reps):
+            fwd(st)
+        e1.record()
+        e1.synchronize()
+        ms = e0.elapsed_time(e1) / args.reps
+        print(f"{cin}->{cout} L{L} src{args.src} epi{epi} cfg{cfg} fp32: {ms:.4f} ms "
+              f"{2 * 9 * cin * cout * h * w * n / (ms * 1e-3) / 1e12:.1f} TF")
+        return
     x = H8Tensor.from_nchw(torch.rand(n, cin, h, w, device=dev) * 2 - 1, prec)
     dst = H8Tensor(n, cout, h, w, dev, prec)
     pool = H8Tensor(n, cout, h // 2, w // 2, dev, prec) if epi == 2 else None
@@ -355,11 +390,66 @@ def ablate(args):
         json.dump(results, open(args.out, "w"), indent=1)
 
 
+LAB32_VARIANTS = [("base", 0), ("noDma", 1), ("noMfma", 2), ("noDma+noMfma", 3), ("noEpi", 4), ("noSync", 8),
+                  ("noDma+noSync", 9), ("noEpi+noSync", 12), ("noDma+noEpi+noSync", 13)]
+LAB32_SHAPES = [(32, 32, 0, 0), (64, 64, 1, 4), (128, 64, 1, 4), (128, 128, 2, 1), (256, 256, 3, 4), (512, 256, 3, 5),
+                (512, 512, 4, 4)]
+
+
+def ablate32(args):
+    """Exact-fp32 conv ablations (librrin_lab32.so): interleaved rounds, median per variant."""
+    from tests.hip_helpers import pack
+    lab = C.CDLL(os.path.join(REPO, "rrin_amd", "librrin_lab32.so"))
+    fn = lab.rrin_conv3x3_lab32
+    fn.restype = C.c_int
+    fn.argtypes = [C.POINTER(_lib.ConvDesc), C.c_int32, C.c_void_p]
+    dev = torch.device("cuda:0")
+    st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    results = []
+    for cin, cout, L, cfg in LAB32_SHAPES:
+        n, h, w = args.batch, args.height >> L, args.width >> L
+        torch.manual_seed(cin * 1000 + cout)
+        x = PPTensor.from_nchw(torch.rand(n, cin, h, w, device=dev) * 2 - 1)
+        dst = PPTensor(n, cout, h, w, dev)
+        wp, bp = pack(torch.randn(cout, cin, 3, 3) / (3 * cin ** 0.5), torch.randn(cout) * 0.1, cfg, dev=dev)
+        d = _lib.ConvDesc()
+        d.n, d.cin, d.cout, d.cfg, d.src_mode, d.epi_mode, d.slope = n, cin, cout, cfg, 0, _lib.EPI_LEAKY, 0.1
+        d.src, d.dst = x.view(0, cin), dst.view(0, cout)
+        d.wpack, d.bias = wp.data_ptr(), bp.data_ptr()
+        fl = 2 * 9 * cin * cout * h * w * n
+        times = {name: [] for name, _ in LAB32_VARIANTS}
+        for name, sched in LAB32_VARIANTS:
+            _lib.check(fn(C.byref(d), sched, st), f"lab32 {name}")
+        torch.cuda.synchronize()
+        for _ in range(args.reps):
+            for name, sched in LAB32_VARIANTS:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(3):
+                    fn(C.byref(d), sched, st)
+                e1.record()
+                e1.synchronize()
+                times[name].append(e0.elapsed_time(e1) / 3)
+        base = sorted(times["base"])[len(times["base"]) // 2]
+        line = []
+        for name, sched in LAB32_VARIANTS:
+            ms = sorted(times[name])[len(times[name]) // 2]
+            results.append(dict(cin=cin, cout=cout, level=L, cfg=cfg, variant=name, ms=ms,
+                                tflops=fl / (ms * 1e-3) / 1e12))
+            line.append(f"{name}:{ms:.3f}({ms / base:.2f})")
+        print(f"{cin:4d}->{cout:4d} L{L} cfg{cfg} base {base:.3f} ms {fl / (base * 1e-3) / 1e12:.0f} TF | "
+              + " ".join(line), flush=True)
+    if args.out:
+        json.dump(results, open(args.out, "w"), indent=1)
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("mode", choices=["breakdown", "tune", "single", "ablate"])
+    ap.add_argument("mode", choices=["breakdown", "tune", "single", "ablate", "ablate32"])
     ap.add_argument("--shape", type=int, nargs=5, default=[512, 256, 3, 1, 0],
                     help="single: cin cout level epi cfg")
+    ap.add_argument("--src", type=int, default=0, help="single, fp32: src mode (1 = fused upsample)")
+    ap.add_argument("--sched", type=int, default=None, help="single, fp32: lab32 ablation bits")
     ap.add_argument("--batch", type=int, default=4)
     ap.add_argument("--height", type=int, default=720)
     ap.add_argument("--width", type=int, default=1280)
@@ -369,7 +459,7 @@ def main():
                     help="breakdown: run the first conv of every U-Net with this H8 config (same BM only)")
     ap.add_argument("--precision", default="fp32", choices=["fp32", "fp32_split16", "fp16"])
     args = ap.parse_args()
-    {"breakdown": breakdown, "tune": tune, "single": single, "ablate": ablate}[args.mode](args)
+    {"breakdown": breakdown, "tune": tune, "single": single, "ablate": ablate, "ablate32": ablate32}[args.mode](args)
 
 
 if __name__ == "__main__":
