@@ -48,11 +48,17 @@ F16_PEAK_TFLOPS = 2500.0   # dense f16 MFMA (v_mfma_f32_32x32x16_f16), no sparsi
 HBM_PEAK_GBS = 8000.0
 # Roofline peak in fp32-equivalent TFLOP/s per precision: the split path spends
 # three f16 MFMA products on every fp32 product.
-PEAK = {"fp32": FP32_PEAK_TFLOPS, "fp32_split16": F16_PEAK_TFLOPS / 3, "fp16": F16_PEAK_TFLOPS}
-MFMA_PRODUCTS = {"fp32": 1, "fp32_split16": 3, "fp16": 1}
+PEAK = {"fp32": FP32_PEAK_TFLOPS, "fp32_planar": FP32_PEAK_TFLOPS, "fp32_split16": F16_PEAK_TFLOPS / 3,
+        "fp16": F16_PEAK_TFLOPS}
+MFMA_PRODUCTS = {"fp32": 1, "fp32_planar": 1, "fp32_split16": 3, "fp16": 1}
 # Only "fp32" is fp32 arithmetic (the BASELINE metric); split16 emulates fp32 with fp16 products.
-PREC_LABEL = {"fp32": "fp32", "fp32_split16": "fp32-emulated (fp16 hi+lo x3)", "fp16": "fp16"}
-DTYPE = {"fp32": "f32",
+PREC_LABEL = {"fp32": "fp32", "fp32_planar": "fp32", "fp32_split16": "fp32-emulated (fp16 hi+lo x3)",
+              "fp16": "fp16"}
+KERNEL = {"fp32": "conv3x3_h8_kernel on fp32 records (77 body convs, v_mfma_f32_32x32x2_f32)",
+          "fp32_planar": "conv3x3_mfma_kernel, planar fp32 (77 body convs, v_mfma_f32_32x32x2_f32)",
+          "fp32_split16": "conv3x3_h8_kernel (77 body convs, v_mfma_f32_32x32x16_f16 x3)",
+          "fp16": "conv3x3_h8_kernel (77 body convs, v_mfma_f32_32x32x16_f16)"}
+DTYPE = {"fp32": "f32", "fp32_planar": "f32",
          "fp32_split16": "f16x3 (fp32-emulated: fp16 hi+lo split, 3 f16 MFMA products, f32 accumulate)",
          "fp16": "f16"}
 
@@ -66,7 +72,7 @@ def parse():
     ap.add_argument("--height", type=int, default=720)
     ap.add_argument("--width", type=int, default=1280)
     ap.add_argument("--t", type=float, default=0.5)
-    ap.add_argument("--precision", default="fp32", choices=["fp32", "fp32_split16", "fp16"],
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "fp32_planar", "fp32_split16", "fp16"],
                     help="fp32: exact fp32 (v_mfma_f32_32x32x2_f32, fp32 storage) -- the BASELINE metric; "
                          "fp32_split16: fp32-EMULATED (values as fp16 hi+lo, 3 fp16 products per fp32 "
                          "product, fp32 accumulate); fp16: fp16 storage/products")
@@ -297,9 +303,7 @@ def main():
         roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1),
                     "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None,
                     "mfma_issued_tflops": round(achieved * MFMA_PRODUCTS[args.precision], 1),
-                    "kernel": ("conv3x3_mfma_kernel (77 body convs, v_mfma_f32_32x32x2_f32)"
-                               if args.precision == "fp32" else
-                               "conv3x3_h8_kernel (77 body convs, v_mfma_f32_32x32x16_f16)"),
+                    "kernel": KERNEL[args.precision],
                     "flops_per_launch_avg": conv_fl / max(conv_launches, 1),
                     "avg_launch_ms": conv_ms / max(conv_launches, 1),
                     "conv_busy_ms_per_step": round(conv_busy / args.steps, 3),
@@ -382,10 +386,10 @@ def main():
     }
     alt_out = None
     alt_key = None
-    if world == 1 and not args.no_alt and args.precision in ("fp32", "fp32_split16", "fp16"):
+    if world == 1 and not args.no_alt:
         # secondary line on the same inputs: an fp32 run reports the fp32-emulated
         # split16 path beside it; any other precision reports the exact-fp32 path
-        alt = "fp32_split16" if args.precision == "fp32" else "fp32"
+        alt = "fp32_split16" if args.precision in ("fp32", "fp32_planar") else "fp32"
         alt_key = "fp32_emulated_split16" if alt == "fp32_split16" else "fp32_exact"
         net.precision = alt
         eng2 = net.engine()
@@ -404,8 +408,7 @@ def main():
                         "dtype": DTYPE[alt], "metric": f"interpolated frames/sec at {W}x{H} {PREC_LABEL[alt]}",
                         "conv_tflops": round(tf, 2), "peak": round(PEAK[alt], 1),
                         "conv_frac_of_peak": round(tf / PEAK[alt], 4),
-                        "kernel": ("conv3x3_h8_kernel (v_mfma_f32_32x32x16_f16 x3)" if alt == "fp32_split16"
-                                   else "exact-fp32 conv (v_mfma_f32_32x32x2_f32)"),
+                        "kernel": KERNEL[alt],
                         "streams": args.streams}
         del eng2
         net.precision = args.precision

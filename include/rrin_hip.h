@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define RRIN_ABI_VERSION 6
+#define RRIN_ABI_VERSION 7
 
 #define RRIN_OK 0
 #define RRIN_E_SHAPE (-1)     /* H or W not a multiple of 16, or N < 1          */
@@ -134,9 +134,13 @@ int rrin_pp_to_nchw(const rrin_pp* src, int32_t n, int32_t c, float* dst, void* 
 int rrin_warp_fwd(const float* img, const float* flow, float* out, int32_t n, int32_t c,
                   int32_t h, int32_t w, void* stream);
 
-/* ---- Split-fp16 path ("H8" layout) --------------------------------------- */
+/* ---- Record-layout paths ("H8" family: 16-byte channel records) ---------- */
 /* Precision of a forward / conv:
- *   F32   exact fp32 (v_mfma_f32_32x32x2_f32), PP layout above;
+ *   F32   exact fp32 (v_mfma_f32_32x32x2_f32), PP layout above (planar, legacy);
+ *   F32R  exact fp32 (v_mfma_f32_32x32x2_f32, fp32 storage) on the record layout
+ *         below with 4 fp32 channels per 16-byte record ("R32"); the kernels,
+ *         schedules and fusions of the fp16 paths (persistent grids, sub-pixel
+ *         up convs, fused heads) -- the default fp32 path;
  *   F16X3 every fp32 value v is held as hi = f16(v), lo = f16((v - hi) * 2^11)
  *         (v = hi + lo 2^-11 to ~2^-22 |v|; lo stays normal) and every product as
  *         hi*hi + 2^-11 (hi*lo + lo*hi) in v_mfma_f32_32x32x16_f16 with fp32
@@ -147,7 +151,10 @@ int rrin_warp_fwd(const float* img, const float* flow, float* out, int32_t n, in
  * records (8 halfs, channel-innermost); hp = round_up(h,16)+2,
  * wp = round_up(w,32)+16 records, pixel (y,x) at record (y+1)*wp + x+8.
  * F16X3 keeps two such tensors (hi, lo) with identical geometry. */
-enum rrin_prec { RRIN_PREC_F32 = 0, RRIN_PREC_F16X3 = 1, RRIN_PREC_F16 = 2 };
+enum rrin_prec { RRIN_PREC_F32 = 0, RRIN_PREC_F16X3 = 1, RRIN_PREC_F16 = 2, RRIN_PREC_F32R = 3 };
+/* In the record layout a "group" is the channels of one record: 8 (F16X3, F16)
+ * or 4 (F32R); g_off / groups of an rrin_h8 view count such groups, and the
+ * rrin_*_h8 entry points below accept F32R wherever they take a prec. */
 
 int rrin_make_geom_h8(int32_t h, int32_t w, rrin_geom* g); /* plane in records */
 
@@ -185,6 +192,13 @@ int rrin_conv_h8_cfg_ok(int32_t cfg, int32_t prec); /* 1 if the config fits LDS 
  * every weight chunk resident in LDS needs them to fit) */
 int rrin_conv_h8_cfg_fits(int32_t cfg, int32_t prec, int32_t cin);
 int rrin_conv3x3_h8_fwd(const rrin_conv_h8_desc* d, void* stream);
+
+/* F32R packing: [co_block][chunk of 8 ci][tap][half][bm][4] fp32 (half hh holds
+ * input channels chunk*8 + 4*hh .. +3), unscaled; pass as whi (wlo NULL,
+ * inv_wscale ignored).  bpack: rrin_pack_bias_floats(cout, bm) floats. */
+int64_t rrin_pack_conv3x3_r32_floats(int32_t cout, int32_t cin, int32_t bm);
+int rrin_pack_conv3x3_r32(const float* w, const float* b, int32_t cout, int32_t cin, int32_t bm,
+                          const int32_t* perm, float* wpack, float* bpack);
 
 /* Host packing: [co_block][chunk of 16 ci][tap][half][bm][8] halves, weights
  * pre-scaled by a power of two so max|w| lands in [2^12, 2^13) (keeps lo

@@ -9,7 +9,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "librrin_hip.so")
 
 # enums (rrin_hip.h)
@@ -17,8 +17,17 @@ SRC_DIRECT, SRC_UPSAMPLE2X = 0, 1
 EPI_LINEAR, EPI_LEAKY, EPI_LEAKY_POOL, EPI_LEAKY_REP, EPI_SUBPIXEL = 0, 1, 2, 3, 4
 KIND_CONV, KIND_HEAD, KIND_LAYOUT, KIND_EDGE = 0, 1, 2, 3
 HEAD_PLAIN, HEAD_FLOW, HEAD_REFINE, HEAD_MASK, HEAD_FINAL = 0, 1, 2, 3, 4
-PREC_F32, PREC_F16X3, PREC_F16 = 0, 1, 2
-PRECISIONS = {"fp32": PREC_F32, "fp32_split16": PREC_F16X3, "fp16": PREC_F16}
+PREC_F32, PREC_F16X3, PREC_F16, PREC_F32R = 0, 1, 2, 3
+# "fp32": exact fp32 on the record layout (F32R); "fp32_planar": exact fp32 on the
+# planar PP layout (the first implementation, kept for A/B); "fp32_split16":
+# fp32-emulated (fp16 hi+lo x3); "fp16"
+PRECISIONS = {"fp32": PREC_F32R, "fp32_planar": PREC_F32, "fp32_split16": PREC_F16X3, "fp16": PREC_F16}
+RECORD_PRECS = (PREC_F16X3, PREC_F16, PREC_F32R)
+
+
+def chans_per_record(prec: int) -> int:
+    """Channels of one 16-B record of the record layout: 4 fp32 or 8 halves."""
+    return 4 if prec == PREC_F32R else 8
 
 
 class Geom(C.Structure):
@@ -113,6 +122,9 @@ SIGNATURES = {
     "rrin_pack_conv3x3_h8_halves": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32]),
     "rrin_pack_conv3x3_h8": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p,
                                        C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(C.c_float)]),
+    "rrin_pack_conv3x3_r32_floats": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32]),
+    "rrin_pack_conv3x3_r32": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p,
+                                        C.c_void_p, C.c_void_p]),
     "rrin_subpixel_weights": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p,
                                         C.c_void_p]),
     "rrin_ring_pixels": (C.c_int64, [C.c_int32, C.c_int32]),

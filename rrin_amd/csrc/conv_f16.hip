@@ -107,6 +107,14 @@ struct TileH8 {
   static_assert(16 % TH == 0, "TH must divide the 16-row plane padding");
 };
 
+// keep floats [0, nvalid) of an fp32 record (nvalid in 1..3)
+__device__ inline uint4 mask_floats(uint4 v, int nvalid) {
+  if (nvalid < 2) v.y = 0u;
+  if (nvalid < 3) v.z = 0u;
+  v.w = 0u;
+  return v;
+}
+
 __device__ inline uint4 mask_halves(uint4 v, int nvalid) {
   // keep halves [0, nvalid) of a record (nvalid in 1..7)
   unsigned* d = reinterpret_cast<unsigned*>(&v);
@@ -155,9 +163,17 @@ constexpr int kSpreadTaps = 6, kStaggerTap = 3;
 // CU) chunk 0 of a block's next tile is staged while the last chunk of the
 // current one computes, so only its first tile waits for staging.  WRES needs
 // every tile of a block in one channel block (gridDim.x % co_blocks == 0).
-template <int NW, int WM, int WN, int PLANES, int EPI, bool DMA, int SCHED = 0>
+//
+// F32 (exact fp32, "R32" records): a record holds 4 fp32 channels, a chunk is
+// 2 groups = 8 input channels, and each tap's K8 block is 4
+// v_mfma_f32_32x32x2_f32 (product e: lanes 0-31 channel e, lanes 32-63 channel
+// 4+e of the chunk; one ds_read_b128 per operand feeds all 4).  Same tiles,
+// LDS images and DMA as the fp16 kernel; weights unscaled; whole-record stores.
+template <int NW, int WM, int WN, int PLANES, int EPI, bool DMA, int SCHED = 0, bool F32 = false>
 __global__ void __launch_bounds__(64 * NW) conv3x3_h8_kernel(ConvH8Args a) {
   using T = TileH8<NW, WM, WN, PLANES>;
+  static_assert(!F32 || PLANES == 1, "fp32 records: one plane");
+  constexpr int CPR = F32 ? 4 : 8;  // channels per record
   constexpr int NT = T::NT, BM = T::BM, TH = T::TH, ROWS = T::ROWS;
   constexpr int IN_REC = T::IN_REC, W_REC = T::W_REC;
   constexpr bool kNoW = (SCHED & SCHED_NO_WDMA) != 0, kNoIn = (SCHED & SCHED_NO_IDMA) != 0;
@@ -215,7 +231,7 @@ __global__ void __launch_bounds__(64 * NW) conv3x3_h8_kernel(ConvH8Args a) {
       const int gg = c * 2 + g;
       // groups past cin read the zero top-padding row of group 0 instead
       const int64_t off = (int64_t)tl.img * a.src_img +
-                          (gg * 8 < a.cin ? (int64_t)gg * a.src_gp + (int64_t)(tl.y0 + r) * a.src_wp : 0) +
+                          (gg * CPR < a.cin ? (int64_t)gg * a.src_gp + (int64_t)(tl.y0 + r) * a.src_wp : 0) +
                           tl.x0 + (kH8PadLeft - 1) + col;
       uint4* d = s_in + buf * PLANES * IN_REC + NT * it + (tid & ~63);
       dma16(a.src_hi + off, d);
@@ -250,7 +266,7 @@ __global__ void __launch_bounds__(64 * NW) conv3x3_h8_kernel(ConvH8Args a) {
         const int r = rem / H8_LC;
         const int col = rem - r * H8_LC;
         const int gg = c * 2 + g;
-        const int nval = a.cin - gg * 8;
+        const int nval = a.cin - gg * CPR;
         const int64_t off = (int64_t)tl.img * a.src_img + (int64_t)gg * a.src_gp + (int64_t)(tl.y0 + r) * a.src_wp +
                             tl.x0 + (kH8PadLeft - 1) + col;
 #pragma unroll
@@ -258,7 +274,7 @@ __global__ void __launch_bounds__(64 * NW) conv3x3_h8_kernel(ConvH8Args a) {
           uint4 v = make_uint4(0u, 0u, 0u, 0u);
           if (nval > 0) {
             v = src[p][off];
-            if (nval < 8) v = mask_halves(v, nval);
+            if (nval < CPR) v = F32 ? mask_floats(v, nval) : mask_halves(v, nval);
           }
           rin[p][it] = v;
         }
@@ -302,7 +318,41 @@ __global__ void __launch_bounds__(64 * NW) conv3x3_h8_kernel(ConvH8Args a) {
   // 0-31 carry channels 0-7 of the chunk, lanes 32-63 channels 8-15).
   // Operands of tap t+1 are read before the MFMAs of tap t issue; after_tap(t)
   // runs behind tap t's MFMAs (SPREAD / STAGGER: DMA pieces of the next chunk).
+  auto compute_f32 = [&](int buf, int wslot, auto&& after_tap) {
+    const uint4* si = s_in + (kNoIn ? 0 : buf) * IN_REC + (hh * ROWS + wn * WN) * H8_LC + j;
+    const uint4* sw = s_w + (kNoW ? 0 : wslot) * W_REC + hh * BM + j;
+    floatx4 av[2][WM], bv[2][WN];
+    auto ld = [&](int t, int slot) {
+      const int ky = t / 3, kx = t % 3;
+#pragma unroll
+      for (int mt = 0; mt < WM; ++mt) av[slot][mt] = __builtin_bit_cast(floatx4, sw[t * 2 * BM + mt * 32]);
+#pragma unroll
+      for (int nt = 0; nt < WN; ++nt) bv[slot][nt] = __builtin_bit_cast(floatx4, si[(nt + ky) * H8_LC + kx]);
+    };
+    ld(0, 0);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      if (t + 1 < 9) ld(t + 1, (t + 1) & 1);
+      const int s = t & 1;
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int mt = 0; mt < WM; ++mt)
+#pragma unroll
+          for (int nt = 0; nt < WN; ++nt) {
+            if constexpr (kNoMfma)
+              asm volatile("" ::"v"(av[s][mt][e]), "v"(bv[s][nt][e]));
+            else
+              acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s][mt][e], bv[s][nt][e], acc[mt][nt], 0, 0, 0);
+          }
+      after_tap(t);
+    }
+  };
   auto compute = [&](int buf, int wslot, auto&& after_tap) {
+    if constexpr (F32) {
+      compute_f32(buf, wslot, after_tap);
+      return;
+    }
     const uint4* si[PLANES];
     const uint4* sw[PLANES];
 #pragma unroll
@@ -360,6 +410,19 @@ __global__ void __launch_bounds__(64 * NW) conv3x3_h8_kernel(ConvH8Args a) {
   // ---- epilogue piece (mt, q) of tile tl: V = the combined accumulators
   // (acc + accx 2^-11, weight scale still applied): scale, bias, leaky, split,
   // 8-B half-record stores (+ pool / edge-replicate / sub-pixel ring scratch).
+  // 4 consecutive channels of one pixel (lane hh's share of record co0/8, or
+  // the whole fp32 record co0/4 + hh) -> record `rec` of the group plane set `d`
+  auto store4 = [&](uint4* const* d, int64_t rec, const float* v) {
+    if constexpr (F32) {
+      d[0][rec] = make_uint4(__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
+                             __float_as_uint(v[3]));
+    } else {
+      uint2 hv, lv;
+      split4(v, hv, lv);
+      reinterpret_cast<uint2*>(d[0] + rec)[hh] = hv;
+      if constexpr (PLANES == 2) reinterpret_cast<uint2*>(d[1] + rec)[hh] = lv;
+    }
+  };
   auto epi_piece = [&](const TileId& tl, const auto& V, int mt, int q) {
     const int cob = tl.cob, x0 = tl.x0, img = tl.img;
     const int yb = tl.y0 + wn * WN;
@@ -383,20 +446,18 @@ __global__ void __launch_bounds__(64 * NW) conv3x3_h8_kernel(ConvH8Args a) {
         const int Y = 2 * y + py, X = 2 * x + px;
         float t[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) t[e] = V[mt][nt][4 * q + e] * a.inv_wscale;
+        for (int e = 0; e < 4; ++e) t[e] = F32 ? V[mt][nt][4 * q + e] : V[mt][nt][4 * q + e] * a.inv_wscale;
         const int64_t ri = ring_index(Y, X, HH, WW);
         if (ri >= 0) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) a.edge[((int64_t)img * creal + grp * 8 + 4 * hh + e) * a.ring + ri] = t[e];
         } else {
-          const int64_t rec = (int64_t)grp * a.dst_gp + (int64_t)(Y + 1) * a.dst_wp + X + kH8PadLeft;
+          const int rg = F32 ? 2 * grp + hh : grp;  // record group of channels grp*8 + 4hh ..
+          const int64_t rec = (int64_t)rg * a.dst_gp + (int64_t)(Y + 1) * a.dst_wp + X + kH8PadLeft;
           float v[4];
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = t[e] + bs[e];
-          uint2 hv, lv;
-          split4(v, hv, lv);
-          reinterpret_cast<uint2*>(dst[0] + rec)[hh] = hv;
-          if constexpr (PLANES == 2) reinterpret_cast<uint2*>(dst[1] + rec)[hh] = lv;
+          store4(dst, rec, v);
         }
       }
     } else {
@@ -405,8 +466,8 @@ __global__ void __launch_bounds__(64 * NW) conv3x3_h8_kernel(ConvH8Args a) {
         pdst[0] = a.pool_hi + img * a.pool_img;
         if (PLANES == 2) pdst[1] = a.pool_lo + img * a.pool_img;
       }
-      const int co0 = cob * BM + mt * 32 + 8 * q;  // first channel of the record
-      const int grp = co0 >> 3;
+      const int co0 = cob * BM + mt * 32 + 8 * q;  // first channel of the 8-channel block
+      const int grp = F32 ? (co0 >> 2) + hh : co0 >> 3;  // record group this lane writes
       float bs[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) bs[e] = a.bias[co0 + 4 * hh + e];
@@ -417,27 +478,20 @@ __global__ void __launch_bounds__(64 * NW) conv3x3_h8_kernel(ConvH8Args a) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           float t = V[mt][nt][4 * q + e];
-          t = t * a.inv_wscale + bs[e];
+          t = F32 ? t + bs[e] : t * a.inv_wscale + bs[e];
           if constexpr (EPI != RRIN_EPI_LINEAR) t = leaky(t, a.slope);
           v[nt][e] = t;
         }
         if (co0 < a.cout && y < a.h && x < a.w) {
           const int64_t rec = (int64_t)grp * a.dst_gp + (int64_t)(y + 1) * a.dst_wp + x + kH8PadLeft;
-          uint2 hv, lv;
-          split4(v[nt], hv, lv);
-          reinterpret_cast<uint2*>(dst[0] + rec)[hh] = hv;
-          if constexpr (PLANES == 2) reinterpret_cast<uint2*>(dst[1] + rec)[hh] = lv;
+          store4(dst, rec, v[nt]);
           if constexpr (EPI == RRIN_EPI_LEAKY_REP) {
             // edge replicate into the padding ring (read only by a sub-pixel up conv)
             const int dy0 = y == 0 ? -1 : 0, dy1 = y == a.h - 1 ? 1 : 0;
             const int dx0 = x == 0 ? -1 : 0, dx1 = x == a.w - 1 ? 1 : 0;
             for (int dy = dy0; dy <= dy1; ++dy)
               for (int dx = dx0; dx <= dx1; ++dx)
-                if (dy | dx) {
-                  const int64_t r2 = rec + (int64_t)dy * a.dst_wp + dx;
-                  reinterpret_cast<uint2*>(dst[0] + r2)[hh] = hv;
-                  if constexpr (PLANES == 2) reinterpret_cast<uint2*>(dst[1] + r2)[hh] = lv;
-                }
+                if (dy | dx) store4(dst, rec + (int64_t)dy * a.dst_wp + dx, v[nt]);
           }
         }
       }
@@ -453,10 +507,7 @@ __global__ void __launch_bounds__(64 * NW) conv3x3_h8_kernel(ConvH8Args a) {
           const int y = yb + 2 * p2;
           if (!(j & 1) && co0 < a.cout && y < a.h && x < a.w) {
             const int64_t rec = (int64_t)grp * a.pool_gp + (int64_t)(y / 2 + 1) * a.pool_wp + x / 2 + kH8PadLeft;
-            uint2 hv, lv;
-            split4(s4, hv, lv);
-            reinterpret_cast<uint2*>(pdst[0] + rec)[hh] = hv;
-            if constexpr (PLANES == 2) reinterpret_cast<uint2*>(pdst[1] + rec)[hh] = lv;
+            store4(pdst, rec, s4);
           }
         }
       }
@@ -663,6 +714,7 @@ struct EdgeFixArgs {
   int s_wp, sh, sw, cin;
   _Float16* d_hi;
   _Float16* d_lo;
+  float* d_f32;  // F32R output (d_hi / d_lo unused)
   int64_t d_img, d_gp;
   int d_wp, cout;
   const float* edge;
@@ -674,9 +726,9 @@ struct EdgeFixArgs {
   int tiles_row, tiles_col;  // tiles per row line / per column line
 };
 
-// The 4 low-res records (8 channels, both planes) that bilinear x2 (align_corners
-// = False, edge clamp) blends into U(Y, X), and the blend weights.
-template <int PLANES>
+// The 4 low-res records (8 halves / 4 floats, both planes) that bilinear x2
+// (align_corners = False, edge clamp) blends into U(Y, X), and the blend weights.
+template <int PLANES, bool F32 = false>
 struct Up8 {
   uint4 q[4][PLANES];
   float wa, wc;
@@ -706,9 +758,13 @@ struct Up8 {
     float v[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const half8 h = __builtin_bit_cast(half8, q[k][0]);
-      v[k] = (float)h[e];
-      if constexpr (PLANES == 2) v[k] = join(h[e], __builtin_bit_cast(half8, q[k][PLANES - 1])[e]);
+      if constexpr (F32) {
+        v[k] = __builtin_bit_cast(floatx4, q[k][0])[e];
+      } else {
+        const half8 h = __builtin_bit_cast(half8, q[k][0]);
+        v[k] = (float)h[e];
+        if constexpr (PLANES == 2) v[k] = join(h[e], __builtin_bit_cast(half8, q[k][PLANES - 1])[e]);
+      }
     }
     const float wb = 1.0f - wa, wd = 1.0f - wc;
     const float top = wc * v[0] + wd * v[1];
@@ -725,8 +781,10 @@ struct Up8 {
 // blocks at 640x368) and gives each CU more waves to hide LDS latency.
 constexpr int kFixSubFloats = kFixCi * (kFixPx + 2) + kFixCi * 4 + 7 * kFixCi * kFixCo;
 
-template <int PLANES, int KS>
+template <int PLANES, int KS, bool F32 = false>
 __global__ void __launch_bounds__(256 * KS) edge_fix_h8_kernel(EdgeFixArgs a) {
+  constexpr int CPR = F32 ? 4 : 8;            // channels per record
+  constexpr int GPC = kFixCi / CPR;           // record groups per ci chunk
   extern __shared__ __attribute__((aligned(16))) float s_fix[];
   const int ks = threadIdx.x >> 8;  // K group (wave-uniform)
   float* s_base = s_fix + ks * kFixSubFloats;
@@ -759,21 +817,25 @@ __global__ void __launch_bounds__(256 * KS) edge_fix_h8_kernel(EdgeFixArgs a) {
   const uint4* rlo = PLANES == 2 ? a.s_lo + (int64_t)img * a.s_img : nullptr;
 
   // per-thread staging work of one ci chunk, fetched one chunk ahead
-  constexpr int kItems = (kFixCi / 8) * (kFixPx + 2);  // U: record groups x line positions
-  static_assert(kItems <= 256, "one U item per thread");
-  Up8<PLANES> ru, rx;
+  constexpr int kItems = GPC * (kFixPx + 2);  // U: record groups x line positions
+  constexpr int kUIt = (kItems + 255) / 256;
+  Up8<PLANES, F32> ru[kUIt], rx;
   float4 rw[7];
-  const int u_gl = tid / (kFixPx + 2), u_j = tid - u_gl * (kFixPx + 2);
   const int w_ci = tid >> 3, w_cq = (tid & 7) * 4;
   auto fetch = [&](int c0) {
-    if (tid < kItems) {
-      const int q = min(max(pos0 - 1 + u_j, 0), full - 1);
-      if (c0 + u_gl * 8 < a.cin) ru.fetch(a, rhi, rlo, (c0 >> 3) + u_gl, row ? fixed : q, row ? q : fixed);
-      else ru.zero();
+#pragma unroll
+    for (int it = 0; it < kUIt; ++it) {
+      const int idx = tid + 256 * it;
+      if (idx < kItems) {
+        const int u_gl = idx / (kFixPx + 2), u_j = idx - u_gl * (kFixPx + 2);
+        const int q = min(max(pos0 - 1 + u_j, 0), full - 1);
+        if (c0 + u_gl * CPR < a.cin) ru[it].fetch(a, rhi, rlo, c0 / CPR + u_gl, row ? fixed : q, row ? q : fixed);
+        else ru[it].zero();
+      }
     }
-    if (corners && tid < 16) {  // 4 extra slots x 4 record groups
-      const int sl = tid >> 2, gl = tid & 3;
-      if (c0 + gl * 8 < a.cin) rx.fetch(a, rhi, rlo, (c0 >> 3) + gl, fixed + xky(sl) - 1, sl < 2 ? 0 : W - 1);
+    if (corners && tid < 4 * GPC) {  // 4 extra slots x GPC record groups
+      const int sl = tid / GPC, gl = tid % GPC;
+      if (c0 + gl * CPR < a.cin) rx.fetch(a, rhi, rlo, c0 / CPR + gl, fixed + xky(sl) - 1, sl < 2 ? 0 : W - 1);
       else rx.zero();
     }
     const bool ok = c0 + w_ci < a.cin && co0 + w_cq < a.cout;
@@ -787,12 +849,18 @@ __global__ void __launch_bounds__(256 * KS) edge_fix_h8_kernel(EdgeFixArgs a) {
     }
   };
   auto stage = [&]() {
-    if (tid < kItems)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) s_u[u_gl * 8 + e][u_j] = ru.value(e);
-    if (corners && tid < 16)
+    for (int it = 0; it < kUIt; ++it) {
+      const int idx = tid + 256 * it;
+      if (idx < kItems) {
+        const int u_gl = idx / (kFixPx + 2), u_j = idx - u_gl * (kFixPx + 2);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) s_ux[(tid & 3) * 8 + e][tid >> 2] = rx.value(e);
+        for (int e = 0; e < CPR; ++e) s_u[u_gl * CPR + e][u_j] = ru[it].value(e);
+      }
+    }
+    if (corners && tid < 4 * GPC)
+#pragma unroll
+      for (int e = 0; e < CPR; ++e) s_ux[(tid % GPC) * CPR + e][tid / GPC] = rx.value(e);
 #pragma unroll
     for (int sl = 0; sl < 7; ++sl)
       if (sl < nslot) *reinterpret_cast<float4*>(&s_w[sl][w_ci][w_cq]) = rw[sl];
@@ -855,11 +923,15 @@ __global__ void __launch_bounds__(256 * KS) edge_fix_h8_kernel(EdgeFixArgs a) {
     if (co >= a.cout) break;
     float v = (a.edge[((int64_t)img * a.cout + co) * a.ring + e] - acc[i]) + a.bias[co];
     if (a.leaky) v = v > 0.f ? v : v * a.slope;
-    const int64_t k = (((int64_t)img * a.d_img + (int64_t)(co >> 3) * a.d_gp + (int64_t)(Y + 1) * a.d_wp + X +
-                        kH8PadLeft) * 8) + (co & 7);
-    const _Float16 vh = (_Float16)v;
-    a.d_hi[k] = vh;
-    if constexpr (PLANES == 2) a.d_lo[k] = lo_of(v, vh);
+    const int64_t k = (((int64_t)img * a.d_img + (int64_t)(co / CPR) * a.d_gp + (int64_t)(Y + 1) * a.d_wp + X +
+                        kH8PadLeft) * CPR) + (co % CPR);
+    if constexpr (F32) {
+      a.d_f32[k] = v;
+    } else {
+      const _Float16 vh = (_Float16)v;
+      a.d_hi[k] = vh;
+      if constexpr (PLANES == 2) a.d_lo[k] = lo_of(v, vh);
+    }
   }
 }
 
@@ -949,6 +1021,8 @@ struct HeadH8Args {
   int64_t fr_img, fr_gp;
   int fr_wp;
   int h, w_, tiles_x, tiles_y;
+  uint4* g32;       // F32R: g16 as 4 records of 4 fp32 channels (g_img / g_gp / g_wp in records)
+  uint4* fr32;      // F32R: raw Flow output, 1 record (nullable)
 };
 
 template <int COUT, int MODE, int PLANES>
@@ -1192,6 +1266,282 @@ __global__ void flow_tblend_h8_kernel(const _Float16* __restrict__ fhi, const _F
   }
 }
 
+// ---- F32R (exact fp32, 4 channels per record) layout / glue kernels -----------------
+__device__ inline int64_t r32_elem_index(int64_t img_stride, int64_t gp, int wp, int img, int ch, int y, int x) {
+  return ((int64_t)img * img_stride + (int64_t)(ch >> 2) * gp + (int64_t)(y + 1) * wp + x + kH8PadLeft) * 4 +
+         (ch & 3);
+}
+__device__ inline uint4 f4rec(float a, float b, float c, float d) {
+  return make_uint4(__float_as_uint(a), __float_as_uint(b), __float_as_uint(c), __float_as_uint(d));
+}
+
+__global__ void nchw_to_r32_kernel(const float* __restrict__ src, float* dst, int64_t img_stride, int64_t gp, int wp,
+                                   int ch_off, int c, int h, int w, int64_t total) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int x = (int)(i % w);
+  int64_t t = i / w;
+  const int y = (int)(t % h);
+  t /= h;
+  const int ch = (int)(t % c);
+  const int n = (int)(t / c);
+  dst[r32_elem_index(img_stride, gp, wp, n, ch_off + ch, y, x)] = src[i];
+}
+
+__global__ void r32_to_nchw_kernel(const float* __restrict__ src, int64_t img_stride, int64_t gp, int wp, int ch_off,
+                                   float* dst, int c, int h, int w, int64_t total) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int x = (int)(i % w);
+  int64_t t = i / w;
+  const int y = (int)(t % h);
+  t /= h;
+  const int ch = (int)(t % c);
+  const int n = (int)(t / c);
+  dst[i] = src[r32_elem_index(img_stride, gp, wp, n, ch_off + ch, y, x)];
+}
+
+// x = cat(x0, x1) (model.py:33) into g16: record 0 = x0 0-2, x1 0; record 1 =
+// x1 1-2, 0, 0; records 2-3 zero (whole-record stores).
+__global__ void pack_g16_r32_kernel(const float* __restrict__ i0, const float* __restrict__ i1, uint4* g,
+                                    int64_t img_stride, int64_t gp, int wp, int h, int w, int64_t total) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int x = (int)(i % w);
+  const int64_t t = i / w;
+  const int y = (int)(t % h);
+  const int img = (int)(t / h);
+  const int64_t hw = (int64_t)h * w;
+  const int64_t px = (int64_t)img * 3 * hw + (int64_t)y * w + x;
+  const float a0 = i0[px], a1 = i0[px + hw], a2 = i0[px + 2 * hw];
+  const float b0 = i1[px], b1 = i1[px + hw], b2 = i1[px + 2 * hw];
+  const int64_t rec = (int64_t)img * img_stride + (int64_t)(y + 1) * wp + x + kH8PadLeft;
+  g[rec] = f4rec(a0, a1, a2, b0);
+  g[rec + gp] = f4rec(b1, b2, 0.f, 0.f);
+  g[rec + 2 * gp] = make_uint4(0u, 0u, 0u, 0u);
+  g[rec + 3 * gp] = make_uint4(0u, 0u, 0u, 0u);
+}
+
+// Ft0 / Ft1 (model.py:38-39) from a kept raw Flow record -> g16 channels 6-9
+__global__ void flow_tblend_r32_kernel(const uint4* __restrict__ fr, int64_t f_img, int f_wp, uint4* g, int64_t g_img,
+                                       int64_t g_gp, int g_wp, const float* coef, int h, int w, int64_t total) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int x = (int)(i % w);
+  const int64_t t = i / w;
+  const int y = (int)(t % h);
+  const int img = (int)(t / h);
+  const float* cf = coef + img * 8;
+  const floatx4 f = __builtin_bit_cast(floatx4, fr[(int64_t)img * f_img + (int64_t)(y + 1) * f_wp + x + kH8PadLeft]);
+  float o[4];
+  for (int k = 0; k < 2; ++k) {
+#pragma clang fp contract(off)
+    o[k] = cf[0] * f[k] + cf[1] * f[2 + k];
+    o[2 + k] = cf[2] * f[k] - cf[3] * f[2 + k];
+  }
+  const int64_t rec = (int64_t)img * g_img + (int64_t)(y + 1) * g_wp + x + kH8PadLeft;
+  const floatx4 r1 = __builtin_bit_cast(floatx4, g[rec + g_gp]);
+  const floatx4 r2 = __builtin_bit_cast(floatx4, g[rec + 2 * g_gp]);
+  g[rec + g_gp] = f4rec(r1[0], r1[1], o[0], o[1]);
+  g[rec + 2 * g_gp] = f4rec(o[2], o[3], r2[2], r2[3]);
+}
+
+// bilinear x2 (unet.py:77, align_corners=False, edge clamp) of fp32 records
+__global__ void up2x_r32_kernel(const uint4* __restrict__ s, int64_t s_img, int64_t s_gp, int s_wp, int sh, int sw,
+                                uint4* d, int64_t d_img, int64_t d_gp, int d_wp, int groups, int64_t total) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int w = 2 * sw, h = 2 * sh;
+  const int x = (int)(i % w);
+  int64_t t = i / w;
+  const int y = (int)(t % h);
+  t /= h;
+  const int g = (int)(t % groups);
+  const int img = (int)(t / groups);
+  int ra, rb, ca, cb;
+  float wa, wc;
+  if (y & 1) { ra = y >> 1; rb = min(ra + 1, sh - 1); wa = 0.75f; }
+  else { rb = y >> 1; ra = max(rb - 1, 0); wa = 0.25f; }
+  if (x & 1) { ca = x >> 1; cb = min(ca + 1, sw - 1); wc = 0.75f; }
+  else { cb = x >> 1; ca = max(cb - 1, 0); wc = 0.25f; }
+  const float wb = 1.0f - wa, wd = 1.0f - wc;
+  const int64_t base = img * s_img + g * s_gp + kH8PadLeft;
+  const floatx4 q0 = __builtin_bit_cast(floatx4, s[base + (int64_t)(ra + 1) * s_wp + ca]);
+  const floatx4 q1 = __builtin_bit_cast(floatx4, s[base + (int64_t)(ra + 1) * s_wp + cb]);
+  const floatx4 q2 = __builtin_bit_cast(floatx4, s[base + (int64_t)(rb + 1) * s_wp + ca]);
+  const floatx4 q3 = __builtin_bit_cast(floatx4, s[base + (int64_t)(rb + 1) * s_wp + cb]);
+  float o[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float top = wc * q0[e] + wd * q1[e];  // horizontal first (upsample_bilinear2d order)
+    const float bot = wc * q2[e] + wd * q3[e];
+    o[e] = wa * top + wb * bot;
+  }
+  d[img * d_img + g * d_gp + (int64_t)(y + 1) * d_wp + x + kH8PadLeft] = f4rec(o[0], o[1], o[2], o[3]);
+}
+
+// Head conv (Cout <= 4) + Net glue on fp32 records: as head_h8_kernel, with the
+// 32-channel input as 8 records of 4 channels and g16 as 4 records; every g16
+// update is a whole 16-B record (records the glue only partly changes are read
+// first), no partial-record writes.
+template <int COUT, int MODE>
+__global__ void __launch_bounds__(256) head_r32_kernel(HeadH8Args a) {
+  constexpr int CIN = 32, HROWS = 18, HLC = 40;
+  __shared__ __attribute__((aligned(16))) float s_in[8 * HROWS * HLC];
+  const int tid = threadIdx.x;
+  int bid = blockIdx.x;
+  const int tx = bid % a.tiles_x;
+  bid /= a.tiles_x;
+  const int ty = bid % a.tiles_y;
+  const int img = bid / a.tiles_y;
+  const int x0 = tx * 32, y0 = ty * 16;
+  const int r2 = 2 * (tid >> 5), xl = tid & 31;
+
+  float acc2[2][COUT];
+#pragma unroll
+  for (int co = 0; co < COUT; ++co) acc2[0][co] = acc2[1][co] = a.bias[co];
+  // records of rows y0-1..y0+16, cols x0-1..x0+32 of 8 channels (2 record groups),
+  // fetched one channel octet ahead into registers, then stored to planar LDS
+  constexpr int kRec = HROWS * H8_LC, kIt = (kRec + 255) / 256;
+  uint4 pre[kIt][2];
+  auto fetch = [&](int g8) {
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) {
+      const int idx = tid + 256 * it;
+      if (idx < kRec) {
+        const int rr = idx / H8_LC, col = idx - rr * H8_LC;
+        const int64_t rec = img * a.src_img + (int64_t)(2 * g8) * a.src_gp + (int64_t)(y0 + rr) * a.src_wp + x0 +
+                            (kH8PadLeft - 1) + col;
+        pre[it][0] = a.src_hi[rec];
+        pre[it][1] = a.src_hi[rec + a.src_gp];
+      }
+    }
+  };
+  fetch(0);
+  for (int g8 = 0; g8 < CIN / 8; ++g8) {
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) {
+      const int idx = tid + 256 * it;
+      if (idx < kRec) {
+        const int rr = idx / H8_LC, col = idx - rr * H8_LC;
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          s_in[(e * HROWS + rr) * HLC + col + 3] = __builtin_bit_cast(floatx4, pre[it][e >> 2])[e & 3];
+      }
+    }
+    __syncthreads();
+    if (g8 + 1 < CIN / 8) fetch(g8 + 1);
+#pragma unroll
+    for (int ci = 0; ci < 8; ++ci) {
+      float rows[4][3];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) rows[k][kx] = s_in[(ci * HROWS + r2 + k) * HLC + xl + 3 + kx];
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+          for (int co = 0; co < COUT; ++co) {
+            const float w = a.w[((co * CIN) + g8 * 8 + ci) * 9 + ky * 3 + kx];
+            acc2[0][co] = fmaf(w, rows[ky][kx], acc2[0][co]);
+            acc2[1][co] = fmaf(w, rows[ky + 1][kx], acc2[1][co]);
+          }
+    }
+    __syncthreads();
+  }
+
+  for (int p = 0; p < 2; ++p) {
+    float acc[COUT];
+#pragma unroll
+    for (int co = 0; co < COUT; ++co) acc[co] = acc2[p][co];
+    const int y = y0 + r2 + p, x = x0 + xl;
+    if (y >= a.h || x >= a.w_) continue;
+    const int64_t rec0 = img * a.g_img + (int64_t)(y + 1) * a.g_wp + x + kH8PadLeft;
+    auto ld = [&](int k) { return __builtin_bit_cast(floatx4, a.g32[rec0 + k * a.g_gp]); };
+    auto st = [&](int k, float v0, float v1, float v2, float v3) { a.g32[rec0 + k * a.g_gp] = f4rec(v0, v1, v2, v3); };
+    const float* cf = a.coef + img * 8;
+    if constexpr (MODE == RRIN_HEAD_PLAIN) {
+      float* gf = reinterpret_cast<float*>(a.g32);
+      for (int co = 0; co < COUT; ++co) gf[r32_elem_index(a.g_img, a.g_gp, a.g_wp, img, co, y, x)] = acc[co];
+    } else if constexpr (MODE == RRIN_HEAD_FLOW) {
+#pragma clang fp contract(off)
+      if (a.fr32) a.fr32[img * a.fr_img + (int64_t)(y + 1) * a.fr_wp + x + kH8PadLeft] = f4rec(acc[0], acc[1], acc[2], acc[3]);
+      float f0[2], f1[2];
+      for (int k = 0; k < 2; ++k) {
+        f0[k] = cf[0] * acc[k] + cf[1] * acc[2 + k];
+        f1[k] = cf[2] * acc[k] - cf[3] * acc[2 + k];
+      }
+      const floatx4 r1 = ld(1), r2v = ld(2);
+      st(1, r1[0], r1[1], f0[0], f0[1]);
+      st(2, f1[0], f1[1], r2v[2], r2v[3]);
+    } else if constexpr (MODE == RRIN_HEAD_REFINE) {
+#pragma clang fp contract(off)
+      const floatx4 q0 = ld(0), q1 = ld(1), q2 = ld(2);
+      const float f0[2] = {q1[2] + acc[0], q1[3] + acc[1]};
+      float o1[8];
+      o1[0] = q2[0] + acc[2];
+      o1[1] = q2[1] + acc[3];
+      const WarpTaps t0 = warp_taps(x, y, f0[0], f0[1], a.h, a.w_);
+      const WarpTaps t1 = warp_taps(x, y, o1[0], o1[1], a.h, a.w_);
+      // backwarp x0 (ch 0-2) with Ft0 and x1 (ch 3-5) with Ft1: records 0-1 per tap
+      auto warp3 = [&](const WarpTaps& t, int c0, float* o) {
+        float q[4][8];
+        const bool ok[4] = {t.vy0 && t.vx0, t.vy0 && t.vx1, t.vy1 && t.vx0, t.vy1 && t.vx1};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (ok[k]) {
+            const int64_t r = img * a.g_img + (int64_t)(t.y0 + (k >> 1) + 1) * a.g_wp + t.x0 + (k & 1) + kH8PadLeft;
+            const floatx4 lo = __builtin_bit_cast(floatx4, a.g32[r]);
+            const floatx4 hi = __builtin_bit_cast(floatx4, a.g32[r + a.g_gp]);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              q[k][e] = lo[e];
+              q[k][4 + e] = hi[e];
+            }
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) q[k][e] = 0.0f;
+          }
+        }
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+          o[c] = q[0][c0 + c] * t.nw + q[1][c0 + c] * t.ne + q[2][c0 + c] * t.sw + q[3][c0 + c] * t.se;
+      };
+      warp3(t0, 0, o1 + 2);
+      warp3(t1, 3, o1 + 5);
+      (void)q0;
+      st(1, q1[0], q1[1], f0[0], f0[1]);
+      st(2, o1[0], o1[1], o1[2], o1[3]);
+      st(3, o1[4], o1[5], o1[6], o1[7]);
+    } else if constexpr (MODE == RRIN_HEAD_MASK) {
+#pragma clang fp contract(off)
+      const floatx4 r1 = ld(1), r2v = ld(2), r3 = ld(3);
+      const float g1[8] = {r2v[0], r2v[1], r2v[2], r2v[3], r3[0], r3[1], r3[2], r3[3]};  // ch 8-15
+      const float m0 = 1.0f / (1.0f + expf(-acc[0]));
+      const float m1 = 1.0f / (1.0f + expf(-acc[1]));
+      const float w1 = cf[4] * m0, w2 = cf[5] * m1;
+      const float den = w1 + w2 + 1e-8f;
+      float o[3];
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch) o[ch] = (w1 * g1[2 + ch] + w2 * g1[5 + ch]) / den;
+      st(1, r1[0], r1[1], o[0], o[1]);
+      st(2, o[2], r2v[1], r2v[2], r2v[3]);
+    } else {  // FINAL
+#pragma clang fp contract(off)
+      const floatx4 r1 = ld(1), r2v = ld(2);
+      const float base[3] = {r1[2], r1[3], r2v[0]};
+      float* o = a.out + ((int64_t)img * 3) * a.h * a.w_ + (int64_t)y * a.w_ + x;
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch) {
+        const float v = acc[ch] + base[ch];
+        o[(int64_t)ch * a.h * a.w_] = v < 0.0f ? 0.0f : (v > 1.0f ? 1.0f : v);
+      }
+    }
+  }
+}
+
 // ---- host helpers ------------------------------------------------------------------
 // fp32 -> fp16 bits, round to nearest even (host packing).
 static uint16_t f2h_rne(float f) {
@@ -1289,10 +1639,10 @@ static int num_cus() {
   return n[dev];
 }
 
-template <int NW, int WM, int WN, int PLANES, int EPI, bool DMA, int SCHED>
+template <int NW, int WM, int WN, int PLANES, int EPI, bool DMA, int SCHED, bool F32 = false>
 static int launch_h8_k(const ConvH8Args& args, int persist, hipStream_t st) {
   using T = TileH8<NW, WM, WN, PLANES>;
-  auto k = conv3x3_h8_kernel<NW, WM, WN, PLANES, EPI, DMA, SCHED>;
+  auto k = conv3x3_h8_kernel<NW, WM, WN, PLANES, EPI, DMA, SCHED, F32>;
   constexpr bool wres = DMA && (SCHED & SCHED_WRES) != 0;
   const size_t lds = h8_lds_bytes<NW, WM, WN, PLANES>(wres, args.nchunks);
   if (lds > kMaxLds) return RRIN_E_CONFIG;
@@ -1321,24 +1671,34 @@ static int launch_h8_k(const ConvH8Args& args, int persist, hipStream_t st) {
   return hip_code(hipGetLastError());
 }
 
-template <int NW, int WM, int WN, int PLANES, int EPI, int SCHED>
+template <int NW, int WM, int WN, int PLANES, int EPI, int SCHED, bool F32 = false>
 static int launch_h8_t(const ConvH8Args& args, int persist, hipStream_t st) {
   using T = TileH8<NW, WM, WN, PLANES>;
   if constexpr (T::LDS > kMaxLds) {
     return RRIN_E_CONFIG;
   } else {
     if (args.cin % 8 == 0 || args.tail_finite)
-      return launch_h8_k<NW, WM, WN, PLANES, EPI, true, SCHED>(args, persist, st);
+      return launch_h8_k<NW, WM, WN, PLANES, EPI, true, SCHED, F32>(args, persist, st);
     if constexpr (EPI == RRIN_EPI_LEAKY_REP || EPI == RRIN_EPI_SUBPIXEL) {
       return RRIN_E_CONFIG;  // decoder-side modes: always whole channel groups
     } else {
-      return launch_h8_k<NW, WM, WN, PLANES, EPI, false, 0>(args, persist, st);  // knobs need DMA
+      return launch_h8_k<NW, WM, WN, PLANES, EPI, false, 0, F32>(args, persist, st);  // knobs need DMA
     }
   }
 }
 
 template <int NW, int WM, int WN, int SCHED>
-static int launch_h8_cfg(const ConvH8Args& args, int planes, int epi, int persist, hipStream_t st) {
+static int launch_h8_cfg(const ConvH8Args& args, int prec, int epi, int persist, hipStream_t st) {
+  const int planes = prec == RRIN_PREC_F16X3 ? 2 : 1;
+  if (prec == RRIN_PREC_F32R) {
+    switch (epi) {
+      case RRIN_EPI_LINEAR: return launch_h8_t<NW, WM, WN, 1, RRIN_EPI_LINEAR, SCHED, true>(args, persist, st);
+      case RRIN_EPI_LEAKY: return launch_h8_t<NW, WM, WN, 1, RRIN_EPI_LEAKY, SCHED, true>(args, persist, st);
+      case RRIN_EPI_LEAKY_POOL: return launch_h8_t<NW, WM, WN, 1, RRIN_EPI_LEAKY_POOL, SCHED, true>(args, persist, st);
+      case RRIN_EPI_LEAKY_REP: return launch_h8_t<NW, WM, WN, 1, RRIN_EPI_LEAKY_REP, SCHED, true>(args, persist, st);
+      default: return launch_h8_t<NW, WM, WN, 1, RRIN_EPI_SUBPIXEL, SCHED, true>(args, persist, st);
+    }
+  }
   if (planes == 2) {
     switch (epi) {
       case RRIN_EPI_LINEAR: return launch_h8_t<NW, WM, WN, 2, RRIN_EPI_LINEAR, SCHED>(args, persist, st);
@@ -1359,6 +1719,7 @@ static int launch_h8_cfg(const ConvH8Args& args, int planes, int epi, int persis
 
 static bool h8_ok(const rrin_h8& v, int prec) {
   if (!v.hi || (prec == RRIN_PREC_F16X3 && !v.lo)) return false;
+  if (prec == RRIN_PREC_F32R && v.lo) return false;  // one plane
   const rrin_geom g = make_geom_h8(v.g.h, v.g.w);
   return g.hp == v.g.hp && g.wp == v.g.wp && g.plane == v.g.plane;
 }
@@ -1368,11 +1729,16 @@ static inline int64_t ring_pixels(int h, int w) {
 }
 
 static inline int planes_of(int prec) { return prec == RRIN_PREC_F16X3 ? 2 : 1; }
+// record-layout precisions: F16X3 / F16 (8 halves per record), F32R (4 floats)
+static inline bool rec_prec(int prec) {
+  return prec == RRIN_PREC_F16X3 || prec == RRIN_PREC_F16 || prec == RRIN_PREC_F32R;
+}
+static inline int chans_per_rec(int prec) { return prec == RRIN_PREC_F32R ? 4 : 8; }
 
 // Validate a conv descriptor and turn it into kernel arguments.
 static int h8_prepare(const rrin_conv_h8_desc* d, ConvH8Args& a) {
   if (!d || !d->whi || !d->bias) return RRIN_E_ARG;
-  if (d->prec != RRIN_PREC_F16X3 && d->prec != RRIN_PREC_F16) return RRIN_E_ARG;
+  if (!rec_prec(d->prec)) return RRIN_E_ARG;
   if (d->prec == RRIN_PREC_F16X3 && !d->wlo) return RRIN_E_ARG;
   if (d->cfg < 0 || d->cfg >= kNumCfgH8 ||
       (planes_of(d->prec) == 2 ? kCfgH8[d->cfg].lds2 : kCfgH8[d->cfg].lds1) > kMaxLds)
@@ -1383,13 +1749,14 @@ static int h8_prepare(const rrin_conv_h8_desc* d, ConvH8Args& a) {
   const bool sub = d->epi_mode == RRIN_EPI_SUBPIXEL;
   const int h = d->src.g.h, w = d->src.g.w;  // the grid the conv runs on
   if (d->dst.g.h != (sub ? 2 * h : h) || d->dst.g.w != (sub ? 2 * w : w)) return RRIN_E_SHAPE;
-  if (d->cin > 8 * d->src.groups || (sub ? d->cout / 4 : d->cout) > 8 * d->dst.groups) return RRIN_E_ARG;
+  const int cpr = chans_per_rec(d->prec);
+  if (d->cin > cpr * d->src.groups || (sub ? d->cout / 4 : d->cout) > cpr * d->dst.groups) return RRIN_E_ARG;
   if (sub && ((d->cout & 31) || !d->edge)) return RRIN_E_ARG;
   if (!(d->slope >= 0.f && d->slope <= 1.f)) return RRIN_E_ARG;  // leaky() as max(t, slope t)
   if (d->epi_mode == RRIN_EPI_LEAKY_POOL) {
     if (!kCfgH8[d->cfg].pool_ok) return RRIN_E_CONFIG;  // a wave must own both rows of a pool pair
     if (!h8_ok(d->pool, d->prec) || (h & 1) || (w & 1) || d->pool.g.h * 2 != h || d->pool.g.w * 2 != w ||
-        d->cout > 8 * d->pool.groups)
+        d->cout > cpr * d->pool.groups)
       return RRIN_E_SHAPE;
   }
   const int planes = planes_of(d->prec);
@@ -1402,7 +1769,7 @@ static int h8_prepare(const rrin_conv_h8_desc* d, ConvH8Args& a) {
   a.src_gp = d->src.g.plane;
   a.src_wp = d->src.g.wp;
   a.cin = d->cin;
-  a.nchunks = (d->cin + 15) / 16;
+  a.nchunks = (d->cin + 2 * cpr - 1) / (2 * cpr);  // 2 record groups per chunk
   const int64_t dg = (int64_t)d->dst.g_off * d->dst.g.plane;
   a.dst_hi = static_cast<uint4*>(d->dst.hi) + dg;
   a.dst_lo = planes == 2 ? static_cast<uint4*>(d->dst.lo) + dg : nullptr;
@@ -1421,7 +1788,7 @@ static int h8_prepare(const rrin_conv_h8_desc* d, ConvH8Args& a) {
   a.w_hi = static_cast<const uint4*>(d->whi);
   a.w_lo = planes == 2 ? static_cast<const uint4*>(d->wlo) : nullptr;
   a.bias = d->bias;
-  a.inv_wscale = d->inv_wscale;
+  a.inv_wscale = d->prec == RRIN_PREC_F32R ? 1.0f : d->inv_wscale;
   a.slope = d->slope;
   a.tail_finite = d->tail_finite;
   a.h = h;
@@ -1457,14 +1824,14 @@ extern "C" int rrin_conv_h8_cfg_th(int32_t cfg) {
 }
 extern "C" int rrin_conv_h8_cfg_ok(int32_t cfg, int32_t prec) {
   if (cfg < 0 || cfg >= kNumCfgH8) return 0;
-  if (prec != RRIN_PREC_F16X3 && prec != RRIN_PREC_F16) return 0;
+  if (!rec_prec(prec)) return 0;
   return (planes_of(prec) == 2 ? kCfgH8[cfg].lds2 : kCfgH8[cfg].lds1) <= kMaxLds ? 1 : 0;
 }
 
 extern "C" int rrin_conv_h8_cfg_fits(int32_t cfg, int32_t prec, int32_t cin) {
   if (!rrin_conv_h8_cfg_ok(cfg, prec) || cin < 1) return 0;
   const CfgH8& c = kCfgH8[cfg];
-  const int nch = (cin + 15) / 16;
+  const int nch = (cin + 2 * chans_per_rec(prec) - 1) / (2 * chans_per_rec(prec));
   if (!(c.sched & SCHED_WRES) || nch <= 2) return 1;
   const int planes = planes_of(prec);
   const size_t lds = (planes == 2 ? c.lds2 : c.lds1) + (size_t)(nch - 2) * c.wslab * planes;
@@ -1475,12 +1842,11 @@ extern "C" int rrin_conv3x3_h8_fwd(const rrin_conv_h8_desc* d, void* stream) {
   ConvH8Args a;
   const int rc = h8_prepare(d, a);
   if (rc) return rc;
-  const int planes = planes_of(d->prec);
   hipStream_t st = (hipStream_t)stream;
   switch (d->cfg) {
 #define X(id, nw, wm, wn, sc, pe) \
   case id:                        \
-    return launch_h8_cfg<nw, wm, wn, sc>(a, planes, d->epi_mode, pe, st);
+    return launch_h8_cfg<nw, wm, wn, sc>(a, d->prec, d->epi_mode, pe, st);
     RRIN_H8_CFGS(X)
 #undef X
   }
@@ -1491,28 +1857,45 @@ extern "C" int rrin_conv3x3_h8_fwd(const rrin_conv_h8_desc* d, void* stream) {
 // Kernel lab (tools/conv_lab.py ablate; built only into librrin_lab.so, `make
 // lab`): one F16X3 LEAKY conv of tile config cfg 0, 1 or 6 with the schedule
 // knobs `sched` (SCHED_*, ablations included) and grid `persist` (as PE).
-template <int NW, int WM, int WN>
+template <int NW, int WM, int WN, bool F32>
 static int lab_cfg(const ConvH8Args& a, int sched, int persist, hipStream_t st) {
+  constexpr int P = F32 ? 1 : 2;
   switch (sched) {
 #define L(v) \
   case v:    \
-    return launch_h8_k<NW, WM, WN, 2, RRIN_EPI_LEAKY, true, v>(a, persist, st);
-    L(0) L(1) L(2) L(3) L(4) L(7) L(8) L(16) L(32) L(48) L(64) L(96) L(128) L(144)
+    return launch_h8_k<NW, WM, WN, P, RRIN_EPI_LEAKY, true, v, F32>(a, persist, st);
+    L(0) L(1) L(2) L(3) L(4) L(7) L(8) L(11) L(12) L(15) L(16) L(32) L(48) L(64) L(96) L(128) L(144)
 #undef L
   }
   return RRIN_E_CONFIG;
 }
 
+// F16X3 (cfg 0, 1, 6) or F32R (cfg 0, 1, 3, 4, 5, 6, 16) LEAKY conv with schedule bits
 extern "C" int rrin_conv3x3_h8_lab(const rrin_conv_h8_desc* d, int32_t sched, int32_t persist, void* stream) {
-  if (!d || d->prec != RRIN_PREC_F16X3 || d->epi_mode != RRIN_EPI_LEAKY || (d->cin % 8)) return RRIN_E_ARG;
+  if (!d || (d->prec != RRIN_PREC_F16X3 && d->prec != RRIN_PREC_F32R) || d->epi_mode != RRIN_EPI_LEAKY ||
+      (d->cin % 8))
+    return RRIN_E_ARG;
+  if (d->prec == RRIN_PREC_F32R && (sched & SCHED_MFMA16)) return RRIN_E_CONFIG;
   ConvH8Args a;
   const int rc = h8_prepare(d, a);
   if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;
+  if (d->prec == RRIN_PREC_F32R) {
+    switch (d->cfg) {
+      case 0: return lab_cfg<8, 2, 2, true>(a, sched, persist, st);
+      case 1: return lab_cfg<8, 1, 2, true>(a, sched, persist, st);
+      case 3: return lab_cfg<4, 1, 4, true>(a, sched, persist, st);
+      case 4: return lab_cfg<4, 2, 1, true>(a, sched, persist, st);
+      case 5: return lab_cfg<8, 4, 2, true>(a, sched, persist, st);
+      case 6: return lab_cfg<4, 1, 2, true>(a, sched, persist, st);
+      case 16: return lab_cfg<4, 1, 1, true>(a, sched, persist, st);
+    }
+    return RRIN_E_CONFIG;
+  }
   switch (d->cfg) {
-    case 0: return lab_cfg<8, 2, 2>(a, sched, persist, st);
-    case 1: return lab_cfg<8, 1, 2>(a, sched, persist, st);
-    case 6: return lab_cfg<4, 1, 2>(a, sched, persist, st);
+    case 0: return lab_cfg<8, 2, 2, false>(a, sched, persist, st);
+    case 1: return lab_cfg<8, 1, 2, false>(a, sched, persist, st);
+    case 6: return lab_cfg<4, 1, 2, false>(a, sched, persist, st);
   }
   return RRIN_E_CONFIG;
 }
@@ -1565,6 +1948,33 @@ extern "C" int rrin_pack_conv3x3_h8(const float* w, const float* b, int32_t cout
   return 0;
 }
 
+extern "C" int64_t rrin_pack_conv3x3_r32_floats(int32_t cout, int32_t cin, int32_t bm) {
+  if (cout < 1 || cin < 1 || bm < 32 || bm % 32) return RRIN_E_ARG;
+  const int64_t cob = (cout + bm - 1) / bm, nch = (cin + 7) / 8;
+  return cob * nch * 9 * 2 * bm * 4;
+}
+
+extern "C" int rrin_pack_conv3x3_r32(const float* w, const float* b, int32_t cout, int32_t cin, int32_t bm,
+                                     const int32_t* perm, float* wpack, float* bpack) {
+  if (!w || !b || !wpack || !bpack || cout < 1 || cin < 1 || bm < 32 || bm % 32) return RRIN_E_ARG;
+  if (perm)
+    for (int c = 0; c < cin; ++c)
+      if (perm[c] < 0 || perm[c] >= cin) return RRIN_E_ARG;
+  const int cob_n = (cout + bm - 1) / bm, nch = (cin + 7) / 8;
+  int64_t o = 0;
+  for (int cob = 0; cob < cob_n; ++cob)
+    for (int c = 0; c < nch; ++c)
+      for (int tap = 0; tap < 9; ++tap)
+        for (int hh = 0; hh < 2; ++hh)
+          for (int col = 0; col < bm; ++col)
+            for (int e = 0; e < 4; ++e) {
+              const int co = cob * bm + col, ch = c * 8 + hh * 4 + e;
+              wpack[o++] = (co < cout && ch < cin) ? w[((int64_t)co * cin + (perm ? perm[ch] : ch)) * 9 + tap] : 0.f;
+            }
+  for (int co = 0; co < cob_n * bm; ++co) bpack[co] = co < cout ? b[co] : 0.f;
+  return 0;
+}
+
 extern "C" int64_t rrin_ring_pixels(int32_t h, int32_t w) {
   if (h < 1 || w < 1) return RRIN_E_ARG;
   return ring_pixels(h, w);
@@ -1597,30 +2007,31 @@ extern "C" int rrin_subpixel_weights(const float* w, const float* b, int32_t cou
   return 0;
 }
 
-template <int PLANES, int KS>
+template <int PLANES, int KS, bool F32 = false>
 static int edge_fix_launch(const EdgeFixArgs& a, dim3 grid, hipStream_t st) {
   constexpr size_t lds = (size_t)KS * kFixSubFloats * sizeof(float);
   static_assert(lds <= 160 * 1024, "edge fix LDS");
   static_assert(kFixSubFloats >= 4 * 256, "K-group sums fit a staging region");
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)edge_fix_h8_kernel<PLANES, KS>,
+    hipError_t e = hipFuncSetAttribute((const void*)edge_fix_h8_kernel<PLANES, KS, F32>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return (int)e;
     attr_set = true;
   }
-  hipLaunchKernelGGL((edge_fix_h8_kernel<PLANES, KS>), grid, dim3(256 * KS), lds, st, a);
+  hipLaunchKernelGGL((edge_fix_h8_kernel<PLANES, KS, F32>), grid, dim3(256 * KS), lds, st, a);
   return hip_code(hipGetLastError());
 }
 
 extern "C" int rrin_subpixel_edge_fix_h8(const rrin_edge_fix_desc* d, void* stream) {
   if (!d || !d->edge || !d->wedge || !d->bias) return RRIN_E_ARG;
-  if (d->prec != RRIN_PREC_F16X3 && d->prec != RRIN_PREC_F16) return RRIN_E_ARG;
+  if (!rec_prec(d->prec)) return RRIN_E_ARG;
   if (d->n < 1 || d->cin < 8 || (d->cin & 7) || d->cout < 8 || (d->cout & 7)) return RRIN_E_ARG;
   if (d->epi_mode != RRIN_EPI_LINEAR && d->epi_mode != RRIN_EPI_LEAKY) return RRIN_E_ARG;
   if (!h8_ok(d->src, d->prec) || !h8_ok(d->dst, d->prec)) return RRIN_E_SHAPE;
   if (d->dst.g.h != 2 * d->src.g.h || d->dst.g.w != 2 * d->src.g.w) return RRIN_E_SHAPE;
-  if (d->cin > 8 * d->src.groups || d->cout > 8 * d->dst.groups) return RRIN_E_ARG;
+  const int cpr = chans_per_rec(d->prec);
+  if (d->cin > cpr * d->src.groups || d->cout > cpr * d->dst.groups) return RRIN_E_ARG;
   const int planes = planes_of(d->prec);
   EdgeFixArgs a;
   memset(&a, 0, sizeof(a));
@@ -1633,8 +2044,12 @@ extern "C" int rrin_subpixel_edge_fix_h8(const rrin_edge_fix_desc* d, void* stre
   a.sh = d->src.g.h;
   a.sw = d->src.g.w;
   a.cin = d->cin;
-  a.d_hi = static_cast<_Float16*>(d->dst.hi) + dg * 8;
-  a.d_lo = planes == 2 ? static_cast<_Float16*>(d->dst.lo) + dg * 8 : nullptr;
+  if (d->prec == RRIN_PREC_F32R) {
+    a.d_f32 = static_cast<float*>(d->dst.hi) + dg * 4;
+  } else {
+    a.d_hi = static_cast<_Float16*>(d->dst.hi) + dg * 8;
+    a.d_lo = planes == 2 ? static_cast<_Float16*>(d->dst.lo) + dg * 8 : nullptr;
+  }
   a.d_img = d->dst.img_stride;
   a.d_gp = d->dst.g.plane;
   a.d_wp = d->dst.g.wp;
@@ -1656,6 +2071,13 @@ extern "C" int rrin_subpixel_edge_fix_h8(const rrin_edge_fix_desc* d, void* stre
   int ks = d->cin % (2 * kFixCi) == 0 && d->cin >= 4 * kFixCi ? 2 : 1;
   if (planes == 1 && d->cin % (4 * kFixCi) == 0 && d->cin >= 8 * kFixCi) ks = 4;
   hipStream_t st = (hipStream_t)stream;
+  if (d->prec == RRIN_PREC_F32R) {
+    switch (ks) {
+      case 4: return edge_fix_launch<1, 4, true>(a, grid, st);
+      case 2: return edge_fix_launch<1, 2, true>(a, grid, st);
+      default: return edge_fix_launch<1, 1, true>(a, grid, st);
+    }
+  }
   switch (planes * 8 + ks) {
     case 2 * 8 + 2: return edge_fix_launch<2, 2>(a, grid, st);
     case 2 * 8 + 1: return edge_fix_launch<2, 1>(a, grid, st);
@@ -1666,7 +2088,7 @@ extern "C" int rrin_subpixel_edge_fix_h8(const rrin_edge_fix_desc* d, void* stre
 }
 
 extern "C" int rrin_upsample2x_h8(const rrin_h8* src, const rrin_h8* dst, int32_t n, int32_t prec, void* stream) {
-  if (!src || !dst || n < 1 || (prec != RRIN_PREC_F16X3 && prec != RRIN_PREC_F16)) return RRIN_E_ARG;
+  if (!src || !dst || n < 1 || !rec_prec(prec)) return RRIN_E_ARG;
   if (!h8_ok(*src, prec) || !h8_ok(*dst, prec)) return RRIN_E_SHAPE;
   if (dst->g.h != 2 * src->g.h || dst->g.w != 2 * src->g.w || dst->groups < src->groups) return RRIN_E_SHAPE;
   const int64_t total = (int64_t)n * src->groups * dst->g.h * dst->g.w;
@@ -1675,7 +2097,10 @@ extern "C" int rrin_upsample2x_h8(const rrin_h8* src, const rrin_h8* dst, int32_
   const uint4* shi = static_cast<const uint4*>(src->hi) + so;
   uint4* dhi = static_cast<uint4*>(dst->hi) + dof;
   hipStream_t st = (hipStream_t)stream;
-  if (planes_of(prec) == 2) {
+  if (prec == RRIN_PREC_F32R) {
+    hipLaunchKernelGGL(up2x_r32_kernel, dim3(grid), dim3(256), 0, st, shi, src->img_stride, src->g.plane, src->g.wp,
+                       src->g.h, src->g.w, dhi, dst->img_stride, dst->g.plane, dst->g.wp, src->groups, total);
+  } else if (planes_of(prec) == 2) {
     hipLaunchKernelGGL(up2x_h8_kernel<2>, dim3(grid), dim3(256), 0, st, shi,
                        static_cast<const uint4*>(src->lo) + so, src->img_stride, src->g.plane, src->g.wp, src->g.h,
                        src->g.w, dhi, static_cast<uint4*>(dst->lo) + dof, dst->img_stride, dst->g.plane, dst->g.wp,
@@ -1690,11 +2115,17 @@ extern "C" int rrin_upsample2x_h8(const rrin_h8* src, const rrin_h8* dst, int32_
 
 extern "C" int rrin_nchw_to_h8(const float* src, int32_t n, int32_t c, int32_t ch_off, const rrin_h8* dst,
                                int32_t prec, void* stream) {
-  if (!src || !dst || n < 1 || c < 1 || ch_off < 0 || ch_off + c > 8 * dst->groups) return RRIN_E_ARG;
-  if (prec != RRIN_PREC_F16X3 && prec != RRIN_PREC_F16) return RRIN_E_ARG;
+  if (!src || !dst || n < 1 || c < 1 || ch_off < 0 || !rec_prec(prec)) return RRIN_E_ARG;
+  if (ch_off + c > chans_per_rec(prec) * dst->groups) return RRIN_E_ARG;
   if (!h8_ok(*dst, prec)) return RRIN_E_SHAPE;
   const int64_t total = (int64_t)n * c * dst->g.h * dst->g.w;
   const int grid = (int)((total + 255) / 256);
+  if (prec == RRIN_PREC_F32R) {
+    hipLaunchKernelGGL(nchw_to_r32_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, src,
+                       static_cast<float*>(dst->hi) + (int64_t)dst->g_off * dst->g.plane * 4, dst->img_stride,
+                       dst->g.plane, dst->g.wp, ch_off, c, dst->g.h, dst->g.w, total);
+    return hip_code(hipGetLastError());
+  }
   const int64_t go = (int64_t)dst->g_off * dst->g.plane * 8;
   hipLaunchKernelGGL(nchw_to_h8_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, src,
                      static_cast<_Float16*>(dst->hi) + go,
@@ -1705,11 +2136,17 @@ extern "C" int rrin_nchw_to_h8(const float* src, int32_t n, int32_t c, int32_t c
 
 extern "C" int rrin_h8_to_nchw(const rrin_h8* src, int32_t n, int32_t c, int32_t ch_off, float* dst, int32_t prec,
                                void* stream) {
-  if (!src || !dst || n < 1 || c < 1 || ch_off < 0 || ch_off + c > 8 * src->groups) return RRIN_E_ARG;
-  if (prec != RRIN_PREC_F16X3 && prec != RRIN_PREC_F16) return RRIN_E_ARG;
+  if (!src || !dst || n < 1 || c < 1 || ch_off < 0 || !rec_prec(prec)) return RRIN_E_ARG;
+  if (ch_off + c > chans_per_rec(prec) * src->groups) return RRIN_E_ARG;
   if (!h8_ok(*src, prec)) return RRIN_E_SHAPE;
   const int64_t total = (int64_t)n * c * src->g.h * src->g.w;
   const int grid = (int)((total + 255) / 256);
+  if (prec == RRIN_PREC_F32R) {
+    hipLaunchKernelGGL(r32_to_nchw_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                       static_cast<const float*>(src->hi) + (int64_t)src->g_off * src->g.plane * 4, src->img_stride,
+                       src->g.plane, src->g.wp, ch_off, dst, c, src->g.h, src->g.w, total);
+    return hip_code(hipGetLastError());
+  }
   const int64_t go = (int64_t)src->g_off * src->g.plane * 8;
   hipLaunchKernelGGL(h8_to_nchw_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream,
                      static_cast<const _Float16*>(src->hi) + go,
@@ -1720,7 +2157,9 @@ extern "C" int rrin_h8_to_nchw(const rrin_h8* src, int32_t n, int32_t c, int32_t
 
 template <int COUT, int MODE>
 static int head_h8_launch(const HeadH8Args& a, int planes, int grid, hipStream_t st) {
-  if (planes == 2)
+  if (planes == 0)  // F32R
+    hipLaunchKernelGGL((head_r32_kernel<COUT, MODE>), dim3(grid), dim3(256), 0, st, a);
+  else if (planes == 2)
     hipLaunchKernelGGL((head_h8_kernel<COUT, MODE, 2>), dim3(grid), dim3(256), 0, st, a);
   else
     hipLaunchKernelGGL((head_h8_kernel<COUT, MODE, 1>), dim3(grid), dim3(256), 0, st, a);
@@ -1730,13 +2169,14 @@ static int head_h8_launch(const HeadH8Args& a, int planes, int grid, hipStream_t
 // Validate a head descriptor and turn it into kernel arguments (grid: blocks).
 static int head_prepare(const rrin_head_h8_desc* d, HeadH8Args& a, int& grid) {
   if (!d || !d->w || !d->bias || d->cin != 32 || d->n < 1) return RRIN_E_ARG;
-  if (d->prec != RRIN_PREC_F16X3 && d->prec != RRIN_PREC_F16) return RRIN_E_ARG;
+  if (!rec_prec(d->prec)) return RRIN_E_ARG;
   if (!h8_ok(d->src, d->prec) || !h8_ok(d->g16, d->prec)) return RRIN_E_SHAPE;
   const int h = d->src.g.h, w = d->src.g.w;
-  if (d->g16.g.h != h || d->g16.g.w != w || d->src.groups < 4) return RRIN_E_SHAPE;
+  const int cpr = chans_per_rec(d->prec);
+  if (d->g16.g.h != h || d->g16.g.w != w || d->src.groups * cpr < 32) return RRIN_E_SHAPE;
   if (d->mode != RRIN_HEAD_PLAIN) {
-    if (d->g16.groups < 2 || d->g16.g_off != 0 || !d->coef) return RRIN_E_ARG;
-  } else if (8 * d->g16.groups < d->cout) {
+    if (d->g16.groups * cpr < 16 || d->g16.g_off != 0 || !d->coef) return RRIN_E_ARG;
+  } else if (cpr * d->g16.groups < d->cout) {
     return RRIN_E_ARG;
   }
   if (d->mode == RRIN_HEAD_FINAL && !d->out) return RRIN_E_ARG;
@@ -1749,8 +2189,12 @@ static int head_prepare(const rrin_head_h8_desc* d, HeadH8Args& a, int& grid) {
   a.src_gp = d->src.g.plane;
   a.src_wp = d->src.g.wp;
   const int64_t gg = (int64_t)d->g16.g_off * d->g16.g.plane * 8;
-  a.g_hi = static_cast<_Float16*>(d->g16.hi) + gg;
-  a.g_lo = planes == 2 ? static_cast<_Float16*>(d->g16.lo) + gg : nullptr;
+  if (d->prec == RRIN_PREC_F32R) {
+    a.g32 = static_cast<uint4*>(d->g16.hi) + (int64_t)d->g16.g_off * d->g16.g.plane;
+  } else {
+    a.g_hi = static_cast<_Float16*>(d->g16.hi) + gg;
+    a.g_lo = planes == 2 ? static_cast<_Float16*>(d->g16.lo) + gg : nullptr;
+  }
   a.g_img = d->g16.img_stride;
   a.g_gp = d->g16.g.plane;
   a.g_wp = d->g16.g.wp;
@@ -1761,8 +2205,12 @@ static int head_prepare(const rrin_head_h8_desc* d, HeadH8Args& a, int& grid) {
   if (d->mode == RRIN_HEAD_FLOW && d->flow_raw.hi) {
     if (!h8_ok(d->flow_raw, d->prec) || d->flow_raw.g.h != h || d->flow_raw.g.w != w) return RRIN_E_SHAPE;
     const int64_t fo = (int64_t)d->flow_raw.g_off * d->flow_raw.g.plane * 8;
-    a.fr_hi = static_cast<_Float16*>(d->flow_raw.hi) + fo;
-    a.fr_lo = planes == 2 ? static_cast<_Float16*>(d->flow_raw.lo) + fo : nullptr;
+    if (d->prec == RRIN_PREC_F32R) {
+      a.fr32 = static_cast<uint4*>(d->flow_raw.hi) + (int64_t)d->flow_raw.g_off * d->flow_raw.g.plane;
+    } else {
+      a.fr_hi = static_cast<_Float16*>(d->flow_raw.hi) + fo;
+      a.fr_lo = planes == 2 ? static_cast<_Float16*>(d->flow_raw.lo) + fo : nullptr;
+    }
     a.fr_img = d->flow_raw.img_stride;
     a.fr_gp = d->flow_raw.g.plane;
     a.fr_wp = d->flow_raw.g.wp;
@@ -1780,7 +2228,7 @@ extern "C" int rrin_head_h8_fwd(const rrin_head_h8_desc* d, void* stream) {
   int grid = 0;
   const int rc = head_prepare(d, a, grid);
   if (rc) return rc;
-  const int planes = planes_of(d->prec);
+  const int planes = d->prec == RRIN_PREC_F32R ? 0 : planes_of(d->prec);
   hipStream_t st = (hipStream_t)stream;
   switch (d->mode) {
     case RRIN_HEAD_PLAIN:
@@ -1802,12 +2250,20 @@ extern "C" int rrin_head_h8_fwd(const rrin_head_h8_desc* d, void* stream) {
 
 extern "C" int rrin_flow_tblend_h8(const rrin_h8* fr, const rrin_h8* g16, const float* coef, int32_t n, int32_t prec,
                                    void* stream) {
-  if (!fr || !g16 || !coef || n < 1 || (prec != RRIN_PREC_F16X3 && prec != RRIN_PREC_F16)) return RRIN_E_ARG;
-  if (!h8_ok(*fr, prec) || !h8_ok(*g16, prec) || g16->g_off != 0 || g16->groups < 2) return RRIN_E_SHAPE;
+  if (!fr || !g16 || !coef || n < 1 || !rec_prec(prec)) return RRIN_E_ARG;
+  if (!h8_ok(*fr, prec) || !h8_ok(*g16, prec) || g16->g_off != 0 || g16->groups * chans_per_rec(prec) < 16)
+    return RRIN_E_SHAPE;
   if (fr->g.h != g16->g.h || fr->g.w != g16->g.w) return RRIN_E_SHAPE;
   const int h = g16->g.h, w = g16->g.w;
   const int64_t total = (int64_t)n * h * w;
   const int grid = (int)((total + 255) / 256);
+  if (prec == RRIN_PREC_F32R) {
+    hipLaunchKernelGGL(flow_tblend_r32_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                       static_cast<const uint4*>(fr->hi) + (int64_t)fr->g_off * fr->g.plane, fr->img_stride,
+                       fr->g.wp, static_cast<uint4*>(g16->hi), g16->img_stride, g16->g.plane, g16->g.wp, coef, h, w,
+                       total);
+    return hip_code(hipGetLastError());
+  }
   const int64_t fo = (int64_t)fr->g_off * fr->g.plane * 8;
   const _Float16* fhi = static_cast<const _Float16*>(fr->hi) + fo;
   hipStream_t st = (hipStream_t)stream;
@@ -1825,12 +2281,15 @@ extern "C" int rrin_flow_tblend_h8(const rrin_h8* fr, const rrin_h8* g16, const 
 
 extern "C" int rrin_pack_g16_h8(const float* i0, const float* i1, int32_t n, const rrin_h8* g16, int32_t prec,
                                 void* stream) {
-  if (!i0 || !i1 || !g16 || n < 1 || (prec != RRIN_PREC_F16X3 && prec != RRIN_PREC_F16)) return RRIN_E_ARG;
-  if (!h8_ok(*g16, prec) || g16->g_off != 0 || g16->groups < 2) return RRIN_E_SHAPE;
+  if (!i0 || !i1 || !g16 || n < 1 || !rec_prec(prec)) return RRIN_E_ARG;
+  if (!h8_ok(*g16, prec) || g16->g_off != 0 || g16->groups * chans_per_rec(prec) < 16) return RRIN_E_SHAPE;
   const int64_t total = (int64_t)n * g16->g.h * g16->g.w;
   const int grid = (int)((total + 255) / 256);
   hipStream_t st = (hipStream_t)stream;
-  if (planes_of(prec) == 2)
+  if (prec == RRIN_PREC_F32R)
+    hipLaunchKernelGGL(pack_g16_r32_kernel, dim3(grid), dim3(256), 0, st, i0, i1, static_cast<uint4*>(g16->hi),
+                       g16->img_stride, g16->g.plane, g16->g.wp, g16->g.h, g16->g.w, total);
+  else if (planes_of(prec) == 2)
     hipLaunchKernelGGL(pack_g16_h8_kernel<2>, dim3(grid), dim3(256), 0, st, i0, i1, static_cast<uint4*>(g16->hi),
                        static_cast<uint4*>(g16->lo), g16->img_stride, g16->g.plane, g16->g.wp, g16->g.h, g16->g.w,
                        total);

@@ -36,9 +36,10 @@ inline int chans(int level) { return 32 << level; }  // unet.py:26, wf=5
 inline int convs_of(int depth) { return 2 * depth + 1 + 3 * (depth - 1); }
 
 struct Buf {
-  float* base;  // F32: fp32 PP planes; F16*: hi records
+  float* base;  // F32: fp32 PP planes; F16* / F32R: (hi) records
   void* lo;     // F16X3: lo records
   int ch;
+  int cpr;      // record layouts: channels per 16-B record (8: F16*, 4: F32R)
   rrin_geom g;
 };
 
@@ -68,11 +69,13 @@ void make_plan(int n, int h, int w, int prec, char* base, Plan& p) {
   p.prec = prec;
   const bool f32 = prec == RRIN_PREC_F32;
   const int planes = prec == RRIN_PREC_F16X3 ? 2 : 1;
+  const int cpr = prec == RRIN_PREC_F32R ? 4 : 8;
   int64_t off = 0;
   auto take = [&](int ch, const rrin_geom& g) {
     Buf b;
-    // F32: ch fp32 planes; F16*: ch/8 record planes of 16 B (same 4 B/value with lo)
-    const int64_t bytes = f32 ? (int64_t)n * ch * g.plane * 4 : (int64_t)n * ((ch + 7) / 8) * g.plane * 16;
+    // F32: ch fp32 planes; F16*: ch/8 record planes of 16 B (same 4 B/value with lo);
+    // F32R: ch/4 record planes of 16 B
+    const int64_t bytes = f32 ? (int64_t)n * ch * g.plane * 4 : (int64_t)n * ((ch + cpr - 1) / cpr) * g.plane * 16;
     b.base = base ? reinterpret_cast<float*>(base + off) : nullptr;
     off += align256(bytes);
     b.lo = nullptr;
@@ -81,22 +84,23 @@ void make_plan(int n, int h, int w, int prec, char* base, Plan& p) {
       off += align256(bytes);
     }
     b.ch = ch;
+    b.cpr = cpr;
     b.g = g;
     return b;
   };
   for (int L = 0; L < kMaxDepth; ++L) p.g[L] = f32 ? make_geom(h >> L, w >> L) : make_geom_h8(h >> L, w >> L);
   p.G = take(16, p.g[0]);
   for (int L = 0; L < kMaxDepth; ++L) {
-    p.X[L] = L ? take(chans(L - 1), p.g[L]) : Buf{nullptr, nullptr, 0, p.g[0]};
+    p.X[L] = L ? take(chans(L - 1), p.g[L]) : Buf{nullptr, nullptr, 0, cpr, p.g[0]};
     p.T[L] = take(chans(L), p.g[L]);
     if (L < kMaxDepth - 1) p.CAT[L] = take(2 * chans(L), p.g[L]);
   }
   p.BOT = take(chans(kMaxDepth - 1), p.g[kMaxDepth - 1]);
   for (int L = 0; L < kMaxDepth - 1; ++L)
-    p.UPT[L] = f32 ? Buf{nullptr, nullptr, 0, p.g[L]} : take(2 * chans(L), p.g[L]);
+    p.UPT[L] = f32 ? Buf{nullptr, nullptr, 0, cpr, p.g[L]} : take(2 * chans(L), p.g[L]);
   int64_t edge_floats = 0;
   for (int L = 0; L < kMaxDepth; ++L) {
-    p.LRB[L] = (f32 || L == 0) ? Buf{nullptr, nullptr, 0, p.g[L]} : take(chans(L), p.g[L]);
+    p.LRB[L] = (f32 || L == 0) ? Buf{nullptr, nullptr, 0, cpr, p.g[L]} : take(chans(L), p.g[L]);
     if (L < kMaxDepth - 1) {
       const int64_t hh = h >> L, ww = w >> L;
       const int64_t e = (int64_t)n * chans(L) * (2 * ww + 2 * (hh - 2));
@@ -108,7 +112,7 @@ void make_plan(int n, int h, int w, int prec, char* base, Plan& p) {
     p.EDGE = base ? reinterpret_cast<float*>(base + off) : nullptr;
     off += align256(edge_floats * 4);
   }
-  p.FLOWRAW = take(f32 ? 4 : 8, p.g[0]);
+  p.FLOWRAW = take(f32 ? 4 : cpr, p.g[0]);
   p.bytes = off;
 }
 
@@ -118,9 +122,9 @@ rrin_h8 hview(const Buf& b, int ch_off, int channels, const rrin_geom& g) {
   rrin_h8 v;
   v.hi = b.base;
   v.lo = b.lo;
-  v.img_stride = (int64_t)((b.ch + 7) / 8) * g.plane;
-  v.g_off = ch_off / 8;
-  v.groups = (channels + 7) / 8;
+  v.img_stride = (int64_t)((b.ch + b.cpr - 1) / b.cpr) * g.plane;
+  v.g_off = ch_off / b.cpr;
+  v.groups = (channels + b.cpr - 1) / b.cpr;
   v.g = g;
   return v;
 }
@@ -369,7 +373,7 @@ extern "C" int rrin_net_conv_count(void) {
 
 extern "C" int64_t rrin_net_workspace_bytes(int32_t n, int32_t h, int32_t w, int32_t prec) {
   if (n < 1 || h < 16 || w < 16 || (h % 16) || (w % 16)) return RRIN_E_SHAPE;
-  if (prec < RRIN_PREC_F32 || prec > RRIN_PREC_F16) return RRIN_E_ARG;
+  if (prec < RRIN_PREC_F32 || prec > RRIN_PREC_F32R) return RRIN_E_ARG;
   Plan p;
   make_plan(n, h, w, prec, nullptr, p);
   return p.bytes;
@@ -379,7 +383,7 @@ extern "C" int rrin_net_fwd(const rrin_net_desc* d, void* stream) {
   if (!d || !d->i0 || !d->i1 || !d->out || !d->coef || !d->convs || !d->heads || !d->workspace)
     return RRIN_E_ARG;
   if (d->n < 1 || d->h < 16 || d->w < 16 || (d->h % 16) || (d->w % 16)) return RRIN_E_SHAPE;
-  if (d->prec < RRIN_PREC_F32 || d->prec > RRIN_PREC_F16) return RRIN_E_ARG;
+  if (d->prec < RRIN_PREC_F32 || d->prec > RRIN_PREC_F32R) return RRIN_E_ARG;
   Plan p;
   make_plan(d->n, d->h, d->w, d->prec, reinterpret_cast<char*>(d->workspace), p);
   if (d->workspace_bytes < p.bytes) return RRIN_E_WORKSPACE;

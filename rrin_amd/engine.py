@@ -76,6 +76,17 @@ H8_TUNED = {
 # MEDIUM_PX (1280x720 x 1, 5.79 -> 5.34 ms), else "large" (H8_TUNED).
 # profiles/r01_v13/tune_*.txt; split16 only (the fp16 path keeps H8_TUNED at
 # every size).
+# Exact fp32 on fp32 records (F32R): per-shape choice from the sweep of every
+# config on every conv shape at 1280x720, 2 pairs per launch -- the part size of
+# the 2-stream bench (tools/conv_lab.py tune --precision fp32 --batch 2,
+# profiles/r02/tune_fp32r_1280x720x2.txt).  BM 128 x TH 16 (cfg 5) wins at level
+# 2; the 45x80 bottom wants the many small persistent tiles of cfg 16.
+H8_TUNED[_lib.PREC_F32R] = {(6, 32, 0): 13, (9, 32, 0): 9, (10, 32, 0): 13, (16, 32, 0): 8, (32, 32, 0): 9,
+                            (32, 64, 1): 8, (64, 32, 0): 9, (64, 128, 1): 1, (64, 64, 1): 1, (64, 128, 2): 5,
+                            (128, 64, 1): 4, (128, 256, 2): 5, (128, 128, 2): 5, (128, 256, 3): 0,
+                            (256, 128, 2): 5, (256, 512, 3): 5, (256, 256, 3): 3, (256, 512, 4): 16,
+                            (512, 256, 3): 3, (512, 512, 4): 16}
+
 SMALL_PX = 500_000
 MEDIUM_PX = 1_200_000
 H8_TUNED_BY_SIZE = {
@@ -274,8 +285,21 @@ class RRINEngine:
             return p
         halves, biases, meta = [], [], []
         hoff = boff = 0
+        f32 = self.prec == _lib.PREC_F32R
         for (w, b, cin, cout, level, perm_arr, edge), cfg in zip(self._h8_convs, cfgs):
             bm = L.rrin_conv_h8_cfg_bm(cfg)
+            if f32:  # fp32 records: unscaled fp32 weights (offsets in floats)
+                wp = np.empty(L.rrin_pack_conv3x3_r32_floats(cout, cin, bm), np.float32)
+                bp = np.empty(L.rrin_pack_bias_floats(cout, bm), np.float32)
+                _lib.check(L.rrin_pack_conv3x3_r32(w.ctypes.data, b.ctypes.data, cout, cin, bm,
+                                                   perm_arr.ctypes.data if perm_arr is not None else None,
+                                                   wp.ctypes.data, bp.ctypes.data), "rrin_pack_conv3x3_r32")
+                meta.append((hoff, None, boff, cfg, 1.0, edge))
+                halves.append(wp)
+                hoff += wp.size
+                biases.append(bp)
+                boff += bp.size
+                continue
             nh = L.rrin_pack_conv3x3_h8_halves(cout, cin, bm)
             whi = np.empty(nh, np.uint16)
             wlo = np.empty(nh, np.uint16) if self.prec == _lib.PREC_F16X3 else None
@@ -294,14 +318,16 @@ class RRINEngine:
                 hoff += nh
             biases.append(bp)
             boff += bp.size
-        blob = torch.from_numpy(np.concatenate(halves).view(np.int16)).to(self.device)
+        elem = 4 if f32 else 2  # bytes per packed weight
+        cat = np.concatenate(halves)
+        blob = torch.from_numpy(cat if f32 else cat.view(np.int16)).to(self.device)
         bias_blob = torch.from_numpy(np.concatenate(biases)).to(self.device)
         hb, bb = blob.data_ptr(), bias_blob.data_ptr()
         table = (_lib.ConvWeights * len(meta))()
         for i, (ho, lo, bo, cfg, inv, edge) in enumerate(meta):
             e = table[i]
-            e.whi = hb + 2 * ho
-            e.wlo = hb + 2 * lo if lo is not None else None
+            e.whi = hb + elem * ho
+            e.wlo = hb + elem * lo if lo is not None else None
             e.bias = bb + 4 * bo
             e.cfg = cfg
             e.inv_wscale = inv

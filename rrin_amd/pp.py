@@ -57,28 +57,31 @@ def _stream(device) -> C.c_void_p:
 
 
 class H8Tensor:
-    """Channel-blocked fp16 activation tensor (H8 layout, include/rrin_hip.h):
+    """Channel-record activation tensor (record layout, include/rrin_hip.h):
     ``hi`` (and for fp32_split16 ``lo``) are ``[n, ceil(c/8), hp, wp, 8]``
-    half tensors, pixel (y,x) at ``[.., y+1, x+8, :]``; padding zero."""
+    half tensors (fp32 records, PREC_F32R: ``[n, ceil(c/4), hp, wp, 4]``
+    float), pixel (y,x) at ``[.., y+1, x+8, :]``; padding zero."""
 
     def __init__(self, n: int, c: int, h: int, w: int, device, prec: int):
         self.n, self.c, self.h, self.w, self.prec = n, c, h, w, prec
         self.g = _lib.geom_h8(h, w)
-        self.groups = (c + 7) // 8
-        shape = (n, self.groups, self.g.hp, self.g.wp, 8)
-        self.hi = torch.zeros(shape, dtype=torch.float16, device=device)
+        self.cpr = _lib.chans_per_record(prec)
+        self.groups = (c + self.cpr - 1) // self.cpr
+        shape = (n, self.groups, self.g.hp, self.g.wp, self.cpr)
+        dt = torch.float32 if prec == _lib.PREC_F32R else torch.float16
+        self.hi = torch.zeros(shape, dtype=dt, device=device)
         self.lo = torch.zeros(shape, dtype=torch.float16, device=device) if prec == _lib.PREC_F16X3 else None
 
     def view(self, ch_off: int = 0, channels: int | None = None) -> _lib.H8:
         channels = self.c - ch_off if channels is None else channels
-        if ch_off % 8:
-            raise ValueError("H8 views start on an 8-channel group")
+        if ch_off % self.cpr:
+            raise ValueError("record views start on a record group")
         v = _lib.H8()
         v.hi = self.hi.data_ptr()
         v.lo = self.lo.data_ptr() if self.lo is not None else None
         v.img_stride = self.groups * self.g.plane
-        v.g_off = ch_off // 8
-        v.groups = (channels + 7) // 8
+        v.g_off = ch_off // self.cpr
+        v.groups = (channels + self.cpr - 1) // self.cpr
         v.g = self.g
         return v
 

@@ -1,4 +1,8 @@
-"""GPU: split-fp16 (fp32_split16) and fp16 paths of librrin_hip.so.
+"""GPU: the record-layout paths of librrin_hip.so -- exact fp32 on fp32 records
+(R32, the default "fp32" precision), split-fp16 (fp32_split16) and fp16.
+
+R32 is exact fp32 arithmetic (fp32 storage, v_mfma_f32_32x32x2_f32 products,
+fp32 accumulation): held to 1e-5 against float64.
 
 fp32_split16 holds each fp32 value as fp16 hi+lo and forms each product from
 three exact fp16 products with fp32 accumulation (error ~2^-21 relative per
@@ -19,8 +23,9 @@ from tests import hip_helpers as H
 from tests.golden.spec import CONV_CLASSES
 
 pytestmark = pytest.mark.gpu
-X3, F16 = _lib.PREC_F16X3, _lib.PREC_F16
-TOL = {X3: dict(rtol=1e-4, atol=1e-4), F16: dict(rtol=2e-2, atol=2e-2)}
+X3, F16, R32 = _lib.PREC_F16X3, _lib.PREC_F16, _lib.PREC_F32R
+PRECS = [R32, X3, F16]
+TOL = {X3: dict(rtol=1e-4, atol=1e-4), F16: dict(rtol=2e-2, atol=2e-2), R32: dict(rtol=1e-5, atol=1e-5)}
 
 
 def ref_conv(x, w, b, slope=None):
@@ -50,12 +55,20 @@ def pack_h8(w, b, cfg, prec, dev, perm=None):
     b = b.detach().cpu().float().contiguous().numpy()
     cout, cin = w.shape[:2]
     bm = lib.rrin_conv_h8_cfg_bm(cfg)
+    pa = np.asarray(perm, np.int32) if perm is not None else None
+    if prec == R32:  # fp32 records: unscaled fp32 weights, no lo blob
+        wp = np.zeros(lib.rrin_pack_conv3x3_r32_floats(cout, cin, bm), np.float32)
+        bp = np.zeros(lib.rrin_pack_bias_floats(cout, bm), np.float32)
+        _lib.check(lib.rrin_pack_conv3x3_r32(w.ctypes.data, b.ctypes.data, cout, cin, bm,
+                                             pa.ctypes.data if pa is not None else None, wp.ctypes.data,
+                                             bp.ctypes.data))
+        wt = torch.from_numpy(wp).to(dev)
+        return wt, wt, torch.from_numpy(bp).to(dev), 1.0
     nh = lib.rrin_pack_conv3x3_h8_halves(cout, cin, bm)
     whi = np.zeros(nh, np.uint16)
     wlo = np.zeros(nh, np.uint16)
     bp = np.zeros(lib.rrin_pack_bias_floats(cout, bm), np.float32)
     inv = C.c_float()
-    pa = np.asarray(perm, np.int32) if perm is not None else None
     _lib.check(lib.rrin_pack_conv3x3_h8(w.ctypes.data, b.ctypes.data, cout, cin, bm,
                                         pa.ctypes.data if pa is not None else None, prec, whi.ctypes.data,
                                         wlo.ctypes.data, bp.ctypes.data, C.byref(inv)))
@@ -86,18 +99,18 @@ def conv_h8(src: H8Tensor, w, b, cfg, prec, epi=_lib.EPI_LINEAR, dst=None, dst_o
     return dst, pool
 
 
-@pytest.mark.parametrize("prec", [X3, F16])
+@pytest.mark.parametrize("prec", PRECS)
 def test_h8_roundtrip(gpu, prec):
     x = torch.randn(2, 11, 23, 40, device=gpu) * 3
     t = H8Tensor.from_nchw(x, prec, c_alloc=24, ch_off=3)
     y = t.to_nchw(3, 11)
-    rel = 2.0 ** -21 if prec == X3 else 2.0 ** -10
-    floor = 2.0 ** -34 if prec == X3 else 2.0 ** -24   # fp16 subnormal floor of lo (x 2^-11) / hi
+    rel = {X3: 2.0 ** -21, F16: 2.0 ** -10, R32: 0.0}[prec]
+    floor = {X3: 2.0 ** -34, F16: 2.0 ** -24, R32: 0.0}[prec]   # fp16 subnormal floor of lo (x 2^-11) / hi
     assert bool(((y - x).abs() <= rel * x.abs() + floor).all())
     assert not t.hi[:, :, 0].any() and not t.hi[:, :, :, :8].any() and not t.hi[:, :, 24:].any()
 
 
-@pytest.mark.parametrize("prec", [X3, F16])
+@pytest.mark.parametrize("prec", PRECS)
 @pytest.mark.parametrize("cin,cout", CONV_CLASSES)
 def test_h8_conv_golden(gpu, golden, prec, cin, cout):
     if cout % 8:
@@ -112,7 +125,7 @@ def test_h8_conv_golden(gpu, golden, prec, cin, cout):
                                    err_msg=f"cfg {cfg}")
 
 
-@pytest.mark.parametrize("prec", [X3, F16])
+@pytest.mark.parametrize("prec", PRECS)
 @pytest.mark.parametrize("n,cin,cout,h,w", [(2, 64, 32, 40, 72), (1, 128, 64, 46, 80), (1, 256, 256, 12, 20),
                                             (2, 16, 32, 32, 64)])
 def test_h8_conv_pool(gpu, prec, n, cin, cout, h, w):
@@ -131,7 +144,7 @@ def test_h8_conv_pool(gpu, prec, n, cin, cout, h, w):
                                    err_msg=f"cfg {cfg}")
 
 
-@pytest.mark.parametrize("prec", [X3, F16])
+@pytest.mark.parametrize("prec", PRECS)
 def test_h8_conv_partial_channels_and_perm(gpu, prec):
     x = torch.rand(2, 16, 32, 48, device=gpu)
     wt, b = keyed_conv(10, 32, "perm")
@@ -143,7 +156,7 @@ def test_h8_conv_partial_channels_and_perm(gpu, prec):
     np.testing.assert_allclose(dst.to_nchw().cpu().double().numpy(), ref.numpy(), **TOL[prec])
 
 
-@pytest.mark.parametrize("prec", [X3, F16])
+@pytest.mark.parametrize("prec", PRECS)
 @pytest.mark.parametrize("n,c,h,w", [(1, 64, 20, 36), (2, 16, 5, 7), (1, 512, 5, 10)])
 def test_h8_upsample(gpu, prec, n, c, h, w):
     x = torch.rand(n, c, h, w, device=gpu) * 2 - 1
@@ -153,7 +166,7 @@ def test_h8_upsample(gpu, prec, n, c, h, w):
     _lib.check(_lib.lib().rrin_upsample2x_h8(C.byref(sv), C.byref(dv), n, prec, H.stream(gpu)))
     torch.cuda.synchronize()
     ref = F.interpolate(x.double().cpu(), scale_factor=2, mode="bilinear", align_corners=False)
-    tol = 1e-6 if prec == X3 else 2e-3
+    tol = 2e-3 if prec == F16 else 1e-6
     np.testing.assert_allclose(dst.to_nchw().cpu().double().numpy(), ref.numpy(), rtol=0, atol=tol)
 
 
@@ -164,7 +177,7 @@ def test_h8_pool_rejected_for_single_row_waves(gpu):
         conv_h8(H8Tensor.from_nchw(x, X3), wt, b, 4, X3, epi=_lib.EPI_LEAKY_POOL)
 
 
-@pytest.mark.parametrize("prec", [X3, F16])
+@pytest.mark.parametrize("prec", PRECS)
 @pytest.mark.parametrize("cin", [6, 9, 10])
 def test_h8_conv_dma_finite_tail(gpu, prec, cin):
     """tail_finite=1: whole records staged by LDS-DMA; the finite tail channels
@@ -177,7 +190,7 @@ def test_h8_conv_dma_finite_tail(gpu, prec, cin):
         np.testing.assert_allclose(dst.to_nchw().cpu().double().numpy(), ref.numpy(), **TOL[prec])
 
 
-@pytest.mark.parametrize("prec", [X3, F16])
+@pytest.mark.parametrize("prec", PRECS)
 def test_pack_g16(gpu, prec):
     i0 = torch.rand(2, 3, 32, 48, device=gpu)
     i1 = torch.rand(2, 3, 32, 48, device=gpu)
@@ -189,7 +202,7 @@ def test_pack_g16(gpu, prec):
     _lib.check(_lib.lib().rrin_pack_g16_h8(i0.data_ptr(), i1.data_ptr(), 2, C.byref(v), prec, H.stream(gpu)))
     torch.cuda.synchronize()
     out = g.to_nchw()
-    tol = 2.0 ** -20 if prec == X3 else 2.0 ** -10
+    tol = {X3: 2.0 ** -20, F16: 2.0 ** -10, R32: 0.0}[prec]
     assert float((out[:, :3] - i0).abs().max()) <= tol and float((out[:, 3:6] - i1).abs().max()) <= tol
     assert not out[:, 6:].any()
 
@@ -207,7 +220,7 @@ def replicate_ring(t: H8Tensor):
         a[:, :, 0:h + 2, 8 + w] = a[:, :, 0:h + 2, 7 + w]
 
 
-@pytest.mark.parametrize("prec", [X3, F16])
+@pytest.mark.parametrize("prec", PRECS)
 def test_h8_leaky_rep_writes_replicated_ring(gpu, prec):
     x = torch.rand(2, 32, 13, 45, device=gpu) * 2 - 1
     wt, b = keyed_conv(32, 64, "rep")
@@ -263,7 +276,7 @@ def subpixel_upconv(src: H8Tensor, w, b, cfg, prec, dst=None):
     return dst
 
 
-@pytest.mark.parametrize("prec", [X3, F16])
+@pytest.mark.parametrize("prec", PRECS)
 @pytest.mark.parametrize("n,cin,cout,sh,sw", [(2, 64, 32, 20, 36), (1, 128, 64, 23, 40), (1, 256, 128, 5, 7),
                                               (2, 512, 256, 3, 5), (1, 64, 32, 1, 1)])
 def test_h8_subpixel_upconv(gpu, prec, n, cin, cout, sh, sw):
@@ -283,7 +296,7 @@ def test_h8_subpixel_upconv(gpu, prec, n, cin, cout, sh, sw):
         assert not dst.hi[:, :, 0].any() and not dst.hi[:, :, :, :8].any()  # zero padding kept
 
 
-@pytest.mark.parametrize("prec", [X3, F16])
+@pytest.mark.parametrize("prec", PRECS)
 @pytest.mark.parametrize("cin,epi", [(32, _lib.EPI_LEAKY_POOL), (64, _lib.EPI_LEAKY), (32, _lib.EPI_LINEAR)])
 def test_h8_conv_many_tiles_per_block(gpu, prec, cin, epi):
     """Shapes with more tiles than a persistent grid holds, so each block loops
@@ -305,7 +318,7 @@ def test_h8_conv_many_tiles_per_block(gpu, prec, cin, epi):
                                        err_msg=f"cfg {cfg} pool")
 
 
-@pytest.mark.parametrize("prec", [X3, F16])
+@pytest.mark.parametrize("prec", PRECS)
 def test_h8_subpixel_many_tiles_per_block(gpu, prec):
     """Sub-pixel up conv (ring scratch + phase epilogue) on a grid with several
     tiles per block, every config."""
@@ -336,7 +349,7 @@ def head_h8(src: H8Tensor, dst: H8Tensor, w, b, mode, coef=None, out=None, prec=
     torch.cuda.synchronize(dev)
 
 
-@pytest.mark.parametrize("prec", [X3, F16])
+@pytest.mark.parametrize("prec", PRECS)
 @pytest.mark.parametrize("cout", [2, 3, 4])
 @pytest.mark.parametrize("n,h,w,scale", [(2, 40, 72, 1.0), (1, 20, 50, 1e-3), (3, 16, 32, 300.0)])
 def test_h8_head_plain(gpu, prec, cout, n, h, w, scale):
@@ -348,6 +361,7 @@ def test_h8_head_plain(gpu, prec, cout, n, h, w, scale):
     dst = H8Tensor(n, 16, h, w, gpu, prec)
     head_h8(H8Tensor.from_nchw(x, prec), dst, wt, b, _lib.HEAD_PLAIN, prec=prec)
     ref = ref_conv(x, wt, b)
-    tol = dict(rtol=1e-4, atol=1e-4 * max(scale, 1.0)) if prec == X3 else dict(rtol=2e-2, atol=2e-2 * max(scale, 1.0))
+    tol = {X3: dict(rtol=1e-4, atol=1e-4 * max(scale, 1.0)), R32: dict(rtol=1e-5, atol=1e-5 * max(scale, 1.0)),
+           F16: dict(rtol=2e-2, atol=2e-2 * max(scale, 1.0))}[prec]
     np.testing.assert_allclose(dst.to_nchw(0, cout).cpu().double().numpy(), ref.numpy(), **tol)
     assert not dst.to_nchw(cout, 16 - cout).any()

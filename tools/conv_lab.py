@@ -105,7 +105,7 @@ def breakdown(args):
         for i in range(cnt.value):
             tot.setdefault(i, []).append((kinds[i], ms[i], fl[i]))
     lib.rrin_prof_destroy(h)
-    sch = schedule(args.height, args.width, args.precision != "fp32", net.subpixel_max_level)
+    sch = schedule(args.height, args.width, args.precision != "fp32_planar", net.subpixel_max_level)
     rows = []
     conv_i = 0
     for i, entry in enumerate(sch):
@@ -190,7 +190,7 @@ def tune_h8(args):
 
 
 def tune(args):
-    if args.precision != "fp32":
+    if args.precision != "fp32_planar":
         return tune_h8(args)
     dev = torch.device("cuda:0")
     lib = _lib.lib()
@@ -253,7 +253,7 @@ def single(args):
     prec = _lib.PRECISIONS[args.precision]
     cin, cout, L, epi, cfg = args.shape
     n, h, w = args.batch, args.height >> L, args.width >> L
-    if args.precision == "fp32":  # exact-fp32 PP conv; --src 1 = fused upsample of a half-size input
+    if args.precision == "fp32_planar":  # exact-fp32 PP conv; --src 1 = fused upsample of a half-size input
         from tests.hip_helpers import pack
         src = args.src
         hs, ws_ = (h // 2, w // 2) if src == 1 else (h, w)
@@ -285,7 +285,7 @@ def single(args):
         e1.record()
         e1.synchronize()
         ms = e0.elapsed_time(e1) / args.reps
-        print(f"{cin}->{cout} L{L} src{args.src} epi{epi} cfg{cfg} fp32: {ms:.4f} ms "
+        print(f"{cin}->{cout} L{L} src{args.src} epi{epi} cfg{cfg} fp32_planar: {ms:.4f} ms "
               f"{2 * 9 * cin * cout * h * w * n / (ms * 1e-3) / 1e12:.1f} TF")
         return
     x = H8Tensor.from_nchw(torch.rand(n, cin, h, w, device=dev) * 2 - 1, prec)
@@ -300,10 +300,17 @@ def single(args):
         d.pool = pool.view(0, cout)
     d.whi, d.wlo, d.bias = whi.data_ptr(), wlo.data_ptr(), bp.data_ptr()
     st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    if args.sched is not None:  # lab build: schedule / ablation bits, persistent grid factor
+        lab = C.CDLL(os.path.join(REPO, "rrin_amd", "librrin_lab.so"))
+        lab.rrin_conv3x3_h8_lab.argtypes = [C.POINTER(_lib.ConvH8Desc), C.c_int32, C.c_int32, C.c_void_p]
+        run = lambda: _lib.check(lab.rrin_conv3x3_h8_lab(C.byref(d), args.sched, args.persist, st))  # noqa: E731
+    else:
+        run = lambda: _lib.check(lib.rrin_conv3x3_h8_fwd(C.byref(d), st))  # noqa: E731
+    run()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(args.reps):
-        _lib.check(lib.rrin_conv3x3_h8_fwd(C.byref(d), st))
+        run()
     e1.record()
     e1.synchronize()
     ms = e0.elapsed_time(e1) / args.reps
@@ -322,6 +329,14 @@ LAB_SHAPES = [(32, 32, 0, 6), (64, 32, 0, 6), (64, 32, 0, 1), (64, 64, 1, 0), (1
               (256, 128, 2, 0), (256, 256, 3, 0), (512, 256, 3, 0), (512, 512, 4, 0)]
 
 
+# fp32 records (--precision fp32): the tuned config of each shape (engine.H8_TUNED)
+LAB_SHAPES_R32 = [(32, 32, 0, 6), (64, 32, 0, 1), (64, 64, 1, 1), (128, 64, 1, 4), (128, 128, 2, 5),
+                  (256, 128, 2, 5), (256, 256, 3, 3), (512, 512, 4, 16)]
+LAB_VARIANTS_R32 = [("base", 0, 0), ("persist", 0, 1), ("spread", 16, 0), ("persist+spread", 16, 1),
+                    ("noW", 1, 0), ("noIn", 2, 0), ("noLoads", 3, 0), ("noMfma", 4, 0), ("noEpi", 8, 0),
+                    ("noLoads+noEpi", 11, 0), ("persist+noLoads+noEpi", 11, 1)]
+
+
 def ablate(args):
     from rrin_amd.pp import H8Tensor
     from tests.test_gpu_h8 import pack_h8
@@ -331,10 +346,12 @@ def ablate(args):
     fn.argtypes = [C.POINTER(_lib.ConvH8Desc), C.c_int32, C.c_int32, C.c_void_p]
     lib = _lib.lib()
     dev = torch.device("cuda:0")
-    prec = _lib.PREC_F16X3
+    r32 = args.precision == "fp32"
+    prec = _lib.PREC_F32R if r32 else _lib.PREC_F16X3
+    variants = LAB_VARIANTS_R32 if r32 else LAB_VARIANTS
     st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
     results = []
-    for cin, cout, L, cfg in LAB_SHAPES:
+    for cin, cout, L, cfg in (LAB_SHAPES_R32 if r32 else LAB_SHAPES):
         n, h, w = args.batch, args.height >> L, args.width >> L
         torch.manual_seed(cin * 1000 + cout)
         x = H8Tensor.from_nchw(torch.rand(n, cin, h, w, device=dev) * 2 - 1, prec)
@@ -348,22 +365,24 @@ def ablate(args):
         d.whi, d.wlo, d.bias = whi.data_ptr(), wlo.data_ptr(), bp.data_ptr()
         _lib.check(lib.rrin_conv3x3_h8_fwd(C.byref(d), st))
         torch.cuda.synchronize()
-        ref = (dst.hi.clone(), dst.lo.clone())
+        ref = (dst.hi.clone(), dst.lo.clone() if dst.lo is not None else None)
         fl = 2 * 9 * cin * cout * h * w * n
         ok, times = {}, {}
-        for name, sched, pers in LAB_VARIANTS:
+        for name, sched, pers in variants:
             dst.hi.zero_()
-            dst.lo.zero_()
+            if dst.lo is not None:
+                dst.lo.zero_()
             rc = fn(C.byref(d), sched, pers, st)
             torch.cuda.synchronize()
             if rc != 0:
                 ok[name] = f"rc{rc}"
                 continue
             if sched & 143 == 0:
-                ok[name] = "ok" if torch.equal(dst.hi, ref[0]) and torch.equal(dst.lo, ref[1]) else "MISMATCH"
+                same = torch.equal(dst.hi, ref[0]) and (dst.lo is None or torch.equal(dst.lo, ref[1]))
+                ok[name] = "ok" if same else "MISMATCH"
             times[name] = []
         for _ in range(args.reps):  # interleaved rounds (guide rule 24)
-            for name, sched, pers in LAB_VARIANTS:
+            for name, sched, pers in variants:
                 if name not in times:
                     continue
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -375,7 +394,7 @@ def ablate(args):
                 times[name].append(e0.elapsed_time(e1) / 3)
         base = sorted(times["base"])[len(times["base"]) // 2]
         line = []
-        for name, sched, pers in LAB_VARIANTS:
+        for name, sched, pers in variants:
             if name not in times:
                 line.append(f"{name}:{ok.get(name)}")
                 continue
@@ -449,7 +468,9 @@ def main():
     ap.add_argument("--shape", type=int, nargs=5, default=[512, 256, 3, 1, 0],
                     help="single: cin cout level epi cfg")
     ap.add_argument("--src", type=int, default=0, help="single, fp32: src mode (1 = fused upsample)")
-    ap.add_argument("--sched", type=int, default=None, help="single, fp32: lab32 ablation bits")
+    ap.add_argument("--sched", type=int, default=None,
+                    help="single: lab schedule / ablation bits (fp32_planar: librrin_lab32.so; records: librrin_lab.so)")
+    ap.add_argument("--persist", type=int, default=0, help="single, records + --sched: persistent grid factor")
     ap.add_argument("--batch", type=int, default=4)
     ap.add_argument("--height", type=int, default=720)
     ap.add_argument("--width", type=int, default=1280)
@@ -457,7 +478,7 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--first-cfg", type=int, default=None,
                     help="breakdown: run the first conv of every U-Net with this H8 config (same BM only)")
-    ap.add_argument("--precision", default="fp32", choices=["fp32", "fp32_split16", "fp16"])
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "fp32_planar", "fp32_split16", "fp16"])
     args = ap.parse_args()
     {"breakdown": breakdown, "tune": tune, "single": single, "ablate": ablate, "ablate32": ablate32}[args.mode](args)
 

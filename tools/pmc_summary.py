@@ -68,7 +68,7 @@ def main():
         json.dump({"correction": "hbm = (2*FETCH_SIZE + WRITE_SIZE) KiB (gfx950 FETCH_SIZE = 1/2 of wide reads)",
                    "steps": a.steps, "kernels": res}, open(a.out, "w"), indent=1)
     if a.table:
-        fam_name = "conv3x3_mfma_kernel" if a.precision == "fp32" else "conv3x3_h8_kernel"
+        fam_name = "conv3x3_mfma_kernel" if a.precision == "fp32_planar" else "conv3x3_h8_kernel"
         tab = json.load(open(a.table)) if os.path.exists(a.table) else {}
         r = res[fam_name]
         tab[f"{a.precision}@{a.config}"] = {
