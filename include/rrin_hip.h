@@ -9,7 +9,13 @@
  *     PyTorch caching allocator);
  *   - every entry returns int: 0 = ok, > 0 = a hipError_t, < 0 = RRIN_E_* for a
  *     violated shape/argument precondition; rrin_strerror() decodes it;
- *   - stateless and stream-ordered: calls only enqueue work on `stream`.
+ *   - stateless and stream-ordered: calls only enqueue work on `stream`; no
+ *     call's result depends on another call.  Everything a call needs comes in
+ *     its arguments (the optional launch profiler of rrin_net_fwd included);
+ *     the only process-wide data are thread-safe per-device launch caches
+ *     (a kernel's dynamic-LDS attribute, resident blocks per CU).  Entry points
+ *     may be called from several host threads; one rrin_prof must not be
+ *     shared by concurrent calls.
  *
  * Activation layout used between kernels ("padded planar", PP): per image and
  * channel a plane of hp x wp fp32 with hp = round_up(h,16)+2, wp = round_up(w,32)+64;

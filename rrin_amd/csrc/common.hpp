@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+
 #include "../../include/rrin_hip.h"
 
 namespace rrin {
@@ -35,6 +37,32 @@ __host__ __device__ inline float* pp_chan(const rrin_pp& v, int n, int c) {
 }
 
 inline int hip_code(hipError_t e) { return e == hipSuccess ? 0 : (int)e; }
+
+// ---- per-device launch caches ------------------------------------------------
+// The library keeps no state that affects results.  It caches, per device and
+// kernel, facts about launching it (the dynamic-LDS attribute has been set; the
+// resident blocks per CU); these caches are keyed by device and thread-safe
+// (atomics; a race only repeats an idempotent query).
+constexpr int kMaxDevices = 64;
+
+inline int current_device() {
+  int d = 0;
+  return (hipGetDevice(&d) == hipSuccess && d >= 0 && d < kMaxDevices) ? d : 0;
+}
+
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device).
+struct LdsAttr {
+  std::atomic<uint64_t> done{0};
+  int ensure(const void* kernel, int lds_bytes) {
+    const int dev = current_device();
+    const uint64_t bit = 1ull << dev;
+    if (done.load(std::memory_order_acquire) & bit) return 0;
+    hipError_t e = hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+    if (e != hipSuccess) return (int)e;
+    done.fetch_or(bit, std::memory_order_release);
+    return 0;
+  }
+};
 
 // ---- H8 (channel-blocked fp16 records) geometry -----------------------------
 constexpr int kH8PadLeft = 8;  // records: pixel x at record x+8 (128-B aligned rows)

@@ -1632,11 +1632,14 @@ static constexpr int kNumCfgH8 = sizeof(kCfgH8) / sizeof(kCfgH8[0]);
 static constexpr size_t kMaxLds = 160 * 1024;
 
 static int num_cus() {
-  static int n[16] = {0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return 256;
-  if (!n[dev] && hipDeviceGetAttribute(&n[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) n[dev] = 256;
-  return n[dev];
+  static std::atomic<int> n[kMaxDevices] = {};
+  const int dev = current_device();
+  int v = n[dev].load(std::memory_order_relaxed);
+  if (!v) {
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v < 1) v = 256;
+    n[dev].store(v, std::memory_order_relaxed);
+  }
+  return v;
 }
 
 template <int NW, int WM, int WN, int PLANES, int EPI, bool DMA, int SCHED, bool F32 = false>
@@ -1646,21 +1649,20 @@ static int launch_h8_k(const ConvH8Args& args, int persist, hipStream_t st) {
   constexpr bool wres = DMA && (SCHED & SCHED_WRES) != 0;
   const size_t lds = h8_lds_bytes<NW, WM, WN, PLANES>(wres, args.nchunks);
   if (lds > kMaxLds) return RRIN_E_CONFIG;
-  static bool attr_set = false;
-  static int per_cu[40] = {0};  // resident blocks per CU, by LDS footprint (WRES: chunk count)
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds);
-    if (e != hipSuccess) return (int)e;
-    attr_set = true;
-  }
+  static LdsAttr attr;
+  // resident blocks per CU, per device and LDS footprint (WRES: chunk count)
+  static std::atomic<int> per_cu[kMaxDevices][40] = {};
+  if (int e = attr.ensure((const void*)k, (int)kMaxLds)) return e;
   const int64_t ntiles = (int64_t)args.co_blocks * args.tiles_x * args.tiles_y * args.n;
   int64_t grid = ntiles;
   if (persist > 0) {
-    int& pc = per_cu[wres ? (args.nchunks < 40 ? args.nchunks : 39) : 0];
+    std::atomic<int>& slot = per_cu[current_device()][wres ? (args.nchunks < 40 ? args.nchunks : 39) : 0];
+    int pc = slot.load(std::memory_order_relaxed);
     if (!pc) {
       hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, (const void*)k, T::NT, lds);
       if (e != hipSuccess) return (int)e;
       if (pc < 1) pc = 1;
+      slot.store(pc, std::memory_order_relaxed);
     }
     int64_t g = (int64_t)persist * pc * num_cus();
     g -= g % args.co_blocks;  // WRES: every tile of a block in the block's channel block
@@ -2012,13 +2014,8 @@ static int edge_fix_launch(const EdgeFixArgs& a, dim3 grid, hipStream_t st) {
   constexpr size_t lds = (size_t)KS * kFixSubFloats * sizeof(float);
   static_assert(lds <= 160 * 1024, "edge fix LDS");
   static_assert(kFixSubFloats >= 4 * 256, "K-group sums fit a staging region");
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)edge_fix_h8_kernel<PLANES, KS, F32>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return (int)e;
-    attr_set = true;
-  }
+  static LdsAttr attr;
+  if (int e = attr.ensure((const void*)edge_fix_h8_kernel<PLANES, KS, F32>, (int)lds)) return e;
   hipLaunchKernelGGL((edge_fix_h8_kernel<PLANES, KS, F32>), grid, dim3(256 * KS), lds, st, a);
   return hip_code(hipGetLastError());
 }

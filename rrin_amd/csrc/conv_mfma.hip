@@ -381,12 +381,8 @@ static int launch_t(const ConvArgs& args, int grid, hipStream_t st) {
   using T = Tile<A, B, C, D>;
   constexpr size_t lds = SRC == RRIN_SRC_UPSAMPLE2X ? T::LDS_BYTES_UP : T::LDS_BYTES;
   auto k = conv3x3_mfma_kernel<A, B, C, D, SRC, EPI, SCHED>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return (int)e;
-    attr_set = true;
-  }
+  static LdsAttr attr;
+  if (int e = attr.ensure((const void*)k, (int)lds)) return e;
   hipLaunchKernelGGL(k, dim3(grid), dim3(256), lds, st, args);
   return hip_code(hipGetLastError());
 }

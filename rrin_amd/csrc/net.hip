@@ -46,6 +46,7 @@ struct Buf {
 // Workspace plan: offsets are identical in size query and forward.
 struct Plan {
   int n, prec;
+  rrin_prof* prof;        // the caller's launch profiler of this call (nullable)
   rrin_geom g[kMaxDepth];
   Buf G;                  // 16 ch at level 0
   Buf X[kMaxDepth];       // level input (L >= 1): C_{L-1} ch
@@ -67,6 +68,7 @@ int64_t align256(int64_t b) { return (b + 255) & ~(int64_t)255; }
 void make_plan(int n, int h, int w, int prec, char* base, Plan& p) {
   p.n = n;
   p.prec = prec;
+  p.prof = nullptr;
   const bool f32 = prec == RRIN_PREC_F32;
   const int planes = prec == RRIN_PREC_F16X3 ? 2 : 1;
   const int cpr = prec == RRIN_PREC_F32R ? 4 : 8;
@@ -159,11 +161,9 @@ struct ProfScope {
   }
 };
 
-rrin_prof* g_prof = nullptr;  // set for the duration of one rrin_net_fwd call
-
 int conv(const Plan& p, const rrin_conv_weights& cw, int cin, int cout, int src_mode, int epi,
          const rrin_pp& src, const rrin_pp& dst, const rrin_pp* pool, hipStream_t st) {
-  ProfScope ps(g_prof, st, RRIN_KIND_CONV, 2.0 * 9 * cin * cout * (double)dst.g.h * dst.g.w * p.n);
+  ProfScope ps(p.prof, st, RRIN_KIND_CONV, 2.0 * 9 * cin * cout * (double)dst.g.h * dst.g.w * p.n);
   rrin_conv_desc d;
   memset(&d, 0, sizeof(d));
   d.n = p.n;
@@ -236,7 +236,7 @@ int run_unet(const Plan& p, const UNetSpec& u, const rrin_conv_weights* cw, cons
   hd.coef = nd->coef;
   hd.out = nd->out;
   if (u.head_mode == RRIN_HEAD_FLOW) hd.flow_raw = view(p.FLOWRAW, p.n, 0, 4);
-  ProfScope ps(g_prof, st, RRIN_KIND_HEAD, 2.0 * 9 * 32 * u.out_ch * (double)x.g.h * x.g.w * p.n);
+  ProfScope ps(p.prof, st, RRIN_KIND_HEAD, 2.0 * 9 * 32 * u.out_ch * (double)x.g.h * x.g.w * p.n);
   return rrin_head_fwd(&hd, st);
 }
 
@@ -244,7 +244,7 @@ int conv_h8(const Plan& p, const rrin_conv_weights& cw, int cin, int cout, int e
             const rrin_h8& dst, const rrin_h8* pool, hipStream_t st, float* edge = nullptr) {
   // algorithmic FLOPs of the reference conv (a sub-pixel conv has 4 phase rows per real channel)
   const int creal = epi == RRIN_EPI_SUBPIXEL ? cout / 4 : cout;
-  ProfScope ps(g_prof, st, RRIN_KIND_CONV, 2.0 * 9 * cin * creal * (double)dst.g.h * dst.g.w * p.n);
+  ProfScope ps(p.prof, st, RRIN_KIND_CONV, 2.0 * 9 * cin * creal * (double)dst.g.h * dst.g.w * p.n);
   rrin_conv_h8_desc d;
   memset(&d, 0, sizeof(d));
   d.n = p.n;
@@ -283,7 +283,7 @@ int upconv_subpixel(const Plan& p, const rrin_conv_weights& cw, int C, const rri
   e.edge = p.EDGE;
   e.wedge = cw.wedge;
   e.bias = cw.bias_raw;
-  ProfScope ps(g_prof, st, RRIN_KIND_EDGE, 0.0);
+  ProfScope ps(p.prof, st, RRIN_KIND_EDGE, 0.0);
   return rrin_subpixel_edge_fix_h8(&e, st);
 }
 
@@ -325,7 +325,7 @@ int run_unet_h8(const Plan& p, const UNetSpec& u, const rrin_conv_weights* cw, c
     } else {
       const rrin_h8 upin = hview(p.UPT[L], 0, 2 * C);
       {
-        ProfScope ps(g_prof, st, RRIN_KIND_LAYOUT, 0.0);
+        ProfScope ps(p.prof, st, RRIN_KIND_LAYOUT, 0.0);
         RRIN_TRY(rrin_upsample2x_h8(&x, &upin, p.n, p.prec, st));
       }
       RRIN_TRY(conv_h8(p, cu, 2 * C, C, RRIN_EPI_LINEAR, upin, up, nullptr, st));
@@ -353,7 +353,7 @@ int run_unet_h8(const Plan& p, const UNetSpec& u, const rrin_conv_weights* cw, c
   hd.coef = nd->coef;
   hd.out = nd->out;
   if (u.head_mode == RRIN_HEAD_FLOW) hd.flow_raw = hview(p.FLOWRAW, 0, 4);
-  ProfScope ps(g_prof, st, RRIN_KIND_HEAD, 2.0 * 9 * 32 * u.out_ch * (double)x.g.h * x.g.w * p.n);
+  ProfScope ps(p.prof, st, RRIN_KIND_HEAD, 2.0 * 9 * 32 * u.out_ch * (double)x.g.h * x.g.w * p.n);
   return rrin_head_h8_fwd(&hd, st);
 }
 
@@ -387,13 +387,13 @@ extern "C" int rrin_net_fwd(const rrin_net_desc* d, void* stream) {
   Plan p;
   make_plan(d->n, d->h, d->w, d->prec, reinterpret_cast<char*>(d->workspace), p);
   if (d->workspace_bytes < p.bytes) return RRIN_E_WORKSPACE;
+  p.prof = d->prof;  // per call: concurrent calls never share launch state
   hipStream_t st = (hipStream_t)stream;
   if (d->prec != RRIN_PREC_F32) {
-    g_prof = d->prof;
     const rrin_h8 gall = hview(p.G, 0, 16);
     int rc = 0;
     {
-      ProfScope ps(g_prof, st, RRIN_KIND_LAYOUT, 0.0);
+      ProfScope ps(p.prof, st, RRIN_KIND_LAYOUT, 0.0);
       // x0, x1 into channels 0-5; channels 6-15 zeroed, so the first convs (cin 6/9/10)
       // can stage whole records (their tail channels are finite and meet zero weights)
       rc = rrin_pack_g16_h8(d->i0, d->i1, d->n, &gall, d->prec, st);
@@ -407,17 +407,15 @@ extern "C" int rrin_net_fwd(const rrin_net_desc* d, void* stream) {
       if (!(u == 0 && d->skip_flow)) rc = run_unet_h8(p, kUNets[u], d->convs + k, d->heads[u], d, st);
       k += convs_of(kUNets[u].depth);
     }
-    g_prof = nullptr;
     return rc;
   }
 
   // x = cat(x0, x1) into g16 channels 0-5 (model.py:33)
   const rrin_pp gx0 = view(p.G, p.n, 0, 3);
   const rrin_pp gx1 = view(p.G, p.n, 3, 3);
-  g_prof = d->prof;
   int rc = 0;
   {
-    ProfScope ps(g_prof, st, RRIN_KIND_LAYOUT, 0.0);
+    ProfScope ps(p.prof, st, RRIN_KIND_LAYOUT, 0.0);
     rc = rrin_nchw_to_pp(d->i0, d->n, 3, &gx0, st);
     if (!rc) rc = rrin_nchw_to_pp(d->i1, d->n, 3, &gx1, st);
     if (!rc && d->skip_flow) {  // Flow U-Net skipped: t-blend of the kept raw Flow
@@ -431,7 +429,6 @@ extern "C" int rrin_net_fwd(const rrin_net_desc* d, void* stream) {
     if (!(u == 0 && d->skip_flow)) rc = run_unet(p, kUNets[u], d->convs + k, d->heads[u], d, st);
     k += convs_of(kUNets[u].depth);
   }
-  g_prof = nullptr;
   return rc;
 }
 
