@@ -340,6 +340,7 @@ def main():
                 roofline["algorithmic_bytes_per_step_gb"] = round(B * alg / 1e9, 2)
                 roofline["traffic_source"] = "profiles/pmc_traffic.json[" + key + "]"
 
+    eng.check_range()  # fp16-stored precisions: no activation left the fp16 range (raises otherwise)
     gather_check = None
     if world > 1:
         # the gathered output of the last step equals every rank's own shard in
@@ -400,6 +401,7 @@ def main():
         h2 = C.c_void_p()
         _lib.check(lib.rrin_prof_create(cap2, C.byref(h2)), "rrin_prof_create")
         el2, o2 = time_steps(eng2, i0, i1, args.t, args.steps, dev, h2.value, args.streams)
+        eng2.check_range()
         cbusy, cfl, _ = read_prof(lib, h2.value, cap2)
         lib.rrin_prof_destroy(h2.value)
         alt_out = o2[0:1].cpu()

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define RRIN_ABI_VERSION 7
+#define RRIN_ABI_VERSION 8
 
 #define RRIN_OK 0
 #define RRIN_E_SHAPE (-1)     /* H or W not a multiple of 16, or N < 1          */
@@ -126,6 +126,8 @@ typedef struct rrin_head_desc {
   float* out;            /* FINAL: NCHW [n][3][h][w] contiguous               */
   rrin_pp flow_raw;      /* FLOW (optional, base NULL = skip): raw 4-ch Flow output kept
                             for reuse across t                    */
+  float* raw_out;        /* optional (NULL = off): the head conv's output before any glue,
+                            NCHW [n][cout][h][w] fp32 (intermediate-tap parity tests) */
 } rrin_head_desc;
 
 int rrin_head_fwd(const rrin_head_desc* d, void* stream);
@@ -188,6 +190,8 @@ typedef struct rrin_conv_h8_desc {
   const void* wlo;             /* NULL for F16 */
   const float* bias;           /* padded fp32 bias */
   float* edge;                 /* EPI_SUBPIXEL: [n][cout/4][rrin_ring_pixels(H,W)] fp32 */
+  int32_t* status;             /* optional (F16X3 / F16): set to 1 when a stored value does not
+                                  fit fp16 (|v| > 65504, inf or NaN) -- see rrin_net_desc.status */
 } rrin_conv_h8_desc;
 
 int rrin_conv_h8_cfg_count(void);
@@ -236,6 +240,7 @@ typedef struct rrin_edge_fix_desc {
   const float* edge;           /* pre-bias ring values from the EPI_SUBPIXEL conv */
   const float* wedge;          /* original weights as [cin][9][cout] fp32       */
   const float* bias;           /* original bias [cout]                          */
+  int32_t* status;             /* optional: fp16 range flag, as rrin_conv_h8_desc */
 } rrin_edge_fix_desc;
 int rrin_subpixel_edge_fix_h8(const rrin_edge_fix_desc* d, void* stream);
 
@@ -259,6 +264,8 @@ typedef struct rrin_head_h8_desc {
   const float* coef;
   float* out;            /* FINAL: NCHW fp32 */
   rrin_h8 flow_raw;      /* FLOW (optional, hi NULL = skip): raw 4-ch Flow output */
+  float* raw_out;        /* optional: head conv output before the glue, NCHW fp32 */
+  int32_t* status;       /* optional: fp16 range flag; FINAL writes NaN pixels when it is set */
 } rrin_head_h8_desc;
 int rrin_head_h8_fwd(const rrin_head_h8_desc* d, void* stream);
 
@@ -323,6 +330,14 @@ typedef struct rrin_net_desc {
                            reuse its raw Flow (Flow U-Net skipped, t-blend only)      */
   int32_t prec;         /* rrin_prec of the whole forward */
   rrin_prof* prof;      /* nullable: record events around every launch */
+  float* taps;          /* nullable (test / debug): the four U-Nets' raw outputs (their `last`
+                           conv, before the model.py glue) as NCHW fp32, concatenated:
+                           Flow [n][4][h][w] | refine_flow [n][4] | Mask [n][2] | final [n][3]
+                           (unet.py:51 outputs used at model.py:35,42,52,62); n*13*h*w floats */
+  int32_t* status;      /* optional device int32 (F16X3 / F16 range guard): zeroed at the start
+                           of the forward, set to 1 if any activation stored as fp16 overflows
+                           (|v| > 65504, inf, NaN); the output is then all NaN (poisoned) instead
+                           of silently wrong.  fp32 paths never set it. */
 } rrin_net_desc;
 
 int rrin_net_conv_count(void);                 /* 77 = 81 convs - 4 heads      */

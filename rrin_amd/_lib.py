@@ -9,7 +9,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "librrin_hip.so")
 
 # enums (rrin_hip.h)
@@ -49,7 +49,7 @@ class ConvDesc(C.Structure):
 class HeadDesc(C.Structure):
     _fields_ = [("n", C.c_int32), ("cin", C.c_int32), ("cout", C.c_int32), ("mode", C.c_int32),
                 ("src", PP), ("g16", PP), ("w", C.c_void_p), ("bias", C.c_void_p),
-                ("coef", C.c_void_p), ("out", C.c_void_p), ("flow_raw", PP)]
+                ("coef", C.c_void_p), ("out", C.c_void_p), ("flow_raw", PP), ("raw_out", C.c_void_p)]
 
 
 class ConvWeights(C.Structure):
@@ -67,19 +67,20 @@ class ConvH8Desc(C.Structure):
     _fields_ = [("n", C.c_int32), ("cin", C.c_int32), ("cout", C.c_int32), ("cfg", C.c_int32),
                 ("prec", C.c_int32), ("epi_mode", C.c_int32), ("slope", C.c_float), ("inv_wscale", C.c_float),
                 ("tail_finite", C.c_int32), ("pad_", C.c_int32), ("src", H8), ("dst", H8), ("pool", H8), ("whi", C.c_void_p), ("wlo", C.c_void_p),
-                ("bias", C.c_void_p), ("edge", C.c_void_p)]
+                ("bias", C.c_void_p), ("edge", C.c_void_p), ("status", C.c_void_p)]
 
 
 class EdgeFixDesc(C.Structure):
     _fields_ = [("n", C.c_int32), ("cin", C.c_int32), ("cout", C.c_int32), ("prec", C.c_int32),
                 ("epi_mode", C.c_int32), ("slope", C.c_float), ("src", H8), ("dst", H8),
-                ("edge", C.c_void_p), ("wedge", C.c_void_p), ("bias", C.c_void_p)]
+                ("edge", C.c_void_p), ("wedge", C.c_void_p), ("bias", C.c_void_p), ("status", C.c_void_p)]
 
 
 class HeadH8Desc(C.Structure):
     _fields_ = [("n", C.c_int32), ("cin", C.c_int32), ("cout", C.c_int32), ("mode", C.c_int32),
                 ("prec", C.c_int32), ("pad_", C.c_int32), ("src", H8), ("g16", H8), ("w", C.c_void_p),
-                ("bias", C.c_void_p), ("coef", C.c_void_p), ("out", C.c_void_p), ("flow_raw", H8)]
+                ("bias", C.c_void_p), ("coef", C.c_void_p), ("out", C.c_void_p), ("flow_raw", H8),
+                ("raw_out", C.c_void_p), ("status", C.c_void_p)]
 
 
 class HeadWeights(C.Structure):
@@ -91,7 +92,8 @@ class NetDesc(C.Structure):
                 ("i0", C.c_void_p), ("i1", C.c_void_p), ("out", C.c_void_p), ("coef", C.c_void_p),
                 ("convs", C.POINTER(ConvWeights)), ("heads", C.POINTER(HeadWeights)),
                 ("workspace", C.c_void_p), ("workspace_bytes", C.c_int64),
-                ("skip_flow", C.c_int32), ("prec", C.c_int32), ("prof", C.c_void_p)]
+                ("skip_flow", C.c_int32), ("prec", C.c_int32), ("prof", C.c_void_p), ("taps", C.c_void_p),
+                ("status", C.c_void_p)]
 
 
 # every symbol include/rrin_hip.h declares: name -> (restype, argtypes)

@@ -212,9 +212,9 @@ def interpolate_folder(model, src, dest, sf, batch=4, resume=False, device=None,
             ev.record()
         pending.append((ev, host, metas0, metas1, [base_of(k) for k in ks]))
         while len(pending) > 1:  # retire the previous batch while this one computes
-            _retire(pending.pop(0), sf, dest, put)
+            _retire(pending.pop(0), sf, dest, put, model)
     while pending:
-        _retire(pending.pop(0), sf, dest, put)
+        _retire(pending.pop(0), sf, dest, put, model)
     for f in futures:
         f.result()
     if pool is not None:
@@ -250,10 +250,12 @@ def _gather_step(outs, metas0, metas1, nloc, shards, s_, batch, sf, group, devic
     return outs_all, m0, m1, ks
 
 
-def _retire(item, sf, dest, put):
+def _retire(item, sf, dest, put, model=None):
     ev, host, metas0, metas1, bases = item
     if ev is not None:
         ev.synchronize()
+    if model is not None and hasattr(model, "check_range"):
+        model.check_range(wait=False)  # fp16-stored precisions: raise instead of writing NaN frames
     for p, (m0, m1, base) in enumerate(zip(metas0, metas1, bases)):
         for i in range(sf):
             put(lambda t, m, path: save_image(to_uint8_image(t, m), path), host[i][p], m0,

@@ -38,6 +38,7 @@ constexpr int H8_LC = 34;  // staged input row: records of pixels x0-1 .. x0+32
 // |v| >= ~1e-4 (unscaled, v - hi ~ 2^-12 v would be subnormal below |v| = 0.125
 // and lose its bits): v = hi + lo * 2^-11.
 constexpr float kLoScale = 2048.0f;
+constexpr float kF16Max = 65504.0f;  // largest finite fp16
 constexpr float kLoUnscale = 1.0f / 2048.0f;
 __device__ inline _Float16 lo_of(float v, _Float16 hi) { return (_Float16)((v - (float)hi) * kLoScale); }
 __device__ inline float join(_Float16 hi, _Float16 lo) { return fmaf((float)lo, kLoUnscale, (float)hi); }
@@ -81,6 +82,7 @@ struct ConvH8Args {
   int tail_finite;
   float* edge;  // EPI_SUBPIXEL: [n][cout/4][ring] pre-bias values of the 2h x 2w ring
   int64_t ring;
+  int* status;  // optional fp16 range flag (F16X3 / F16)
 };
 
 // Ring index of pixel (y, x) of an H x W image (rrin_ring_pixels order: top
@@ -417,6 +419,11 @@ __global__ void __launch_bounds__(64 * NW) conv3x3_h8_kernel(ConvH8Args a) {
       d[0][rec] = make_uint4(__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
                              __float_as_uint(v[3]));
     } else {
+      // fp16 range guard: a value fp16 cannot hold would become inf / NaN and
+      // could end as a finite but wrong pixel (e.g. a warp of an inf flow
+      // samples zeros); flag it (the FINAL head then poisons the output)
+      if (a.status && !(fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))) <= kF16Max))
+        *a.status = 1;
       uint2 hv, lv;
       split4(v, hv, lv);
       reinterpret_cast<uint2*>(d[0] + rec)[hh] = hv;
@@ -724,6 +731,7 @@ struct EdgeFixArgs {
   float slope;
   int leaky;
   int tiles_row, tiles_col;  // tiles per row line / per column line
+  int* status;               // optional fp16 range flag
 };
 
 // The 4 low-res records (8 halves / 4 floats, both planes) that bilinear x2
@@ -928,6 +936,7 @@ __global__ void __launch_bounds__(256 * KS) edge_fix_h8_kernel(EdgeFixArgs a) {
     if constexpr (F32) {
       a.d_f32[k] = v;
     } else {
+      if (a.status && !(fabsf(v) <= kF16Max)) *a.status = 1;
       const _Float16 vh = (_Float16)v;
       a.d_hi[k] = vh;
       if constexpr (PLANES == 2) a.d_lo[k] = lo_of(v, vh);
@@ -1023,6 +1032,8 @@ struct HeadH8Args {
   int h, w_, tiles_x, tiles_y;
   uint4* g32;       // F32R: g16 as 4 records of 4 fp32 channels (g_img / g_gp / g_wp in records)
   uint4* fr32;      // F32R: raw Flow output, 1 record (nullable)
+  float* raw;       // optional: head conv output before the glue, NCHW [n][COUT][h][w]
+  int* status;      // optional fp16 range flag: glue stores set it, FINAL poisons on it
 };
 
 template <int COUT, int MODE, int PLANES>
@@ -1119,6 +1130,8 @@ __global__ void __launch_bounds__(256) head_h8_kernel(HeadH8Args a) {
   // n consecutive channels starting at half `e0` of record `rec` (one 2/4/8/16-B store per plane)
   auto store = [&](int64_t rec, int e0, const float* v, int n) {
     _Float16 hv[8], lv[8];
+    for (int e = 0; e < n; ++e)
+      if (a.status && !(fabsf(v[e]) <= kF16Max)) *a.status = 1;
     for (int e = 0; e < n; ++e) {
       hv[e] = (_Float16)v[e];
       lv[e] = lo_of(v[e], hv[e]);
@@ -1142,6 +1155,9 @@ __global__ void __launch_bounds__(256) head_h8_kernel(HeadH8Args a) {
     }
   };
   const float* cf = a.coef + img * 8;
+  if (a.raw)
+#pragma unroll
+    for (int co = 0; co < COUT; ++co) a.raw[(((int64_t)img * COUT + co) * a.h + y) * a.w_ + x] = acc[co];
 
   if constexpr (MODE == RRIN_HEAD_PLAIN) {
     for (int co = 0; co < COUT; ++co) {
@@ -1155,6 +1171,8 @@ __global__ void __launch_bounds__(256) head_h8_kernel(HeadH8Args a) {
     // round the raw flow to its stored form first, so that a later t-blend of the
     // kept raw flow (skip_flow) reproduces these Ft bit for bit
     _Float16 rh[4], rl[4];
+    for (int k = 0; k < 4; ++k)
+      if (a.status && !(fabsf(acc[k]) <= kF16Max)) *a.status = 1;
     for (int k = 0; k < 4; ++k) {
       rh[k] = (_Float16)acc[k];
       rl[k] = lo_of(acc[k], rh[k]);
@@ -1224,10 +1242,11 @@ __global__ void __launch_bounds__(256) head_h8_kernel(HeadH8Args a) {
     load8(rec1, g1);
     const float base[3] = {g0[6], g0[7], g1[0]};
     float* o = a.out + ((int64_t)img * 3) * a.h * a.w_ + (int64_t)y * a.w_ + x;
+    const bool poison = a.status && *a.status != 0;  // an fp16 overflow upstream (range guard)
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch) {
       const float v = acc[ch] + base[ch];
-      o[(int64_t)ch * a.h * a.w_] = v < 0.0f ? 0.0f : (v > 1.0f ? 1.0f : v);
+      o[(int64_t)ch * a.h * a.w_] = poison ? __builtin_nanf("") : (v < 0.0f ? 0.0f : (v > 1.0f ? 1.0f : v));
     }
   }
   }
@@ -1462,6 +1481,9 @@ __global__ void __launch_bounds__(256) head_r32_kernel(HeadH8Args a) {
     auto ld = [&](int k) { return __builtin_bit_cast(floatx4, a.g32[rec0 + k * a.g_gp]); };
     auto st = [&](int k, float v0, float v1, float v2, float v3) { a.g32[rec0 + k * a.g_gp] = f4rec(v0, v1, v2, v3); };
     const float* cf = a.coef + img * 8;
+    if (a.raw)
+#pragma unroll
+      for (int co = 0; co < COUT; ++co) a.raw[(((int64_t)img * COUT + co) * a.h + y) * a.w_ + x] = acc[co];
     if constexpr (MODE == RRIN_HEAD_PLAIN) {
       float* gf = reinterpret_cast<float*>(a.g32);
       for (int co = 0; co < COUT; ++co) gf[r32_elem_index(a.g_img, a.g_gp, a.g_wp, img, co, y, x)] = acc[co];
@@ -1793,6 +1815,7 @@ static int h8_prepare(const rrin_conv_h8_desc* d, ConvH8Args& a) {
   a.inv_wscale = d->prec == RRIN_PREC_F32R ? 1.0f : d->inv_wscale;
   a.slope = d->slope;
   a.tail_finite = d->tail_finite;
+  a.status = d->status;
   a.h = h;
   a.w = w;
   if (sub) {
@@ -2057,6 +2080,7 @@ extern "C" int rrin_subpixel_edge_fix_h8(const rrin_edge_fix_desc* d, void* stre
   a.ring = ring_pixels(d->dst.g.h, d->dst.g.w);
   a.slope = d->slope;
   a.leaky = d->epi_mode == RRIN_EPI_LEAKY;
+  a.status = d->status;
   const int H = d->dst.g.h, W = d->dst.g.w;
   a.tiles_row = (W + kFixPx - 1) / kFixPx;
   a.tiles_col = (H - 2 + kFixPx - 1) / kFixPx;
@@ -2199,6 +2223,8 @@ static int head_prepare(const rrin_head_h8_desc* d, HeadH8Args& a, int& grid) {
   a.bias = d->bias;
   a.coef = d->coef;
   a.out = d->out;
+  a.raw = d->raw_out;
+  a.status = d->status;
   if (d->mode == RRIN_HEAD_FLOW && d->flow_raw.hi) {
     if (!h8_ok(d->flow_raw, d->prec) || d->flow_raw.g.h != h || d->flow_raw.g.w != w) return RRIN_E_SHAPE;
     const int64_t fo = (int64_t)d->flow_raw.g_off * d->flow_raw.g.plane * 8;

@@ -34,6 +34,7 @@ struct HeadArgs {
   int64_t fr_img, fr_plane;
   int fr_wp;
   int h, w_, tiles_x, tiles_y;
+  float* raw;        // optional: conv output before the glue, NCHW
 };
 
 constexpr int HC = 8;        // channels per staged chunk
@@ -96,6 +97,9 @@ __global__ void __launch_bounds__(256) head_kernel(HeadArgs a) {
   const int64_t pix = (int64_t)(y + 1) * a.g_wp + x + kPadLeft;
   auto G = [&](int ch) -> float& { return gi[(int64_t)ch * a.g_plane + pix]; };
   const float* cf = a.coef + img * 8;
+  if (a.raw)
+#pragma unroll
+    for (int co = 0; co < COUT; ++co) a.raw[(((int64_t)img * COUT + co) * a.h + y) * a.w_ + x] = acc[co];
 
   if constexpr (MODE == RRIN_HEAD_PLAIN) {
 #pragma unroll
@@ -262,6 +266,7 @@ extern "C" int rrin_head_fwd(const rrin_head_desc* d, void* stream) {
   a.bias = d->bias;
   a.coef = d->coef;
   a.out = d->out;
+  a.raw = d->raw_out;
   a.flow_raw = nullptr;
   if (d->mode == RRIN_HEAD_FLOW && d->flow_raw.base) {
     if (d->flow_raw.channels < 4 || d->flow_raw.g.h != h || d->flow_raw.g.w != w || d->flow_raw.g.wp != gg.wp)

@@ -47,6 +47,7 @@ struct Buf {
 struct Plan {
   int n, prec;
   rrin_prof* prof;        // the caller's launch profiler of this call (nullable)
+  int32_t* status;        // the caller's fp16 range flag (nullable)
   rrin_geom g[kMaxDepth];
   Buf G;                  // 16 ch at level 0
   Buf X[kMaxDepth];       // level input (L >= 1): C_{L-1} ch
@@ -69,6 +70,7 @@ void make_plan(int n, int h, int w, int prec, char* base, Plan& p) {
   p.n = n;
   p.prec = prec;
   p.prof = nullptr;
+  p.status = nullptr;
   const bool f32 = prec == RRIN_PREC_F32;
   const int planes = prec == RRIN_PREC_F16X3 ? 2 : 1;
   const int cpr = prec == RRIN_PREC_F32R ? 4 : 8;
@@ -181,6 +183,18 @@ int conv(const Plan& p, const rrin_conv_weights& cw, int cin, int cout, int src_
   return rrin_conv3x3_fwd(&d, st);
 }
 
+// Debug taps (rrin_net_desc.taps): where U-Net u's raw output goes, or NULL.
+float* tap_of(const rrin_net_desc* nd, const UNetSpec& u) {
+  if (!nd->taps) return nullptr;
+  const int64_t px = (int64_t)nd->n * nd->h * nd->w;
+  int64_t off = 0;
+  for (const auto& v : kUNets) {
+    if (&v == &u) return nd->taps + off;
+    off += v.out_ch * px;
+  }
+  return nullptr;
+}
+
 #define RRIN_TRY(x)          \
   do {                       \
     int _rc = (x);           \
@@ -235,6 +249,7 @@ int run_unet(const Plan& p, const UNetSpec& u, const rrin_conv_weights* cw, cons
   hd.bias = hw.bias;
   hd.coef = nd->coef;
   hd.out = nd->out;
+  hd.raw_out = tap_of(nd, u);
   if (u.head_mode == RRIN_HEAD_FLOW) hd.flow_raw = view(p.FLOWRAW, p.n, 0, 4);
   ProfScope ps(p.prof, st, RRIN_KIND_HEAD, 2.0 * 9 * 32 * u.out_ch * (double)x.g.h * x.g.w * p.n);
   return rrin_head_fwd(&hd, st);
@@ -263,6 +278,7 @@ int conv_h8(const Plan& p, const rrin_conv_weights& cw, int cin, int cout, int e
   d.wlo = cw.wlo;
   d.bias = cw.bias;
   d.edge = edge;
+  d.status = p.status;
   return rrin_conv3x3_h8_fwd(&d, st);
 }
 
@@ -283,6 +299,7 @@ int upconv_subpixel(const Plan& p, const rrin_conv_weights& cw, int C, const rri
   e.edge = p.EDGE;
   e.wedge = cw.wedge;
   e.bias = cw.bias_raw;
+  e.status = p.status;
   ProfScope ps(p.prof, st, RRIN_KIND_EDGE, 0.0);
   return rrin_subpixel_edge_fix_h8(&e, st);
 }
@@ -352,6 +369,8 @@ int run_unet_h8(const Plan& p, const UNetSpec& u, const rrin_conv_weights* cw, c
   hd.bias = hw.bias;
   hd.coef = nd->coef;
   hd.out = nd->out;
+  hd.raw_out = tap_of(nd, u);
+  hd.status = p.status;
   if (u.head_mode == RRIN_HEAD_FLOW) hd.flow_raw = hview(p.FLOWRAW, 0, 4);
   ProfScope ps(p.prof, st, RRIN_KIND_HEAD, 2.0 * 9 * 32 * u.out_ch * (double)x.g.h * x.g.w * p.n);
   return rrin_head_h8_fwd(&hd, st);
@@ -389,6 +408,10 @@ extern "C" int rrin_net_fwd(const rrin_net_desc* d, void* stream) {
   if (d->workspace_bytes < p.bytes) return RRIN_E_WORKSPACE;
   p.prof = d->prof;  // per call: concurrent calls never share launch state
   hipStream_t st = (hipStream_t)stream;
+  if (d->status && (d->prec == RRIN_PREC_F16X3 || d->prec == RRIN_PREC_F16)) {
+    p.status = d->status;
+    if (hipError_t e = hipMemsetAsync(d->status, 0, sizeof(int32_t), st)) return (int)e;
+  }
   if (d->prec != RRIN_PREC_F32) {
     const rrin_h8 gall = hview(p.G, 0, 16);
     int rc = 0;

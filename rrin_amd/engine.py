@@ -222,6 +222,8 @@ class RRINEngine:
         self._ws = OrderedDict()
         self._flow_valid = {}
         self._sides = []
+        self._status = {}
+        self._pending_status = []
 
     def _init_h8(self, net):
         """Pack for the split-fp16 (F16X3) or fp16 (F16) path: [cob][16-ch chunk][tap][half][bm][8]
@@ -269,6 +271,8 @@ class RRINEngine:
         self._ws = OrderedDict()
         self._flow_valid = {}
         self._sides = []
+        self._status = {}           # slot -> device int32 range flag (fp16-stored precisions)
+        self._pending_status = []   # (event, pinned host copy) of flags not checked yet
 
     def _pack_h8(self, size: str):
         """(halves blob, bias blob, ConvWeights table, cfgs) of size class ``size``, cached;
@@ -384,7 +388,7 @@ class RRINEngine:
         return self._sides[:k]
 
     def forward(self, i0: torch.Tensor, i1: torch.Tensor, t=0.5, prof=None, reuse_flow: bool = False,
-                streams: int = 1, split=None) -> torch.Tensor:
+                streams: int = 1, split=None, taps: dict | None = None) -> torch.Tensor:
         """One Net.forward.  ``reuse_flow=True`` promises that (i0, i1) is the pair
         of the previous call with the same shape: the Flow U-Net (t-independent,
         model.py:35, 30 % of the FLOPs) is skipped and its kept raw output is
@@ -392,7 +396,12 @@ class RRINEngine:
         into that many contiguous parts, each with its own workspace, enqueued
         on its own HIP stream: the parts' kernels overlap, filling each other's
         launch gaps and last-wave tails (pairs are independent, so the output is
-        bitwise the same).  ``split`` gives the part sizes explicitly."""
+        bitwise the same).  ``split`` gives the part sizes explicitly.
+
+        ``taps`` (test / debug, one stream only): a dict that receives the four
+        U-Nets' raw outputs (their ``last`` conv before the model.py glue,
+        unet.py:51 as used at model.py:35,42,52,62) as NCHW fp32 tensors under
+        "Flow", "refine_flow", "Mask", "final"."""
         if i0.device != self.device or i1.device != self.device:
             raise RuntimeError(f"inputs on {i0.device}/{i1.device}, model on {self.device}")
         if i0.dtype != torch.float32 or i1.dtype != torch.float32:
@@ -403,6 +412,7 @@ class RRINEngine:
         if h % 16 or w % 16 or n < 1:
             raise RuntimeError(f"H and W must be multiples of 16 (the Flow U-Net pools 4 times); "
                                f"got {h}x{w} (reference fails at model.py:41)")
+        self._poll_range()
         i0 = i0.contiguous()
         i1 = i1.contiguous()
         out = torch.empty_like(i0)
@@ -419,6 +429,13 @@ class RRINEngine:
         else:
             k = max(1, min(int(streams), n))
             bounds = [(n * j // k, n * (j + 1) // k) for j in range(k)]
+        tapbuf = None
+        if taps is not None:
+            if len(bounds) != 1:
+                raise ValueError("taps need a single forward part (streams=1)")
+            if reuse_flow:
+                raise ValueError("taps need the Flow U-Net to run (reuse_flow=False)")
+            tapbuf = torch.full((13 * n * h * w,), float("nan"), dtype=torch.float32, device=self.device)
         with torch.cuda.device(self.device):
             main = torch.cuda.current_stream(self.device)
             # workspaces first: a new one is zero-filled on the main stream, before the fork
@@ -428,12 +445,18 @@ class RRINEngine:
                 s.wait_stream(main)
             for j, (lo, hi) in enumerate(bounds):
                 st = main if j == 0 else sides[j - 1]
-                self._forward_part(i0[lo:hi], i1[lo:hi], out[lo:hi], coef[lo:hi], j, wss[j], st, prof, reuse_flow)
+                self._forward_part(i0[lo:hi], i1[lo:hi], out[lo:hi], coef[lo:hi], j, wss[j], st, prof, reuse_flow,
+                                   tapbuf)
             for s in sides:
                 main.wait_stream(s)
+        if tapbuf is not None:
+            off = 0
+            for name, c in zip(UNET_ORDER, (4, 4, 2, 3)):
+                taps[name] = tapbuf[off:off + n * c * h * w].view(n, c, h, w)
+                off += n * c * h * w
         return out
 
-    def _forward_part(self, i0, i1, out, coef, slot, ws, stream, prof, reuse_flow):
+    def _forward_part(self, i0, i1, out, coef, slot, ws, stream, prof, reuse_flow, tapbuf=None):
         n, _, h, w = i0.shape
         key = (n, h, w, slot)
         skip = bool(reuse_flow) and self._flow_valid.get(key, False)
@@ -447,5 +470,46 @@ class RRINEngine:
         d.skip_flow = 1 if skip else 0
         d.prec = self.prec
         d.prof = prof
+        d.taps = tapbuf.data_ptr() if tapbuf is not None else None
+        st = self._status_of(slot) if self.prec in (_lib.PREC_F16X3, _lib.PREC_F16) else None
+        d.status = st.data_ptr() if st is not None else None
         _lib.check(self.lib.rrin_net_fwd(C.byref(d), C.c_void_p(stream.cuda_stream)), "rrin_net_fwd")
         self._flow_valid[key] = True
+        if st is not None:
+            host = torch.empty(1, dtype=torch.int32, pin_memory=True)
+            with torch.cuda.stream(stream):
+                host.copy_(st, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(stream)
+            self._pending_status.append((ev, host))
+
+    # ---- fp16 range guard (fp32_split16 / fp16) ---------------------------------
+    # Activations of these precisions are stored as fp16; a value beyond 65504
+    # sets the forward's status flag and poisons its output with NaN (device
+    # side, no sync).  The flag is also checked on the host: the next forward
+    # raises once the flagged one has finished, and check_range() waits and raises.
+    def _status_of(self, slot):
+        st = self._status.get(slot)
+        if st is None:
+            st = torch.zeros(1, dtype=torch.int32, device=self.device)
+            self._status[slot] = st
+        return st
+
+    def _poll_range(self, wait: bool = False):
+        keep = []
+        for ev, host in self._pending_status:
+            if wait:
+                ev.synchronize()
+            elif not ev.query():
+                keep.append((ev, host))
+                continue
+            if int(host.item()) != 0:
+                self._pending_status = []
+                raise RuntimeError(
+                    f"rrin_amd: an activation exceeded the fp16 range (|v| > 65504) in precision "
+                    f"'{self.precision}'; the affected outputs are NaN.  Use precision='fp32' (exact fp32).")
+        self._pending_status = keep
+
+    def check_range(self):
+        """Wait for every forward issued so far and raise if one overflowed fp16."""
+        self._poll_range(wait=True)

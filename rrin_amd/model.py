@@ -89,6 +89,14 @@ class Net(nn.Module):
             self._engine_fp = fp
         return self._engine
 
+    def check_range(self, wait: bool = True):
+        """fp32_split16 / fp16: raise if an activation overflowed fp16 in a
+        forward issued so far (those outputs are NaN-poisoned on the device).
+        ``wait=False`` only looks at the forwards that have already finished.
+        A no-op for the fp32 precisions."""
+        if self._engine is not None:
+            self._engine._poll_range(wait=wait)
+
     def interpolate(self, input0, input1, ts):
         """All intermediate frames of one (batch of) pair(s): ``[forward(I0, I1, t) for t in ts]``
         with the t-independent Flow U-Net computed once (the

@@ -56,7 +56,7 @@ def test_net_golden_odd_levels(gpu, golden, nets):
 
 
 @pytest.mark.parametrize("h,w,n,which", [(256, 256, 1, "stress"), (368, 640, 1, "default"),
-                                         (720, 1280, 1, "default")])
+                                         (720, 1280, 1, "default"), (720, 1280, 1, "stress")])
 def test_net_vs_oracle(gpu, nets, h, w, n, which):
     """Larger sizes against the CPU oracle (same torch-op sequence as the reference)."""
     i0, i1 = synthetic_batch(n, h, w, first_index=17)
