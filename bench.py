@@ -87,6 +87,9 @@ def parse():
     ap.add_argument("--streams", type=int, default=2,
                     help="HIP streams the rank's pairs are split over (their kernels overlap, filling each "
                          "other's launch gaps and last-wave tails; outputs are bitwise those of one stream)")
+    ap.add_argument("--dist-init", action="store_true",
+                    help="initialise torch.distributed and run the all-gather path even at WORLD_SIZE 1 "
+                         "(exercises RCCL / the gather check on a single GPU)")
     ap.add_argument("--split", default=None,
                     help="explicit pairs per stream, e.g. 1,3 (overrides --streams' even split)")
     return ap.parse_args()
@@ -187,7 +190,13 @@ def main():
     local = local % max(torch.cuda.device_count(), 1)  # rehearsal: several ranks may share a GPU
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    distributed = world > 1 or args.dist_init
+    if distributed:
+        if args.dist_init and world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29533")
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -202,7 +211,7 @@ def main():
     i0, i1 = synthetic_batch(B, H, W, first_index=rank * B)
     i0, i1 = i0.to(dev), i1.to(dev)
     # the all-gather of step k overlaps the compute of step k+1 (double-buffered outputs)
-    gather = GatherPipeline((world * B, 3, H, W), torch.float32, dev) if world > 1 else None
+    gather = GatherPipeline((world * B, 3, H, W), torch.float32, dev) if distributed else None
     eng = net.engine()
     lib = _lib.lib()
     split = [int(c) for c in args.split.split(",")] if args.split else None
@@ -233,7 +242,7 @@ def main():
         _lib.check(lib.rrin_prof_create(cap, C.byref(h)), "rrin_prof_create")
         prof = h.value
 
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -242,10 +251,10 @@ def main():
     if gather is not None:
         gather.drain()  # every step's gather is inside the timed region
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if distributed:
         tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
@@ -254,7 +263,7 @@ def main():
     # ~1 % of the rate at 720p x4, ~15 % at 640x368 x1): reported beside `value`
     unprofiled = None
     if prof is not None:
-        if world > 1:
+        if distributed:
             dist.barrier()
         torch.cuda.synchronize(dev)
         u0 = time.perf_counter()
@@ -263,10 +272,10 @@ def main():
         if gather is not None:
             gather.drain()
         torch.cuda.synchronize(dev)
-        if world > 1:
+        if distributed:
             dist.barrier()
         uel = time.perf_counter() - u0
-        if world > 1:
+        if distributed:
             tt = torch.tensor([uel], device=dev, dtype=torch.float64)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             uel = float(tt.item())
@@ -342,7 +351,7 @@ def main():
 
     eng.check_range()  # fp16-stored precisions: no activation left the fp16 range (raises otherwise)
     gather_check = None
-    if world > 1:
+    if distributed:
         # the gathered output of the last step equals every rank's own shard in
         # rank order: per-rank checksums of the local output vs the gather's slices
         gather.drain()
@@ -422,7 +431,7 @@ def main():
             res[alt_key]["parity"] = res["parity"].pop("alt")
     if rank == 0:
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
 
 

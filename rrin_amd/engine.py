@@ -103,11 +103,39 @@ H8_TUNED_BY_SIZE = {
 }
 
 
+LARGE_PX = 2_500_000
+XLARGE_PX = 6_000_000
+# Bigger forward parts (one stream over 720p x 4, the 4K share of config C5):
+# fp32 records "xlarge" = the sweep at 1280x720 x 4 (3.7 Mpx per launch,
+# profiles/r02/tune_fp32r_1280x720x4.txt), "xxlarge" = the sweep at 3840x2176 x 1
+# (8.4 Mpx, profiles/r02/c5_4k/tune_fp32r_3840x2176x1.txt); fp16 "xxlarge" = the
+# C5 4K sweep (profiles/r02/c5_4k/tune_fp16_3840x2176x1.txt).  A class a
+# precision has no table for uses H8_TUNED.
+H8_TUNED_BY_SIZE["xlarge"] = {
+    _lib.PREC_F32R: {(6, 32, 0): 13, (9, 32, 0): 15, (10, 32, 0): 15, (16, 32, 0): 15, (32, 32, 0): 9,
+                     (32, 64, 1): 8, (64, 32, 0): 9, (64, 64, 1): 1, (64, 128, 1): 1, (64, 128, 2): 4,
+                     (128, 64, 1): 1, (128, 128, 2): 5, (128, 256, 2): 1, (128, 256, 3): 5, (256, 128, 2): 5,
+                     (256, 256, 3): 5, (256, 512, 3): 5, (256, 512, 4): 4, (512, 256, 3): 5, (512, 512, 4): 4}}
+H8_TUNED_BY_SIZE["xxlarge"] = {
+    _lib.PREC_F32R: {(6, 32, 0): 9, (9, 32, 0): 13, (10, 32, 0): 9, (16, 32, 0): 8, (32, 32, 0): 9,
+                     (32, 64, 1): 9, (64, 32, 0): 9, (64, 64, 1): 1, (64, 128, 1): 1, (64, 128, 2): 5,
+                     (128, 64, 1): 1, (128, 128, 2): 5, (128, 256, 2): 5, (128, 256, 3): 5, (256, 128, 2): 5,
+                     (256, 256, 3): 5, (256, 512, 3): 5, (256, 512, 4): 4, (512, 256, 3): 5, (512, 512, 4): 4},
+    _lib.PREC_F16: {(6, 32, 0): 13, (9, 32, 0): 13, (10, 32, 0): 15, (16, 32, 0): 9, (32, 32, 0): 9,
+                    (32, 64, 1): 10, (64, 32, 0): 9, (64, 64, 1): 10, (64, 128, 1): 10, (64, 128, 2): 10,
+                    (128, 64, 1): 10, (128, 128, 2): 11, (128, 256, 2): 11, (128, 256, 3): 10, (256, 128, 2): 11,
+                    (256, 256, 3): 11, (256, 512, 3): 11, (256, 512, 4): 1, (512, 256, 3): 11, (512, 512, 4): 11}}
+
+
 def size_class(pixels: int) -> str:
     """Tile-table class of a forward part of ``pixels`` = n*h*w output pixels."""
     if pixels <= SMALL_PX:
         return "small"
-    return "medium" if pixels <= MEDIUM_PX else "large"
+    if pixels <= MEDIUM_PX:
+        return "medium"
+    if pixels <= LARGE_PX:
+        return "large"
+    return "xlarge" if pixels <= XLARGE_PX else "xxlarge"
 
 
 def choose_cfg_h8(cin: int, cout: int, prec: int, level: int = 0, size: str = "large") -> int:

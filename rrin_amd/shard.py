@@ -28,11 +28,11 @@ def gather_frames(local: torch.Tensor, group=None, out: torch.Tensor | None = No
     ``async_op=True`` returns ``(out, work)``: on RCCL the gather runs on the
     communicator's stream and ``work.wait()`` orders the caller's stream after
     it; gloo (CPU tests / single-GPU rehearsal) completes before returning."""
-    world = dist.get_world_size(group)
     work = None
-    if world == 1:
+    if not (dist.is_available() and dist.is_initialized()):  # single process, no group: identity
         out = local if out is None else out.copy_(local)
         return (out, work) if async_op else out
+    world = dist.get_world_size(group)   # world 1 still goes through the backend (RCCL rehearsal)
     local = local.contiguous()
     if out is None:
         out = torch.empty((world * local.shape[0],) + tuple(local.shape[1:]),

@@ -208,7 +208,7 @@ def test_size_class_tables_bitwise(gpu, nets, precision):
         i0, i1 = synthetic_batch(2, 128, 192)
         i0, i1 = i0.to(gpu), i1.to(gpu)
         outs = {}
-        for cls in ("small", "medium", "large"):
+        for cls in ("small", "medium", "large", "xlarge", "xxlarge"):
             table = eng._pack_h8(cls)[2]
             eng.conv_table_for = lambda n, h, w, t=table: t
             with torch.no_grad():
@@ -216,6 +216,7 @@ def test_size_class_tables_bitwise(gpu, nets, precision):
             del eng.conv_table_for
         assert torch.equal(outs["small"], outs["large"])
         assert torch.equal(outs["medium"], outs["large"])
+        assert torch.equal(outs["xlarge"], outs["large"]) and torch.equal(outs["xxlarge"], outs["large"])
     finally:
         net.precision = "fp32"
 

@@ -141,3 +141,5 @@ def test_size_class_tables():
     assert engine.size_class(640 * 368) == "small"
     assert engine.size_class(1280 * 720) == "medium"
     assert engine.size_class(2 * 1280 * 720) == "large"
+    assert engine.size_class(4 * 1280 * 720) == "xlarge"
+    assert engine.size_class(3840 * 2176) == "xxlarge"
