@@ -341,6 +341,28 @@ typedef struct rrin_net_desc {
 } rrin_net_desc;
 
 int rrin_net_conv_count(void);                 /* 77 = 81 convs - 4 heads      */
+
+/* One U-Net alone -- the reference UNet(in_channels, n_classes, depth).forward
+ * (unet.py:40-51): x NCHW [n][in_ch][h][w] -> y NCHW [n][out_ch][h][w], with
+ * the Net's kernels and workspace plan (rrin_net_workspace_bytes of the same
+ * n, h, w, prec); in_ch <= 16, out_ch 2..4, depth 2..5.  convs: the U-Net's
+ * rrin_unet_conv_count(depth) body convs in UNet order (down a/b per level,
+ * mid, up/a/b per level), packed as for rrin_net_fwd (no input permutation);
+ * head: its `last` conv, OIHW.  Channels [in_ch, 16) of the workspace's input
+ * buffer must be finite (a zero-filled workspace only ever used for U-Nets of
+ * one in_ch keeps them zero). */
+typedef struct rrin_unet_desc {
+  int32_t n, h, w, in_ch, out_ch, depth, prec, pad_;
+  const float* x;
+  float* y;
+  const rrin_conv_weights* convs;  /* host array */
+  rrin_head_weights head;
+  void* workspace;
+  int64_t workspace_bytes;
+  rrin_prof* prof;                 /* nullable */
+} rrin_unet_desc;
+int64_t rrin_unet_conv_count(int32_t depth);
+int rrin_unet_fwd(const rrin_unet_desc* d, void* stream);
 int64_t rrin_net_workspace_bytes(int32_t n, int32_t h, int32_t w, int32_t prec);
 int rrin_net_fwd(const rrin_net_desc* d, void* stream);
 

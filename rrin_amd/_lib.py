@@ -96,6 +96,13 @@ class NetDesc(C.Structure):
                 ("status", C.c_void_p)]
 
 
+class UNetDesc(C.Structure):
+    _fields_ = [("n", C.c_int32), ("h", C.c_int32), ("w", C.c_int32), ("in_ch", C.c_int32), ("out_ch", C.c_int32),
+                ("depth", C.c_int32), ("prec", C.c_int32), ("pad_", C.c_int32), ("x", C.c_void_p), ("y", C.c_void_p),
+                ("convs", C.POINTER(ConvWeights)), ("head", HeadWeights), ("workspace", C.c_void_p),
+                ("workspace_bytes", C.c_int64), ("prof", C.c_void_p)]
+
+
 # every symbol include/rrin_hip.h declares: name -> (restype, argtypes)
 SIGNATURES = {
     "rrin_make_geom": (C.c_int, [C.c_int32, C.c_int32, C.POINTER(Geom)]),
@@ -142,6 +149,8 @@ SIGNATURES = {
     "rrin_flow_tblend_h8": (C.c_int, [C.POINTER(H8), C.POINTER(H8), C.c_void_p, C.c_int32, C.c_int32,
                                       C.c_void_p]),
     "rrin_net_fwd": (C.c_int, [C.POINTER(NetDesc), C.c_void_p]),
+    "rrin_unet_conv_count": (C.c_int64, [C.c_int32]),
+    "rrin_unet_fwd": (C.c_int, [C.POINTER(UNetDesc), C.c_void_p]),
     "rrin_prof_create": (C.c_int, [C.c_int32, C.POINTER(C.c_void_p)]),
     "rrin_prof_destroy": (C.c_int, [C.c_void_p]),
     "rrin_prof_reset": (C.c_int, [C.c_void_p]),

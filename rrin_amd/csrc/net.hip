@@ -183,6 +183,14 @@ int conv(const Plan& p, const rrin_conv_weights& cw, int cin, int cout, int src_
   return rrin_conv3x3_fwd(&d, st);
 }
 
+// Where a U-Net's head sends its results: per-image t coefficients and the
+// Net output (Net glue modes), and the optional raw conv output (NCHW).
+struct HeadIO {
+  const float* coef;
+  float* out;
+  float* raw;
+};
+
 // Debug taps (rrin_net_desc.taps): where U-Net u's raw output goes, or NULL.
 float* tap_of(const rrin_net_desc* nd, const UNetSpec& u) {
   if (!nd->taps) return nullptr;
@@ -203,7 +211,7 @@ float* tap_of(const rrin_net_desc* nd, const UNetSpec& u) {
 
 // One U-Net (unet.py:40-51) from g16 channels [0, in_ch) to its head.
 int run_unet(const Plan& p, const UNetSpec& u, const rrin_conv_weights* cw, const rrin_head_weights& hw,
-             const rrin_net_desc* nd, hipStream_t st) {
+             const HeadIO& io, hipStream_t st) {
   const int D = u.depth;
   int k = 0;
   // ---- down path (unet.py:42-46)
@@ -247,9 +255,9 @@ int run_unet(const Plan& p, const UNetSpec& u, const rrin_conv_weights* cw, cons
   hd.g16 = view(p.G, p.n, 0, 16);
   hd.w = hw.w;
   hd.bias = hw.bias;
-  hd.coef = nd->coef;
-  hd.out = nd->out;
-  hd.raw_out = tap_of(nd, u);
+  hd.coef = io.coef;
+  hd.out = io.out;
+  hd.raw_out = io.raw;
   if (u.head_mode == RRIN_HEAD_FLOW) hd.flow_raw = view(p.FLOWRAW, p.n, 0, 4);
   ProfScope ps(p.prof, st, RRIN_KIND_HEAD, 2.0 * 9 * 32 * u.out_ch * (double)x.g.h * x.g.w * p.n);
   return rrin_head_fwd(&hd, st);
@@ -309,7 +317,7 @@ int upconv_subpixel(const Plan& p, const rrin_conv_weights& cw, int C, const rri
 // writes the low-res tensor into LRB with edge-replicate padding) or runs after
 // an explicit upsample pass into UPT.
 int run_unet_h8(const Plan& p, const UNetSpec& u, const rrin_conv_weights* cw, const rrin_head_weights& hw,
-                const rrin_net_desc* nd, hipStream_t st) {
+                const HeadIO& io, hipStream_t st) {
   const int D = u.depth;
   int k = 0;
   rrin_h8 x;
@@ -367,9 +375,9 @@ int run_unet_h8(const Plan& p, const UNetSpec& u, const rrin_conv_weights* cw, c
   hd.g16 = hview(p.G, 0, 16);
   hd.w = hw.w;
   hd.bias = hw.bias;
-  hd.coef = nd->coef;
-  hd.out = nd->out;
-  hd.raw_out = tap_of(nd, u);
+  hd.coef = io.coef;
+  hd.out = io.out;
+  hd.raw_out = io.raw;
   hd.status = p.status;
   if (u.head_mode == RRIN_HEAD_FLOW) hd.flow_raw = hview(p.FLOWRAW, 0, 4);
   ProfScope ps(p.prof, st, RRIN_KIND_HEAD, 2.0 * 9 * 32 * u.out_ch * (double)x.g.h * x.g.w * p.n);
@@ -427,7 +435,8 @@ extern "C" int rrin_net_fwd(const rrin_net_desc* d, void* stream) {
     }
     int k = 0;
     for (int u = 0; u < 4 && !rc; ++u) {
-      if (!(u == 0 && d->skip_flow)) rc = run_unet_h8(p, kUNets[u], d->convs + k, d->heads[u], d, st);
+      if (!(u == 0 && d->skip_flow))
+        rc = run_unet_h8(p, kUNets[u], d->convs + k, d->heads[u], HeadIO{d->coef, d->out, tap_of(d, kUNets[u])}, st);
       k += convs_of(kUNets[u].depth);
     }
     return rc;
@@ -449,10 +458,47 @@ extern "C" int rrin_net_fwd(const rrin_net_desc* d, void* stream) {
   }
   int k = 0;
   for (int u = 0; u < 4 && !rc; ++u) {
-    if (!(u == 0 && d->skip_flow)) rc = run_unet(p, kUNets[u], d->convs + k, d->heads[u], d, st);
+    if (!(u == 0 && d->skip_flow))
+      rc = run_unet(p, kUNets[u], d->convs + k, d->heads[u], HeadIO{d->coef, d->out, tap_of(d, kUNets[u])}, st);
     k += convs_of(kUNets[u].depth);
   }
   return rc;
+}
+
+// One U-Net alone (reference UNet.forward, unet.py:40-51): NCHW in -> NCHW out,
+// the same kernels and workspace plan as the Net (input in the Net buffer's
+// channels [0, in_ch), head in PLAIN mode with its raw NCHW output as y).
+extern "C" int64_t rrin_unet_conv_count(int32_t depth) {
+  return (depth < 2 || depth > kMaxDepth) ? RRIN_E_ARG : convs_of(depth);
+}
+
+extern "C" int rrin_unet_fwd(const rrin_unet_desc* d, void* stream) {
+  if (!d || !d->x || !d->y || !d->convs || !d->head.w || !d->head.bias || !d->workspace) return RRIN_E_ARG;
+  if (d->n < 1 || d->h < 16 || d->w < 16 || (d->h % 16) || (d->w % 16)) return RRIN_E_SHAPE;
+  if (d->in_ch < 1 || d->in_ch > 16 || d->out_ch < 2 || d->out_ch > 4 || d->depth < 2 || d->depth > kMaxDepth)
+    return RRIN_E_ARG;
+  if (d->prec < RRIN_PREC_F32 || d->prec > RRIN_PREC_F32R) return RRIN_E_ARG;
+  Plan p;
+  make_plan(d->n, d->h, d->w, d->prec, reinterpret_cast<char*>(d->workspace), p);
+  if (d->workspace_bytes < p.bytes) return RRIN_E_WORKSPACE;
+  p.prof = d->prof;
+  hipStream_t st = (hipStream_t)stream;
+  const UNetSpec u{d->in_ch, d->out_ch, d->depth, RRIN_HEAD_PLAIN};
+  const HeadIO io{nullptr, nullptr, d->y};
+  int rc;
+  {
+    ProfScope ps(p.prof, st, RRIN_KIND_LAYOUT, 0.0);
+    if (d->prec == RRIN_PREC_F32) {
+      const rrin_pp gx = view(p.G, p.n, 0, d->in_ch);
+      rc = rrin_nchw_to_pp(d->x, d->n, d->in_ch, &gx, st);
+    } else {
+      const rrin_h8 gx = hview(p.G, 0, 16);
+      rc = rrin_nchw_to_h8(d->x, d->n, d->in_ch, 0, &gx, d->prec, st);
+    }
+  }
+  if (rc) return rc;
+  return d->prec == RRIN_PREC_F32 ? run_unet(p, u, d->convs, d->head, io, st)
+                                  : run_unet_h8(p, u, d->convs, d->head, io, st);
 }
 
 extern "C" int rrin_prof_create(int32_t capacity, rrin_prof** out) {

@@ -181,9 +181,15 @@ def t_coefficients(t, n: int) -> torch.Tensor:
 class RRINEngine:
     MAX_WORKSPACES = 4
 
-    def __init__(self, net, precision: str = "fp32", subpixel_max_level: int = 2):
+    def __init__(self, net, precision: str = "fp32", subpixel_max_level: int = 2, units=None):
+        """``units``: the U-Nets to pack, as (name, UNet, first-conv input permutation);
+        default the Net's four in execution order (UNET_ORDER, FIRST_CONV_PERM)."""
         self.lib = _lib.lib()
         self.subpixel_max_level = subpixel_max_level
+        if units is None:
+            units = [(name, getattr(net, name), FIRST_CONV_PERM[name]) for name in UNET_ORDER]
+        self.units = units
+        self.expected_convs = sum(2 * u.depth + 1 + 3 * (u.depth - 1) for _, u, _ in units)
         params = list(net.parameters())
         self.device = params[0].device
         if self.device.type != "cuda":
@@ -202,8 +208,7 @@ class RRINEngine:
             return
         self._levels32 = []         # grid level per body conv (fp32 path)
         self._table32_small = None  # small size class: TH 4 tiles at levels >= 1
-        for name in UNET_ORDER:
-            unet = getattr(net, name)
+        for name, unet, first_perm in self.units:
             convs = unet.conv_list()
             for idx, (tag, conv) in enumerate(convs):
                 w = conv.weight.detach().to("cpu", torch.float32).contiguous().numpy()
@@ -220,7 +225,7 @@ class RRINEngine:
                 nb = L.rrin_pack_bias_floats(cout, bm)
                 wp = np.empty(nw, np.float32)
                 bp = np.empty(nb, np.float32)
-                perm = FIRST_CONV_PERM[name] if idx == 0 else None
+                perm = first_perm if idx == 0 else None
                 perm_arr = np.asarray(perm, np.int32) if perm is not None else None
                 _lib.check(L.rrin_pack_conv3x3(w.ctypes.data, b.ctypes.data, cout, cin, bm,
                                                perm_arr.ctypes.data if perm_arr is not None else None,
@@ -233,8 +238,8 @@ class RRINEngine:
                 if pad:
                     blobs.append(np.zeros(pad, np.float32))
                     off += pad
-        if len(meta) != L.rrin_net_conv_count():
-            raise RuntimeError(f"packed {len(meta)} convs, library expects {L.rrin_net_conv_count()}")
+        if len(meta) != self.expected_convs:
+            raise RuntimeError(f"packed {len(meta)} convs, expected {self.expected_convs}")
         self.blob = torch.from_numpy(np.concatenate(blobs)).to(self.device)
         base = self.blob.data_ptr()
         self.conv_table = (_lib.ConvWeights * len(meta))()
@@ -242,7 +247,7 @@ class RRINEngine:
             self.conv_table[i].wpack = base + 4 * wo
             self.conv_table[i].bias = base + 4 * bo
             self.conv_table[i].cfg = cfg
-        self.head_table = (_lib.HeadWeights * 4)()
+        self.head_table = (_lib.HeadWeights * len(self.heads_t))()
         for i, (w, b) in enumerate(self.heads_t):
             self.head_table[i].w = w.data_ptr()
             self.head_table[i].bias = b.data_ptr()
@@ -261,8 +266,7 @@ class RRINEngine:
         L = self.lib
         self.edge_t = []  # device tensors referenced by the tables (sub-pixel convs)
         self._h8_convs = []  # (w, b, cin, cout rows, grid level, first-conv perm, edge) per body conv
-        for name in UNET_ORDER:
-            unet = getattr(net, name)
+        for name, unet, first_perm in self.units:
             for idx, (tag, conv) in enumerate(unet.conv_list()):
                 w = conv.weight.detach().to("cpu", torch.float32).contiguous().numpy()
                 b = conv.bias.detach().to("cpu", torch.float32).contiguous().numpy()
@@ -284,12 +288,12 @@ class RRINEngine:
                             torch.from_numpy(b.copy()).to(self.device))
                     self.edge_t.append(edge)
                     w, b, cout = ws, bs, 4 * cout
-                perm = FIRST_CONV_PERM[name] if idx == 0 else None
+                perm = first_perm if idx == 0 else None
                 perm_arr = np.asarray(perm, np.int32) if perm is not None else None
                 self._h8_convs.append((w, b, cin, cout, level, perm_arr, edge))
-        if len(self._h8_convs) != L.rrin_net_conv_count():
-            raise RuntimeError(f"packed {len(self._h8_convs)} convs, library expects {L.rrin_net_conv_count()}")
-        self.head_table = (_lib.HeadWeights * 4)()
+        if len(self._h8_convs) != self.expected_convs:
+            raise RuntimeError(f"packed {len(self._h8_convs)} convs, expected {self.expected_convs}")
+        self.head_table = (_lib.HeadWeights * len(self.heads_t))()
         for i, (w, b) in enumerate(self.heads_t):
             self.head_table[i].w = w.data_ptr()
             self.head_table[i].bias = b.data_ptr()
@@ -483,6 +487,31 @@ class RRINEngine:
                 taps[name] = tapbuf[off:off + n * c * h * w].view(n, c, h, w)
                 off += n * c * h * w
         return out
+
+    def unet_forward(self, x: torch.Tensor) -> torch.Tensor:
+        """The single packed U-Net (engine built with one unit) on x [N,C,H,W]:
+        rrin_unet_fwd, the reference UNet.forward (unet.py:40-51)."""
+        if len(self.units) != 1:
+            raise RuntimeError("unet_forward needs an engine built for one U-Net")
+        _, unet, _ = self.units[0]
+        if x.device != self.device or x.dtype != torch.float32 or x.dim() != 4 or x.shape[1] != unet.in_channels:
+            raise ValueError(f"expected a float32 [N,{unet.in_channels},H,W] tensor on {self.device}")
+        n, c, h, w = x.shape
+        if h % 16 or w % 16:
+            raise RuntimeError(f"H and W must be multiples of 16, got {h}x{w}")
+        x = x.contiguous()
+        y = torch.empty((n, unet.n_classes, h, w), dtype=torch.float32, device=self.device)
+        d = _lib.UNetDesc()
+        d.n, d.h, d.w, d.in_ch, d.out_ch, d.depth, d.prec = n, h, w, c, unet.n_classes, unet.depth, self.prec
+        d.x, d.y = x.data_ptr(), y.data_ptr()
+        d.convs = self.conv_table_for(n, h, w)
+        d.head = self.head_table[0]
+        ws = self.workspace(n, h, w, slot=100)   # own workspace: its input channels [C, 16) stay zero
+        d.workspace, d.workspace_bytes = ws.data_ptr(), ws.numel()
+        with torch.cuda.device(self.device):
+            st = torch.cuda.current_stream(self.device)
+            _lib.check(self.lib.rrin_unet_fwd(C.byref(d), C.c_void_p(st.cuda_stream)), "rrin_unet_fwd")
+        return y
 
     def _forward_part(self, i0, i1, out, coef, slot, ws, stream, prof, reuse_flow, tapbuf=None):
         n, _, h, w = i0.shape

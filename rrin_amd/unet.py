@@ -1,12 +1,13 @@
 """Parameter tree of one RRIN U-Net, key-compatible with the reference.
 
-The reference U-Net (`/root/reference/unet.py:9-95`) is only used here for
-its *parameter naming*: a checkpoint written by the reference `train.py:158-161`
+The module tree reproduces the reference U-Net's (`/root/reference/unet.py:9-95`)
+*parameter naming*: a checkpoint written by the reference `train.py:158-161`
 must load with ``load_state_dict(strict=True)`` (`convert.py:103`).  The
-arithmetic is NOT done by these modules — `rrin_amd.engine` walks the tree and
-launches HIP kernels with the packed weights.  The modules therefore carry no
-``forward``; they are plain containers whose attribute paths reproduce the
-reference key layout:
+arithmetic is done by `rrin_amd.engine`, which walks the tree and launches HIP
+kernels with the packed weights: inside ``Net.forward`` for the whole Net, and
+for a ``UNet`` called on its own (``UNet.forward`` without autograd ->
+``rrin_unet_fwd``, same kernels).  With autograd on, ``UNet.forward`` is the
+PyTorch-operator training path.  Attribute paths (the reference key layout):
 
     down_path.{i}.block.{0,2}.{weight,bias}          unet.py:23-28, 59-63
     midconv.{weight,bias}                            unet.py:29
@@ -74,6 +75,24 @@ class UNet(nn.Module):
         self.up_path = nn.ModuleList(
             _UpStage(widths[i + 1], widths[i]) for i in reversed(range(depth - 1)))
         self.last = _conv3x3(widths[0], n_classes)
+        # HIP path of a standalone UNet call (not part of the reference contract):
+        # arithmetic as Net.precision ("fp32" exact by default)
+        self.precision = "fp32"
+        self._engine = None
+        self._engine_key = None
+
+    def _hip_engine(self):
+        from .engine import RRINEngine
+        key = (self.precision, tuple((p.data_ptr(), p._version) for p in self.parameters()))
+        if self._engine is None or self._engine_key != key:
+            self._engine = None
+            self._engine = RRINEngine(self, self.precision, units=[("unet", self, None)])
+            self._engine_key = key
+        return self._engine
+
+    def _apply(self, fn, *args, **kwargs):
+        self._engine = None  # device / dtype moves repack
+        return super()._apply(fn, *args, **kwargs)
 
     # -- helpers used by the engine --------------------------------------
     def conv_list(self):
@@ -91,13 +110,12 @@ class UNet(nn.Module):
         return out
 
     def forward(self, x):
-        """Autograd (training) path only: the reference U-Net math with PyTorch
-        operators (unet.py:40-51, 59-63, 76-94), so that ``train.py:98`` can
-        back-propagate through ``rrin_amd.Net``.  Inference never comes here:
-        without autograd this raises, and ``Net.forward`` runs the HIP kernels."""
-        if not torch.is_grad_enabled():
-            raise RuntimeError("rrin_amd.UNet.forward is the autograd (training) path; inference runs "
-                               "rrin_amd.Net's HIP engine (call the Net under torch.no_grad())")
+        """Reference ``UNet.forward`` (unet.py:40-51).  Without autograd: the HIP
+        kernels (``rrin_unet_fwd``; the input must be fp32 on a ROCm device, H
+        and W multiples of 16).  With autograd on (training): the same math with
+        PyTorch operators, differentiable."""
+        if not torch.is_grad_enabled() or not (x.requires_grad or any(p.requires_grad for p in self.parameters())):
+            return self._hip_engine().unet_forward(x)
         bridges = []
         for i, d in enumerate(self.down_path):
             x = d.block(x)

@@ -182,3 +182,33 @@ def test_split16_overflow_is_loud(gpu):
     with torch.no_grad():
         out32 = net(i0.to(gpu), i1.to(gpu), 0.5).cpu()
     assert err_psnr(out32, ref_out)[0] <= GATE
+
+
+@pytest.mark.parametrize("precision,tol", [("fp32", 1e-5), ("fp32_planar", 1e-5), ("fp32_split16", 1e-4),
+                                           ("fp16", 3e-2)])
+def test_unet_alone_golden(gpu, golden, precision, tol):
+    """A U-Net called on its own (reference UNet.forward, unet.py:40-51) through
+    rrin_unet_fwd: refine_flow on a random 10-channel input against the output the
+    unmodified reference wrote (tests/golden/unet_refine.npz)."""
+    g = golden("unet_refine")
+    net = make_net(gpu, keyed_state_dict(Net().state_dict()))
+    net.refine_flow.precision = precision
+    with torch.no_grad():
+        y = net.refine_flow(torch.from_numpy(g["x"]).to(gpu)).cpu()
+    want = torch.from_numpy(g["y"])
+    scale = max(1.0, float(want.abs().max()))
+    assert y.shape == want.shape
+    assert float((y - want).abs().max()) <= tol * scale
+
+
+@pytest.mark.parametrize("name,cin", [("Flow", 6), ("Mask", 16), ("final", 9)])
+def test_unet_alone_vs_oracle(gpu, name, cin):
+    """Each U-Net alone (depth 5 and 4, in_ch 6 / 16 / 9) vs the oracle's unet_forward."""
+    sd = keyed_state_dict(Net().state_dict(), stress=True)
+    net = make_net(gpu, sd)
+    x = torch.rand(2, cin, 64, 96, generator=torch.Generator().manual_seed(cin)) * 2 - 1
+    with torch.no_grad():
+        y = getattr(net, name)(x.to(gpu)).cpu()
+        ref_y = ref.unet_forward(sd, name, x)
+    scale = max(1.0, float(ref_y.abs().max()))
+    assert float((y - ref_y).abs().max()) <= 1e-5 * scale

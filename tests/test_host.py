@@ -49,10 +49,18 @@ def test_autograd_path_matches_golden_and_trains():
     assert float(net.final.last.weight.grad.abs().sum()) > 0
 
 
-def test_unet_forward_is_autograd_only():
+def test_unet_forward_paths():
+    """UNet.forward: without autograd the HIP engine (CPU tensors raise: no CPU
+    fallback); with autograd the torch-op path, equal to the reference UNet's
+    own output (golden unet_refine.npz, refine_flow alone, key-seeded weights)."""
     net = Net()
-    with torch.no_grad(), pytest.raises(RuntimeError, match="autograd"):
+    with torch.no_grad(), pytest.raises(RuntimeError, match="ROCm device"):
         net.Flow(torch.zeros(1, 6, 16, 16))
+    net.load_state_dict(keyed_state_dict(net.state_dict()), strict=True)
+    g = np.load(os.path.join(GOLDEN, "unet_refine.npz"))
+    y = net.refine_flow(torch.from_numpy(g["x"]))
+    assert y.requires_grad
+    assert torch.allclose(y, torch.from_numpy(g["y"]), atol=1e-5, rtol=0)
 
 
 def test_packed_weights_follow_inplace_edits():
