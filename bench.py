@@ -32,8 +32,16 @@ import os
 import sys
 import time
 
-import torch
-import torch.distributed as dist
+# HIP hardware queues per process (HIP's default is 4).  The forward's two
+# streams must land on different hardware queues to overlap; with RCCL's own
+# streams in the process (N > 1) four queues are not enough and HIP maps the two
+# onto one queue: 72.3 vs 78.3 pairs/s with the RCCL gather at world size 1
+# (profiles/r02/hw_queues_ab.txt).  Set before the first HIP call.
+os.environ["GPU_MAX_HW_QUEUES"] = (sys.argv[sys.argv.index("--hw-queues") + 1]
+                                   if "--hw-queues" in sys.argv else "8")
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
@@ -90,6 +98,9 @@ def parse():
     ap.add_argument("--dist-init", action="store_true",
                     help="initialise torch.distributed and run the all-gather path even at WORLD_SIZE 1 "
                          "(exercises RCCL / the gather check on a single GPU)")
+    ap.add_argument("--hw-queues", default="8", help="GPU_MAX_HW_QUEUES for this process (read before HIP init)")
+    ap.add_argument("--side-priority", type=int, default=0,
+                    help="stream priority of the forward's side streams (torch.cuda.Stream priority; -1 = high)")
     ap.add_argument("--split", default=None,
                     help="explicit pairs per stream, e.g. 1,3 (overrides --streams' even split)")
     return ap.parse_args()
@@ -213,6 +224,7 @@ def main():
     # the all-gather of step k overlaps the compute of step k+1 (double-buffered outputs)
     gather = GatherPipeline((world * B, 3, H, W), torch.float32, dev) if distributed else None
     eng = net.engine()
+    eng.side_priority = args.side_priority
     lib = _lib.lib()
     split = [int(c) for c in args.split.split(",")] if args.split else None
     if split:

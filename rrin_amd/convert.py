@@ -302,6 +302,11 @@ def convert(args):
     folder checks, the other ranks wait at a barrier."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    if world > 1 and int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 8:
+        # RCCL's streams plus the forward's two: give HIP enough hardware queues
+        # that the two forward streams do not share one (DESIGN.md §7); read at
+        # HIP init, which has not happened yet in this process
+        os.environ["GPU_MAX_HW_QUEUES"] = "8"
     if args.no_cuda or not torch.cuda.is_available():
         raise RuntimeError("rrin_amd runs on ROCm GPUs only (the reference also moves the model to .cuda() "
                            "unconditionally, convert.py:110)")

@@ -414,9 +414,12 @@ class RRINEngine:
             self._ws.move_to_end(key)
         return ws
 
+    side_priority = 0  # torch.cuda.Stream priority of the side streams (-1: high)
+
     def _side_streams(self, k: int):
         if len(self._sides) < k:
-            self._sides += [torch.cuda.Stream(self.device) for _ in range(k - len(self._sides))]
+            self._sides += [torch.cuda.Stream(self.device, priority=self.side_priority)
+                            for _ in range(k - len(self._sides))]
         return self._sides[:k]
 
     def forward(self, i0: torch.Tensor, i1: torch.Tensor, t=0.5, prof=None, reuse_flow: bool = False,
