@@ -376,8 +376,12 @@ class RRINEngine:
         self._packs[size] = p
         return p
 
+    force_size_class = None  # A/B knob: use this tile-table class for every forward part
+
     def conv_table_for(self, n: int, h: int, w: int):
         """ConvWeights table of a forward part of n pairs at h x w (its tile-table size class)."""
+        if self.force_size_class is not None and self.prec != _lib.PREC_F32:
+            return self._pack_h8(self.force_size_class)[2]
         if self.prec == _lib.PREC_F32:
             if size_class(n * h * w) != "small":
                 return self.conv_table
