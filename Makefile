@@ -2,10 +2,11 @@
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH  ?= gfx950
 # No packed FP32 VALU ops (v_pk_fma/mul/add_f32) in any kernel: measured on MI355X,
-# the low element of a v_pk_fma_f32 in lanes 48-63 of a wave came out perturbed
-# when a co-resident workgroup of another kernel on the CU ran LDS-DMA + MFMA
-# (DESIGN.md §9).  The flag also reaches the host compile, which ignores it
-# (one "not a recognized feature" line per file).
+# a v_pk_fma_f32 whose low result reads src1's high half through op_sel:[0,1,0]
+# gives a perturbed low element (lanes 48-63) while a co-resident workgroup of
+# another kernel runs LDS-DMA + MFMA; the splat / op_sel_hi forms stay exact and
+# packed code measured no faster.  The flag also reaches the host
+# compile, which ignores it (one "not a recognized feature" line per file).
 NOPK := -Xclang -target-feature -Xclang -packed-fp32-ops
 CXXFLAGS := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function -Iinclude $(NOPK)
 SRC_DIR := rrin_amd/csrc
@@ -35,11 +36,31 @@ $(LAB): $(SRC_DIR)/conv_f16.hip $(SRC_DIR)/common.hpp include/rrin_hip.h
 $(LAB32): $(SRC_DIR)/conv_mfma.hip $(SRC_DIR)/common.hpp include/rrin_hip.h
 	$(HIPCC) $(CXXFLAGS) -DRRIN_LAB -shared -o $@ $<
 
+# Packed-FP32 experiment: library variants with packed FP32 ops
+# in every kernel (pk_all), only the ring fix-up (pk_edge) or only the convs
+# (pk_conv), or the fix-up's FMAs in hand-placed packed form (pk_asm1/2).  Not used by the product; tools/gpu_pk.sh swaps them in on a box.
+PKV := rrin_amd/librrin_hip_pk_all.so rrin_amd/librrin_hip_pk_edge.so rrin_amd/librrin_hip_pk_conv.so \
+       rrin_amd/librrin_hip_pk_asm1.so rrin_amd/librrin_hip_pk_asm2.so
+pk-variants: $(PKV)
+
+rrin_amd/librrin_hip_pk_all.so: $(SRCS) $(SRC_DIR)/common.hpp include/rrin_hip.h
+	$(HIPCC) $(filter-out $(NOPK),$(CXXFLAGS)) -shared -o $@ $(SRCS)
+
+rrin_amd/librrin_hip_pk_edge.so: $(SRCS) $(SRC_DIR)/common.hpp include/rrin_hip.h
+	$(HIPCC) $(CXXFLAGS) -DRRIN_PK_EDGE -shared -o $@ $(SRCS)
+
+rrin_amd/librrin_hip_pk_conv.so: $(SRCS) $(SRC_DIR)/common.hpp include/rrin_hip.h
+	$(HIPCC) $(CXXFLAGS) -DRRIN_PK_CONV -shared -o $@ $(SRCS)
+
+# ring fix-up FMAs as hand-placed v_pk_fma_f32: 1 splat src1, 2 op_sel form
+rrin_amd/librrin_hip_pk_asm%.so: $(SRCS) $(SRC_DIR)/common.hpp include/rrin_hip.h
+	$(HIPCC) $(CXXFLAGS) -DRRIN_PK_EDGE_ASM=$* -shared -o $@ $(SRCS)
+
 # kernel register / LDS / occupancy report
 resource: $(SRCS)
 	$(HIPCC) $(CXXFLAGS) -Rpass-analysis=kernel-resource-usage -c $(SRC_DIR)/conv_mfma.hip -o /dev/null
 
 clean:
-	rm -rf build $(LIB) $(LAB) $(LAB32)
+	rm -rf build $(LIB) $(LAB) $(LAB32) $(PKV)
 
-.PHONY: all lab clean resource
+.PHONY: all lab clean resource pk-variants

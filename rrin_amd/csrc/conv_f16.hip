@@ -27,6 +27,38 @@
 
 namespace rrin {
 
+// Packed-FP32 experiment only (Makefile `pk-variants`): the library
+// is built without packed FP32 VALU ops; these re-enable them per kernel family.
+#if defined(RRIN_PK_CONV)
+#define RRIN_PK_CONV_ATTR __attribute__((target("packed-fp32-ops")))
+#else
+#define RRIN_PK_CONV_ATTR
+#endif
+#if defined(RRIN_PK_EDGE) || defined(RRIN_PK_EDGE_ASM)
+#define RRIN_PK_EDGE_ATTR __attribute__((target("packed-fp32-ops")))
+#else
+#define RRIN_PK_EDGE_ATTR
+#endif
+// RRIN_PK_EDGE_ASM: the ring fix-up's FMAs as hand-placed v_pk_fma_f32 (everything
+// else unpacked): 1 = src1 an explicit splat pair {u, u}, no op_sel; 2 = the form
+// the compiler emits, src1 {x, u} read through op_sel:[0,1,0] (low result takes
+// the high half).
+#if defined(RRIN_PK_EDGE_ASM)
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ inline void pk_fma4(f32x2& a01, f32x2& a23, float4 w, float u) {
+  const f32x2 w01 = {w.x, w.y}, w23 = {w.z, w.w};
+#if RRIN_PK_EDGE_ASM == 1
+  const f32x2 uu = {u, u};
+  asm("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(a01) : "v"(w01), "v"(uu));
+  asm("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(a23) : "v"(w23), "v"(uu));
+#else
+  const f32x2 xu = {0.f, u};
+  asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,1,0]" : "+v"(a01) : "v"(w01), "v"(xu));
+  asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,1,0]" : "+v"(a23) : "v"(w23), "v"(xu));
+#endif
+}
+#endif
+
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
@@ -172,7 +204,7 @@ constexpr int kSpreadTaps = 6, kStaggerTap = 3;
 // 4+e of the chunk; one ds_read_b128 per operand feeds all 4).  Same tiles,
 // LDS images and DMA as the fp16 kernel; weights unscaled; whole-record stores.
 template <int NW, int WM, int WN, int PLANES, int EPI, bool DMA, int SCHED = 0, bool F32 = false>
-__global__ void __launch_bounds__(64 * NW) conv3x3_h8_kernel(ConvH8Args a) {
+__global__ void RRIN_PK_CONV_ATTR __launch_bounds__(64 * NW) conv3x3_h8_kernel(ConvH8Args a) {
   using T = TileH8<NW, WM, WN, PLANES>;
   static_assert(!F32 || PLANES == 1, "fp32 records: one plane");
   constexpr int CPR = F32 ? 4 : 8;  // channels per record
@@ -790,7 +822,7 @@ struct Up8 {
 constexpr int kFixSubFloats = kFixCi * (kFixPx + 2) + kFixCi * 4 + 7 * kFixCi * kFixCo;
 
 template <int PLANES, int KS, bool F32 = false>
-__global__ void __launch_bounds__(256 * KS) edge_fix_h8_kernel(EdgeFixArgs a) {
+__global__ void RRIN_PK_EDGE_ATTR __launch_bounds__(256 * KS) edge_fix_h8_kernel(EdgeFixArgs a) {
   constexpr int CPR = F32 ? 4 : 8;            // channels per record
   constexpr int GPC = kFixCi / CPR;           // record groups per ci chunk
   extern __shared__ __attribute__((aligned(16))) float s_fix[];
@@ -875,6 +907,16 @@ __global__ void __launch_bounds__(256 * KS) edge_fix_h8_kernel(EdgeFixArgs a) {
   };
 
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#if defined(RRIN_PK_EDGE_ASM)
+  f32x2 a01 = {0.f, 0.f}, a23 = {0.f, 0.f};
+#define FIX_FMA(w, u) pk_fma4(a01, a23, w, u)
+#else
+#define FIX_FMA(w, u)                  \
+  acc[0] = fmaf(w.x, u, acc[0]);       \
+  acc[1] = fmaf(w.y, u, acc[1]);       \
+  acc[2] = fmaf(w.z, u, acc[2]);       \
+  acc[3] = fmaf(w.w, u, acc[3])
+#endif
   const int pos = pos0 + px;
   const bool cl = has_l && pos == 0, cr = has_r && pos == W - 1;
   // every K group runs the same number of chunks (launch: cin % (KS * kFixCi) == 0)
@@ -889,10 +931,7 @@ __global__ void __launch_bounds__(256 * KS) edge_fix_h8_kernel(EdgeFixArgs a) {
       for (int k = 0; k < 3; ++k) {
         const float u = s_u[ci][px + k];
         const float4 w = *reinterpret_cast<const float4*>(&s_w[k][ci][cg * 4]);
-        acc[0] = fmaf(w.x, u, acc[0]);
-        acc[1] = fmaf(w.y, u, acc[1]);
-        acc[2] = fmaf(w.z, u, acc[2]);
-        acc[3] = fmaf(w.w, u, acc[3]);
+        FIX_FMA(w, u);
       }
       if (cl || cr) {
         const int sb = cl ? 0 : 2;
@@ -900,15 +939,16 @@ __global__ void __launch_bounds__(256 * KS) edge_fix_h8_kernel(EdgeFixArgs a) {
         for (int m = 0; m < 2; ++m) {
           const float u = s_ux[ci][sb + m];
           const float4 w = *reinterpret_cast<const float4*>(&s_w[3 + sb + m][ci][cg * 4]);
-          acc[0] = fmaf(w.x, u, acc[0]);
-          acc[1] = fmaf(w.y, u, acc[1]);
-          acc[2] = fmaf(w.z, u, acc[2]);
-          acc[3] = fmaf(w.w, u, acc[3]);
+          FIX_FMA(w, u);
         }
       }
     }
     __syncthreads();
   }
+#undef FIX_FMA
+#if defined(RRIN_PK_EDGE_ASM)
+  acc[0] = a01.x; acc[1] = a01.y; acc[2] = a23.x; acc[3] = a23.y;
+#endif
   if constexpr (KS > 1) {
     // groups 1.. park their sums in their own (now idle) staging region
     if (ks > 0) {
