@@ -92,6 +92,8 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (production); gloo only to rehearse N ranks on fewer GPUs")
     ap.add_argument("--cpu-pairs", type=int, default=2, help="pairs timed on the CPU baseline")
+    ap.add_argument("--cpu-all-threads", action="store_true",
+                    help="also time one CPU pair on os.cpu_count() threads (beyond the job's CPU quota)")
     ap.add_argument("--streams", type=int, default=2,
                     help="HIP streams the rank's pairs are split over (their kernels overlap, filling each "
                          "other's launch gaps and last-wave tails; outputs are bitwise those of one stream)")
@@ -128,6 +130,9 @@ def host_cpu_share():
                      "omp_num_threads": env or None}
 
 
+CPU_ALL_THREADS = False
+
+
 def cpu_baseline(sd, h, w, pairs, t, gpu_out0, alt_out0=None):
     """Time the CPU oracle on pair 0 and compare its output with the GPU's."""
     from oracle.ref_net import net_forward  # checker / baseline only
@@ -155,8 +160,15 @@ def cpu_baseline(sd, h, w, pairs, t, gpu_out0, alt_out0=None):
                          "host_cpus = every CPU of the machine"}
     allc = os.cpu_count() or threads
     if allc > threads:
-        # SURVEY §8d asks for all host cores: one more pair on os.cpu_count() threads
-        # (more threads than the job's CPU quota oversubscribe it; reported beside)
+        # the job may use `threads` of the host's `allc` CPUs (cgroup quota): a
+        # linear projection to every core is the upper bound the CPU reference
+        # could reach on this host -- reported beside, never as `value`
+        res["projected_all_host_cores"] = {
+            "value": res["value"] * allc / threads, "cores": allc,
+            "note": "linear scaling of the measured rate to os.cpu_count() cores (upper bound, not measured)"}
+    if CPU_ALL_THREADS and allc > threads:
+        # measured on os.cpu_count() threads: oversubscribes the job's quota
+        # (on the GPU box 256 threads on 16 CPUs: 0.015 pairs/s)
         torch.set_num_threads(allc)
         with torch.no_grad():
             t0 = time.perf_counter()
@@ -453,6 +465,8 @@ def main():
         del eng2
         net.precision = args.precision
     if rank == 0 and world == 1 and args.cpu_baseline == "auto":
+        global CPU_ALL_THREADS
+        CPU_ALL_THREADS = args.cpu_all_threads
         res["cpu_baseline"], res["parity"] = cpu_baseline({k: v.detach().cpu() for k, v in sd.items()}, H, W,
                                                           args.cpu_pairs, args.t, last[0][0:1].cpu(),
                                                           alt_out)

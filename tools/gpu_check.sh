@@ -16,9 +16,9 @@ run() {  # name limit cmd...
   return 0
 }
 STEPS=${STEPS:-tests,smoke,bench,prof}
-[[ $STEPS == *tests* ]] && run tests 900 python -m pytest tests -m gpu -q
+[[ $STEPS == *tests* ]] && run tests 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread
 [[ $STEPS == *smoke* ]] && run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-[[ $STEPS == *bench* ]] && run bench 600 python bench.py --steps 5 --warmup 2
+[[ $STEPS == *bench* ]] && run bench 600 python bench.py
 [[ $STEPS == *bsplit* ]] && run bench_split 600 python bench.py --steps 5 --warmup 2 --precision fp32_split16
 [[ $STEPS == *bf16* ]] && run bench_fp16 600 python bench.py --steps 5 --warmup 2 --precision fp16 --cpu-baseline off
 [[ $STEPS == *mgpu* ]] && run mgpu 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 3 --warmup 1 --batch 2 --dist-backend gloo
