@@ -111,6 +111,20 @@ XLARGE_PX = 6_000_000
 # (8.4 Mpx, profiles/r02/c5_4k/tune_fp32r_3840x2176x1.txt); fp16 "xxlarge" = the
 # C5 4K sweep (profiles/r02/c5_4k/tune_fp16_3840x2176x1.txt).  A class a
 # precision has no table for uses H8_TUNED.
+# Exact fp32 (F32R) "small" / "medium": the sweeps at 640x368 x 1 (config C2;
+# the untuned large table's BM 128 tiles left the 46x80 L3 grid with 8-16 TF/s,
+# summed conv time 12.84 -> 5.34 ms) and 1280x720 x 1 (18.12 -> 14.45 ms);
+# profiles/r02/tune_fp32r_640x368x1.txt, tune_fp32r_1280x720x1.txt.
+H8_TUNED_BY_SIZE["small"][_lib.PREC_F32R] = {
+    (6, 32, 0): 15, (9, 32, 0): 15, (10, 32, 0): 1, (16, 32, 0): 9, (32, 32, 0): 9, (32, 64, 1): 1, (64, 32, 0): 9,
+    (64, 64, 1): 1, (64, 128, 1): 0, (64, 128, 2): 4, (128, 64, 1): 1, (128, 128, 2): 12, (128, 256, 2): 1,
+    (128, 256, 3): 16, (256, 128, 2): 4, (256, 256, 3): 6, (256, 512, 3): 16, (256, 512, 4): 16, (512, 256, 3): 16,
+    (512, 512, 4): 16}
+H8_TUNED_BY_SIZE["medium"][_lib.PREC_F32R] = {
+    (6, 32, 0): 15, (9, 32, 0): 1, (10, 32, 0): 9, (16, 32, 0): 6, (32, 32, 0): 8, (32, 64, 1): 0, (64, 32, 0): 6,
+    (64, 64, 1): 0, (64, 128, 1): 9, (64, 128, 2): 0, (128, 64, 1): 0, (128, 128, 2): 0, (128, 256, 2): 5,
+    (128, 256, 3): 1, (256, 128, 2): 11, (256, 256, 3): 1, (256, 512, 3): 11, (256, 512, 4): 16, (512, 256, 3): 1,
+    (512, 512, 4): 16}
 H8_TUNED_BY_SIZE["xlarge"] = {
     _lib.PREC_F32R: {(6, 32, 0): 13, (9, 32, 0): 15, (10, 32, 0): 15, (16, 32, 0): 15, (32, 32, 0): 9,
                      (32, 64, 1): 8, (64, 32, 0): 9, (64, 64, 1): 1, (64, 128, 1): 1, (64, 128, 2): 4,
