@@ -202,6 +202,9 @@ int rrin_conv_h8_cfg_ok(int32_t cfg, int32_t prec); /* 1 if the config fits LDS 
  * every weight chunk resident in LDS needs them to fit) */
 int rrin_conv_h8_cfg_fits(int32_t cfg, int32_t prec, int32_t cin);
 int rrin_conv3x3_h8_fwd(const rrin_conv_h8_desc* d, void* stream);
+/* 1 if cfg is the Winograd F(2x2,3x3) exact-fp32 config (F32R only, BM 32 x TH 8):
+ * its weights are packed by rrin_pack_conv3x3_wino, not rrin_pack_conv3x3_r32 */
+int rrin_conv_h8_cfg_wino(int32_t cfg);
 
 /* F32R packing: [co_block][chunk of 8 ci][tap][half][bm][4] fp32 (half hh holds
  * input channels chunk*8 + 4*hh .. +3), unscaled; pass as whi (wlo NULL,
@@ -209,6 +212,15 @@ int rrin_conv3x3_h8_fwd(const rrin_conv_h8_desc* d, void* stream);
 int64_t rrin_pack_conv3x3_r32_floats(int32_t cout, int32_t cin, int32_t bm);
 int rrin_pack_conv3x3_r32(const float* w, const float* b, int32_t cout, int32_t cin, int32_t bm,
                           const int32_t* perm, float* wpack, float* bpack);
+
+/* Winograd packing (F32R, the rrin_conv_h8_cfg_wino config): U = G g G^T per
+ * (co, ci) computed in double and rounded once to fp32, laid out
+ * [co_block of 32][chunk of 4 ci][xi 16][co 32][4 ci] (xi = 4*row + col of the
+ * 4x4 transform, G = [1 0 0; .5 .5 .5; .5 -.5 .5; 0 0 1]).  bpack:
+ * rrin_pack_bias_floats(cout, 32) floats. */
+int64_t rrin_pack_conv3x3_wino_floats(int32_t cout, int32_t cin);
+int rrin_pack_conv3x3_wino(const float* w, const float* b, int32_t cout, int32_t cin, const int32_t* perm,
+                           float* wpack, float* bpack);
 
 /* Host packing: [co_block][chunk of 16 ci][tap][half][bm][8] halves, weights
  * pre-scaled by a power of two so max|w| lands in [2^12, 2^13) (keeps lo

@@ -128,6 +128,10 @@ SIGNATURES = {
     "rrin_conv_h8_cfg_ok": (C.c_int, [C.c_int32, C.c_int32]),
     "rrin_conv_h8_cfg_fits": (C.c_int, [C.c_int32, C.c_int32, C.c_int32]),
     "rrin_conv3x3_h8_fwd": (C.c_int, [C.POINTER(ConvH8Desc), C.c_void_p]),
+    "rrin_conv_h8_cfg_wino": (C.c_int, [C.c_int32]),
+    "rrin_pack_conv3x3_wino_floats": (C.c_int64, [C.c_int32, C.c_int32]),
+    "rrin_pack_conv3x3_wino": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p,
+                                         C.c_void_p]),
     "rrin_pack_conv3x3_h8_halves": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32]),
     "rrin_pack_conv3x3_h8": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p,
                                        C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(C.c_float)]),

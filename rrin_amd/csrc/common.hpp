@@ -138,6 +138,56 @@ __device__ inline float warp_apply_f(const WarpTaps& t, F get) {
 }
 #pragma clang fp contract(on)
 
+// ---- record-layout conv kernels (conv_f16.hip, conv_wino.hip) -------------
+// LeakyReLU for 0 <= slope <= 1 (h8_prepare checks): one mul + one max
+__device__ inline float leaky(float t, float slope) { return fmaxf(t, t * slope); }
 
+struct ConvH8Args {
+  const uint4* src_hi;
+  const uint4* src_lo;
+  int64_t src_img, src_gp;  // records per image / per group plane
+  int src_wp;
+  int cin, nchunks;         // chunks of 16 input channels
+  uint4* dst_hi;
+  uint4* dst_lo;
+  int64_t dst_img, dst_gp;
+  int dst_wp, cout;
+  uint4* pool_hi;
+  uint4* pool_lo;
+  int64_t pool_img, pool_gp;
+  int pool_wp;
+  const uint4* w_hi;
+  const uint4* w_lo;
+  const float* bias;
+  float inv_wscale, slope;
+  int h, w, co_blocks, tiles_x, tiles_y, n;
+  int tail_finite;
+  float* edge;  // EPI_SUBPIXEL: [n][cout/4][ring] pre-bias values of the 2h x 2w ring
+  int64_t ring;
+  int* status;  // optional fp16 range flag (F16X3 / F16)
+};
+
+// Ring index of pixel (y, x) of an H x W image (rrin_ring_pixels order: top
+// row, bottom row, left column, right column; corners in the rows), -1 inside.
+__device__ inline int64_t ring_index(int y, int x, int H, int W) {
+  if (y == 0) return x;
+  if (y == H - 1) return (int64_t)W + x;
+  if (x == 0) return 2 * (int64_t)W + (y - 1);
+  if (x == W - 1) return 2 * (int64_t)W + (H - 2) + (y - 1);
+  return -1;
+}
+
+// LDS-DMA: one 16-byte record per lane straight from global memory into the
+// lane-linear LDS image (global_load_lds_dwordx4; LDS address = wave-uniform
+// base + lane*16), no VGPRs and no LDS store pass.
+__device__ inline void dma16(const uint4* src, uint4* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+// Winograd F(2x2,3x3) exact-fp32 conv (conv_wino.hip): tile config kWinoCfg of
+// the record-layout table (F32R only), its LDS bytes per block and launcher.
+constexpr size_t kWinoLds = (size_t)(2 * 352 + 2 * 16 * 64 + 2 * 16 * 32) * 16;
+int launch_wino(const ConvH8Args& a, int epi, hipStream_t st);
 
 }  // namespace rrin

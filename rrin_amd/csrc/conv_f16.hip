@@ -89,43 +89,8 @@ __device__ inline void split4(const float* v, uint2& hv, uint2& lv) {
   lv = make_uint2(__builtin_bit_cast(unsigned, __builtin_convertvector((float2v){l0, l1}, half2v)),
                   __builtin_bit_cast(unsigned, __builtin_convertvector((float2v){l2, l3}, half2v)));
 }
-// LeakyReLU for 0 <= slope <= 1 (h8_prepare checks): one mul + one max
-__device__ inline float leaky(float t, float slope) { return fmaxf(t, t * slope); }
 
-struct ConvH8Args {
-  const uint4* src_hi;
-  const uint4* src_lo;
-  int64_t src_img, src_gp;  // records per image / per group plane
-  int src_wp;
-  int cin, nchunks;         // chunks of 16 input channels
-  uint4* dst_hi;
-  uint4* dst_lo;
-  int64_t dst_img, dst_gp;
-  int dst_wp, cout;
-  uint4* pool_hi;
-  uint4* pool_lo;
-  int64_t pool_img, pool_gp;
-  int pool_wp;
-  const uint4* w_hi;
-  const uint4* w_lo;
-  const float* bias;
-  float inv_wscale, slope;
-  int h, w, co_blocks, tiles_x, tiles_y, n;
-  int tail_finite;
-  float* edge;  // EPI_SUBPIXEL: [n][cout/4][ring] pre-bias values of the 2h x 2w ring
-  int64_t ring;
-  int* status;  // optional fp16 range flag (F16X3 / F16)
-};
 
-// Ring index of pixel (y, x) of an H x W image (rrin_ring_pixels order: top
-// row, bottom row, left column, right column; corners in the rows), -1 inside.
-__device__ inline int64_t ring_index(int y, int x, int H, int W) {
-  if (y == 0) return x;
-  if (y == H - 1) return (int64_t)W + x;
-  if (x == 0) return 2 * (int64_t)W + (y - 1);
-  if (x == W - 1) return 2 * (int64_t)W + (H - 2) + (y - 1);
-  return -1;
-}
 
 template <int NW, int WM, int WN, int PLANES>
 struct TileH8 {
@@ -162,13 +127,6 @@ __device__ inline uint4 mask_halves(uint4 v, int nvalid) {
   return v;
 }
 
-// LDS-DMA: one 16-byte record per lane straight from global memory into the
-// lane-linear LDS image (global_load_lds_dwordx4; LDS address = wave-uniform
-// base + lane*16), no VGPRs and no LDS store pass.
-__device__ inline void dma16(const uint4* src, uint4* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
-}
 
 // Schedule knobs of the kernel (template SCHED; the cfg table picks them per
 // layer, tools/conv_lab.py ablate times them).  SPREAD issues the next chunk's
@@ -1689,8 +1647,11 @@ static const CfgH8 kCfgH8[] = {
    (wn % 2) == 0, sc, pe},
     RRIN_H8_CFGS(X)
 #undef X
+    // kWinoCfg: Winograd F(2x2,3x3) on fp32 records (conv_wino.hip), BM 32 x TH 8
+    {32, 8, kWinoLds, (size_t)1 << 30, 0, true, 0, 0},
 };
 static constexpr int kNumCfgH8 = sizeof(kCfgH8) / sizeof(kCfgH8[0]);
+static constexpr int kWinoCfg = kNumCfgH8 - 1;
 static constexpr size_t kMaxLds = 160 * 1024;
 
 static int num_cus() {
@@ -1865,6 +1826,11 @@ static int h8_prepare(const rrin_conv_h8_desc* d, ConvH8Args& a) {
   a.co_blocks = (d->cout + ci.bm - 1) / ci.bm;
   a.tiles_x = (w + 31) / 32;
   a.tiles_y = (h + ci.th - 1) / ci.th;
+  if (d->cfg == kWinoCfg) {
+    if (d->prec != RRIN_PREC_F32R) return RRIN_E_CONFIG;
+    if ((d->cin & 3) && !d->tail_finite) return RRIN_E_CONFIG;  // stages whole records only
+    a.nchunks = (d->cin + 3) / 4;  // one record group per K chunk
+  }
   a.n = d->n;
   if ((int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n > 0x7fffffff) return RRIN_E_SHAPE;
   return 0;
@@ -1887,9 +1853,11 @@ extern "C" int rrin_conv_h8_cfg_bm(int32_t cfg) {
 extern "C" int rrin_conv_h8_cfg_th(int32_t cfg) {
   return (cfg >= 0 && cfg < kNumCfgH8) ? kCfgH8[cfg].th : RRIN_E_CONFIG;
 }
+extern "C" int rrin_conv_h8_cfg_wino(int32_t cfg) { return cfg == kWinoCfg ? 1 : 0; }
 extern "C" int rrin_conv_h8_cfg_ok(int32_t cfg, int32_t prec) {
   if (cfg < 0 || cfg >= kNumCfgH8) return 0;
   if (!rec_prec(prec)) return 0;
+  if (cfg == kWinoCfg && prec != RRIN_PREC_F32R) return 0;
   return (planes_of(prec) == 2 ? kCfgH8[cfg].lds2 : kCfgH8[cfg].lds1) <= kMaxLds ? 1 : 0;
 }
 
@@ -1908,6 +1876,7 @@ extern "C" int rrin_conv3x3_h8_fwd(const rrin_conv_h8_desc* d, void* stream) {
   const int rc = h8_prepare(d, a);
   if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;
+  if (d->cfg == kWinoCfg) return launch_wino(a, d->epi_mode, st);
   switch (d->cfg) {
 #define X(id, nw, wm, wn, sc, pe) \
   case id:                        \

@@ -339,11 +339,16 @@ class RRINEngine:
         for (w, b, cin, cout, level, perm_arr, edge), cfg in zip(self._h8_convs, cfgs):
             bm = L.rrin_conv_h8_cfg_bm(cfg)
             if f32:  # fp32 records: unscaled fp32 weights (offsets in floats)
-                wp = np.empty(L.rrin_pack_conv3x3_r32_floats(cout, cin, bm), np.float32)
                 bp = np.empty(L.rrin_pack_bias_floats(cout, bm), np.float32)
-                _lib.check(L.rrin_pack_conv3x3_r32(w.ctypes.data, b.ctypes.data, cout, cin, bm,
-                                                   perm_arr.ctypes.data if perm_arr is not None else None,
-                                                   wp.ctypes.data, bp.ctypes.data), "rrin_pack_conv3x3_r32")
+                pa = perm_arr.ctypes.data if perm_arr is not None else None
+                if L.rrin_conv_h8_cfg_wino(cfg):  # Winograd F(2x2,3x3): transformed weights
+                    wp = np.empty(L.rrin_pack_conv3x3_wino_floats(cout, cin), np.float32)
+                    _lib.check(L.rrin_pack_conv3x3_wino(w.ctypes.data, b.ctypes.data, cout, cin, pa,
+                                                        wp.ctypes.data, bp.ctypes.data), "rrin_pack_conv3x3_wino")
+                else:
+                    wp = np.empty(L.rrin_pack_conv3x3_r32_floats(cout, cin, bm), np.float32)
+                    _lib.check(L.rrin_pack_conv3x3_r32(w.ctypes.data, b.ctypes.data, cout, cin, bm, pa,
+                                                       wp.ctypes.data, bp.ctypes.data), "rrin_pack_conv3x3_r32")
                 meta.append((hoff, None, boff, cfg, 1.0, edge))
                 halves.append(wp)
                 hoff += wp.size

@@ -43,6 +43,12 @@ def keyed_conv(cin, cout, key="h8"):
 NO_POOL_CFGS = (4, 16)
 
 
+def wino_cfg():
+    """Id of the Winograd F(2x2,3x3) exact-fp32 config (R32 only)."""
+    lib = _lib.lib()
+    return next(c for c in range(lib.rrin_conv_h8_cfg_count()) if lib.rrin_conv_h8_cfg_wino(c))
+
+
 def cfgs(prec, cout, cin):
     lib = _lib.lib()
     return [c for c in range(lib.rrin_conv_h8_cfg_count())
@@ -56,6 +62,14 @@ def pack_h8(w, b, cfg, prec, dev, perm=None):
     cout, cin = w.shape[:2]
     bm = lib.rrin_conv_h8_cfg_bm(cfg)
     pa = np.asarray(perm, np.int32) if perm is not None else None
+    if prec == R32 and lib.rrin_conv_h8_cfg_wino(cfg):  # Winograd: U = G g G^T per point
+        wp = np.zeros(lib.rrin_pack_conv3x3_wino_floats(cout, cin), np.float32)
+        bp = np.zeros(lib.rrin_pack_bias_floats(cout, bm), np.float32)
+        _lib.check(lib.rrin_pack_conv3x3_wino(w.ctypes.data, b.ctypes.data, cout, cin,
+                                              pa.ctypes.data if pa is not None else None, wp.ctypes.data,
+                                              bp.ctypes.data))
+        wt = torch.from_numpy(wp).to(dev)
+        return wt, wt, torch.from_numpy(bp).to(dev), 1.0
     if prec == R32:  # fp32 records: unscaled fp32 weights, no lo blob
         wp = np.zeros(lib.rrin_pack_conv3x3_r32_floats(cout, cin, bm), np.float32)
         bp = np.zeros(lib.rrin_pack_bias_floats(cout, bm), np.float32)
@@ -185,7 +199,7 @@ def test_h8_conv_dma_finite_tail(gpu, prec, cin):
     x = torch.rand(2, 16, 32, 48, device=gpu) * 2 - 1
     wt, b = keyed_conv(cin, 32, "tail")
     ref = ref_conv(x[:, :cin], wt, b)
-    for cfg in (1, 6):
+    for cfg in (1, 6) + ((wino_cfg(),) if prec == R32 else ()):
         dst, _ = conv_h8(H8Tensor.from_nchw(x, prec), wt, b, cfg, prec, cin=cin, tail_finite=1)
         np.testing.assert_allclose(dst.to_nchw().cpu().double().numpy(), ref.numpy(), **TOL[prec])
 
@@ -225,7 +239,7 @@ def test_h8_leaky_rep_writes_replicated_ring(gpu, prec):
     x = torch.rand(2, 32, 13, 45, device=gpu) * 2 - 1
     wt, b = keyed_conv(32, 64, "rep")
     ref = ref_conv(x, wt, b, 0.1)
-    for cfg in (0, 6):
+    for cfg in (0, 6) + ((wino_cfg(),) if prec == R32 else ()):
         dst, _ = conv_h8(H8Tensor.from_nchw(x, prec), wt, b, cfg, prec, epi=_lib.EPI_LEAKY_REP)
         np.testing.assert_allclose(dst.to_nchw().cpu().double().numpy(), ref.numpy(), **TOL[prec])
         # the ring must equal the replicated border; everything else in the padding stays zero

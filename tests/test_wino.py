@@ -1,0 +1,96 @@
+"""CPU: the Winograd F(2x2, 3x3) form of the exact-fp32 conv (conv_wino.hip).
+
+The host packing (rrin_pack_conv3x3_wino: U = G g G^T per output/input channel
+pair, in double, rounded once to fp32) and the kernel's transforms, restated
+here in float64 -- input V = B^T d B per 2x2 output patch, per-point channel
+contraction, output Y = A^T M A -- must reproduce the direct 3x3 conv (zero
+padding, reference unet.py:29) of the same weights.  The GPU tests
+(tests/test_gpu_h8.py, the Winograd config in every config sweep) check the
+kernel itself against float64."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from rrin_amd import _lib
+
+BT = np.array([[1, 0, -1, 0], [0, 1, 1, 0], [0, -1, 1, 0], [0, 1, 0, -1]], np.float64)
+AT = np.array([[1, 1, 1, 0], [0, 1, -1, -1]], np.float64)
+
+
+def pack_wino(w, b, perm=None):
+    lib = _lib.lib()
+    cout, cin = w.shape[:2]
+    wp = np.zeros(lib.rrin_pack_conv3x3_wino_floats(cout, cin), np.float32)
+    bp = np.zeros(lib.rrin_pack_bias_floats(cout, 32), np.float32)
+    pa = np.asarray(perm, np.int32) if perm is not None else None
+    _lib.check(lib.rrin_pack_conv3x3_wino(w.ctypes.data, b.ctypes.data, cout, cin,
+                                          pa.ctypes.data if pa is not None else None, wp.ctypes.data,
+                                          bp.ctypes.data))
+    return wp, bp
+
+
+def unpack_u(wp, cout, cin):
+    """[cob][chunk][xi][co32][4] -> U[xi][co][ci] (float64)."""
+    cob, nch = (cout + 31) // 32, (cin + 3) // 4
+    u = wp.reshape(cob, nch, 16, 32, 4).transpose(2, 0, 3, 1, 4).reshape(16, cob * 32, nch * 4)
+    return u[:, :cout, :cin].astype(np.float64)
+
+
+def wino_conv(x, u, bias):
+    """float64 restatement of the kernel's dataflow: x [cin][h][w] (h, w even)."""
+    cin, h, w = x.shape
+    xp = np.zeros((cin, h + 2, w + 2))
+    xp[:, 1:h + 1, 1:w + 1] = x
+    # 4x4 windows at stride 2: [cin][ph][pw][4][4]
+    win = np.lib.stride_tricks.sliding_window_view(xp, (4, 4), axis=(1, 2))[:, ::2, ::2]
+    v = np.einsum("ab,cpqbd,ed->cpqae", BT, win, BT)              # B^T d B
+    m = np.einsum("xoc,cpqx->opqx", u.reshape(16, *u.shape[1:]), v.reshape(*v.shape[:3], 16))
+    m = m.reshape(*m.shape[:3], 4, 4)
+    y = np.einsum("ra,opqab,sb->oprqs", AT, m, AT)                # A^T M A
+    co = y.shape[0]
+    return y.reshape(co, h, w) + bias[:, None, None]
+
+
+@pytest.mark.parametrize("cin,cout", [(6, 32), (10, 32), (32, 64), (64, 32)])
+def test_wino_packing_reproduces_direct_conv(cin, cout):
+    g = torch.Generator().manual_seed(cin * 1000 + cout)
+    w = (torch.randn(cout, cin, 3, 3, generator=g) / (3 * cin ** 0.5)).numpy()
+    b = (torch.randn(cout, generator=g) * 0.1).numpy()
+    x = (torch.rand(cin, 12, 18, generator=g) * 2 - 1).numpy()
+    wp, bp = pack_wino(w, b)
+    np.testing.assert_array_equal(bp[:cout], b)
+    assert not bp[cout:].any()
+    y = wino_conv(x.astype(np.float64), unpack_u(wp, cout, cin), b.astype(np.float64))
+    ref = F.conv2d(torch.from_numpy(x[None]).double(), torch.from_numpy(w).double(),
+                   torch.from_numpy(b).double(), padding=1)[0].numpy()
+    np.testing.assert_allclose(y, ref, rtol=0, atol=2e-6)
+
+
+def test_wino_packing_layout_and_perm():
+    """Padding channels are zero; the input permutation selects reference channels."""
+    cout, cin = 40, 10
+    rng = np.random.default_rng(3)
+    w = rng.standard_normal((cout, cin, 3, 3)).astype(np.float32)
+    b = rng.standard_normal(cout).astype(np.float32)
+    perm = [4, 5, 6, 7, 8, 9, 0, 1, 2, 3]
+    wp, _ = pack_wino(w, b, perm)
+    full = wp.reshape(2, 3, 16, 32, 4).transpose(2, 0, 3, 1, 4).reshape(16, 64, 12)
+    assert not full[:, cout:].any() and not full[:, :, cin:].any()
+    u_perm = unpack_u(wp, cout, cin)
+    u_ref = unpack_u(pack_wino(np.ascontiguousarray(w[:, perm]), b)[0], cout, cin)
+    np.testing.assert_array_equal(u_perm, u_ref)
+    # point xi = (0, 0) is the corner tap g[0][0] itself (G row 0 = [1 0 0])
+    np.testing.assert_array_equal(u_ref[0], w[:, perm, 0, 0].astype(np.float64))
+
+
+def test_wino_config_entry():
+    lib = _lib.lib()
+    ids = [c for c in range(lib.rrin_conv_h8_cfg_count()) if lib.rrin_conv_h8_cfg_wino(c)]
+    assert len(ids) == 1
+    c = ids[0]
+    assert lib.rrin_conv_h8_cfg_bm(c) == 32 and lib.rrin_conv_h8_cfg_th(c) == 8
+    assert lib.rrin_conv_h8_cfg_ok(c, _lib.PREC_F32R) == 1
+    assert lib.rrin_conv_h8_cfg_ok(c, _lib.PREC_F16X3) == 0 and lib.rrin_conv_h8_cfg_ok(c, _lib.PREC_F16) == 0
+    assert lib.rrin_pack_conv3x3_wino_floats(33, 5) == 2 * 2 * 16 * 32 * 4
+    assert lib.rrin_pack_conv3x3_wino_floats(0, 5) < 0
