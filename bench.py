@@ -47,9 +47,10 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 from rrin_amd import Net, _lib  # noqa: E402
+from rrin_amd import engine as engine_mod  # noqa: E402
 from rrin_amd.shard import GatherPipeline  # noqa: E402
 from rrin_amd.synthetic import keyed_state_dict, synthetic_batch  # noqa: E402
-from rrin_amd.unet import conv_bytes, conv_flops, roofline_bound_s  # noqa: E402
+from rrin_amd.unet import conv_bytes, conv_flops, conv_work, roofline_bound_s  # noqa: E402
 
 FP32_PEAK_TFLOPS = 157.3   # MI355X dense fp32 (MFMA 32x32x2 f32 = VALU rate), MI355X_MICROARCH.md
 F16_PEAK_TFLOPS = 2500.0   # dense f16 MFMA (v_mfma_f32_32x32x16_f16), no sparsity
@@ -66,6 +67,8 @@ KERNEL = {"fp32": "conv3x3_h8_kernel on fp32 records (77 body convs, v_mfma_f32_
           "fp32_planar": "conv3x3_mfma_kernel, planar fp32 (77 body convs, v_mfma_f32_32x32x2_f32)",
           "fp32_split16": "conv3x3_h8_kernel (77 body convs, v_mfma_f32_32x32x16_f16 x3)",
           "fp16": "conv3x3_h8_kernel (77 body convs, v_mfma_f32_32x32x16_f16)"}
+KERNEL_WINO = ("conv3x3_wino_kernel: Winograd F(2x2,3x3) on fp32 records (77 body convs; fp32 input/output "
+               "transforms, v_mfma_f32_32x32x2_f32 contraction per transform point)")
 DTYPE = {"fp32": "f32", "fp32_planar": "f32",
          "fp32_split16": "f16x3 (fp32-emulated: fp16 hi+lo split, 3 f16 MFMA products, f32 accumulate)",
          "fp16": "f16"}
@@ -105,6 +108,9 @@ def parse():
                     help="stream priority of the forward's side streams (torch.cuda.Stream priority; -1 = high)")
     ap.add_argument("--size-class", default=None, choices=["small", "medium", "large", "xlarge", "xxlarge"],
                     help="A/B: force the tile table of this size class for every forward part")
+    ap.add_argument("--no-wino", action="store_true",
+                    help="A/B: exact fp32 on the direct-form conv (v_mfma_f32_32x32x2_f32 per tap) instead of "
+                         "Winograd F(2x2,3x3)")
     ap.add_argument("--split", default=None,
                     help="explicit pairs per stream, e.g. 1,3 (overrides --streams' even split)")
     return ap.parse_args()
@@ -241,6 +247,8 @@ def main():
         else:
             dist.init_process_group("gloo")
 
+    if args.no_wino:
+        engine_mod.WINO = False
     net = Net()
     sd = keyed_state_dict(net.state_dict())
     net.load_state_dict(sd, strict=True)
@@ -350,10 +358,18 @@ def main():
         head_ms_step = head_ms / args.steps
         achieved = conv_fl / (conv_busy * 1e-3) / 1e12
         peak = PEAK[args.precision]
+        algo = eng.conv_algorithm(B // max(1, args.streams), H, W)
+        units = ("Flow", "refine_flow", "Mask", "final")
+        direct_fl = args.steps * B * sum(fl for u in units for _, fl, _, _ in conv_work(getattr(net, u), H, W))
         roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1),
                     "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None,
                     "mfma_issued_tflops": round(achieved * MFMA_PRODUCTS[args.precision], 1),
-                    "kernel": KERNEL[args.precision],
+                    "kernel": KERNEL_WINO if algo == "winograd" and args.precision == "fp32" else KERNEL[args.precision],
+                    "conv_algorithm": algo,
+                    "flops_basis": ("FLOPs of the algorithm the convs run: Winograd F(2x2,3x3) = 16 multiply-adds "
+                                    "per 2x2 output patch and channel pair (4/9 of the direct form's)"
+                                    if algo == "winograd" else "direct-form conv FLOPs (2*9*Cin*Cout*H*W)"),
+                    "direct_equivalent_tflops": round(direct_fl / (conv_busy * 1e-3) / 1e12, 2),
                     "flops_per_launch_avg": conv_fl / max(conv_launches, 1),
                     "avg_launch_ms": conv_ms / max(conv_launches, 1),
                     "conv_busy_ms_per_step": round(conv_busy / args.steps, 3),
@@ -367,7 +383,8 @@ def main():
                     "subpixel_ring_fix_ms_per_step": round(edge_ms / args.steps, 3)}
         # SURVEY §8d per-layer bound: sum_l max(FLOP_l / peak, bytes_l / 8 TB/s) over the body convs
         bpv = 2 if args.precision == "fp16" else 4
-        tlb = B * sum(roofline_bound_s(getattr(net, u), H, W, bpv, peak * 1e12, HBM_PEAK_GBS * 1e9)
+        fscale = 4.0 / 9.0 if algo == "winograd" else 1.0
+        tlb = B * sum(roofline_bound_s(getattr(net, u), H, W, bpv, peak * 1e12, HBM_PEAK_GBS * 1e9, fscale)
                       for u in ("Flow", "refine_flow", "Mask", "final"))
         roofline["t_lb_conv_ms_per_step"] = round(1e3 * tlb, 3)
         roofline["t_lb_frac_of_conv_time"] = round(1e3 * tlb / (conv_busy / args.steps), 4)
@@ -459,6 +476,7 @@ def main():
         res[alt_key] = {"value": round(B * args.steps / el2, 3), "ms_per_step": round(1e3 * el2 / args.steps, 3),
                         "dtype": DTYPE[alt], "metric": f"interpolated frames/sec at {W}x{H} {PREC_LABEL[alt]}",
                         "conv_tflops": round(tf, 2), "peak": round(PEAK[alt], 1),
+                        "conv_algorithm": eng2.conv_algorithm(B // max(1, args.streams), H, W),
                         "conv_frac_of_peak": round(tf / PEAK[alt], 4),
                         "kernel": KERNEL[alt],
                         "streams": args.streams}

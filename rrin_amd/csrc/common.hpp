@@ -187,7 +187,7 @@ __device__ inline void dma16(const uint4* src, uint4* lds_wave_base) {
 
 // Winograd F(2x2,3x3) exact-fp32 conv (conv_wino.hip): tile config kWinoCfg of
 // the record-layout table (F32R only), its LDS bytes per block and launcher.
-constexpr size_t kWinoLds = (size_t)(2 * 352 + 2 * 16 * 64 + 2 * 16 * 32) * 16;
+constexpr size_t kWinoLds = (size_t)(2 * 704 + 2 * 16 * 2 * 32) * 16;
 int launch_wino(const ConvH8Args& a, int epi, hipStream_t st);
 
 }  // namespace rrin

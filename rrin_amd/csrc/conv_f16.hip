@@ -1829,7 +1829,7 @@ static int h8_prepare(const rrin_conv_h8_desc* d, ConvH8Args& a) {
   if (d->cfg == kWinoCfg) {
     if (d->prec != RRIN_PREC_F32R) return RRIN_E_CONFIG;
     if ((d->cin & 3) && !d->tail_finite) return RRIN_E_CONFIG;  // stages whole records only
-    a.nchunks = (d->cin + 3) / 4;  // one record group per K chunk
+    a.nchunks = (d->cin + 7) / 8;  // two record groups per K chunk
   }
   a.n = d->n;
   if ((int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n > 0x7fffffff) return RRIN_E_SHAPE;

@@ -19,15 +19,18 @@
 //   A^T = [1 1 1 0; 0 1 -1 -1]
 //
 // Block: 256 threads = 4 waves, tile = 32 output channels x 32 px x 8 rows =
-// 64 patches (16 wide x 4 tall).  Wave (xh, ph): transform rows xi_y in
+// 64 patches (16 wide x 4 tall).  Wave (xh, ph) owns transform rows xi_y in
 // {2xh, 2xh+1} (8 of the 16 points: 8 accumulators of 32 co x 32 patches, 128
 // registers, so two blocks share a CU and cover each other's barriers) of the
-// patch rows 2ph, 2ph+1.  K chunk = one record group (4 channels): per point 2
-// MFMAs (product e: lanes 0-31 channel e, lanes 32-63 channel 2+e).
-// Per chunk, all stages in LDS and double buffered:
-//   raw input tile 10 x 34 records  (LDS-DMA, two chunks ahead)
-//   U slab [xi][co] 16 x 32 records (LDS-DMA, one chunk ahead)
-//   V      [xi][patch] 16 x 64      (input transform by the block, one chunk ahead)
+// patch rows 2ph, 2ph+1.  K chunk = 8 channels (2 record groups): per point 4
+// MFMAs (product e: lanes 0-31 channel e, lanes 32-63 channel 4+e).
+// Each lane transforms exactly the B operands it feeds: the window rows of its
+// patch (3 of 4: the two B^T rows of its xi_y pair), its 4 channels, straight
+// from the LDS image of the raw input -- V never goes through LDS.
+// Per chunk, double buffered in LDS (LDS-DMA, one chunk ahead):
+//   raw input tile 2 groups x 10 rows x 34 cols (even columns, then odd, so
+//                  the stride-2 window reads of 16 lanes are conflict-free)
+//   U slab [xi][half][co] 16 x 2 x 32 records
 // The output transform's two halves (xi_y 0-1, 2-3) meet through LDS: wave
 // xh = 0 finishes output row 0 of each patch, xh = 1 row 1.
 #include "common.hpp"
@@ -38,17 +41,17 @@ typedef float wfloatx16 __attribute__((ext_vector_type(16)));
 typedef float wfloatx4 __attribute__((ext_vector_type(4)));
 typedef float wfloatx2 __attribute__((ext_vector_type(2)));
 
-constexpr int kWnRawCols = 34, kWnRaw = 10 * kWnRawCols, kWnRawStride = 352;
-constexpr int kWnV = 16 * 64;  // records per V buffer
-constexpr int kWnU = 16 * 32;  // records per U buffer
-static_assert(kWinoLds == (size_t)(2 * kWnRawStride + 2 * kWnV + 2 * kWnU) * 16, "LDS size");
+constexpr int kWnRawCols = 34, kWnRawG = 10 * kWnRawCols, kWnRaw = 2 * kWnRawG, kWnRawStride = 704;
+constexpr int kWnU = 16 * 2 * 32;  // records per U buffer: [xi][half][co]
+static_assert(kWinoLds == (size_t)(2 * kWnRawStride + 2 * kWnU) * 16, "LDS size");
+// LDS position of raw column col (0..33) within its row: even columns first
+__device__ inline int wn_col(int col) { return (col & 1) * 17 + (col >> 1); }
 
 template <int EPI>
 __global__ __launch_bounds__(256, 2) void conv3x3_wino_kernel(ConvH8Args a) {
   extern __shared__ __attribute__((aligned(16))) uint4 smem4[];
-  uint4* s_raw = smem4;                      // [2][kWnRawStride]
-  uint4* s_v = smem4 + 2 * kWnRawStride;     // [2][16][64]
-  uint4* s_u = s_v + 2 * kWnV;               // [2][16][32]
+  uint4* s_raw = smem4;                      // [2][kWnRawStride]: [group][row][wn_col]
+  uint4* s_u = smem4 + 2 * kWnRawStride;     // [2][16][2][32]
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int xh = wv & 1, ph = wv >> 1, j = lane & 31, hh = lane >> 5;
@@ -69,81 +72,93 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wino_kernel(ConvH8Args a) {
   const int img = t / a.tiles_y;
   const int nch = a.nchunks;
 
-  // ---- staging: raw input rows y0-1..y0+8, cols x0-1..x0+32 of record group c
+  // ---- staging: raw input rows y0-1..y0+8, cols x0-1..x0+32 of record groups 2c, 2c+1.
+  // Per thread and DMA piece (3): its group of the chunk, its offset inside the
+  // group plane, and the offset of the same column in the zero top-padding row
+  // of group 0 (read instead by groups past cin, which meet zero weights).
   const uint4* src = a.src_hi + (int64_t)img * a.src_img + (int64_t)y0 * a.src_wp + x0 + (kH8PadLeft - 1);
+  int p_g[3], p_off[3], p_zoff[3];
+#pragma unroll
+  for (int it = 0; it < 3; ++it) {
+    const int idx = tid + 256 * it;
+    const int g = idx >= kWnRawG ? 1 : 0;
+    const int rem = idx - g * kWnRawG;
+    const int r = rem / kWnRawCols, pos = rem - r * kWnRawCols;
+    const int col = pos < 17 ? 2 * pos : 2 * (pos - 17) + 1;
+    p_g[it] = g;
+    p_off[it] = r * a.src_wp + col;
+    p_zoff[it] = -y0 * a.src_wp + col;
+  }
   auto issue_raw = [&](int c, int buf) {
 #pragma unroll
-    for (int it = 0; it < 2; ++it) {
-      const int idx = tid + 256 * it;
-      if (idx < kWnRaw) {
-        const int r = idx / kWnRawCols, col = idx - r * kWnRawCols;
-        dma16(src + (int64_t)c * a.src_gp + (int64_t)r * a.src_wp + col,
-              s_raw + buf * kWnRawStride + 256 * it + (tid & ~63));
+    for (int it = 0; it < 3; ++it) {
+      if (it < 2 || tid + 512 < kWnRaw) {
+        const int gg = 2 * c + p_g[it];
+        const int64_t off = gg * 4 < a.cin ? (int64_t)gg * a.src_gp + p_off[it] : (int64_t)p_zoff[it];
+        dma16(src + off, s_raw + buf * kWnRawStride + 256 * it + (tid & ~63));
       }
     }
   };
-  const uint4* wsrc = a.w_hi + (int64_t)cob * nch * kWnU;
+  const uint4* wsrc = a.w_hi + (int64_t)cob * nch * kWnU + tid;
   auto issue_u = [&](int c, int buf) {
 #pragma unroll
-    for (int it = 0; it < 2; ++it)
-      dma16(wsrc + (int64_t)c * kWnU + tid + 256 * it, s_u + buf * kWnU + 256 * it + (tid & ~63));
+    for (int it = 0; it < 4; ++it) dma16(wsrc + (int64_t)c * kWnU + 256 * it, s_u + buf * kWnU + 256 * it + (tid & ~63));
   };
 
-  // ---- input transform: thread (patch tp, xi row txy) -> V[txy*4 + xi_x][tp], 4 channels
-  const int tp = tid & 63, txy = tid >> 6;
-  const int tpr = 2 * (tp >> 5) + ((tp & 31) >> 4), tjx = tp & 15;
-  const int tra = txy == 0 ? 0 : 1, trb = txy == 3 ? 3 : 2;  // the two window rows of B^T row txy
-  auto transform = [&](int rb, int vb) {
-    const uint4* base = s_raw + rb * kWnRawStride + (2 * tpr) * kWnRawCols + 2 * tjx;
-    wfloatx4 tt[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const wfloatx4 da = __builtin_bit_cast(wfloatx4, base[tra * kWnRawCols + k]);
-      const wfloatx4 db = __builtin_bit_cast(wfloatx4, base[trb * kWnRawCols + k]);
-      tt[k] = txy == 1 ? da + db : (txy == 2 ? db - da : da - db);
-    }
-    uint4* vd = s_v + vb * kWnV + txy * 4 * 64 + tp;
-    vd[0] = __builtin_bit_cast(uint4, tt[0] - tt[2]);
-    vd[64] = __builtin_bit_cast(uint4, tt[1] + tt[2]);
-    vd[128] = __builtin_bit_cast(uint4, tt[2] - tt[1]);
-    vd[192] = __builtin_bit_cast(uint4, tt[1] - tt[3]);
-  };
-
-  // ---- channel contraction: 8 points (xi = 8 xh + l) x 2 products per chunk
+  // ---- per chunk: this lane's B operands V[xi][4hh + e][patch j] from its window:
+  // B^T rows 2xh, 2xh+1 as t0 = d[ra] - d[rb], t1 = d[rc] + sgn d[rd] (no branch on xh),
+  // then 8 points x 4 products
   wfloatx16 acc[8];
 #pragma unroll
   for (int l = 0; l < 8; ++l)
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[l][i] = 0.f;
+  const int pr = 2 * ph + (j >> 4), jx = j & 15;
+  const int ra = xh ? 2 : 0, rb = xh ? 1 : 2, rd = xh ? 3 : 2;  // rc = 1
+  const float sgn = xh ? -1.f : 1.f;
   auto compute = [&](int b) {
-    const wfloatx2* su = reinterpret_cast<const wfloatx2*>(s_u + b * kWnU + 8 * xh * 32 + j) + hh;
-    const wfloatx2* sv = reinterpret_cast<const wfloatx2*>(s_v + b * kWnV + 8 * xh * 64 + ph * 32 + j) + hh;
-    wfloatx2 av[8], bv[8];
+    const uint4* su = s_u + b * kWnU + 8 * xh * 64 + hh * 32 + j;
+    wfloatx4 u[8];
 #pragma unroll
-    for (int l = 0; l < 8; ++l) {
-      av[l] = su[l * 32 * 2];
-      bv[l] = sv[l * 64 * 2];
+    for (int l = 0; l < 8; ++l) u[l] = __builtin_bit_cast(wfloatx4, su[l * 64]);
+    const uint4* rw = s_raw + b * kWnRawStride + hh * kWnRawG + (2 * pr) * kWnRawCols;
+    wfloatx4 tv[2][4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int pc = wn_col(2 * jx + k);
+      const wfloatx4 da = __builtin_bit_cast(wfloatx4, rw[ra * kWnRawCols + pc]);
+      const wfloatx4 db = __builtin_bit_cast(wfloatx4, rw[rb * kWnRawCols + pc]);
+      const wfloatx4 dc = __builtin_bit_cast(wfloatx4, rw[kWnRawCols + pc]);
+      const wfloatx4 dd = __builtin_bit_cast(wfloatx4, rw[rd * kWnRawCols + pc]);
+      tv[0][k] = da - db;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) tv[1][k][e] = fmaf(sgn, dd[e], dc[e]);
+    }
+    wfloatx4 v[8];
+#pragma unroll
+    for (int yl = 0; yl < 2; ++yl) {
+      const wfloatx4* c4 = tv[yl];
+      v[4 * yl + 0] = c4[0] - c4[2];
+      v[4 * yl + 1] = c4[1] + c4[2];
+      v[4 * yl + 2] = c4[2] - c4[1];
+      v[4 * yl + 3] = c4[1] - c4[3];
     }
 #pragma unroll
-    for (int e = 0; e < 2; ++e)
+    for (int e = 0; e < 4; ++e)
 #pragma unroll
-      for (int l = 0; l < 8; ++l) acc[l] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[l][e], bv[l][e], acc[l], 0, 0, 0);
+      for (int l = 0; l < 8; ++l) acc[l] = __builtin_amdgcn_mfma_f32_32x32x2f32(u[l][e], v[l][e], acc[l], 0, 0, 0);
   };
 
   issue_raw(0, 0);
-  if (nch > 1) issue_raw(1, 1);
   issue_u(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  transform(0, 0);
-  __syncthreads();
   for (int c = 0; c < nch; ++c) {
     const int b = c & 1;
-    // raw buffer b held chunk c (transformed last iteration); U / V buffer b^1 were read last iteration
-    if (c + 2 < nch) issue_raw(c + 2, b);
+    // buffers b^1 were last read in the previous chunk, before the barrier that ended it
     if (c + 1 < nch) {
+      issue_raw(c + 1, b ^ 1);
       issue_u(c + 1, b ^ 1);
-      transform(b ^ 1, b ^ 1);
     }
     compute(b);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -162,7 +177,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wino_kernel(ConvH8Args a) {
       q[yl][1][i] = (m1 - m2) - m3;
     }
   // wave xh 0 hands its Q1 (yl 1) to its partner, wave xh 1 its Q2 (yl 0)
-  wfloatx4* xch = reinterpret_cast<wfloatx4*>(s_v);
+  wfloatx4* xch = reinterpret_cast<wfloatx4*>(s_u);
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     wfloatx4 g;
@@ -186,7 +201,6 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wino_kernel(ConvH8Args a) {
   }
 
   // ---- epilogue: this lane's pixels (y, x0 + 2 jx + c), 16 channels 8 qq + 4 hh + e
-  const int pr = 2 * ph + (j >> 4), jx = j & 15;
   const int y = y0 + 2 * pr + xh;
   uint4* dst = a.dst_hi + (int64_t)img * a.dst_img;
   auto store4 = [&](int64_t rec, const float* v) {
@@ -247,7 +261,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wino_kernel(ConvH8Args a) {
     }
     if constexpr (EPI == RRIN_EPI_LEAKY_POOL) {
       // row 1 of each patch (wave xh 1) meets row 0 (wave xh 0) in LDS; avg = 0.25 ((v00 + v10) + (v01 + v11))
-      wfloatx4* xp = reinterpret_cast<wfloatx4*>(s_u);
+      wfloatx4* xp = reinterpret_cast<wfloatx4*>(s_raw);
       if (xh) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
@@ -315,7 +329,7 @@ using namespace rrin;
 
 extern "C" int64_t rrin_pack_conv3x3_wino_floats(int32_t cout, int32_t cin) {
   if (cout < 1 || cin < 1) return RRIN_E_ARG;
-  const int64_t cob = (cout + 31) / 32, nch = (cin + 3) / 4;
+  const int64_t cob = (cout + 31) / 32, nch = (cin + 7) / 8;
   return cob * nch * kWnU * 4;
 }
 
@@ -326,22 +340,23 @@ extern "C" int rrin_pack_conv3x3_wino(const float* w, const float* b, int32_t co
     for (int c = 0; c < cin; ++c)
       if (perm[c] < 0 || perm[c] >= cin) return RRIN_E_ARG;
   static const double G[4][3] = {{1.0, 0.0, 0.0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0.0, 0.0, 1.0}};
-  const int cob_n = (cout + 31) / 32, nch = (cin + 3) / 4;
+  const int cob_n = (cout + 31) / 32, nch = (cin + 7) / 8;
   int64_t o = 0;
   for (int cob = 0; cob < cob_n; ++cob)
     for (int c = 0; c < nch; ++c)
       for (int xi = 0; xi < 16; ++xi)
-        for (int col = 0; col < 32; ++col)
-          for (int e = 0; e < 4; ++e) {
-            const int co = cob * 32 + col, ch = c * 4 + e;
-            double u = 0.0;
-            if (co < cout && ch < cin) {
-              const float* g = w + ((int64_t)co * cin + (perm ? perm[ch] : ch)) * 9;
-              for (int ky = 0; ky < 3; ++ky)
-                for (int kx = 0; kx < 3; ++kx) u += G[xi >> 2][ky] * G[xi & 3][kx] * (double)g[ky * 3 + kx];
+        for (int hh = 0; hh < 2; ++hh)
+          for (int col = 0; col < 32; ++col)
+            for (int e = 0; e < 4; ++e) {
+              const int co = cob * 32 + col, ch = c * 8 + hh * 4 + e;
+              double u = 0.0;
+              if (co < cout && ch < cin) {
+                const float* g = w + ((int64_t)co * cin + (perm ? perm[ch] : ch)) * 9;
+                for (int ky = 0; ky < 3; ++ky)
+                  for (int kx = 0; kx < 3; ++kx) u += G[xi >> 2][ky] * G[xi & 3][kx] * (double)g[ky * 3 + kx];
+              }
+              wpack[o++] = (float)u;
             }
-            wpack[o++] = (float)u;
-          }
   for (int co = 0; co < cob_n * 32; ++co) bpack[co] = co < cout ? b[co] : 0.f;
   return 0;
 }

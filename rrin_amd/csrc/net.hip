@@ -265,9 +265,12 @@ int run_unet(const Plan& p, const UNetSpec& u, const rrin_conv_weights* cw, cons
 
 int conv_h8(const Plan& p, const rrin_conv_weights& cw, int cin, int cout, int epi, const rrin_h8& src,
             const rrin_h8& dst, const rrin_h8* pool, hipStream_t st, float* edge = nullptr) {
-  // algorithmic FLOPs of the reference conv (a sub-pixel conv has 4 phase rows per real channel)
+  // algorithmic FLOPs of the conv (a sub-pixel conv has 4 phase rows per real channel): 9
+  // multiply-adds per output and input channel in the direct form, 4 in Winograd F(2x2,3x3)
+  // (16 per 2x2 patch)
   const int creal = epi == RRIN_EPI_SUBPIXEL ? cout / 4 : cout;
-  ProfScope ps(p.prof, st, RRIN_KIND_CONV, 2.0 * 9 * cin * creal * (double)dst.g.h * dst.g.w * p.n);
+  const int macs = p.prec == RRIN_PREC_F32R && rrin_conv_h8_cfg_wino(cw.cfg) ? 4 : 9;
+  ProfScope ps(p.prof, st, RRIN_KIND_CONV, 2.0 * macs * cin * creal * (double)dst.g.h * dst.g.w * p.n);
   rrin_conv_h8_desc d;
   memset(&d, 0, sizeof(d));
   d.n = p.n;

@@ -152,12 +152,28 @@ def size_class(pixels: int) -> str:
     return "xlarge" if pixels <= XLARGE_PX else "xxlarge"
 
 
+# Exact fp32 (F32R): Winograd F(2x2,3x3) (conv_wino.hip) for the body convs of
+# these size classes -- 1.3-1.7x the best direct-form config on every conv shape
+# at 1280x720 x 2 (profiles/r02/wino/).  Other classes, and WINO = False (A/B),
+# use the direct-form tables below.
+WINO = True
+WINO_SIZES = ("medium", "large", "xlarge", "xxlarge")
+
+
+def wino_cfg() -> int:
+    lib = _lib.lib()
+    return next(c for c in range(lib.rrin_conv_h8_cfg_count()) if lib.rrin_conv_h8_cfg_wino(c))
+
+
 def choose_cfg_h8(cin: int, cout: int, prec: int, level: int = 0, size: str = "large") -> int:
-    """Tile config of the split-fp16 / fp16 conv (conv_f16.hip table) for a conv
+    """Tile config of the record-layout conv (conv_f16.hip table) for a conv
     running on the grid of U-Net level ``level`` (a sub-pixel up conv runs on the
     low-res grid with 4x the output rows) in a forward part of size class
-    ``size``: the swept choice (H8_TUNED_BY_SIZE, H8_TUNED), else a level rule
-    from the same sweep."""
+    ``size``: exact fp32 takes the Winograd config (WINO_SIZES); otherwise the
+    swept choice (H8_TUNED_BY_SIZE, H8_TUNED), else a level rule from the same
+    sweep."""
+    if prec == _lib.PREC_F32R and WINO and size in WINO_SIZES:
+        return wino_cfg()
     table = H8_TUNED_BY_SIZE.get(size, {}).get(prec) or H8_TUNED.get(prec, {})
     cfg = table.get((cin, cout, level))
     if cfg is not None and _lib.lib().rrin_conv_h8_cfg_fits(cfg, prec, cin):
@@ -396,6 +412,14 @@ class RRINEngine:
         return p
 
     force_size_class = None  # A/B knob: use this tile-table class for every forward part
+
+    def conv_algorithm(self, n: int, h: int, w: int) -> str:
+        """'winograd', 'direct' or 'mixed': the form of the body convs of a forward part."""
+        if self.prec == _lib.PREC_F32:
+            return "direct"
+        t = self.conv_table_for(n, h, w)
+        k = sum(1 for i in range(self.expected_convs) if self.lib.rrin_conv_h8_cfg_wino(t[i].cfg))
+        return "winograd" if k == self.expected_convs else ("direct" if k == 0 else "mixed")
 
     def conv_table_for(self, n: int, h: int, w: int):
         """ConvWeights table of a forward part of n pairs at h x w (its tile-table size class)."""

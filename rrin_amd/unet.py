@@ -175,7 +175,10 @@ def conv_bytes(unet: UNet, h: int, w: int, bytes_per_value: int = 4) -> tuple[in
     return sum(r for _, _, r, _ in work), sum(wb for _, _, _, wb in work)
 
 
-def roofline_bound_s(unet: UNet, h: int, w: int, bytes_per_value: int, peak_flops: float, bw: float) -> float:
+def roofline_bound_s(unet: UNet, h: int, w: int, bytes_per_value: int, peak_flops: float, bw: float,
+                     flop_scale: float = 1.0) -> float:
     """Per-layer roofline bound T_LB = sum over body convs of max(FLOP/peak, bytes/BW)
-    (SURVEY §8d), in seconds for one image."""
-    return sum(max(fl / peak_flops, (r + wb) / bw) for _, fl, r, wb in conv_work(unet, h, w, bytes_per_value))
+    (SURVEY §8d), in seconds for one image.  ``flop_scale``: FLOPs of the algorithm
+    the convs run per direct-form FLOP (Winograd F(2x2,3x3): 4/9)."""
+    return sum(max(flop_scale * fl / peak_flops, (r + wb) / bw)
+               for _, fl, r, wb in conv_work(unet, h, w, bytes_per_value))

@@ -51,8 +51,10 @@ def wino_cfg():
 
 def cfgs(prec, cout, cin):
     lib = _lib.lib()
+    # the Winograd config stages whole records only: cin % 4 != 0 needs tail_finite (test_h8_conv_dma_finite_tail)
     return [c for c in range(lib.rrin_conv_h8_cfg_count())
-            if lib.rrin_conv_h8_cfg_fits(c, prec, cin) and lib.rrin_conv_h8_cfg_bm(c) <= max(32, 2 * cout)]
+            if lib.rrin_conv_h8_cfg_fits(c, prec, cin) and lib.rrin_conv_h8_cfg_bm(c) <= max(32, 2 * cout)
+            and not (lib.rrin_conv_h8_cfg_wino(c) and cin % 4)]
 
 
 def pack_h8(w, b, cfg, prec, dev, perm=None):

@@ -31,9 +31,9 @@ def pack_wino(w, b, perm=None):
 
 
 def unpack_u(wp, cout, cin):
-    """[cob][chunk][xi][co32][4] -> U[xi][co][ci] (float64)."""
-    cob, nch = (cout + 31) // 32, (cin + 3) // 4
-    u = wp.reshape(cob, nch, 16, 32, 4).transpose(2, 0, 3, 1, 4).reshape(16, cob * 32, nch * 4)
+    """[cob][chunk of 8][xi][half][co32][4] -> U[xi][co][ci] (float64)."""
+    cob, nch = (cout + 31) // 32, (cin + 7) // 8
+    u = wp.reshape(cob, nch, 16, 2, 32, 4).transpose(2, 0, 4, 1, 3, 5).reshape(16, cob * 32, nch * 8)
     return u[:, :cout, :cin].astype(np.float64)
 
 
@@ -75,7 +75,7 @@ def test_wino_packing_layout_and_perm():
     b = rng.standard_normal(cout).astype(np.float32)
     perm = [4, 5, 6, 7, 8, 9, 0, 1, 2, 3]
     wp, _ = pack_wino(w, b, perm)
-    full = wp.reshape(2, 3, 16, 32, 4).transpose(2, 0, 3, 1, 4).reshape(16, 64, 12)
+    full = wp.reshape(2, 2, 16, 2, 32, 4).transpose(2, 0, 4, 1, 3, 5).reshape(16, 64, 16)
     assert not full[:, cout:].any() and not full[:, :, cin:].any()
     u_perm = unpack_u(wp, cout, cin)
     u_ref = unpack_u(pack_wino(np.ascontiguousarray(w[:, perm]), b)[0], cout, cin)
@@ -92,5 +92,5 @@ def test_wino_config_entry():
     assert lib.rrin_conv_h8_cfg_bm(c) == 32 and lib.rrin_conv_h8_cfg_th(c) == 8
     assert lib.rrin_conv_h8_cfg_ok(c, _lib.PREC_F32R) == 1
     assert lib.rrin_conv_h8_cfg_ok(c, _lib.PREC_F16X3) == 0 and lib.rrin_conv_h8_cfg_ok(c, _lib.PREC_F16) == 0
-    assert lib.rrin_pack_conv3x3_wino_floats(33, 5) == 2 * 2 * 16 * 32 * 4
+    assert lib.rrin_pack_conv3x3_wino_floats(33, 5) == 2 * 1 * 16 * 2 * 32 * 4
     assert lib.rrin_pack_conv3x3_wino_floats(0, 5) < 0

@@ -161,6 +161,7 @@ def tune_h8(args):
             whi, wlo, bp, inv = pack_h8(wt, b, cfg, prec, dev)
             d = _lib.ConvH8Desc()
             d.n, d.cin, d.cout, d.cfg, d.prec, d.epi_mode, d.slope, d.inv_wscale = n, cin, kout, cfg, prec, epi, 0.1, inv
+            d.tail_finite = 1  # channels past cin are zero (as the Net's g16 buffer): whole-record staging
             d.src, d.dst = x.view(0, cin), dst.view(0, cout)
             if edge is not None:
                 d.edge = edge.data_ptr()
