@@ -394,7 +394,9 @@ def main():
         # (tools/gpu_check.sh pmc -> tools/pmc_summary.py; rocprofv3 cannot
         # collect counters inside this process's timed region)
         tab = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_traffic.json")
-        key = f"{args.precision}@{W}x{H}x{B}" + (f"s{args.streams}" if args.streams > 1 else "")
+        # exact fp32: "fp32" = the Winograd kernel, "fp32-direct" = the direct form (--no-wino)
+        kp = args.precision + ("-direct" if args.precision == "fp32" and roofline["conv_algorithm"] == "direct" else "")
+        key = f"{kp}@{W}x{H}x{B}" + (f"s{args.streams}" if args.streams > 1 else "")
         if os.path.exists(tab):
             ent = json.load(open(tab)).get(key)
             if ent is not None:

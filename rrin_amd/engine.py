@@ -153,11 +153,12 @@ def size_class(pixels: int) -> str:
 
 
 # Exact fp32 (F32R): Winograd F(2x2,3x3) (conv_wino.hip) for the body convs of
-# these size classes -- 1.3-1.7x the best direct-form config on every conv shape
-# at 1280x720 x 2 (profiles/r02/wino/).  Other classes, and WINO = False (A/B),
-# use the direct-form tables below.
+# these size classes -- faster than the best direct-form config on every conv
+# shape of the Net but the 6-channel first conv (1280x720 x 2: 1.3-1.7x; 640x368
+# x 1: 1.0-1.6x; profiles/r02/wino/tune_*).  WINO = False (A/B) uses the
+# direct-form tables below.
 WINO = True
-WINO_SIZES = ("medium", "large", "xlarge", "xxlarge")
+WINO_SIZES = ("small", "medium", "large", "xlarge", "xxlarge")
 
 
 def wino_cfg() -> int:

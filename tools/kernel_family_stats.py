@@ -3,7 +3,7 @@
 instantiations of one kernel summed), to compare the conv family's average
 launch duration with the one bench.py measures with HIP events.
 
-  python tools/kernel_family_stats.py profiles/r01_v9/kernel_stats_split16.csv [kernel_trace.csv FORWARDS]
+  python tools/kernel_family_stats.py profiles/r01_v9/kernel_stats_split16.csv [kernel_trace.csv FORWARDS [FAMILY]]
 
 With a kernel_trace.csv and the number of forward steps it holds (warm-up
 included), also the conv family's busy time per step = the union of its
@@ -50,4 +50,4 @@ def busy(trace, forwards, fam_name="conv3x3_h8_kernel"):
 if __name__ == "__main__":
     main(sys.argv[1])
     if len(sys.argv) > 3:
-        busy(sys.argv[2], int(sys.argv[3]))
+        busy(sys.argv[2], int(sys.argv[3]), *sys.argv[4:5])

@@ -46,6 +46,9 @@ def main():
                     help="merge the conv family's per-launch bytes into this table (read by bench.py)")
     ap.add_argument("--precision", default="fp32_split16")
     ap.add_argument("--config", default="1280x720x4", help="WxHxB of the profiled bench run")
+    ap.add_argument("--family", default=None,
+                    help="conv kernel family (default by precision; exact fp32 runs conv3x3_wino_kernel)")
+    ap.add_argument("--key", default=None, help="table key prefix (default: --precision)")
     a = ap.parse_args()
     fetch = load(a.fetch, "FETCH_SIZE")
     write = load(a.write, "WRITE_SIZE")
@@ -68,10 +71,11 @@ def main():
         json.dump({"correction": "hbm = (2*FETCH_SIZE + WRITE_SIZE) KiB (gfx950 FETCH_SIZE = 1/2 of wide reads)",
                    "steps": a.steps, "kernels": res}, open(a.out, "w"), indent=1)
     if a.table:
-        fam_name = "conv3x3_mfma_kernel" if a.precision == "fp32_planar" else "conv3x3_h8_kernel"
+        fam_name = a.family or {"fp32_planar": "conv3x3_mfma_kernel", "fp32": "conv3x3_wino_kernel"}.get(
+            a.precision, "conv3x3_h8_kernel")
         tab = json.load(open(a.table)) if os.path.exists(a.table) else {}
         r = res[fam_name]
-        tab[f"{a.precision}@{a.config}"] = {
+        tab[f"{a.key or a.precision}@{a.config}"] = {
             "kernel_family": fam_name, "hbm_bytes_per_launch": r["hbm_bytes_per_dispatch"],
             "hbm_bytes_per_step": r["hbm_bytes_per_step"], "launches_per_step": r["dispatches_per_step"],
             "correction": "hbm = (2*FETCH_SIZE + WRITE_SIZE) KiB, separate --pmc passes",
