@@ -189,5 +189,8 @@ __device__ inline void dma16(const uint4* src, uint4* lds_wave_base) {
 // the record-layout table (F32R only), its LDS bytes per block and launcher.
 constexpr size_t kWinoLds = (size_t)(2 * 704 + 2 * 16 * 2 * 32) * 16;
 int launch_wino(const ConvH8Args& a, int epi, hipStream_t st);
+#ifdef RRIN_LAB
+int launch_wino_lab(const ConvH8Args& a, int abl, hipStream_t st);  // ablation bits (conv_wino.hip)
+#endif
 
 }  // namespace rrin

@@ -1652,6 +1652,7 @@ static const CfgH8 kCfgH8[] = {
 };
 static constexpr int kNumCfgH8 = sizeof(kCfgH8) / sizeof(kCfgH8[0]);
 static constexpr int kWinoCfg = kNumCfgH8 - 1;
+static inline bool is_wino(int cfg) { return cfg == kWinoCfg; }
 static constexpr size_t kMaxLds = 160 * 1024;
 
 static int num_cus() {
@@ -1826,7 +1827,7 @@ static int h8_prepare(const rrin_conv_h8_desc* d, ConvH8Args& a) {
   a.co_blocks = (d->cout + ci.bm - 1) / ci.bm;
   a.tiles_x = (w + 31) / 32;
   a.tiles_y = (h + ci.th - 1) / ci.th;
-  if (d->cfg == kWinoCfg) {
+  if (is_wino(d->cfg)) {
     if (d->prec != RRIN_PREC_F32R) return RRIN_E_CONFIG;
     if ((d->cin & 3) && !d->tail_finite) return RRIN_E_CONFIG;  // stages whole records only
     a.nchunks = (d->cin + 7) / 8;  // two record groups per K chunk
@@ -1853,11 +1854,11 @@ extern "C" int rrin_conv_h8_cfg_bm(int32_t cfg) {
 extern "C" int rrin_conv_h8_cfg_th(int32_t cfg) {
   return (cfg >= 0 && cfg < kNumCfgH8) ? kCfgH8[cfg].th : RRIN_E_CONFIG;
 }
-extern "C" int rrin_conv_h8_cfg_wino(int32_t cfg) { return cfg == kWinoCfg ? 1 : 0; }
+extern "C" int rrin_conv_h8_cfg_wino(int32_t cfg) { return is_wino(cfg) ? 1 : 0; }
 extern "C" int rrin_conv_h8_cfg_ok(int32_t cfg, int32_t prec) {
   if (cfg < 0 || cfg >= kNumCfgH8) return 0;
   if (!rec_prec(prec)) return 0;
-  if (cfg == kWinoCfg && prec != RRIN_PREC_F32R) return 0;
+  if (is_wino(cfg) && prec != RRIN_PREC_F32R) return 0;
   return (planes_of(prec) == 2 ? kCfgH8[cfg].lds2 : kCfgH8[cfg].lds1) <= kMaxLds ? 1 : 0;
 }
 
@@ -1876,7 +1877,7 @@ extern "C" int rrin_conv3x3_h8_fwd(const rrin_conv_h8_desc* d, void* stream) {
   const int rc = h8_prepare(d, a);
   if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;
-  if (d->cfg == kWinoCfg) return launch_wino(a, d->epi_mode, st);
+  if (is_wino(d->cfg)) return launch_wino(a, d->epi_mode, st);
   switch (d->cfg) {
 #define X(id, nw, wm, wn, sc, pe) \
   case id:                        \
@@ -1906,6 +1907,11 @@ static int lab_cfg(const ConvH8Args& a, int sched, int persist, hipStream_t st) 
 
 // F16X3 (cfg 0, 1, 6) or F32R (cfg 0, 1, 3, 4, 5, 6, 16) LEAKY conv with schedule bits
 extern "C" int rrin_conv3x3_h8_lab(const rrin_conv_h8_desc* d, int32_t sched, int32_t persist, void* stream) {
+  if (d && is_wino(d->cfg) && d->epi_mode == RRIN_EPI_LEAKY) {  // Winograd: sched = ablation bits
+    ConvH8Args a;
+    const int rc = h8_prepare(d, a);
+    return rc ? rc : launch_wino_lab(a, sched, (hipStream_t)stream);
+  }
   if (!d || (d->prec != RRIN_PREC_F16X3 && d->prec != RRIN_PREC_F32R) || d->epi_mode != RRIN_EPI_LEAKY ||
       (d->cin % 8))
     return RRIN_E_ARG;

@@ -47,7 +47,10 @@ static_assert(kWinoLds == (size_t)(2 * kWnRawStride + 2 * kWnU) * 16, "LDS size"
 // LDS position of raw column col (0..33) within its row: even columns first
 __device__ inline int wn_col(int col) { return (col & 1) * 17 + (col >> 1); }
 
-template <int EPI>
+// ABL: kernel-lab ablations only (built into librrin_lab.so under RRIN_LAB; the
+// product library instantiates ABL = 0): 1 no weight DMA after chunk 0, 2 no raw
+// DMA after chunk 0, 4 no MFMAs (operands kept live), 8 no transform arithmetic.
+template <int EPI, int ABL = 0>
 __global__ __launch_bounds__(256, 2) void conv3x3_wino_kernel(ConvH8Args a) {
   extern __shared__ __attribute__((aligned(16))) uint4 smem4[];
   uint4* s_raw = smem4;                      // [2][kWnRawStride]: [group][row][wn_col]
@@ -113,7 +116,10 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wino_kernel(ConvH8Args a) {
   for (int l = 0; l < 8; ++l)
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[l][i] = 0.f;
-  const int pr = 2 * ph + (j >> 4), jx = j & 15;
+  // MFMA column j -> patch (row pr, column jx).  The second row's columns are
+  // rotated by 12 so the window reads of the two rows (68 records apart) fall on
+  // distinct banks in every ds_read_b128 lane group ({0-3,12-15,20-27}, {4-11,16-19,28-31}).
+  const int pr = 2 * ph + (j >> 4), jx = (j + 12 * (j >> 4)) & 15;
   const int ra = xh ? 2 : 0, rb = xh ? 1 : 2, rd = xh ? 3 : 2;  // rc = 1
   const float sgn = xh ? -1.f : 1.f;
   auto compute = [&](int b) {
@@ -130,14 +136,24 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wino_kernel(ConvH8Args a) {
       const wfloatx4 db = __builtin_bit_cast(wfloatx4, rw[rb * kWnRawCols + pc]);
       const wfloatx4 dc = __builtin_bit_cast(wfloatx4, rw[kWnRawCols + pc]);
       const wfloatx4 dd = __builtin_bit_cast(wfloatx4, rw[rd * kWnRawCols + pc]);
-      tv[0][k] = da - db;
+      if constexpr ((ABL & 8) != 0) {
+        tv[0][k] = da;
+        tv[1][k] = dc;
+      } else {
+        tv[0][k] = da - db;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) tv[1][k][e] = fmaf(sgn, dd[e], dc[e]);
+        for (int e = 0; e < 4; ++e) tv[1][k][e] = fmaf(sgn, dd[e], dc[e]);
+      }
     }
     wfloatx4 v[8];
 #pragma unroll
     for (int yl = 0; yl < 2; ++yl) {
       const wfloatx4* c4 = tv[yl];
+      if constexpr ((ABL & 8) != 0) {
+#pragma unroll
+        for (int x = 0; x < 4; ++x) v[4 * yl + x] = c4[x];
+        continue;
+      }
       v[4 * yl + 0] = c4[0] - c4[2];
       v[4 * yl + 1] = c4[1] + c4[2];
       v[4 * yl + 2] = c4[2] - c4[1];
@@ -146,7 +162,12 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wino_kernel(ConvH8Args a) {
 #pragma unroll
     for (int e = 0; e < 4; ++e)
 #pragma unroll
-      for (int l = 0; l < 8; ++l) acc[l] = __builtin_amdgcn_mfma_f32_32x32x2f32(u[l][e], v[l][e], acc[l], 0, 0, 0);
+      for (int l = 0; l < 8; ++l) {
+        if constexpr ((ABL & 4) != 0)
+          asm volatile("" ::"v"(u[l][e]), "v"(v[l][e]));
+        else
+          acc[l] = __builtin_amdgcn_mfma_f32_32x32x2f32(u[l][e], v[l][e], acc[l], 0, 0, 0);
+      }
   };
 
   issue_raw(0, 0);
@@ -157,8 +178,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wino_kernel(ConvH8Args a) {
     const int b = c & 1;
     // buffers b^1 were last read in the previous chunk, before the barrier that ended it
     if (c + 1 < nch) {
-      issue_raw(c + 1, b ^ 1);
-      issue_u(c + 1, b ^ 1);
+      if constexpr (!(ABL & 2)) issue_raw(c + 1, b ^ 1);
+      if constexpr (!(ABL & 1)) issue_u(c + 1, b ^ 1);
     }
     compute(b);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -302,15 +323,32 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wino_kernel(ConvH8Args a) {
   }
 }
 
-template <int EPI>
+template <int EPI, int ABL = 0>
 static int launch_wino_k(const ConvH8Args& a, hipStream_t st) {
-  auto k = conv3x3_wino_kernel<EPI>;
+  auto k = conv3x3_wino_kernel<EPI, ABL>;
   static LdsAttr attr;
   if (int e = attr.ensure((const void*)k, (int)kWinoLds)) return e;
   const int64_t grid = (int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n;
   hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256), kWinoLds, st, a);
   return hip_code(hipGetLastError());
 }
+
+#ifdef RRIN_LAB
+// kernel lab (librrin_lab.so only): the LEAKY conv with ablation bits
+int launch_wino_lab(const ConvH8Args& a, int abl, hipStream_t st) {
+  switch (abl) {
+    case 0: return launch_wino_k<RRIN_EPI_LEAKY, 0>(a, st);
+    case 1: return launch_wino_k<RRIN_EPI_LEAKY, 1>(a, st);
+    case 2: return launch_wino_k<RRIN_EPI_LEAKY, 2>(a, st);
+    case 3: return launch_wino_k<RRIN_EPI_LEAKY, 3>(a, st);
+    case 4: return launch_wino_k<RRIN_EPI_LEAKY, 4>(a, st);
+    case 8: return launch_wino_k<RRIN_EPI_LEAKY, 8>(a, st);
+    case 11: return launch_wino_k<RRIN_EPI_LEAKY, 11>(a, st);
+    case 15: return launch_wino_k<RRIN_EPI_LEAKY, 15>(a, st);
+  }
+  return RRIN_E_CONFIG;
+}
+#endif
 
 int launch_wino(const ConvH8Args& a, int epi, hipStream_t st) {
   switch (epi) {

@@ -43,10 +43,10 @@ def keyed_conv(cin, cout, key="h8"):
 NO_POOL_CFGS = (4, 16)
 
 
-def wino_cfg():
-    """Id of the Winograd F(2x2,3x3) exact-fp32 config (R32 only)."""
+def wino_cfgs():
+    """Ids of the Winograd F(2x2,3x3) exact-fp32 configs (R32 only)."""
     lib = _lib.lib()
-    return next(c for c in range(lib.rrin_conv_h8_cfg_count()) if lib.rrin_conv_h8_cfg_wino(c))
+    return tuple(c for c in range(lib.rrin_conv_h8_cfg_count()) if lib.rrin_conv_h8_cfg_wino(c))
 
 
 def cfgs(prec, cout, cin):
@@ -201,7 +201,7 @@ def test_h8_conv_dma_finite_tail(gpu, prec, cin):
     x = torch.rand(2, 16, 32, 48, device=gpu) * 2 - 1
     wt, b = keyed_conv(cin, 32, "tail")
     ref = ref_conv(x[:, :cin], wt, b)
-    for cfg in (1, 6) + ((wino_cfg(),) if prec == R32 else ()):
+    for cfg in (1, 6) + (wino_cfgs() if prec == R32 else ()):
         dst, _ = conv_h8(H8Tensor.from_nchw(x, prec), wt, b, cfg, prec, cin=cin, tail_finite=1)
         np.testing.assert_allclose(dst.to_nchw().cpu().double().numpy(), ref.numpy(), **TOL[prec])
 
@@ -241,7 +241,7 @@ def test_h8_leaky_rep_writes_replicated_ring(gpu, prec):
     x = torch.rand(2, 32, 13, 45, device=gpu) * 2 - 1
     wt, b = keyed_conv(32, 64, "rep")
     ref = ref_conv(x, wt, b, 0.1)
-    for cfg in (0, 6) + ((wino_cfg(),) if prec == R32 else ()):
+    for cfg in (0, 6) + (wino_cfgs() if prec == R32 else ()):
         dst, _ = conv_h8(H8Tensor.from_nchw(x, prec), wt, b, cfg, prec, epi=_lib.EPI_LEAKY_REP)
         np.testing.assert_allclose(dst.to_nchw().cpu().double().numpy(), ref.numpy(), **TOL[prec])
         # the ring must equal the replicated border; everything else in the padding stays zero
