@@ -64,3 +64,11 @@ clean:
 	rm -rf build $(LIB) $(LAB) $(LAB32) $(PKV)
 
 .PHONY: all lab clean resource pk-variants
+
+# Persistent-grid threshold A/B (tools/gpu_pers_ab.sh): tiles per block slot from
+# which the Winograd grid is persistent (product: never)
+PERSV := rrin_amd/librrin_hip_pers3.so rrin_amd/librrin_hip_pers8.so
+pers-variants: $(PERSV)
+
+rrin_amd/librrin_hip_pers%.so: $(SRCS) $(SRC_DIR)/common.hpp include/rrin_hip.h
+	$(HIPCC) $(CXXFLAGS) -DRRIN_WINO_PERS_MIN=$* -shared -o $@ $(SRCS)

@@ -50,11 +50,16 @@ __device__ inline int wn_col(int col) { return (col & 1) * 17 + (col >> 1); }
 // ABL: kernel-lab ablations only (built into librrin_lab.so under RRIN_LAB; the
 // product library instantiates ABL = 0): 1 no weight DMA after chunk 0, 2 no raw
 // DMA after chunk 0, 4 no MFMAs (operands kept live), 8 no transform arithmetic.
-template <int EPI, int ABL = 0>
+// PERS: persistent grid (2 blocks per CU); a block loops over the tiles bid,
+// bid + grid, ... and stages chunk 0 of its next tile during the last chunk of the
+// current one, so only its first tile waits for staging.  The output-transform
+// exchange then uses the U buffer of the last chunk + its own 16 KB (kWinoPersLds).
+template <int EPI, int ABL = 0, bool PERS = false>
 __global__ __launch_bounds__(256, 2) void conv3x3_wino_kernel(ConvH8Args a) {
   extern __shared__ __attribute__((aligned(16))) uint4 smem4[];
   uint4* s_raw = smem4;                      // [2][kWnRawStride]: [group][row][wn_col]
   uint4* s_u = smem4 + 2 * kWnRawStride;     // [2][16][2][32]
+  uint4* s_x = s_u + 2 * kWnU;               // PERS: [4 waves][4][64] exchange records
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int xh = wv & 1, ph = wv >> 1, j = lane & 31, hh = lane >> 5;
@@ -66,21 +71,32 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wino_kernel(ConvH8Args a) {
   }
   const int ntiles = a.co_blocks * a.tiles_x * a.tiles_y * a.n;
   if (bid >= ntiles) return;
-  int t = bid;
-  const int cob = t % a.co_blocks;
-  t /= a.co_blocks;
-  const int x0 = (t % a.tiles_x) * 32;
-  t /= a.tiles_x;
-  const int y0 = (t % a.tiles_y) * 8;
-  const int img = t / a.tiles_y;
   const int nch = a.nchunks;
 
-  // ---- staging: raw input rows y0-1..y0+8, cols x0-1..x0+32 of record groups 2c, 2c+1.
-  // Per thread and DMA piece (3): its group of the chunk, its offset inside the
-  // group plane, and the offset of the same column in the zero top-padding row
-  // of group 0 (read instead by groups past cin, which meet zero weights).
-  const uint4* src = a.src_hi + (int64_t)img * a.src_img + (int64_t)y0 * a.src_wp + x0 + (kH8PadLeft - 1);
-  int p_g[3], p_off[3], p_zoff[3];
+  // Tile t -> (channel block, column, row, image); staging bases of its raw input
+  // rows y0-1..y0+8, cols x0-1..x0+32 and of its U slabs.
+  struct Tile {
+    int cob, x0, y0, img;
+    const uint4* src;
+    const uint4* wsrc;
+  };
+  auto tile_of = [&](int t) {
+    Tile T;
+    T.cob = t % a.co_blocks;
+    t /= a.co_blocks;
+    T.x0 = (t % a.tiles_x) * 32;
+    t /= a.tiles_x;
+    T.y0 = (t % a.tiles_y) * 8;
+    T.img = t / a.tiles_y;
+    T.src = a.src_hi + (int64_t)T.img * a.src_img + (int64_t)T.y0 * a.src_wp + T.x0 + (kH8PadLeft - 1);
+    T.wsrc = a.w_hi + (int64_t)T.cob * nch * kWnU + tid;
+    return T;
+  };
+
+  // ---- staging.  Per thread and DMA piece (3): its group of the chunk, its offset
+  // inside the group plane, and its column (groups past cin read the same column
+  // of the zero top-padding row of group 0 instead: they meet zero weights).
+  int p_g[3], p_off[3], p_col[3];
 #pragma unroll
   for (int it = 0; it < 3; ++it) {
     const int idx = tid + 256 * it;
@@ -90,251 +106,295 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wino_kernel(ConvH8Args a) {
     const int col = pos < 17 ? 2 * pos : 2 * (pos - 17) + 1;
     p_g[it] = g;
     p_off[it] = r * a.src_wp + col;
-    p_zoff[it] = -y0 * a.src_wp + col;
+    p_col[it] = col;
   }
-  auto issue_raw = [&](int c, int buf) {
+  auto issue_raw = [&](const Tile& T, int c, int buf) {
 #pragma unroll
     for (int it = 0; it < 3; ++it) {
       if (it < 2 || tid + 512 < kWnRaw) {
         const int gg = 2 * c + p_g[it];
-        const int64_t off = gg * 4 < a.cin ? (int64_t)gg * a.src_gp + p_off[it] : (int64_t)p_zoff[it];
-        dma16(src + off, s_raw + buf * kWnRawStride + 256 * it + (tid & ~63));
+        const int64_t off =
+            gg * 4 < a.cin ? (int64_t)gg * a.src_gp + p_off[it] : (int64_t)p_col[it] - (int64_t)T.y0 * a.src_wp;
+        dma16(T.src + off, s_raw + buf * kWnRawStride + 256 * it + (tid & ~63));
       }
     }
   };
-  const uint4* wsrc = a.w_hi + (int64_t)cob * nch * kWnU + tid;
-  auto issue_u = [&](int c, int buf) {
+  auto issue_u = [&](const Tile& T, int c, int buf) {
 #pragma unroll
-    for (int it = 0; it < 4; ++it) dma16(wsrc + (int64_t)c * kWnU + 256 * it, s_u + buf * kWnU + 256 * it + (tid & ~63));
+    for (int it = 0; it < 4; ++it)
+      dma16(T.wsrc + (int64_t)c * kWnU + 256 * it, s_u + buf * kWnU + 256 * it + (tid & ~63));
   };
 
   // ---- per chunk: this lane's B operands V[xi][4hh + e][patch j] from its window:
   // B^T rows 2xh, 2xh+1 as t0 = d[ra] - d[rb], t1 = d[rc] + sgn d[rd] (no branch on xh),
   // then 8 points x 4 products
   wfloatx16 acc[8];
-#pragma unroll
-  for (int l = 0; l < 8; ++l)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) acc[l][i] = 0.f;
   // MFMA column j -> patch (row pr, column jx).  The second row's columns are
   // rotated by 12 so the window reads of the two rows (68 records apart) fall on
   // distinct banks in every ds_read_b128 lane group ({0-3,12-15,20-27}, {4-11,16-19,28-31}).
   const int pr = 2 * ph + (j >> 4), jx = (j + 12 * (j >> 4)) & 15;
   const int ra = xh ? 2 : 0, rb = xh ? 1 : 2, rd = xh ? 3 : 2;  // rc = 1
   const float sgn = xh ? -1.f : 1.f;
-  auto compute = [&](int b) {
-    const uint4* su = s_u + b * kWnU + 8 * xh * 64 + hh * 32 + j;
-    wfloatx4 u[8];
+  // One B^T row yl of this wave's pair (t = d[ra] - d[rb] or d[1] + sgn d[rd]) and
+  // its 4 points' U operands, for chunk buffer b.
+  auto transform = [&](int b, int yl, wfloatx4* u4, wfloatx4* v4) {
+    const uint4* su = s_u + b * kWnU + (8 * xh + 4 * yl) * 64 + hh * 32 + j;
 #pragma unroll
-    for (int l = 0; l < 8; ++l) u[l] = __builtin_bit_cast(wfloatx4, su[l * 64]);
+    for (int x = 0; x < 4; ++x) u4[x] = __builtin_bit_cast(wfloatx4, su[x * 64]);
     const uint4* rw = s_raw + b * kWnRawStride + hh * kWnRawG + (2 * pr) * kWnRawCols;
-    wfloatx4 tv[2][4];
+    wfloatx4 c4[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int pc = wn_col(2 * jx + k);
-      const wfloatx4 da = __builtin_bit_cast(wfloatx4, rw[ra * kWnRawCols + pc]);
-      const wfloatx4 db = __builtin_bit_cast(wfloatx4, rw[rb * kWnRawCols + pc]);
-      const wfloatx4 dc = __builtin_bit_cast(wfloatx4, rw[kWnRawCols + pc]);
-      const wfloatx4 dd = __builtin_bit_cast(wfloatx4, rw[rd * kWnRawCols + pc]);
+      const wfloatx4 d0 = __builtin_bit_cast(wfloatx4, rw[(yl ? 1 : ra) * kWnRawCols + pc]);
+      const wfloatx4 d1 = __builtin_bit_cast(wfloatx4, rw[(yl ? rd : rb) * kWnRawCols + pc]);
       if constexpr ((ABL & 8) != 0) {
-        tv[0][k] = da;
-        tv[1][k] = dc;
+        c4[k] = d0;
+      } else if (yl == 0) {
+        c4[k] = d0 - d1;
       } else {
-        tv[0][k] = da - db;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) tv[1][k][e] = fmaf(sgn, dd[e], dc[e]);
+        for (int e = 0; e < 4; ++e) c4[k][e] = fmaf(sgn, d1[e], d0[e]);
       }
     }
-    wfloatx4 v[8];
+    if constexpr ((ABL & 8) != 0) {
 #pragma unroll
-    for (int yl = 0; yl < 2; ++yl) {
-      const wfloatx4* c4 = tv[yl];
-      if constexpr ((ABL & 8) != 0) {
-#pragma unroll
-        for (int x = 0; x < 4; ++x) v[4 * yl + x] = c4[x];
-        continue;
-      }
-      v[4 * yl + 0] = c4[0] - c4[2];
-      v[4 * yl + 1] = c4[1] + c4[2];
-      v[4 * yl + 2] = c4[2] - c4[1];
-      v[4 * yl + 3] = c4[1] - c4[3];
+      for (int x = 0; x < 4; ++x) v4[x] = c4[x];
+      return;
     }
+    v4[0] = c4[0] - c4[2];
+    v4[1] = c4[1] + c4[2];
+    v4[2] = c4[2] - c4[1];
+    v4[3] = c4[1] - c4[3];
+  };
+  auto mfmas = [&](int yl, const wfloatx4* u4, const wfloatx4* v4) {
 #pragma unroll
     for (int e = 0; e < 4; ++e)
 #pragma unroll
-      for (int l = 0; l < 8; ++l) {
+      for (int x = 0; x < 4; ++x) {
         if constexpr ((ABL & 4) != 0)
-          asm volatile("" ::"v"(u[l][e]), "v"(v[l][e]));
+          asm volatile("" ::"v"(u4[x][e]), "v"(v4[x][e]));
         else
-          acc[l] = __builtin_amdgcn_mfma_f32_32x32x2f32(u[l][e], v[l][e], acc[l], 0, 0, 0);
+          acc[4 * yl + x] = __builtin_amdgcn_mfma_f32_32x32x2f32(u4[x][e], v4[x][e], acc[4 * yl + x], 0, 0, 0);
       }
   };
+  auto compute = [&](int b) {
+    wfloatx4 u0[4], v0[4], u1[4], v1[4];
+    transform(b, 0, u0, v0);
+    mfmas(0, u0, v0);
+    transform(b, 1, u1, v1);
+    mfmas(1, u1, v1);
+  };
 
-  issue_raw(0, 0);
-  issue_u(0, 0);
+  Tile cur = tile_of(bid);
+  int b0 = 0;  // buffer of the current tile's chunk 0
+  issue_raw(cur, 0, 0);
+  issue_u(cur, 0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  for (int c = 0; c < nch; ++c) {
-    const int b = c & 1;
-    // buffers b^1 were last read in the previous chunk, before the barrier that ended it
-    if (c + 1 < nch) {
-      if constexpr (!(ABL & 2)) issue_raw(c + 1, b ^ 1);
-      if constexpr (!(ABL & 1)) issue_u(c + 1, b ^ 1);
-    }
-    compute(b);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-
-  // ---- output transform: Q[yl][c] = sum_x M[xi_y][x] A[x][c] for this wave's xi rows,
-  // then Y[0][c] = Q0 + Q1 + Q2 (wave xh 0), Y[1][c] = Q1 - Q2 - Q3 (wave xh 1)
-  float q[2][2][16];
+  for (int tile = bid;;) {
+    const int next = PERS ? tile + (int)gridDim.x : ntiles;
+    const bool has_next = next < ntiles;
+    Tile nxt = cur;
+    if (has_next) nxt = tile_of(next);
 #pragma unroll
-  for (int yl = 0; yl < 2; ++yl)
+    for (int l = 0; l < 8; ++l)
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const float m0 = acc[4 * yl][i], m1 = acc[4 * yl + 1][i], m2 = acc[4 * yl + 2][i], m3 = acc[4 * yl + 3][i];
-      q[yl][0][i] = (m0 + m1) + m2;
-      q[yl][1][i] = (m1 - m2) - m3;
-    }
-  // wave xh 0 hands its Q1 (yl 1) to its partner, wave xh 1 its Q2 (yl 0)
-  wfloatx4* xch = reinterpret_cast<wfloatx4*>(s_u);
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    wfloatx4 g;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int v = 4 * k + e, c = v >> 4, i = v & 15;
-      g[e] = xh ? q[0][c][i] : q[1][c][i];
-    }
-    xch[(wv * 8 + k) * 64 + lane] = g;
-  }
-  __syncthreads();
-  float yv[2][16];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const wfloatx4 pv = xch[((wv ^ 1) * 8 + k) * 64 + lane];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int v = 4 * k + e, c = v >> 4, i = v & 15;
-      yv[c][i] = xh ? (pv[e] - q[0][c][i]) - q[1][c][i] : (q[0][c][i] + q[1][c][i]) + pv[e];
-    }
-  }
-
-  // ---- epilogue: this lane's pixels (y, x0 + 2 jx + c), 16 channels 8 qq + 4 hh + e
-  const int y = y0 + 2 * pr + xh;
-  uint4* dst = a.dst_hi + (int64_t)img * a.dst_img;
-  auto store4 = [&](int64_t rec, const float* v) {
-    dst[rec] = make_uint4(__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3]));
-  };
-  if constexpr (EPI == RRIN_EPI_SUBPIXEL) {
-    // rows co' = cob*32 + 8 qq + 4 hh + e: group cob of 8 real channels, phase qq = (py, px)
-    const int HH = 2 * a.h, WW = 2 * a.w, creal = a.cout >> 2;
-    if (cob * 32 >= a.cout || y >= a.h) return;
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const int x = x0 + 2 * jx + c;
-      if (x >= a.w) continue;
-#pragma unroll
-      for (int qq = 0; qq < 4; ++qq) {
-        const int Y = 2 * y + (qq >> 1), X = 2 * x + (qq & 1);
-        const int64_t ri = ring_index(Y, X, HH, WW);
-        if (ri >= 0) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            a.edge[((int64_t)img * creal + cob * 8 + 4 * hh + e) * a.ring + ri] = yv[c][4 * qq + e];
-        } else {
-          float v[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = yv[c][4 * qq + e] + a.bias[cob * 32 + 8 * qq + 4 * hh + e];
-          store4((int64_t)(2 * cob + hh) * a.dst_gp + (int64_t)(Y + 1) * a.dst_wp + X + kH8PadLeft, v);
-        }
+      for (int i = 0; i < 16; ++i) acc[l][i] = 0.f;
+    for (int c = 0; c < nch; ++c) {
+      const int b = (b0 + c) & 1;
+      // buffers b^1 were last read in the previous chunk, before the barrier that ended it
+      if (c + 1 < nch) {
+        if constexpr (!(ABL & 2)) issue_raw(cur, c + 1, b ^ 1);
+        if constexpr (!(ABL & 1)) issue_u(cur, c + 1, b ^ 1);
+      } else if (has_next) {  // PERS: the next tile's chunk 0
+        issue_raw(nxt, 0, b ^ 1);
+        issue_u(nxt, 0, b ^ 1);
       }
+      compute(b);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
     }
-  } else {
-    float v[2][16];
+    const int bl = (b0 + nch - 1) & 1;  // buffers of the last chunk: free now
+
+    // ---- output transform: Q[yl][c] = sum_x M[xi_y][x] A[x][c] for this wave's xi rows,
+    // then Y[0][c] = Q0 + Q1 + Q2 (wave xh 0), Y[1][c] = Q1 - Q2 - Q3 (wave xh 1)
+    float q[2][2][16];
 #pragma unroll
-    for (int c = 0; c < 2; ++c)
+    for (int yl = 0; yl < 2; ++yl)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        float tv = yv[c][i] + a.bias[cob * 32 + 8 * (i >> 2) + 4 * hh + (i & 3)];
-        if constexpr (EPI != RRIN_EPI_LINEAR) tv = leaky(tv, a.slope);
-        v[c][i] = tv;
+        const float m0 = acc[4 * yl][i], m1 = acc[4 * yl + 1][i], m2 = acc[4 * yl + 2][i], m3 = acc[4 * yl + 3][i];
+        q[yl][0][i] = (m0 + m1) + m2;
+        q[yl][1][i] = (m1 - m2) - m3;
       }
+    // wave xh 0 hands its Q1 (yl 1) to its partner, wave xh 1 its Q2 (yl 0): records
+    // k 0-3 / 4-7 in the two U buffers, or (PERS: the other buffers hold the next
+    // tile's chunk 0) in the last chunk's U buffer and the exchange area
+    wfloatx4* xlo = reinterpret_cast<wfloatx4*>(PERS ? s_u + bl * kWnU : s_u);
+    wfloatx4* xhi = reinterpret_cast<wfloatx4*>(PERS ? s_x : s_u + kWnU);
+    auto xslot = [&](int w, int k) { return (k < 4 ? xlo : xhi) + (w * 4 + (k & 3)) * 64 + lane; };
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const int x = x0 + 2 * jx + c;
+    for (int k = 0; k < 8; ++k) {
+      wfloatx4 g;
 #pragma unroll
-      for (int qq = 0; qq < 4; ++qq) {
-        if (cob * 32 + 8 * qq < a.cout && y < a.h && x < a.w) {
-          const int64_t rec = (int64_t)(cob * 8 + 2 * qq + hh) * a.dst_gp + (int64_t)(y + 1) * a.dst_wp + x + kH8PadLeft;
-          store4(rec, &v[c][4 * qq]);
-          if constexpr (EPI == RRIN_EPI_LEAKY_REP) {
-            // edge replicate into the padding ring (read only by a sub-pixel up conv)
-            const int dy0 = y == 0 ? -1 : 0, dy1 = y == a.h - 1 ? 1 : 0;
-            const int dx0 = x == 0 ? -1 : 0, dx1 = x == a.w - 1 ? 1 : 0;
-            for (int dy = dy0; dy <= dy1; ++dy)
-              for (int dx = dx0; dx <= dx1; ++dx)
-                if (dy | dx) store4(rec + (int64_t)dy * a.dst_wp + dx, &v[c][4 * qq]);
+      for (int e = 0; e < 4; ++e) {
+        const int v = 4 * k + e, c = v >> 4, i = v & 15;
+        g[e] = xh ? q[0][c][i] : q[1][c][i];
+      }
+      *xslot(wv, k) = g;
+    }
+    __syncthreads();
+    float yv[2][16];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const wfloatx4 pv = *xslot(wv ^ 1, k);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int v = 4 * k + e, c = v >> 4, i = v & 15;
+        yv[c][i] = xh ? (pv[e] - q[0][c][i]) - q[1][c][i] : (q[0][c][i] + q[1][c][i]) + pv[e];
+      }
+    }
+
+    // ---- epilogue: this lane's pixels (y, x0 + 2 jx + c), 16 channels 8 qq + 4 hh + e
+    const int cob = cur.cob, x0 = cur.x0, img = cur.img;
+    const int y = cur.y0 + 2 * pr + xh;
+    uint4* dst = a.dst_hi + (int64_t)img * a.dst_img;
+    auto store4 = [&](int64_t rec, const float* v) {
+      dst[rec] = make_uint4(__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3]));
+    };
+    if constexpr (EPI == RRIN_EPI_SUBPIXEL) {
+      // rows co' = cob*32 + 8 qq + 4 hh + e: group cob of 8 real channels, phase qq = (py, px)
+      const int HH = 2 * a.h, WW = 2 * a.w, creal = a.cout >> 2;
+      if (cob * 32 < a.cout && y < a.h) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const int x = x0 + 2 * jx + c;
+          if (x >= a.w) continue;
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq) {
+            const int Y = 2 * y + (qq >> 1), X = 2 * x + (qq & 1);
+            const int64_t ri = ring_index(Y, X, HH, WW);
+            if (ri >= 0) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e)
+                a.edge[((int64_t)img * creal + cob * 8 + 4 * hh + e) * a.ring + ri] = yv[c][4 * qq + e];
+            } else {
+              float v[4];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] = yv[c][4 * qq + e] + a.bias[cob * 32 + 8 * qq + 4 * hh + e];
+              store4((int64_t)(2 * cob + hh) * a.dst_gp + (int64_t)(Y + 1) * a.dst_wp + X + kH8PadLeft, v);
+            }
           }
         }
       }
-    }
-    if constexpr (EPI == RRIN_EPI_LEAKY_POOL) {
-      // row 1 of each patch (wave xh 1) meets row 0 (wave xh 0) in LDS; avg = 0.25 ((v00 + v10) + (v01 + v11))
-      wfloatx4* xp = reinterpret_cast<wfloatx4*>(s_raw);
-      if (xh) {
+    } else {
+      float v[2][16];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          wfloatx4 g;
+      for (int c = 0; c < 2; ++c)
 #pragma unroll
-          for (int e = 0; e < 4; ++e) g[e] = v[(4 * k + e) >> 4][(4 * k + e) & 15];
-          xp[(ph * 8 + k) * 64 + lane] = g;
+        for (int i = 0; i < 16; ++i) {
+          float tv = yv[c][i] + a.bias[cob * 32 + 8 * (i >> 2) + 4 * hh + (i & 3)];
+          if constexpr (EPI != RRIN_EPI_LINEAR) tv = leaky(tv, a.slope);
+          v[c][i] = tv;
         }
-      }
-      __syncthreads();
-      if (!xh) {
-        float v1[2][16];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const wfloatx4 g = xp[(ph * 8 + k) * 64 + lane];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v1[(4 * k + e) >> 4][(4 * k + e) & 15] = g[e];
-        }
-        const int x = x0 + 2 * jx;
-        uint4* pdst = a.pool_hi + (int64_t)img * a.pool_img;
+      for (int c = 0; c < 2; ++c) {
+        const int x = x0 + 2 * jx + c;
 #pragma unroll
         for (int qq = 0; qq < 4; ++qq) {
           if (cob * 32 + 8 * qq < a.cout && y < a.h && x < a.w) {
-            float s4[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const int i = 4 * qq + e;
-              s4[e] = 0.25f * ((v[0][i] + v1[0][i]) + (v[1][i] + v1[1][i]));
+            const int64_t rec = (int64_t)(cob * 8 + 2 * qq + hh) * a.dst_gp + (int64_t)(y + 1) * a.dst_wp + x + kH8PadLeft;
+            store4(rec, &v[c][4 * qq]);
+            if constexpr (EPI == RRIN_EPI_LEAKY_REP) {
+              // edge replicate into the padding ring (read only by a sub-pixel up conv)
+              const int dy0 = y == 0 ? -1 : 0, dy1 = y == a.h - 1 ? 1 : 0;
+              const int dx0 = x == 0 ? -1 : 0, dx1 = x == a.w - 1 ? 1 : 0;
+              for (int dy = dy0; dy <= dy1; ++dy)
+                for (int dx = dx0; dx <= dx1; ++dx)
+                  if (dy | dx) store4(rec + (int64_t)dy * a.dst_wp + dx, &v[c][4 * qq]);
             }
-            const int64_t rec =
-                (int64_t)(cob * 8 + 2 * qq + hh) * a.pool_gp + (int64_t)(y / 2 + 1) * a.pool_wp + x / 2 + kH8PadLeft;
-            pdst[rec] = make_uint4(__float_as_uint(s4[0]), __float_as_uint(s4[1]), __float_as_uint(s4[2]),
-                                   __float_as_uint(s4[3]));
+          }
+        }
+      }
+      if constexpr (EPI == RRIN_EPI_LEAKY_POOL) {
+        // row 1 of each patch (wave xh 1) meets row 0 (wave xh 0) in LDS (the exchange
+        // records, free again after this barrier); avg = 0.25 ((v00 + v10) + (v01 + v11))
+        __syncthreads();
+        if (xh) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            wfloatx4 g;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) g[e] = v[(4 * k + e) >> 4][(4 * k + e) & 15];
+            *xslot(ph, k) = g;
+          }
+        }
+        __syncthreads();
+        if (!xh) {
+          float v1[2][16];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const wfloatx4 g = *xslot(ph, k);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v1[(4 * k + e) >> 4][(4 * k + e) & 15] = g[e];
+          }
+          const int x = x0 + 2 * jx;
+          uint4* pdst = a.pool_hi + (int64_t)img * a.pool_img;
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq) {
+            if (cob * 32 + 8 * qq < a.cout && y < a.h && x < a.w) {
+              float s4[4];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const int i = 4 * qq + e;
+                s4[e] = 0.25f * ((v[0][i] + v1[0][i]) + (v[1][i] + v1[1][i]));
+              }
+              const int64_t rec =
+                  (int64_t)(cob * 8 + 2 * qq + hh) * a.pool_gp + (int64_t)(y / 2 + 1) * a.pool_wp + x / 2 + kH8PadLeft;
+              pdst[rec] = make_uint4(__float_as_uint(s4[0]), __float_as_uint(s4[1]), __float_as_uint(s4[2]),
+                                     __float_as_uint(s4[3]));
+            }
           }
         }
       }
     }
+    if (!has_next) break;
+    // the next tile's chunk 1 is staged into buffers bl (exchange records) at its start
+    __syncthreads();
+    tile = next;
+    cur = nxt;
+    b0 = bl ^ 1;
   }
 }
 
-template <int EPI, int ABL = 0>
+constexpr size_t kWinoPersLds = kWinoLds + (size_t)4 * 4 * 64 * 16;  // + exchange records
+
+static int wino_num_cus() {
+  static std::atomic<int> n[kMaxDevices] = {};
+  const int dev = current_device();
+  int v = n[dev].load(std::memory_order_relaxed);
+  if (!v) {
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v < 1) v = 256;
+    n[dev].store(v, std::memory_order_relaxed);
+  }
+  return v;
+}
+
+template <int EPI, int ABL = 0, bool PERS = false>
 static int launch_wino_k(const ConvH8Args& a, hipStream_t st) {
-  auto k = conv3x3_wino_kernel<EPI, ABL>;
+  auto k = conv3x3_wino_kernel<EPI, ABL, PERS>;
+  constexpr size_t lds = PERS ? kWinoPersLds : kWinoLds;
   static LdsAttr attr;
-  if (int e = attr.ensure((const void*)k, (int)kWinoLds)) return e;
-  const int64_t grid = (int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n;
-  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256), kWinoLds, st, a);
+  if (int e = attr.ensure((const void*)k, (int)lds)) return e;
+  int64_t grid = (int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n;
+  if (PERS && grid > 2 * (int64_t)wino_num_cus()) grid = 2 * (int64_t)wino_num_cus();  // 2 blocks per CU
+  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256), lds, st, a);
   return hip_code(hipGetLastError());
 }
 
 #ifdef RRIN_LAB
-// kernel lab (librrin_lab.so only): the LEAKY conv with ablation bits
+// kernel lab (librrin_lab.so only): the LEAKY conv with ablation bits; bit 256 = PERS
 int launch_wino_lab(const ConvH8Args& a, int abl, hipStream_t st) {
   switch (abl) {
     case 0: return launch_wino_k<RRIN_EPI_LEAKY, 0>(a, st);
@@ -345,18 +405,39 @@ int launch_wino_lab(const ConvH8Args& a, int abl, hipStream_t st) {
     case 8: return launch_wino_k<RRIN_EPI_LEAKY, 8>(a, st);
     case 11: return launch_wino_k<RRIN_EPI_LEAKY, 11>(a, st);
     case 15: return launch_wino_k<RRIN_EPI_LEAKY, 15>(a, st);
+    case 256: return launch_wino_k<RRIN_EPI_LEAKY, 0, true>(a, st);
+    case 256 + 3: return launch_wino_k<RRIN_EPI_LEAKY, 3, true>(a, st);
+    case 256 + 4: return launch_wino_k<RRIN_EPI_LEAKY, 4, true>(a, st);
   }
   return RRIN_E_CONFIG;
 }
 #endif
 
+// Persistent grid (PERS) only in A/B builds (-DRRIN_WINO_PERS_MIN=k: from k tiles per
+// block slot).  Alone it is faster (kernel lab, profiles/r02/wino_pers: full-resolution
+// convs 2-10 %, level 1 2-3 %; 720p x 1 bench +1.2 %), but the default 2-stream
+// forward loses 4 % (125.1 -> 120.3 pairs/s): a persistent grid holds every block
+// slot for the whole launch, so the other stream's kernels no longer fill the
+// slots one-tile blocks free as they finish.
+#ifndef RRIN_WINO_PERS_MIN
+#define RRIN_WINO_PERS_MIN 0
+#endif
+template <int EPI>
+static int launch_wino_e(const ConvH8Args& a, hipStream_t st) {
+  if constexpr (RRIN_WINO_PERS_MIN > 0) {
+    const int64_t ntiles = (int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n;
+    if (ntiles >= (int64_t)RRIN_WINO_PERS_MIN * 2 * wino_num_cus()) return launch_wino_k<EPI, 0, true>(a, st);
+  }
+  return launch_wino_k<EPI>(a, st);
+}
+
 int launch_wino(const ConvH8Args& a, int epi, hipStream_t st) {
   switch (epi) {
-    case RRIN_EPI_LINEAR: return launch_wino_k<RRIN_EPI_LINEAR>(a, st);
-    case RRIN_EPI_LEAKY: return launch_wino_k<RRIN_EPI_LEAKY>(a, st);
-    case RRIN_EPI_LEAKY_POOL: return launch_wino_k<RRIN_EPI_LEAKY_POOL>(a, st);
-    case RRIN_EPI_LEAKY_REP: return launch_wino_k<RRIN_EPI_LEAKY_REP>(a, st);
-    case RRIN_EPI_SUBPIXEL: return launch_wino_k<RRIN_EPI_SUBPIXEL>(a, st);
+    case RRIN_EPI_LINEAR: return launch_wino_e<RRIN_EPI_LINEAR>(a, st);
+    case RRIN_EPI_LEAKY: return launch_wino_e<RRIN_EPI_LEAKY>(a, st);
+    case RRIN_EPI_LEAKY_POOL: return launch_wino_e<RRIN_EPI_LEAKY_POOL>(a, st);
+    case RRIN_EPI_LEAKY_REP: return launch_wino_e<RRIN_EPI_LEAKY_REP>(a, st);
+    case RRIN_EPI_SUBPIXEL: return launch_wino_e<RRIN_EPI_SUBPIXEL>(a, st);
   }
   return RRIN_E_ARG;
 }

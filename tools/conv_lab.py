@@ -308,6 +308,16 @@ def single(args):
     else:
         run = lambda: _lib.check(lib.rrin_conv3x3_h8_fwd(C.byref(d), st))  # noqa: E731
     run()
+    if args.sched is not None and args.check:  # lab variant vs the product kernel, bitwise
+        ref = H8Tensor(n, cout, h, w, dev, prec)
+        d2 = _lib.ConvH8Desc.from_buffer_copy(d)
+        d2.dst = ref.view(0, cout)
+        _lib.check(lib.rrin_conv3x3_h8_fwd(C.byref(d2), st))
+        torch.cuda.synchronize()
+        same = torch.equal(dst.to_nchw(), ref.to_nchw())
+        print(f"check sched {args.sched} vs product: {'bitwise equal' if same else 'DIFFERENT'}")
+        if not same:
+            sys.exit(3)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(args.reps):
@@ -468,6 +478,7 @@ def main():
     ap.add_argument("mode", choices=["breakdown", "tune", "single", "ablate", "ablate32"])
     ap.add_argument("--shape", type=int, nargs=5, default=[512, 256, 3, 1, 0],
                     help="single: cin cout level epi cfg")
+    ap.add_argument("--check", action="store_true", help="single, lab: compare with the product kernel bitwise")
     ap.add_argument("--src", type=int, default=0, help="single, fp32: src mode (1 = fused upsample)")
     ap.add_argument("--sched", type=int, default=None,
                     help="single: lab schedule / ablation bits (fp32_planar: librrin_lab32.so; records: librrin_lab.so)")

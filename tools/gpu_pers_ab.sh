@@ -1,0 +1,24 @@
+#!/bin/bash
+# Persistent Winograd grid threshold A/B (make pers-variants): the product
+# library (never persistent), persistent from 3 and from 8 tiles per block slot,
+# swapped in for librrin_hip.so in turn; default bench and 720p x 1, interleaved.
+set -u
+mkdir -p gpurun_out/pers
+cp rrin_amd/librrin_hip.so gpurun_out/pers/product.so
+cp rrin_amd/librrin_hip_pers3.so gpurun_out/pers/pers3.so
+cp rrin_amd/librrin_hip_pers8.so gpurun_out/pers/pers8.so
+
+for rep in 1 2; do
+  for v in pers3 pers8 product; do
+    cp gpurun_out/pers/$v.so rrin_amd/librrin_hip.so
+    for cfg in "--batch 4" "--batch 1"; do
+      timeout -k 10 300 python bench.py $cfg --no-alt --cpu-baseline off > gpurun_out/pers/b.log 2>&1
+      rc=$?
+      echo "r$rep $v $cfg: $(grep -o '"value": [0-9.]*' gpurun_out/pers/b.log | head -1) $(grep -o '"frac": [0-9.]*' gpurun_out/pers/b.log | head -1)"
+      if [ $rc -ne 0 ]; then tail -5 gpurun_out/pers/b.log; cp gpurun_out/pers/product.so rrin_amd/librrin_hip.so; exit $rc; fi
+    done
+  done
+done
+cp gpurun_out/pers/product.so rrin_amd/librrin_hip.so
+rm -f gpurun_out/pers/*.so
+exit 0
