@@ -318,16 +318,20 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wino_kernel(ConvH8Args a) {
         }
       }
       if constexpr (EPI == RRIN_EPI_LEAKY_POOL) {
-        // row 1 of each patch (wave xh 1) meets row 0 (wave xh 0) in LDS (the exchange
-        // records, free again after this barrier); avg = 0.25 ((v00 + v10) + (v01 + v11))
-        __syncthreads();
+        // row 1 of each patch (wave xh 1) meets row 0 (wave xh 0) in LDS: one-tile grids
+        // use the raw buffers (idle now), PERS the exchange records (the next tile's chunk
+        // 0 is in the other raw buffer) once every wave has read them (barrier);
+        // avg = 0.25 ((v00 + v10) + (v01 + v11))
+        wfloatx4* xp = reinterpret_cast<wfloatx4*>(s_raw);
+        auto pslot = [&](int k) { return PERS ? xslot(ph, k) : xp + (ph * 8 + k) * 64 + lane; };
+        if constexpr (PERS) __syncthreads();
         if (xh) {
 #pragma unroll
           for (int k = 0; k < 8; ++k) {
             wfloatx4 g;
 #pragma unroll
             for (int e = 0; e < 4; ++e) g[e] = v[(4 * k + e) >> 4][(4 * k + e) & 15];
-            *xslot(ph, k) = g;
+            *pslot(k) = g;
           }
         }
         __syncthreads();
@@ -335,7 +339,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wino_kernel(ConvH8Args a) {
           float v1[2][16];
 #pragma unroll
           for (int k = 0; k < 8; ++k) {
-            const wfloatx4 g = *xslot(ph, k);
+            const wfloatx4 g = *pslot(k);
 #pragma unroll
             for (int e = 0; e < 4; ++e) v1[(4 * k + e) >> 4][(4 * k + e) & 15] = g[e];
           }
