@@ -72,3 +72,7 @@ pers-variants: $(PERSV)
 
 rrin_amd/librrin_hip_pers%.so: $(SRCS) $(SRC_DIR)/common.hpp include/rrin_hip.h
 	$(HIPCC) $(CXXFLAGS) -DRRIN_WINO_PERS_MIN=$* -shared -o $@ $(SRCS)
+
+# persistent with 1 block per CU per launch (the other stream's launch holds the other slot)
+rrin_amd/librrin_hip_pers%b1.so: $(SRCS) $(SRC_DIR)/common.hpp include/rrin_hip.h
+	$(HIPCC) $(CXXFLAGS) -DRRIN_WINO_PERS_MIN=$* -DRRIN_WINO_PERS_BPC=1 -shared -o $@ $(SRCS)

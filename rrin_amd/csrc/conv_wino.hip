@@ -392,7 +392,11 @@ static int launch_wino_k(const ConvH8Args& a, hipStream_t st) {
   static LdsAttr attr;
   if (int e = attr.ensure((const void*)k, (int)lds)) return e;
   int64_t grid = (int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n;
-  if (PERS && grid > 2 * (int64_t)wino_num_cus()) grid = 2 * (int64_t)wino_num_cus();  // 2 blocks per CU
+#ifndef RRIN_WINO_PERS_BPC  // persistent blocks per CU (A/B builds)
+#define RRIN_WINO_PERS_BPC 2
+#endif
+  const int64_t slots = (int64_t)RRIN_WINO_PERS_BPC * wino_num_cus();
+  if (PERS && grid > slots) grid = slots;
   hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256), lds, st, a);
   return hip_code(hipGetLastError());
 }
@@ -430,7 +434,8 @@ template <int EPI>
 static int launch_wino_e(const ConvH8Args& a, hipStream_t st) {
   if constexpr (RRIN_WINO_PERS_MIN > 0) {
     const int64_t ntiles = (int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n;
-    if (ntiles >= (int64_t)RRIN_WINO_PERS_MIN * 2 * wino_num_cus()) return launch_wino_k<EPI, 0, true>(a, st);
+    if (ntiles >= (int64_t)RRIN_WINO_PERS_MIN * RRIN_WINO_PERS_BPC * wino_num_cus())
+      return launch_wino_k<EPI, 0, true>(a, st);
   }
   return launch_wino_k<EPI>(a, st);
 }

@@ -1,15 +1,16 @@
 #!/bin/bash
-# Persistent Winograd grid threshold A/B (make pers-variants): the product
-# library (never persistent), persistent from 3 and from 8 tiles per block slot,
-# swapped in for librrin_hip.so in turn; default bench and 720p x 1, interleaved.
+# Persistent Winograd grid A/B (make pers-variants / librrin_hip_pers<k>[b1].so): the
+# product library (never persistent) and the variants named in $VARIANTS (pers<k>:
+# persistent from k tiles per block slot, 2 blocks per CU; pers<k>b1: 1 block per CU,
+# so the other stream's launch holds the CU's second slot), swapped in for
+# librrin_hip.so in turn; default bench and 720p x 1, interleaved.
 set -u
 mkdir -p gpurun_out/pers
+VARIANTS=${VARIANTS:-pers3 pers8}
 cp rrin_amd/librrin_hip.so gpurun_out/pers/product.so
-cp rrin_amd/librrin_hip_pers3.so gpurun_out/pers/pers3.so
-cp rrin_amd/librrin_hip_pers8.so gpurun_out/pers/pers8.so
-
+for v in $VARIANTS; do cp rrin_amd/librrin_hip_$v.so gpurun_out/pers/$v.so; done
 for rep in 1 2; do
-  for v in pers3 pers8 product; do
+  for v in $VARIANTS product; do
     cp gpurun_out/pers/$v.so rrin_amd/librrin_hip.so
     for cfg in "--batch 4" "--batch 1"; do
       timeout -k 10 300 python bench.py $cfg --no-alt --cpu-baseline off > gpurun_out/pers/b.log 2>&1
