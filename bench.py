@@ -48,7 +48,7 @@ sys.path.insert(0, REPO)
 
 from rrin_amd import Net, _lib  # noqa: E402
 from rrin_amd import engine as engine_mod  # noqa: E402
-from rrin_amd.shard import GatherPipeline  # noqa: E402
+from rrin_amd.shard import GatherPipeline, verify_gather  # noqa: E402
 from rrin_amd.synthetic import keyed_state_dict, synthetic_batch  # noqa: E402
 from rrin_amd.unet import conv_bytes, conv_flops, conv_work, roofline_bound_s  # noqa: E402
 
@@ -364,11 +364,14 @@ def main():
         roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1),
                     "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None,
                     "mfma_issued_tflops": round(achieved * MFMA_PRODUCTS[args.precision], 1),
-                    "kernel": KERNEL_WINO if algo == "winograd" and args.precision == "fp32" else KERNEL[args.precision],
+                    "kernel": (KERNEL_WINO if algo in ("winograd", "mixed") and args.precision == "fp32"
+                               else KERNEL[args.precision]),
                     "conv_algorithm": algo,
                     "flops_basis": ("FLOPs of the algorithm the convs run: Winograd F(2x2,3x3) = 16 multiply-adds "
                                     "per 2x2 output patch and channel pair (4/9 of the direct form's)"
-                                    if algo == "winograd" else "direct-form conv FLOPs (2*9*Cin*Cout*H*W)"),
+                                    + ("; the 6-channel first conv runs the direct form (engine.WINO_DIRECT) and counts "
+                                       "its direct-form FLOPs" if algo == "mixed" else "")
+                                    if algo in ("winograd", "mixed") else "direct-form conv FLOPs (2*9*Cin*Cout*H*W)"),
                     "direct_equivalent_tflops": round(direct_fl / (conv_busy * 1e-3) / 1e12, 2),
                     "flops_per_launch_avg": conv_fl / max(conv_launches, 1),
                     "avg_launch_ms": conv_ms / max(conv_launches, 1),
@@ -383,7 +386,7 @@ def main():
                     "subpixel_ring_fix_ms_per_step": round(edge_ms / args.steps, 3)}
         # SURVEY §8d per-layer bound: sum_l max(FLOP_l / peak, bytes_l / 8 TB/s) over the body convs
         bpv = 2 if args.precision == "fp16" else 4
-        fscale = 4.0 / 9.0 if algo == "winograd" else 1.0
+        fscale = 4.0 / 9.0 if algo in ("winograd", "mixed") else 1.0
         tlb = B * sum(roofline_bound_s(getattr(net, u), H, W, bpv, peak * 1e12, HBM_PEAK_GBS * 1e9, fscale)
                       for u in ("Flow", "refine_flow", "Mask", "final"))
         roofline["t_lb_conv_ms_per_step"] = round(1e3 * tlb, 3)
@@ -412,19 +415,12 @@ def main():
     eng.check_range()  # fp16-stored precisions: no activation left the fp16 range (raises otherwise)
     gather_check = None
     if distributed:
-        # the gathered output of the last step equals every rank's own shard in
-        # rank order: per-rank checksums of the local output vs the gather's slices
+        # the gathered output of the last step holds every rank's own shard in rank
+        # order, bit for bit (rrin_amd.shard.verify_gather: own slice by equality,
+        # every slice's CRC-32 against its owner's)
         gather.drain()
-        local = last_gather[0][0].double()
-        mine = torch.stack([local.sum(), (local * local).sum()])
-        allc = [torch.zeros_like(mine) for _ in range(world)]
-        dist.all_gather(allc, mine.cpu() if args.dist_backend == "gloo" else mine)
-        g = last_gather[0][1].double()
-        ok = all(torch.allclose(torch.stack([g[r * B:(r + 1) * B].sum(), (g[r * B:(r + 1) * B] ** 2).sum()]).cpu(),
-                                allc[r].cpu(), rtol=0, atol=0) for r in range(world))
-        gather_check = {"ok": bool(ok), "what": "sum and sum of squares of every rank's output shard == the "
-                                                "rank-order slice of the all-gathered output (last step)"}
-        if not ok:
+        gather_check = verify_gather(last_gather[0][0], last_gather[0][1])
+        if not gather_check["ok"]:
             raise RuntimeError("all-gathered output does not match the ranks' shards")
 
     pairs = world * B * args.steps
@@ -443,7 +439,8 @@ def main():
         "dtype": DTYPE[args.precision],
         "data": "synthetic (key-seeded weights, randint/255 frame pairs; SURVEY §8c-d)",
         "config": {"workload": f"RRIN Net.forward {W}x{H} {PREC_LABEL[args.precision]}, {B} pairs/GPU/step, "
-                               f"t={args.t}, + all-gather of outputs",
+                               f"t={args.t}" + (f", + all-gather of outputs ({'RCCL' if args.dist_backend == 'nccl' else 'gloo'})"
+                                                  if distributed else ""),
                    "global_batch": world * B, "height": H, "width": W,
                    "parallelism": f"frame-batch dp{world}",
                    "gflop_per_pair": round(sum(conv_flops(getattr(net, u), H, W)
@@ -484,17 +481,21 @@ def main():
                         "streams": args.streams}
         del eng2
         net.precision = args.precision
-    if rank == 0 and world == 1 and args.cpu_baseline == "auto":
+    if rank == 0 and args.cpu_baseline == "auto":
+        # every line carries parity (rank 0's pair 0 = global pair 0 vs the CPU
+        # oracle) and the CPU baseline; at N > 1 the timed CPU sample is that one
+        # parity pair, so the other ranks wait only seconds at the final barrier
         global CPU_ALL_THREADS
-        CPU_ALL_THREADS = args.cpu_all_threads
+        CPU_ALL_THREADS = args.cpu_all_threads and world == 1
         res["cpu_baseline"], res["parity"] = cpu_baseline({k: v.detach().cpu() for k, v in sd.items()}, H, W,
-                                                          args.cpu_pairs, args.t, last[0][0:1].cpu(),
-                                                          alt_out)
+                                                          args.cpu_pairs if world == 1 else 1, args.t,
+                                                          last[0][0:1].cpu(), alt_out)
         if alt_key in res:
             res[alt_key]["parity"] = res["parity"].pop("alt")
     if rank == 0:
         print(json.dumps(res), flush=True)
     if distributed:
+        dist.barrier()  # rank 0's CPU baseline / parity pass ends before any rank leaves
         dist.destroy_process_group()
 
 

@@ -12,15 +12,22 @@
  *   - stateless and stream-ordered: calls only enqueue work on `stream`; no
  *     call's result depends on another call.  Everything a call needs comes in
  *     its arguments (the optional launch profiler of rrin_net_fwd included);
- *     the only process-wide data are thread-safe per-device launch caches
- *     (a kernel's dynamic-LDS attribute, resident blocks per CU).  Entry points
- *     may be called from several host threads; one rrin_prof must not be
- *     shared by concurrent calls.
+ *     the only process-wide data are thread-safe launch caches keyed by the
+ *     device of the stream a launch goes to (a kernel's dynamic-LDS attribute,
+ *     resident blocks per CU), so a caller may pass any device's stream from any
+ *     host thread.  One rrin_prof must not be shared by concurrent calls.
  *
- * Activation layout used between kernels ("padded planar", PP): per image and
- * channel a plane of hp x wp fp32 with hp = round_up(h,16)+2, wp = round_up(w,32)+64;
- * pixel (y,x) lives at (y+1)*wp + (x+32); everything else is zero and is never
- * written.  See DESIGN.md §3.
+ * Activation layouts between kernels:
+ *   - record layout (the default, every `prec` but RRIN_PREC_F32): per image
+ *     and channel group one plane of 16-byte records, hp = round_up(h,16)+2
+ *     rows, wp = round_up(w,32)+16 records, pixel (y,x) at record
+ *     (y+1)*wp + (x+8).  A record holds 4 fp32 channels (RRIN_PREC_F32R, exact
+ *     fp32: "R32") or 8 halves (RRIN_PREC_F16X3 hi / lo planes, RRIN_PREC_F16:
+ *     "H8").  rrin_geom / rrin_make_geom_h8 / rrin_h8 describe it.
+ *   - padded planar ("PP", RRIN_PREC_F32 only: the round-1 fp32 path kept for
+ *     A/B): per image and channel a plane of hp x wp fp32 with
+ *     wp = round_up(w,32)+64, pixel (y,x) at (y+1)*wp + (x+32).
+ * Padding is zero and is never written (it is the convs' zero padding).
  */
 #ifndef RRIN_HIP_H
 #define RRIN_HIP_H
@@ -377,6 +384,59 @@ int64_t rrin_unet_conv_count(int32_t depth);
 int rrin_unet_fwd(const rrin_unet_desc* d, void* stream);
 int64_t rrin_net_workspace_bytes(int32_t n, int32_t h, int32_t w, int32_t prec);
 int rrin_net_fwd(const rrin_net_desc* d, void* stream);
+
+/* ---- Training path (autograd): NCHW fp32 kernels ------------------------- */
+/* With autograd on (the reference trains through Net.forward, train.py:98, and
+ * loss.backward(), train.py:144) rrin_amd.train wraps these in autograd
+ * Functions.  All tensors are contiguous NCHW fp32.
+ *   rrin_tconv3x3 FWD  : out = conv3x3(x, wt) + bias [, leaky]      (unet.py:29,38,59-63,78)
+ *                 DGRAD: out = input gradient of that conv: the conv of
+ *                        g' = g * leaky'(y) (leaky: y = the forward output) with
+ *                        the flipped, transposed weights; x holds g [n][cout][h][w].
+ *   rrin_tconv3x3_wgrad: gw = sum over images and pixels of g' (x) x shifted per
+ *                        tap, gb = sum g'; deterministic split-K (work buffer of
+ *                        rrin_tconv3x3_wgrad_work_floats floats).
+ *   rrin_tpool2_*  : F.avg_pool2d(x, 2) (unet.py:46) and its backward; nc = n*c.
+ *   rrin_tup2_*    : nn.Upsample(x2, bilinear) (unet.py:77) and its backward;
+ *                    h, w = the low-resolution size.
+ *   rrin_twarp_bwd : backward of warp (model.py:8-21; forward = rrin_warp_fwd):
+ *                    gimg (scatter, summed exactly in 64-bit fixed point:
+ *                    deterministic) and gflow; work >= rrin_twarp_bwd_work_bytes. */
+enum rrin_tconv_mode { RRIN_TCONV_FWD = 0, RRIN_TCONV_DGRAD = 1 };
+typedef struct rrin_tconv_desc {
+  int32_t n, cin, cout, h, w;
+  int32_t mode;          /* rrin_tconv_mode                                    */
+  int32_t leaky;         /* FWD: leaky output; DGRAD: g' = g * leaky'(y)       */
+  float slope;           /* leaky slope, 0 < slope <= 1                        */
+  const float* x;        /* FWD: input [n][cin][h][w]; DGRAD: g [n][cout][h][w] */
+  const float* y;        /* DGRAD with leaky: forward output [n][cout][h][w]    */
+  const float* wt;       /* OIHW [cout][cin][3][3]                              */
+  const float* bias;     /* FWD: [cout] (nullable)                              */
+  float* out;            /* FWD: [n][cout][h][w]; DGRAD: [n][cin][h][w]         */
+} rrin_tconv_desc;
+int rrin_tconv3x3(const rrin_tconv_desc* d, void* stream);
+
+typedef struct rrin_twgrad_desc {
+  int32_t n, cin, cout, h, w, leaky;
+  float slope;
+  int32_t pad_;
+  const float* x;        /* forward input [n][cin][h][w]                        */
+  const float* g;        /* output gradient [n][cout][h][w]                     */
+  const float* y;        /* leaky: forward output [n][cout][h][w]               */
+  float* gw;             /* [cout][cin][3][3]                                   */
+  float* gb;             /* [cout] (nullable)                                   */
+  float* work;           /* rrin_tconv3x3_wgrad_work_floats(...) floats         */
+} rrin_twgrad_desc;
+int64_t rrin_tconv3x3_wgrad_work_floats(int32_t n, int32_t cin, int32_t cout, int32_t h, int32_t w);
+int rrin_tconv3x3_wgrad(const rrin_twgrad_desc* d, void* stream);
+
+int rrin_tpool2_fwd(const float* x, float* y, int32_t nc, int32_t h, int32_t w, void* stream);
+int rrin_tpool2_bwd(const float* gy, float* gx, int32_t nc, int32_t h, int32_t w, void* stream);
+int rrin_tup2_fwd(const float* x, float* y, int32_t nc, int32_t h, int32_t w, void* stream);
+int rrin_tup2_bwd(const float* gy, float* gx, int32_t nc, int32_t h, int32_t w, void* stream);
+int64_t rrin_twarp_bwd_work_bytes(int32_t n, int32_t c, int32_t h, int32_t w);
+int rrin_twarp_bwd(const float* img, const float* flow, const float* gout, float* gimg, float* gflow,
+                   void* work, int64_t work_bytes, int32_t n, int32_t c, int32_t h, int32_t w, void* stream);
 
 /* ---- Misc ---------------------------------------------------------------- */
 int rrin_abi_version(void);

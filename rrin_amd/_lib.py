@@ -96,6 +96,22 @@ class NetDesc(C.Structure):
                 ("status", C.c_void_p)]
 
 
+class TConvDesc(C.Structure):
+    _fields_ = [("n", C.c_int32), ("cin", C.c_int32), ("cout", C.c_int32), ("h", C.c_int32), ("w", C.c_int32),
+                ("mode", C.c_int32), ("leaky", C.c_int32), ("slope", C.c_float), ("x", C.c_void_p),
+                ("y", C.c_void_p), ("wt", C.c_void_p), ("bias", C.c_void_p), ("out", C.c_void_p)]
+
+
+class TWgradDesc(C.Structure):
+    _fields_ = [("n", C.c_int32), ("cin", C.c_int32), ("cout", C.c_int32), ("h", C.c_int32), ("w", C.c_int32),
+                ("leaky", C.c_int32), ("slope", C.c_float), ("pad_", C.c_int32), ("x", C.c_void_p),
+                ("g", C.c_void_p), ("y", C.c_void_p), ("gw", C.c_void_p), ("gb", C.c_void_p),
+                ("work", C.c_void_p)]
+
+
+TCONV_FWD, TCONV_DGRAD = 0, 1
+
+
 class UNetDesc(C.Structure):
     _fields_ = [("n", C.c_int32), ("h", C.c_int32), ("w", C.c_int32), ("in_ch", C.c_int32), ("out_ch", C.c_int32),
                 ("depth", C.c_int32), ("prec", C.c_int32), ("pad_", C.c_int32), ("x", C.c_void_p), ("y", C.c_void_p),
@@ -162,6 +178,16 @@ SIGNATURES = {
                                  C.POINTER(C.c_int32)]),
     "rrin_prof_read_spans": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32,
                                        C.POINTER(C.c_int32)]),
+    "rrin_tconv3x3": (C.c_int, [C.POINTER(TConvDesc), C.c_void_p]),
+    "rrin_tconv3x3_wgrad_work_floats": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32]),
+    "rrin_tconv3x3_wgrad": (C.c_int, [C.POINTER(TWgradDesc), C.c_void_p]),
+    "rrin_tpool2_fwd": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p]),
+    "rrin_tpool2_bwd": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p]),
+    "rrin_tup2_fwd": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p]),
+    "rrin_tup2_bwd": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p]),
+    "rrin_twarp_bwd_work_bytes": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32, C.c_int32]),
+    "rrin_twarp_bwd": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                 C.c_int64, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_void_p]),
     "rrin_abi_version": (C.c_int, []),
     "rrin_strerror": (C.c_char_p, [C.c_int]),
 }

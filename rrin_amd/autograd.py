@@ -1,0 +1,211 @@
+"""Training path on MI355X: autograd Functions over the HIP training kernels.
+
+The reference trains through ``Net.forward`` with autograd on (`train.py:98`)
+and ``loss.backward()`` (`train.py:144`).  With autograd on and the model on a
+ROCm device, ``rrin_amd.Net.forward`` / ``UNet.forward`` run the reference
+graph (`model.py:32-65`, `unet.py:40-51`) with these Functions, each a forward
+HIP kernel and its backward HIP kernel(s) from ``csrc/train.hip``:
+
+=====================  ==========================================  ===============================
+Function               forward (reference op)                       backward
+=====================  ==========================================  ===============================
+``conv3x3``            Conv2d(3, pad=1) + bias [+ LeakyReLU(0.1)]   dgrad (flipped W, leaky' fused),
+                       (unet.py:29,38,59-63,78)                     wgrad + bias grad (split-K)
+``avg_pool2``          F.avg_pool2d(x, 2) (unet.py:46)              0.25 spread
+``upsample2``          Upsample(x2, bilinear) (unet.py:77)          transposed stencil (gather)
+``backwarp``           warp = grid_sample (model.py:8-21)           image (fixed-point scatter) and
+                                                                    flow gradients
+=====================  ==========================================  ===============================
+
+The glue between them (cat, the flow t-blend, sigmoid, the blend division,
+the residual add and clamp; `model.py:33-63`) is elementwise PyTorch autograd.
+On a CPU device the model keeps the PyTorch-operator graph (``Net._forward_autograd``).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from . import _lib
+
+LEAKY_SLOPE = 0.1
+
+
+def _stream():
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _f32(t: torch.Tensor) -> torch.Tensor:
+    if t.dtype != torch.float32 or not t.is_cuda:
+        raise TypeError("rrin_amd training kernels take float32 tensors on a ROCm device")
+    return t.contiguous()
+
+
+class _Conv3x3(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, leaky: bool):
+        x, weight = _f32(x), _f32(weight)
+        bias = _f32(bias) if bias is not None else None
+        n, cin, h, w = x.shape
+        cout = weight.shape[0]
+        if weight.shape != (cout, cin, 3, 3):
+            raise ValueError(f"weight {tuple(weight.shape)} for input {tuple(x.shape)}")
+        y = torch.empty((n, cout, h, w), dtype=torch.float32, device=x.device)
+        d = _lib.TConvDesc(n=n, cin=cin, cout=cout, h=h, w=w, mode=_lib.TCONV_FWD, leaky=int(leaky),
+                           slope=LEAKY_SLOPE, x=x.data_ptr(), y=None, wt=weight.data_ptr(),
+                           bias=bias.data_ptr() if bias is not None else None, out=y.data_ptr())
+        _lib.check(_lib.lib().rrin_tconv3x3(C.byref(d), _stream()), "rrin_tconv3x3 (forward)")
+        ctx.leaky = bool(leaky)
+        ctx.has_bias = bias is not None
+        ctx.save_for_backward(x, weight, y if leaky else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight, y = ctx.saved_tensors
+        gy = _f32(gy)
+        n, cin, h, w = x.shape
+        cout = weight.shape[0]
+        L = _lib.lib()
+        st = _stream()
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = torch.empty_like(x)
+            d = _lib.TConvDesc(n=n, cin=cin, cout=cout, h=h, w=w, mode=_lib.TCONV_DGRAD, leaky=int(ctx.leaky),
+                               slope=LEAKY_SLOPE, x=gy.data_ptr(), y=y.data_ptr() if ctx.leaky else None,
+                               wt=weight.data_ptr(), bias=None, out=gx.data_ptr())
+            _lib.check(L.rrin_tconv3x3(C.byref(d), st), "rrin_tconv3x3 (dgrad)")
+        if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
+            gw = torch.empty_like(weight)
+            gb = torch.empty((cout,), dtype=torch.float32, device=x.device)
+            nw = int(L.rrin_tconv3x3_wgrad_work_floats(n, cin, cout, h, w))
+            if nw < 0:
+                _lib.check(nw, "rrin_tconv3x3_wgrad_work_floats")
+            work = torch.empty((nw,), dtype=torch.float32, device=x.device)
+            d = _lib.TWgradDesc(n=n, cin=cin, cout=cout, h=h, w=w, leaky=int(ctx.leaky), slope=LEAKY_SLOPE,
+                                x=x.data_ptr(), g=gy.data_ptr(), y=y.data_ptr() if ctx.leaky else None,
+                                gw=gw.data_ptr(), gb=gb.data_ptr(), work=work.data_ptr())
+            _lib.check(L.rrin_tconv3x3_wgrad(C.byref(d), st), "rrin_tconv3x3_wgrad")
+        return gx, gw, (gb if ctx.has_bias else None), None
+
+
+class _AvgPool2(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        x = _f32(x)
+        n, c, h, w = x.shape
+        y = torch.empty((n, c, h // 2, w // 2), dtype=torch.float32, device=x.device)
+        _lib.check(_lib.lib().rrin_tpool2_fwd(x.data_ptr(), y.data_ptr(), n * c, h, w, _stream()), "rrin_tpool2_fwd")
+        ctx.shape = x.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        gy = _f32(gy)
+        n, c, h, w = ctx.shape
+        gx = torch.empty(ctx.shape, dtype=torch.float32, device=gy.device)
+        _lib.check(_lib.lib().rrin_tpool2_bwd(gy.data_ptr(), gx.data_ptr(), n * c, h, w, _stream()),
+                   "rrin_tpool2_bwd")
+        return gx
+
+
+class _Upsample2(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        x = _f32(x)
+        n, c, h, w = x.shape
+        y = torch.empty((n, c, 2 * h, 2 * w), dtype=torch.float32, device=x.device)
+        _lib.check(_lib.lib().rrin_tup2_fwd(x.data_ptr(), y.data_ptr(), n * c, h, w, _stream()), "rrin_tup2_fwd")
+        ctx.shape = x.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        gy = _f32(gy)
+        n, c, h, w = ctx.shape
+        gx = torch.empty(ctx.shape, dtype=torch.float32, device=gy.device)
+        _lib.check(_lib.lib().rrin_tup2_bwd(gy.data_ptr(), gx.data_ptr(), n * c, h, w, _stream()), "rrin_tup2_bwd")
+        return gx
+
+
+class _Backwarp(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, img, flow):
+        img, flow = _f32(img), _f32(flow)
+        n, c, h, w = img.shape
+        if flow.shape != (n, 2, h, w):
+            raise ValueError(f"flow {tuple(flow.shape)} for image {tuple(img.shape)}")
+        out = torch.empty_like(img)
+        _lib.check(_lib.lib().rrin_warp_fwd(img.data_ptr(), flow.data_ptr(), out.data_ptr(), n, c, h, w, _stream()),
+                   "rrin_warp_fwd")
+        ctx.save_for_backward(img, flow)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        img, flow = ctx.saved_tensors
+        gout = _f32(gout)
+        n, c, h, w = img.shape
+        L = _lib.lib()
+        nb = int(L.rrin_twarp_bwd_work_bytes(n, c, h, w))
+        if nb < 0:
+            _lib.check(nb, "rrin_twarp_bwd_work_bytes")
+        work = torch.empty((nb,), dtype=torch.uint8, device=img.device)
+        gimg = torch.empty_like(img)
+        gflow = torch.empty_like(flow)
+        _lib.check(L.rrin_twarp_bwd(img.data_ptr(), flow.data_ptr(), gout.data_ptr(), gimg.data_ptr(),
+                                    gflow.data_ptr(), work.data_ptr(), nb, n, c, h, w, _stream()), "rrin_twarp_bwd")
+        return gimg, gflow
+
+
+def conv3x3(x, conv: torch.nn.Conv2d, leaky: bool = False):
+    return _Conv3x3.apply(x, conv.weight, conv.bias, leaky)
+
+
+def avg_pool2(x):
+    return _AvgPool2.apply(x)
+
+
+def upsample2(x):
+    return _Upsample2.apply(x)
+
+
+def backwarp(img, flow):
+    return _Backwarp.apply(img, flow)
+
+
+def unet_forward(unet, x):
+    """Reference UNet.forward (unet.py:40-51) on the HIP training Functions."""
+    bridges = []
+    for i, d in enumerate(unet.down_path):
+        x = conv3x3(x, d.block[0], leaky=True)
+        x = conv3x3(x, d.block[2], leaky=True)
+        if i < unet.depth - 1:
+            bridges.append(x)
+            x = avg_pool2(x)
+    x = conv3x3(x, unet.midconv, leaky=True)
+    for j, u in enumerate(unet.up_path):
+        up = conv3x3(upsample2(x), u.up[1], leaky=False)
+        x = torch.cat((up, bridges[-j - 1]), 1)
+        x = conv3x3(x, u.conv_block.block[0], leaky=True)
+        x = conv3x3(x, u.conv_block.block[2], leaky=True)
+    return conv3x3(x, unet.last, leaky=False)
+
+
+def net_forward(net, input0, input1, t=0.5):
+    """Reference Net.forward (model.py:32-65) on the HIP training Functions."""
+    x = torch.cat((input0, input1), 1)
+    flow = unet_forward(net.Flow, x)
+    f01, f10 = flow[:, :2], flow[:, 2:4]
+    ft0 = -(1 - t) * t * f01 + t * t * f10
+    ft1 = (1 - t) * (1 - t) * f01 - t * (1 - t) * f10
+    r = unet_forward(net.refine_flow, torch.cat((ft0, ft1, x), 1))
+    ft0 = ft0 + r[:, :2]
+    ft1 = ft1 + r[:, 2:4]
+    xt1 = backwarp(input0, ft0)
+    xt2 = backwarp(input1, ft1)
+    m = torch.sigmoid(unet_forward(net.Mask, torch.cat((ft0, ft1, x, xt1, xt2), 1)))
+    w1, w2 = (1 - t) * m[:, 0:1], t * m[:, 1:2]
+    out = (w1 * xt1 + w2 * xt2) / (w1 + w2 + 1e-8)
+    return (unet_forward(net.final, torch.cat((input0, input1, out), 1)) + out).clamp(0, 1)

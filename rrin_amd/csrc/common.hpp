@@ -41,23 +41,46 @@ inline int hip_code(hipError_t e) { return e == hipSuccess ? 0 : (int)e; }
 // ---- per-device launch caches ------------------------------------------------
 // The library keeps no state that affects results.  It caches, per device and
 // kernel, facts about launching it (the dynamic-LDS attribute has been set; the
-// resident blocks per CU); these caches are keyed by device and thread-safe
-// (atomics; a race only repeats an idempotent query).
+// resident blocks per CU); these caches are keyed by the device of the stream the
+// launch goes to (not the calling thread's current device: a C-ABI caller may pass
+// another device's stream) and are thread-safe (atomics; a race only repeats an
+// idempotent query).
 constexpr int kMaxDevices = 64;
 
-inline int current_device() {
-  int d = 0;
-  return (hipGetDevice(&d) == hipSuccess && d >= 0 && d < kMaxDevices) ? d : 0;
+// Device of stream st (the null stream: the calling thread's current device).
+inline int stream_device(hipStream_t st) {
+  int d = -1;
+  if (st == nullptr || hipStreamGetDevice(st, &d) != hipSuccess) {
+    if (hipGetDevice(&d) != hipSuccess) d = 0;
+  }
+  return (d >= 0 && d < kMaxDevices) ? d : 0;
 }
 
-// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device).
+// Run f() with device dev current on this thread (hipFuncSetAttribute and the
+// occupancy query act on the current device), restoring the caller's after.
+template <class F>
+inline hipError_t on_device(int dev, F f) {
+  int prev = 0;
+  if (hipGetDevice(&prev) != hipSuccess) prev = dev;
+  if (prev != dev) {
+    const hipError_t e = hipSetDevice(dev);
+    if (e != hipSuccess) return e;
+  }
+  const hipError_t r = f();
+  if (prev != dev) (void)hipSetDevice(prev);
+  return r;
+}
+
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device of st).
 struct LdsAttr {
   std::atomic<uint64_t> done{0};
-  int ensure(const void* kernel, int lds_bytes) {
-    const int dev = current_device();
+  int ensure(const void* kernel, int lds_bytes, hipStream_t st) {
+    const int dev = stream_device(st);
     const uint64_t bit = 1ull << dev;
     if (done.load(std::memory_order_acquire) & bit) return 0;
-    hipError_t e = hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+    hipError_t e = on_device(dev, [&] {
+      return hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+    });
     if (e != hipSuccess) return (int)e;
     done.fetch_or(bit, std::memory_order_release);
     return 0;
@@ -85,6 +108,7 @@ inline rrin_geom make_geom_h8(int h, int w) {
 struct WarpTaps {
   int x0, y0;
   float nw, ne, sw, se;
+  float wx, wy;  // fractional position: ix - floor(ix), iy - floor(iy) (the backward's weights)
   bool vx0, vx1, vy0, vy1;
 };
 
@@ -103,6 +127,8 @@ __device__ inline WarpTaps warp_taps(int gx, int gy, float u, float v, int H, in
   const float e = 1.0f - we;
   const float n = iy - fy;
   const float s = 1.0f - n;
+  t.wx = we;
+  t.wy = n;
   t.nw = s * e;
   t.ne = s * we;
   t.sw = n * e;

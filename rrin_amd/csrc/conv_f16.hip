@@ -1655,9 +1655,8 @@ static constexpr int kWinoCfg = kNumCfgH8 - 1;
 static inline bool is_wino(int cfg) { return cfg == kWinoCfg; }
 static constexpr size_t kMaxLds = 160 * 1024;
 
-static int num_cus() {
+static int num_cus(int dev) {
   static std::atomic<int> n[kMaxDevices] = {};
-  const int dev = current_device();
   int v = n[dev].load(std::memory_order_relaxed);
   if (!v) {
     if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v < 1) v = 256;
@@ -1676,19 +1675,22 @@ static int launch_h8_k(const ConvH8Args& args, int persist, hipStream_t st) {
   static LdsAttr attr;
   // resident blocks per CU, per device and LDS footprint (WRES: chunk count)
   static std::atomic<int> per_cu[kMaxDevices][40] = {};
-  if (int e = attr.ensure((const void*)k, (int)kMaxLds)) return e;
+  if (int e = attr.ensure((const void*)k, (int)kMaxLds, st)) return e;
   const int64_t ntiles = (int64_t)args.co_blocks * args.tiles_x * args.tiles_y * args.n;
   int64_t grid = ntiles;
   if (persist > 0) {
-    std::atomic<int>& slot = per_cu[current_device()][wres ? (args.nchunks < 40 ? args.nchunks : 39) : 0];
+    const int dev = stream_device(st);
+    std::atomic<int>& slot = per_cu[dev][wres ? (args.nchunks < 40 ? args.nchunks : 39) : 0];
     int pc = slot.load(std::memory_order_relaxed);
     if (!pc) {
-      hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, (const void*)k, T::NT, lds);
+      hipError_t e = on_device(dev, [&] {
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, (const void*)k, T::NT, lds);
+      });
       if (e != hipSuccess) return (int)e;
       if (pc < 1) pc = 1;
       slot.store(pc, std::memory_order_relaxed);
     }
-    int64_t g = (int64_t)persist * pc * num_cus();
+    int64_t g = (int64_t)persist * pc * num_cus(dev);
     g -= g % args.co_blocks;  // WRES: every tile of a block in the block's channel block
     if (g < args.co_blocks) g = args.co_blocks;
     if (g < grid) grid = g;
@@ -2053,7 +2055,7 @@ static int edge_fix_launch(const EdgeFixArgs& a, dim3 grid, hipStream_t st) {
   static_assert(lds <= 160 * 1024, "edge fix LDS");
   static_assert(kFixSubFloats >= 4 * 256, "K-group sums fit a staging region");
   static LdsAttr attr;
-  if (int e = attr.ensure((const void*)edge_fix_h8_kernel<PLANES, KS, F32>, (int)lds)) return e;
+  if (int e = attr.ensure((const void*)edge_fix_h8_kernel<PLANES, KS, F32>, (int)lds, st)) return e;
   hipLaunchKernelGGL((edge_fix_h8_kernel<PLANES, KS, F32>), grid, dim3(256 * KS), lds, st, a);
   return hip_code(hipGetLastError());
 }

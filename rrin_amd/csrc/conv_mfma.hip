@@ -382,7 +382,7 @@ static int launch_t(const ConvArgs& args, int grid, hipStream_t st) {
   constexpr size_t lds = SRC == RRIN_SRC_UPSAMPLE2X ? T::LDS_BYTES_UP : T::LDS_BYTES;
   auto k = conv3x3_mfma_kernel<A, B, C, D, SRC, EPI, SCHED>;
   static LdsAttr attr;
-  if (int e = attr.ensure((const void*)k, (int)lds)) return e;
+  if (int e = attr.ensure((const void*)k, (int)lds, st)) return e;
   hipLaunchKernelGGL(k, dim3(grid), dim3(256), lds, st, args);
   return hip_code(hipGetLastError());
 }

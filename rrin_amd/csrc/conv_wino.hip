@@ -48,18 +48,23 @@ static_assert(kWinoLds == (size_t)(2 * kWnRawStride + 2 * kWnU) * 16, "LDS size"
 __device__ inline int wn_col(int col) { return (col & 1) * 17 + (col >> 1); }
 
 // ABL: kernel-lab ablations only (built into librrin_lab.so under RRIN_LAB; the
-// product library instantiates ABL = 0): 1 no weight DMA after chunk 0, 2 no raw
-// DMA after chunk 0, 4 no MFMAs (operands kept live), 8 no transform arithmetic.
-// PERS: persistent grid (2 blocks per CU); a block loops over the tiles bid,
-// bid + grid, ... and stages chunk 0 of its next tile during the last chunk of the
-// current one, so only its first tile waits for staging.  The output-transform
-// exchange then uses the U buffer of the last chunk + its own 16 KB (kWinoPersLds).
-template <int EPI, int ABL = 0, bool PERS = false>
+// product library instantiates ABL = 0): 1 no weight DMA after chunk 1, 2 no raw
+// DMA after chunk 1, 4 no MFMAs (operands kept live), 8 no transform arithmetic.
+//
+// Main loop: a register pipeline over half-chunks (half = one B^T row yl of the
+// wave's pair = 16 MFMAs, point-major: the 4 products of point x back to back on
+// accumulator 4 yl + x).  While the MFMAs of half H issue, the window reads of half
+// H + 1 are in flight, and once point x's 4 MFMAs have issued its U / B registers
+// take point x of half H + 1 (U read from LDS, B transformed in the MFMA shadows):
+// no MFMA waits on an LDS round trip, and one operand set is live.  The chunk's
+// barrier sits at the start of its second half: every read of the chunk's buffers
+// has been consumed by then, so right after it those buffers take chunk c + 2's
+// LDS-DMA and the reads of chunk c + 1 start.
+template <int EPI, int ABL = 0>
 __global__ __launch_bounds__(256, 2) void conv3x3_wino_kernel(ConvH8Args a) {
   extern __shared__ __attribute__((aligned(16))) uint4 smem4[];
   uint4* s_raw = smem4;                      // [2][kWnRawStride]: [group][row][wn_col]
   uint4* s_u = smem4 + 2 * kWnRawStride;     // [2][16][2][32]
-  uint4* s_x = s_u + 2 * kWnU;               // PERS: [4 waves][4][64] exchange records
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int xh = wv & 1, ph = wv >> 1, j = lane & 31, hh = lane >> 5;
@@ -73,30 +78,28 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wino_kernel(ConvH8Args a) {
   if (bid >= ntiles) return;
   const int nch = a.nchunks;
 
-  // Tile t -> (channel block, column, row, image); staging bases of its raw input
-  // rows y0-1..y0+8, cols x0-1..x0+32 and of its U slabs.
+  // tile -> (channel block, column, row, image); staging bases of its raw input
+  // rows y0-1..y0+8, cols x0-1..x0+32 and of its U slabs
   struct Tile {
     int cob, x0, y0, img;
-    const uint4* src;
-    const uint4* wsrc;
-  };
-  auto tile_of = [&](int t) {
-    Tile T;
-    T.cob = t % a.co_blocks;
+  } cur;
+  {
+    int t = bid;
+    cur.cob = t % a.co_blocks;
     t /= a.co_blocks;
-    T.x0 = (t % a.tiles_x) * 32;
+    cur.x0 = (t % a.tiles_x) * 32;
     t /= a.tiles_x;
-    T.y0 = (t % a.tiles_y) * 8;
-    T.img = t / a.tiles_y;
-    T.src = a.src_hi + (int64_t)T.img * a.src_img + (int64_t)T.y0 * a.src_wp + T.x0 + (kH8PadLeft - 1);
-    T.wsrc = a.w_hi + (int64_t)T.cob * nch * kWnU + tid;
-    return T;
-  };
+    cur.y0 = (t % a.tiles_y) * 8;
+    cur.img = t / a.tiles_y;
+  }
+  const uint4* tsrc = a.src_hi + (int64_t)cur.img * a.src_img + (int64_t)cur.y0 * a.src_wp + cur.x0 + (kH8PadLeft - 1);
+  const uint4* wsrc = a.w_hi + (int64_t)cur.cob * nch * kWnU + tid;
 
   // ---- staging.  Per thread and DMA piece (3): its group of the chunk, its offset
-  // inside the group plane, and its column (groups past cin read the same column
-  // of the zero top-padding row of group 0 instead: they meet zero weights).
-  int p_g[3], p_off[3], p_col[3];
+  // inside the group plane (groups past cin read the same column of the zero
+  // top-padding row of group 0 instead: they meet zero weights).
+  int64_t p_off[3];
+  int p_g[3], p_zero[3];
 #pragma unroll
   for (int it = 0; it < 3; ++it) {
     const int idx = tid + 256 * it;
@@ -105,117 +108,184 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wino_kernel(ConvH8Args a) {
     const int r = rem / kWnRawCols, pos = rem - r * kWnRawCols;
     const int col = pos < 17 ? 2 * pos : 2 * (pos - 17) + 1;
     p_g[it] = g;
-    p_off[it] = r * a.src_wp + col;
-    p_col[it] = col;
+    p_off[it] = (int64_t)g * a.src_gp + r * a.src_wp + col;
+    p_zero[it] = col - cur.y0 * a.src_wp;
   }
-  auto issue_raw = [&](const Tile& T, int c, int buf) {
+  auto issue_raw = [&](int c, int buf) {
 #pragma unroll
     for (int it = 0; it < 3; ++it) {
       if (it < 2 || tid + 512 < kWnRaw) {
         const int gg = 2 * c + p_g[it];
-        const int64_t off =
-            gg * 4 < a.cin ? (int64_t)gg * a.src_gp + p_off[it] : (int64_t)p_col[it] - (int64_t)T.y0 * a.src_wp;
-        dma16(T.src + off, s_raw + buf * kWnRawStride + 256 * it + (tid & ~63));
+        const int64_t off = gg * 4 < a.cin ? (int64_t)(2 * c) * a.src_gp + p_off[it] : (int64_t)p_zero[it];
+        dma16(tsrc + off, s_raw + buf * kWnRawStride + 256 * it + (tid & ~63));
       }
     }
   };
-  auto issue_u = [&](const Tile& T, int c, int buf) {
+  auto issue_u = [&](int c, int buf) {
 #pragma unroll
-    for (int it = 0; it < 4; ++it)
-      dma16(T.wsrc + (int64_t)c * kWnU + 256 * it, s_u + buf * kWnU + 256 * it + (tid & ~63));
+    for (int it = 0; it < 4; ++it) dma16(wsrc + (int64_t)c * kWnU + 256 * it, s_u + buf * kWnU + 256 * it + (tid & ~63));
+  };
+  auto issue = [&](int c, int buf) {
+    if (!(ABL & 2) || c < 2) issue_raw(c, buf);
+    if (!(ABL & 1) || c < 2) issue_u(c, buf);
   };
 
-  // ---- per chunk: this lane's B operands V[xi][4hh + e][patch j] from its window:
-  // B^T rows 2xh, 2xh+1 as t0 = d[ra] - d[rb], t1 = d[rc] + sgn d[rd] (no branch on xh),
-  // then 8 points x 4 products
-  wfloatx16 acc[8];
   // MFMA column j -> patch (row pr, column jx).  The second row's columns are
   // rotated by 12 so the window reads of the two rows (68 records apart) fall on
   // distinct banks in every ds_read_b128 lane group ({0-3,12-15,20-27}, {4-11,16-19,28-31}).
   const int pr = 2 * ph + (j >> 4), jx = (j + 12 * (j >> 4)) & 15;
   const int ra = xh ? 2 : 0, rb = xh ? 1 : 2, rd = xh ? 3 : 2;  // rc = 1
   const float sgn = xh ? -1.f : 1.f;
-  // One B^T row yl of this wave's pair (t = d[ra] - d[rb] or d[1] + sgn d[rd]) and
-  // its 4 points' U operands, for chunk buffer b.
-  auto transform = [&](int b, int yl, wfloatx4* u4, wfloatx4* v4) {
-    const uint4* su = s_u + b * kWnU + (8 * xh + 4 * yl) * 64 + hh * 32 + j;
+  // LDS addresses (records) of this lane's operands in buffer 0: U of point
+  // (8 xh + 4 yl + x) at su0 + yl * 256 + x * 64; window records at rw0 + row * 34 + pc[k]
+  const int su0 = 2 * kWnRawStride + (8 * xh) * 64 + hh * 32 + j;
+  const int rw0 = hh * kWnRawG + (2 * pr) * kWnRawCols;
+  int pc[4];
 #pragma unroll
-    for (int x = 0; x < 4; ++x) u4[x] = __builtin_bit_cast(wfloatx4, su[x * 64]);
-    const uint4* rw = s_raw + b * kWnRawStride + hh * kWnRawG + (2 * pr) * kWnRawCols;
-    wfloatx4 c4[4];
+  for (int k = 0; k < 4; ++k) pc[k] = wn_col(2 * jx + k);
+  const int r0a = (ra)*kWnRawCols, r0b = (rb)*kWnRawCols, r1a = kWnRawCols, r1b = (rd)*kWnRawCols;
+
+  wfloatx16 acc[8];
+  wfloatx4 u[4], v[4];  // operands of the half being issued; point x recycled after its MFMAs
+  // U record of point (8 xh + 4 yl + x) of the chunk in buffer b
+  auto read_u = [&](int b, int yl, int x) {
+    return __builtin_bit_cast(wfloatx4, smem4[su0 + b * kWnU + yl * 256 + x * 64]);
+  };
+  // the 8 window records of B^T row yl (rows o0 / o1, 4 columns)
+  auto read_raw = [&](int b, int yl, wfloatx4* d) {
+    const uint4* rw = s_raw + b * kWnRawStride + rw0;
+    const int o0 = yl ? r1a : r0a, o1 = yl ? r1b : r0b;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const int pc = wn_col(2 * jx + k);
-      const wfloatx4 d0 = __builtin_bit_cast(wfloatx4, rw[(yl ? 1 : ra) * kWnRawCols + pc]);
-      const wfloatx4 d1 = __builtin_bit_cast(wfloatx4, rw[(yl ? rd : rb) * kWnRawCols + pc]);
-      if constexpr ((ABL & 8) != 0) {
-        c4[k] = d0;
-      } else if (yl == 0) {
-        c4[k] = d0 - d1;
+      d[2 * k] = __builtin_bit_cast(wfloatx4, rw[o0 + pc[k]]);
+      d[2 * k + 1] = __builtin_bit_cast(wfloatx4, rw[o1 + pc[k]]);
+    }
+  };
+  // column k of B^T row yl: t = d[ra] - d[rb] (yl 0) or d[1] + sgn d[rd] (yl 1)
+  auto row_t = [&](int yl, const wfloatx4* d, int k) {
+    if constexpr ((ABL & 8) != 0) return d[2 * k];
+    wfloatx4 t;
+    if (yl == 0) {
+      t = d[2 * k] - d[2 * k + 1];
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) t[e] = fmaf(sgn, d[2 * k + 1][e], d[2 * k][e]);
+    }
+    return t;
+  };
+  // the 4 MFMAs of point x of half yl (FIRST: chunk 0 starts from zero)
+  auto mfma_point = [&](int yl, int x, bool first) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if constexpr ((ABL & 4) != 0) {
+        asm volatile("" ::"v"(u[x][e]), "v"(v[x][e]));
       } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) c4[k][e] = fmaf(sgn, d1[e], d0[e]);
+        const wfloatx16 c = (first && e == 0) ? wfloatx16{} : acc[4 * yl + x];
+        acc[4 * yl + x] = __builtin_amdgcn_mfma_f32_32x32x2f32(u[x][e], v[x][e], c, 0, 0, 0);
       }
     }
-    if constexpr ((ABL & 8) != 0) {
+  };
+  // one half: MFMAs of half yl (operands in u / v) while half (bn, yn) -- the next
+  // one -- is read from buffer bn and transformed into u / v point by point
+  // hard scheduling fence (RRIN_WINO_FENCE, default on): keeps each stage's
+  // instructions between its fences, so the reads stay ahead of the MFMAs
+#ifndef RRIN_WINO_FENCE
+#define RRIN_WINO_FENCE 1
+#endif
+#ifndef RRIN_WINO_SGB
+#define RRIN_WINO_SGB 0
+#endif
+  auto fence = [&]() {
+    if constexpr (RRIN_WINO_FENCE) __builtin_amdgcn_sched_barrier(0);
+  };
+  auto half = [&](int yl, int bn, int yn, bool first) {
+    wfloatx4 d[8], t[4];
+    read_raw(bn, yn, d);
+    fence();
+    mfma_point(yl, 0, first);
+    u[0] = read_u(bn, yn, 0);
+    fence();
+    t[0] = row_t(yn, d, 0);
+    t[2] = row_t(yn, d, 2);
+    mfma_point(yl, 1, first);
+    v[0] = (ABL & 8) ? t[0] : t[0] - t[2];
+    u[1] = read_u(bn, yn, 1);
+    fence();
+    t[1] = row_t(yn, d, 1);
+    mfma_point(yl, 2, first);
+    v[1] = (ABL & 8) ? t[1] : t[1] + t[2];
+    u[2] = read_u(bn, yn, 2);
+    fence();
+    t[3] = row_t(yn, d, 3);
+    mfma_point(yl, 3, first);
+    v[2] = (ABL & 8) ? t[2] : t[2] - t[1];
+    v[3] = (ABL & 8) ? t[3] : t[1] - t[3];
+    u[3] = read_u(bn, yn, 3);
+    fence();
+#if RRIN_WINO_SGB
+    // pin the order: window reads, point 0, then one MFMA per 2-3 VALU
+    __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
 #pragma unroll
-      for (int x = 0; x < 4; ++x) v4[x] = c4[x];
-      return;
+    for (int i = 0; i < 4; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
     }
-    v4[0] = c4[0] - c4[2];
-    v4[1] = c4[1] + c4[2];
-    v4[2] = c4[2] - c4[1];
-    v4[3] = c4[1] - c4[3];
-  };
-  auto mfmas = [&](int yl, const wfloatx4* u4, const wfloatx4* v4) {
+    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
 #pragma unroll
-    for (int e = 0; e < 4; ++e)
+    for (int i = 0; i < 4; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
 #pragma unroll
-      for (int x = 0; x < 4; ++x) {
-        if constexpr ((ABL & 4) != 0)
-          asm volatile("" ::"v"(u4[x][e]), "v"(v4[x][e]));
-        else
-          acc[4 * yl + x] = __builtin_amdgcn_mfma_f32_32x32x2f32(u4[x][e], v4[x][e], acc[4 * yl + x], 0, 0, 0);
-      }
-  };
-  auto compute = [&](int b) {
-    wfloatx4 u0[4], v0[4], u1[4], v1[4];
-    transform(b, 0, u0, v0);
-    mfmas(0, u0, v0);
-    transform(b, 1, u1, v1);
-    mfmas(1, u1, v1);
+    for (int i = 0; i < 4; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+#endif
   };
 
-  Tile cur = tile_of(bid);
-  int b0 = 0;  // buffer of the current tile's chunk 0
-  issue_raw(cur, 0, 0);
-  issue_u(cur, 0, 0);
+  // ---- prologue: chunk 0 staged, its first half's operands in u / v; chunk 1 in flight
+  issue(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  for (int tile = bid;;) {
-    const int next = PERS ? tile + (int)gridDim.x : ntiles;
-    const bool has_next = next < ntiles;
-    Tile nxt = cur;
-    if (has_next) nxt = tile_of(next);
+  if (nch > 1) issue(1, 1);
+  {
+    wfloatx4 d[8], t[4];
+    read_raw(0, 0, d);
 #pragma unroll
-    for (int l = 0; l < 8; ++l)
+    for (int k = 0; k < 4; ++k) t[k] = row_t(0, d, k);
+    v[0] = (ABL & 8) ? t[0] : t[0] - t[2];
+    v[1] = (ABL & 8) ? t[1] : t[1] + t[2];
+    v[2] = (ABL & 8) ? t[2] : t[2] - t[1];
+    v[3] = (ABL & 8) ? t[3] : t[1] - t[3];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) acc[l][i] = 0.f;
-    for (int c = 0; c < nch; ++c) {
-      const int b = (b0 + c) & 1;
-      // buffers b^1 were last read in the previous chunk, before the barrier that ended it
-      if (c + 1 < nch) {
-        if constexpr (!(ABL & 2)) issue_raw(cur, c + 1, b ^ 1);
-        if constexpr (!(ABL & 1)) issue_u(cur, c + 1, b ^ 1);
-      } else if (has_next) {  // PERS: the next tile's chunk 0
-        issue_raw(nxt, 0, b ^ 1);
-        issue_u(nxt, 0, b ^ 1);
-      }
-      compute(b);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    }
-    const int bl = (b0 + nch - 1) & 1;  // buffers of the last chunk: free now
+    for (int x = 0; x < 4; ++x) u[x] = read_u(0, 0, x);
+  }
+  half(0, 0, 1, true);  // half (0, 0); reads of half (0, 1)
+  // step c: half (c, 1) and half (c + 1, 0), the barrier at its top: chunk c + 1
+  // landed everywhere and every read of chunk c's buffers (b) was consumed before
+  // it, so b takes chunk c + 2's DMA.  No LDS read is pending across the barrier.
+  auto step = [&](int c, bool first) {
+    const int b = c & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (c + 2 < nch) issue(c + 2, b);
+    half(1, b ^ 1, 0, first);   // half (c, 1); reads of half (c + 1, 0)
+    half(0, b ^ 1, 1, false);   // half (c + 1, 0); reads of half (c + 1, 1)
+  };
+  if (nch > 1) step(0, true);
+  for (int c = 1; c + 1 < nch; ++c) step(c, false);
+  // the last chunk's second half (its "next half" reads fetch stale records)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  half(1, ((nch - 1) & 1) ^ 1, 0, nch == 1);
+  // those reads complete before the epilogue reuses the LDS
+  __syncthreads();
 
     // ---- output transform: Q[yl][c] = sum_x M[xi_y][x] A[x][c] for this wave's xi rows,
     // then Y[0][c] = Q0 + Q1 + Q2 (wave xh 0), Y[1][c] = Q1 - Q2 - Q3 (wave xh 1)
@@ -229,10 +299,10 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wino_kernel(ConvH8Args a) {
         q[yl][1][i] = (m1 - m2) - m3;
       }
     // wave xh 0 hands its Q1 (yl 1) to its partner, wave xh 1 its Q2 (yl 0): records
-    // k 0-3 / 4-7 in the two U buffers, or (PERS: the other buffers hold the next
-    // tile's chunk 0) in the last chunk's U buffer and the exchange area
-    wfloatx4* xlo = reinterpret_cast<wfloatx4*>(PERS ? s_u + bl * kWnU : s_u);
-    wfloatx4* xhi = reinterpret_cast<wfloatx4*>(PERS ? s_x : s_u + kWnU);
+    // k 0-3 / 4-7 in the two U buffers (no DMA in flight and every read of them
+    // consumed since the last chunk's barrier)
+    wfloatx4* xlo = reinterpret_cast<wfloatx4*>(s_u);
+    wfloatx4* xhi = reinterpret_cast<wfloatx4*>(s_u + kWnU);
     auto xslot = [&](int w, int k) { return (k < 4 ? xlo : xhi) + (w * 4 + (k & 3)) * 64 + lane; };
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -318,13 +388,10 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wino_kernel(ConvH8Args a) {
         }
       }
       if constexpr (EPI == RRIN_EPI_LEAKY_POOL) {
-        // row 1 of each patch (wave xh 1) meets row 0 (wave xh 0) in LDS: one-tile grids
-        // use the raw buffers (idle now), PERS the exchange records (the next tile's chunk
-        // 0 is in the other raw buffer) once every wave has read them (barrier);
-        // avg = 0.25 ((v00 + v10) + (v01 + v11))
+        // row 1 of each patch (wave xh 1) meets row 0 (wave xh 0) in LDS, in the raw
+        // buffers (idle now); avg = 0.25 ((v00 + v10) + (v01 + v11))
         wfloatx4* xp = reinterpret_cast<wfloatx4*>(s_raw);
-        auto pslot = [&](int k) { return PERS ? xslot(ph, k) : xp + (ph * 8 + k) * 64 + lane; };
-        if constexpr (PERS) __syncthreads();
+        auto pslot = [&](int k) { return xp + (ph * 8 + k) * 64 + lane; };
         if (xh) {
 #pragma unroll
           for (int k = 0; k < 8; ++k) {
@@ -363,46 +430,20 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wino_kernel(ConvH8Args a) {
         }
       }
     }
-    if (!has_next) break;
-    // the next tile's chunk 1 is staged into buffers bl (exchange records) at its start
-    __syncthreads();
-    tile = next;
-    cur = nxt;
-    b0 = bl ^ 1;
-  }
 }
 
-constexpr size_t kWinoPersLds = kWinoLds + (size_t)4 * 4 * 64 * 16;  // + exchange records
-
-static int wino_num_cus() {
-  static std::atomic<int> n[kMaxDevices] = {};
-  const int dev = current_device();
-  int v = n[dev].load(std::memory_order_relaxed);
-  if (!v) {
-    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v < 1) v = 256;
-    n[dev].store(v, std::memory_order_relaxed);
-  }
-  return v;
-}
-
-template <int EPI, int ABL = 0, bool PERS = false>
+template <int EPI, int ABL = 0>
 static int launch_wino_k(const ConvH8Args& a, hipStream_t st) {
-  auto k = conv3x3_wino_kernel<EPI, ABL, PERS>;
-  constexpr size_t lds = PERS ? kWinoPersLds : kWinoLds;
+  auto k = conv3x3_wino_kernel<EPI, ABL>;
   static LdsAttr attr;
-  if (int e = attr.ensure((const void*)k, (int)lds)) return e;
-  int64_t grid = (int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n;
-#ifndef RRIN_WINO_PERS_BPC  // persistent blocks per CU (A/B builds)
-#define RRIN_WINO_PERS_BPC 2
-#endif
-  const int64_t slots = (int64_t)RRIN_WINO_PERS_BPC * wino_num_cus();
-  if (PERS && grid > slots) grid = slots;
-  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256), lds, st, a);
+  if (int e = attr.ensure((const void*)k, (int)kWinoLds, st)) return e;
+  const int64_t grid = (int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n;
+  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256), kWinoLds, st, a);
   return hip_code(hipGetLastError());
 }
 
 #ifdef RRIN_LAB
-// kernel lab (librrin_lab.so only): the LEAKY conv with ablation bits; bit 256 = PERS
+// kernel lab (librrin_lab.so only): the LEAKY conv with ablation bits
 int launch_wino_lab(const ConvH8Args& a, int abl, hipStream_t st) {
   switch (abl) {
     case 0: return launch_wino_k<RRIN_EPI_LEAKY, 0>(a, st);
@@ -413,40 +454,18 @@ int launch_wino_lab(const ConvH8Args& a, int abl, hipStream_t st) {
     case 8: return launch_wino_k<RRIN_EPI_LEAKY, 8>(a, st);
     case 11: return launch_wino_k<RRIN_EPI_LEAKY, 11>(a, st);
     case 15: return launch_wino_k<RRIN_EPI_LEAKY, 15>(a, st);
-    case 256: return launch_wino_k<RRIN_EPI_LEAKY, 0, true>(a, st);
-    case 256 + 3: return launch_wino_k<RRIN_EPI_LEAKY, 3, true>(a, st);
-    case 256 + 4: return launch_wino_k<RRIN_EPI_LEAKY, 4, true>(a, st);
   }
   return RRIN_E_CONFIG;
 }
 #endif
 
-// Persistent grid (PERS) only in A/B builds (-DRRIN_WINO_PERS_MIN=k: from k tiles per
-// block slot).  Alone it is faster (kernel lab, profiles/r02/wino_pers: full-resolution
-// convs 2-10 %, level 1 2-3 %; 720p x 1 bench +1.2 %), but the default 2-stream
-// forward loses 4 % (125.1 -> 120.3 pairs/s): a persistent grid holds every block
-// slot for the whole launch, so the other stream's kernels no longer fill the
-// slots one-tile blocks free as they finish.
-#ifndef RRIN_WINO_PERS_MIN
-#define RRIN_WINO_PERS_MIN 0
-#endif
-template <int EPI>
-static int launch_wino_e(const ConvH8Args& a, hipStream_t st) {
-  if constexpr (RRIN_WINO_PERS_MIN > 0) {
-    const int64_t ntiles = (int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n;
-    if (ntiles >= (int64_t)RRIN_WINO_PERS_MIN * RRIN_WINO_PERS_BPC * wino_num_cus())
-      return launch_wino_k<EPI, 0, true>(a, st);
-  }
-  return launch_wino_k<EPI>(a, st);
-}
-
 int launch_wino(const ConvH8Args& a, int epi, hipStream_t st) {
   switch (epi) {
-    case RRIN_EPI_LINEAR: return launch_wino_e<RRIN_EPI_LINEAR>(a, st);
-    case RRIN_EPI_LEAKY: return launch_wino_e<RRIN_EPI_LEAKY>(a, st);
-    case RRIN_EPI_LEAKY_POOL: return launch_wino_e<RRIN_EPI_LEAKY_POOL>(a, st);
-    case RRIN_EPI_LEAKY_REP: return launch_wino_e<RRIN_EPI_LEAKY_REP>(a, st);
-    case RRIN_EPI_SUBPIXEL: return launch_wino_e<RRIN_EPI_SUBPIXEL>(a, st);
+    case RRIN_EPI_LINEAR: return launch_wino_k<RRIN_EPI_LINEAR>(a, st);
+    case RRIN_EPI_LEAKY: return launch_wino_k<RRIN_EPI_LEAKY>(a, st);
+    case RRIN_EPI_LEAKY_POOL: return launch_wino_k<RRIN_EPI_LEAKY_POOL>(a, st);
+    case RRIN_EPI_LEAKY_REP: return launch_wino_k<RRIN_EPI_LEAKY_REP>(a, st);
+    case RRIN_EPI_SUBPIXEL: return launch_wino_k<RRIN_EPI_SUBPIXEL>(a, st);
   }
   return RRIN_E_ARG;
 }

@@ -1,0 +1,458 @@
+// Training path (autograd on): NCHW fp32 HIP kernels for the forward operators
+// of the reference's differentiable Net.forward and their backward.
+//
+// The reference trains with Net.forward under autograd (train.py:98) and
+// loss.backward() (train.py:144); its operators are nn.Conv2d(3, pad=1) + bias
+// (unet.py:29,38,59,62,78), LeakyReLU(0.1) (unet.py:47,60,63), F.avg_pool2d(2)
+// (unet.py:46), nn.Upsample(x2, bilinear) (unet.py:77) and F.grid_sample in warp
+// (model.py:8-21).  rrin_amd.train (Python) wraps each kernel pair below in a
+// torch.autograd.Function; the model.py glue (cat, t-blend, sigmoid, blend,
+// clamp) stays PyTorch elementwise autograd.
+//
+// conv3x3 is one implicit-GEMM kernel on the fp32 matrix cores
+// (v_mfma_f32_32x32x2_f32, exact fp32 products, fp32 accumulation), block tile
+// 64 x 64, K step 16 staged in LDS, three index maps:
+//   FWD   C[co][p]            = sum_{ci,tap} W[co][ci][tap] x[ci][p + tap]       (+ bias, leaky)
+//   DGRAD C[ci][p]            = sum_{co,tap} W[co][ci][8 - tap] g'[co][p + tap]   (flipped, transposed W)
+//   WGRAD C[co][(ci,tap) | 1] = sum_{img,p} g'[co][p] x[ci][p + tap]            (last column: the bias grad)
+// with g' = g * leaky'(y) applied on the fly (y = the forward's output: with a
+// positive slope its sign is the pre-activation's), so leaky backward is fused
+// into both gradient convs.  WGRAD splits its K (images x pixels) into fixed
+// slices whose partial tiles are summed in slice order: deterministic.
+//
+// grid_sample backward (warp): the flow gradient is local per output pixel;
+// the image gradient is a scatter (bilinear taps at data-dependent positions),
+// accumulated in 64-bit fixed point (2^-scale units, scale from the gradient's
+// max) so the sum is exact and order-independent, hence deterministic.
+#include <string.h>
+
+#include "common.hpp"
+
+namespace rrin {
+
+typedef float tfloatx16 __attribute__((ext_vector_type(16)));
+
+enum { TC_FWD = 0, TC_DGRAD = 1, TC_WGRAD = 2 };
+
+struct TConvArgs {
+  int n, cin, cout, h, w;
+  int leaky;
+  float slope;
+  const float* x;    // FWD / WGRAD: input [n][cin][h][w]
+  const float* g;    // DGRAD / WGRAD: incoming gradient [n][cout][h][w]
+  const float* y;    // leaky backward: forward output [n][cout][h][w]
+  const float* wt;   // OIHW [cout][cin][3][3]
+  const float* bias; // FWD (nullable)
+  float* out;        // FWD y, DGRAD gx, WGRAD partials [slices][cout][cin*9+1]
+  int M, N;          // GEMM dims
+  int64_t K;         // GEMM reduction length
+  int64_t kslice;    // WGRAD: K per slice (multiple of 16)
+};
+
+constexpr int TBM = 64, TBN = 64, TBK = 16;
+
+// A(m, k) and B(k, n) of the three maps; tap = ky * 3 + kx
+template <int MODE>
+__device__ inline float tc_a(const TConvArgs& a, int m, int64_t k, int img) {
+  if constexpr (MODE == TC_FWD) {
+    return (m < a.M && k < a.K) ? a.wt[(int64_t)m * a.K + k] : 0.f;
+  } else if constexpr (MODE == TC_DGRAD) {
+    if (m >= a.M || k >= a.K) return 0.f;
+    const int co = (int)(k / 9), tap = (int)(k - (int64_t)co * 9);
+    return a.wt[((int64_t)co * a.cin + m) * 9 + (8 - tap)];
+  } else {  // WGRAD: g'[img][co = m][p]
+    if (m >= a.M || k >= a.K) return 0.f;
+    const int64_t hw = (int64_t)a.h * a.w;
+    const int im = (int)(k / hw);
+    const int64_t p = k - (int64_t)im * hw;
+    const int64_t o = ((int64_t)im * a.cout + m) * hw + p;
+    float gv = a.g[o];
+    if (a.leaky) gv *= a.y[o] > 0.f ? 1.f : a.slope;
+    return gv;
+  }
+}
+
+template <int MODE>
+__device__ inline float tc_b(const TConvArgs& a, int64_t k, int n, int img) {
+  const int64_t hw = (int64_t)a.h * a.w;
+  if constexpr (MODE == TC_FWD || MODE == TC_DGRAD) {
+    if (k >= a.K || n >= a.N) return 0.f;
+    const int c = (int)(k / 9), tap = (int)(k - (int64_t)c * 9);
+    const int py = n / a.w, px = n - py * a.w;
+    const int yy = py + tap / 3 - 1, xx = px + tap % 3 - 1;
+    if (yy < 0 || yy >= a.h || xx < 0 || xx >= a.w) return 0.f;
+    if constexpr (MODE == TC_FWD) {
+      return a.x[((int64_t)img * a.cin + c) * hw + (int64_t)yy * a.w + xx];
+    } else {
+      const int64_t o = ((int64_t)img * a.cout + c) * hw + (int64_t)yy * a.w + xx;
+      float gv = a.g[o];
+      if (a.leaky) gv *= a.y[o] > 0.f ? 1.f : a.slope;
+      return gv;
+    }
+  } else {  // WGRAD: B(k = (img, p), n = (ci, tap) | bias column)
+    if (k >= a.K || n >= a.N) return 0.f;
+    if (n == a.N - 1) return 1.f;
+    const int im = (int)(k / hw);
+    const int64_t p = k - (int64_t)im * hw;
+    const int py = (int)(p / a.w), px = (int)(p - (int64_t)py * a.w);
+    const int ci = n / 9, tap = n - ci * 9;
+    const int yy = py + tap / 3 - 1, xx = px + tap % 3 - 1;
+    if (yy < 0 || yy >= a.h || xx < 0 || xx >= a.w) return 0.f;
+    return a.x[((int64_t)im * a.cin + ci) * hw + (int64_t)yy * a.w + xx];
+  }
+}
+
+// grid: x = N tiles, y = M tiles, z = images (FWD / DGRAD) or K slices (WGRAD)
+template <int MODE>
+__global__ __launch_bounds__(256) void tconv3x3_kernel(TConvArgs a) {
+  __shared__ float sa[TBK][TBM];
+  __shared__ float sb[TBK][TBN];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wm = wv & 1, wn = wv >> 1;  // wave's 32 x 32 sub-tile
+  const int m0 = blockIdx.y * TBM, n0 = blockIdx.x * TBN;
+  const int img = MODE == TC_WGRAD ? 0 : (int)blockIdx.z;
+  int64_t k0 = 0, k1 = a.K;
+  if constexpr (MODE == TC_WGRAD) {
+    k0 = (int64_t)blockIdx.z * a.kslice;
+    k1 = k0 + a.kslice < a.K ? k0 + a.kslice : a.K;
+  }
+  tfloatx16 acc;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+  // staging: thread -> (k row, 4 consecutive m / n)
+  const int sk = tid >> 4, sc = (tid & 15) * 4;
+  for (int64_t kb = k0; kb < k1; kb += TBK) {
+    const int64_t k = kb + sk;
+    const bool kin = k < k1;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      sa[sk][sc + j] = kin ? tc_a<MODE>(a, m0 + sc + j, k, img) : 0.f;
+      sb[sk][sc + j] = kin ? tc_b<MODE>(a, k, n0 + sc + j, img) : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < TBK; kk += 2) {
+      const float av = sa[kk + (lane >> 5)][wm * 32 + (lane & 31)];
+      const float bv = sb[kk + (lane >> 5)][wn * 32 + (lane & 31)];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  // C[m][n] of register r: m = 8 (r / 4) + 4 (lane / 32) + r % 4, n = lane % 32
+  const int n = n0 + wn * 32 + (lane & 31);
+  if (n >= a.N) return;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int m = m0 + wm * 32 + 8 * (r >> 2) + 4 * (lane >> 5) + (r & 3);
+    if (m >= a.M) continue;
+    float v = acc[r];
+    if constexpr (MODE == TC_FWD) {
+      if (a.bias) v += a.bias[m];
+      if (a.leaky) v = v > 0.f ? v : v * a.slope;
+      a.out[((int64_t)img * a.cout + m) * ((int64_t)a.h * a.w) + n] = v;
+    } else if constexpr (MODE == TC_DGRAD) {
+      a.out[((int64_t)img * a.cin + m) * ((int64_t)a.h * a.w) + n] = v;
+    } else {
+      a.out[((int64_t)blockIdx.z * a.M + m) * a.N + n] = v;
+    }
+  }
+}
+
+// WGRAD: sum the slices' partials in slice order -> gw [cout][cin*9], gb [cout]
+__global__ void twgrad_reduce_kernel(const float* __restrict__ part, int slices, int M, int N, float* gw,
+                                     float* gb) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M * N) return;
+  float s = 0.f;
+  for (int k = 0; k < slices; ++k) s += part[(int64_t)k * M * N + i];
+  const int m = i / N, c = i - m * N;
+  if (c == N - 1) {
+    if (gb) gb[m] = s;
+  } else {
+    gw[(int64_t)m * (N - 1) + c] = s;
+  }
+}
+
+// ---- avg_pool2d(2): y[i][j] = 0.25 ((x00 + x01) + (x10 + x11)) (CPU kernel's order)
+__global__ void tpool2_fwd_kernel(const float* __restrict__ x, float* y, int h, int w, int64_t total) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int ho = h / 2, wo = w / 2;
+  const int xo = (int)(i % wo);
+  const int64_t t = i / wo;
+  const int yo = (int)(t % ho);
+  const int64_t c = t / ho;
+  const float* p = x + c * h * w + (int64_t)(2 * yo) * w + 2 * xo;
+  y[i] = (((p[0] + p[1]) + p[w]) + p[w + 1]) * 0.25f;
+}
+
+__global__ void tpool2_bwd_kernel(const float* __restrict__ gy, float* gx, int h, int w, int64_t total) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int xx = (int)(i % w);
+  const int64_t t = i / w;
+  const int yy = (int)(t % h);
+  const int64_t c = t / h;
+  gx[i] = gy[c * (h / 2) * (w / 2) + (int64_t)(yy / 2) * (w / 2) + xx / 2] * 0.25f;
+}
+
+// ---- Upsample(x2, bilinear, align_corners=False), separable: output o of a line
+// of n inputs reads i0 = floor(s), i1 = min(i0 + 1, n - 1) with s = max((o + .5) / 2 - .5, 0),
+// weights 1 - l, l (l = s - i0).  Forward = the reference formula (unet.py:77).
+__device__ inline void up_taps(int o, int n, int& i0, int& i1, float& l) {
+  float s = ((float)o + 0.5f) * 0.5f - 0.5f;
+  if (s < 0.f) s = 0.f;
+  i0 = (int)s;
+  i1 = i0 + 1 < n ? i0 + 1 : n - 1;
+  l = s - (float)i0;
+}
+
+__global__ void tup2_fwd_kernel(const float* __restrict__ x, float* y, int h, int w, int64_t total) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int W2 = 2 * w, H2 = 2 * h;
+  const int ox = (int)(i % W2);
+  const int64_t t = i / W2;
+  const int oy = (int)(t % H2);
+  const int64_t c = t / H2;
+  int y0, y1, x0, x1;
+  float ly, lx;
+  up_taps(oy, h, y0, y1, ly);
+  up_taps(ox, w, x0, x1, lx);
+  const float* p = x + c * h * w;
+  const float a = p[(int64_t)y0 * w + x0], b = p[(int64_t)y0 * w + x1];
+  const float cc = p[(int64_t)y1 * w + x0], d = p[(int64_t)y1 * w + x1];
+  y[i] = (1.f - ly) * ((1.f - lx) * a + lx * b) + ly * ((1.f - lx) * cc + lx * d);
+}
+
+// backward as a gather: input i of a line receives from outputs 2i-2 .. 2i+3 the
+// weight each of them gave it (both taps may be i at the clamped edge)
+__device__ inline float up_w(int o, int n, int i) {
+  int i0, i1;
+  float l;
+  up_taps(o, n, i0, i1, l);
+  return (i0 == i ? 1.f - l : 0.f) + (i1 == i ? l : 0.f);
+}
+
+__global__ void tup2_bwd_kernel(const float* __restrict__ gy, float* gx, int h, int w, int64_t total) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int ix = (int)(i % w);
+  const int64_t t = i / w;
+  const int iy = (int)(t % h);
+  const int64_t c = t / h;
+  const int W2 = 2 * w, H2 = 2 * h;
+  const float* g = gy + c * H2 * W2;
+  float s = 0.f;
+  for (int oy = 2 * iy - 2; oy <= 2 * iy + 3; ++oy) {
+    if (oy < 0 || oy >= H2) continue;
+    const float wy = up_w(oy, h, iy);
+    if (wy == 0.f) continue;
+    float r = 0.f;
+    for (int ox = 2 * ix - 2; ox <= 2 * ix + 3; ++ox) {
+      if (ox < 0 || ox >= W2) continue;
+      const float wx = up_w(ox, w, ix);
+      if (wx != 0.f) r += wx * g[(int64_t)oy * W2 + ox];
+    }
+    s += wy * r;
+  }
+  gx[i] = s;
+}
+
+// ---- grid_sample backward of warp (model.py:8-21)
+// max |g| per call (order-free) -> fixed-point scale for the image gradient
+__global__ void tabsmax_kernel(const float* __restrict__ g, int64_t total, unsigned* mx) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  float v = i < total ? fabsf(g[i]) : 0.f;
+  if (!(v <= 3.0e38f)) v = 3.0e38f;  // NaN / inf: saturate (the fixed-point sum then saturates too)
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  if ((threadIdx.x & 63) == 0) atomicMax(mx, __float_as_uint(v));
+}
+
+// 2^e such that max|g| * 2^e ~ 2^40 (room for 2^23 contributions per pixel)
+__device__ inline float fx_scale(const unsigned* mx) {
+  const float m = __uint_as_float(*mx);
+  if (!(m > 0.f)) return 1.f;
+  int e;
+  frexpf(m, &e);  // m = f * 2^e, f in [0.5, 1)
+  return ldexpf(1.f, 40 - e);
+}
+
+__global__ void twarp_bwd_kernel(const float* __restrict__ img, const float* __restrict__ flow,
+                                 const float* __restrict__ gout, unsigned long long* acc, float* gflow,
+                                 const unsigned* mx, int c, int h, int w, int64_t total) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int x = (int)(i % w);
+  const int64_t t = i / w;
+  const int y = (int)(t % h);
+  const int n = (int)(t / h);
+  const int64_t hw = (int64_t)h * w;
+  const float u = flow[(int64_t)n * 2 * hw + (int64_t)y * w + x];
+  const float v = flow[(int64_t)n * 2 * hw + hw + (int64_t)y * w + x];
+  const WarpTaps tp = warp_taps(x, y, u, v, h, w);
+  const float sc = fx_scale(mx);
+  float gix = 0.f, giy = 0.f;
+  // tap weights nw = s e, ne = s we, sw = n e, se = n we (common.hpp warp_taps)
+  const float we_ = tp.wx, e_ = 1.0f - tp.wx, n_ = tp.wy, s_ = 1.0f - tp.wy;
+  for (int ch = 0; ch < c; ++ch) {
+    const float go = gout[((int64_t)n * c + ch) * hw + (int64_t)y * w + x];
+    const float* plane = img + ((int64_t)n * c + ch) * hw;
+    const float* p = plane + (int64_t)tp.y0 * w + tp.x0;
+    const float a = (tp.vy0 && tp.vx0) ? p[0] : 0.f;
+    const float b = (tp.vy0 && tp.vx1) ? p[1] : 0.f;
+    const float cc = (tp.vy1 && tp.vx0) ? p[w] : 0.f;
+    const float d = (tp.vy1 && tp.vx1) ? p[w + 1] : 0.f;
+    // d out / d ix, d out / d iy (PyTorch grid_sampler_2d_backward)
+    gix += go * ((b - a) * s_ + (d - cc) * n_);
+    giy += go * ((cc - a) * e_ + (d - b) * we_);
+    unsigned long long* q = acc + ((int64_t)n * c + ch) * hw + (int64_t)tp.y0 * w + tp.x0;
+    auto add = [&](bool ok, int64_t off, float wgt) {
+      if (ok) atomicAdd(q + off, (unsigned long long)(long long)llrintf(go * wgt * sc));
+    };
+    add(tp.vy0 && tp.vx0, 0, tp.nw);
+    add(tp.vy0 && tp.vx1, 1, tp.ne);
+    add(tp.vy1 && tp.vx0, w, tp.sw);
+    add(tp.vy1 && tp.vx1, w + 1, tp.se);
+  }
+  // ix = (gx + 1) W / 2 - 0.5 with gx = 2 (x / W - 0.5): d ix / d u = (W / 2) (2 / W)
+  gflow[(int64_t)n * 2 * hw + (int64_t)y * w + x] = gix * ((float)w / 2.0f) * (2.0f / (float)w);
+  gflow[(int64_t)n * 2 * hw + hw + (int64_t)y * w + x] = giy * ((float)h / 2.0f) * (2.0f / (float)h);
+}
+
+__global__ void tfix_to_float_kernel(const unsigned long long* __restrict__ acc, const unsigned* mx, float* out,
+                                     int64_t total) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  out[i] = (float)((double)(long long)acc[i] / (double)fx_scale(mx));
+}
+
+inline int grid_of(int64_t total) { return (int)((total + 255) / 256); }
+
+}  // namespace rrin
+
+using namespace rrin;
+
+static int tconv_check(const rrin_tconv_desc* d) {
+  if (!d || !d->wt || !d->out || !d->x) return RRIN_E_ARG;
+  if (d->n < 1 || d->cin < 1 || d->cout < 1 || d->h < 1 || d->w < 1) return RRIN_E_ARG;
+  if (d->leaky && !(d->slope > 0.f && d->slope <= 1.f)) return RRIN_E_ARG;
+  if (d->mode == RRIN_TCONV_DGRAD && d->leaky && !d->y) return RRIN_E_ARG;
+  if ((int64_t)d->h * d->w > 0x7fffffff) return RRIN_E_SHAPE;
+  return 0;
+}
+
+extern "C" int rrin_tconv3x3(const rrin_tconv_desc* d, void* stream) {
+  if (int e = tconv_check(d)) return e;
+  if (d->mode != RRIN_TCONV_FWD && d->mode != RRIN_TCONV_DGRAD) return RRIN_E_ARG;
+  TConvArgs a;
+  memset(&a, 0, sizeof(a));
+  a.n = d->n, a.cin = d->cin, a.cout = d->cout, a.h = d->h, a.w = d->w;
+  a.leaky = d->leaky, a.slope = d->slope, a.wt = d->wt, a.bias = d->bias, a.out = d->out;
+  a.N = d->h * d->w;
+  const hipStream_t st = (hipStream_t)stream;
+  if (d->mode == RRIN_TCONV_FWD) {
+    a.x = d->x;
+    a.M = d->cout;
+    a.K = (int64_t)d->cin * 9;
+    dim3 grid((a.N + TBN - 1) / TBN, (a.M + TBM - 1) / TBM, d->n);
+    hipLaunchKernelGGL(tconv3x3_kernel<TC_FWD>, grid, dim3(256), 0, st, a);
+  } else {
+    a.g = d->x;  // the incoming gradient [n][cout][h][w]
+    a.y = d->y;
+    a.M = d->cin;
+    a.K = (int64_t)d->cout * 9;
+    dim3 grid((a.N + TBN - 1) / TBN, (a.M + TBM - 1) / TBM, d->n);
+    hipLaunchKernelGGL(tconv3x3_kernel<TC_DGRAD>, grid, dim3(256), 0, st, a);
+  }
+  return hip_code(hipGetLastError());
+}
+
+// K slice of the weight gradient: whole 16-steps, ~32 slices at most, at least 4096 pixels each
+static int64_t twgrad_kslice(int64_t K) {
+  int64_t ks = (K + 31) / 32;
+  if (ks < 4096) ks = 4096;
+  return (ks + TBK - 1) / TBK * TBK;
+}
+
+extern "C" int64_t rrin_tconv3x3_wgrad_work_floats(int32_t n, int32_t cin, int32_t cout, int32_t h, int32_t w) {
+  if (n < 1 || cin < 1 || cout < 1 || h < 1 || w < 1) return RRIN_E_ARG;
+  const int64_t K = (int64_t)n * h * w, ks = twgrad_kslice(K);
+  const int64_t slices = (K + ks - 1) / ks;
+  return slices * cout * ((int64_t)cin * 9 + 1);
+}
+
+extern "C" int rrin_tconv3x3_wgrad(const rrin_twgrad_desc* d, void* stream) {
+  if (!d || !d->x || !d->g || !d->gw || !d->work || (d->leaky && !d->y)) return RRIN_E_ARG;
+  if (d->n < 1 || d->cin < 1 || d->cout < 1 || d->h < 1 || d->w < 1) return RRIN_E_ARG;
+  if (d->leaky && !(d->slope > 0.f && d->slope <= 1.f)) return RRIN_E_ARG;
+  TConvArgs a;
+  memset(&a, 0, sizeof(a));
+  a.n = d->n, a.cin = d->cin, a.cout = d->cout, a.h = d->h, a.w = d->w;
+  a.leaky = d->leaky, a.slope = d->slope, a.x = d->x, a.g = d->g, a.y = d->y;
+  a.M = d->cout;
+  a.N = d->cin * 9 + 1;
+  a.K = (int64_t)d->n * d->h * d->w;
+  a.kslice = twgrad_kslice(a.K);
+  a.out = d->work;
+  const int slices = (int)((a.K + a.kslice - 1) / a.kslice);
+  const hipStream_t st = (hipStream_t)stream;
+  dim3 grid((a.N + TBN - 1) / TBN, (a.M + TBM - 1) / TBM, slices);
+  hipLaunchKernelGGL(tconv3x3_kernel<TC_WGRAD>, grid, dim3(256), 0, st, a);
+  hipLaunchKernelGGL(twgrad_reduce_kernel, dim3(grid_of((int64_t)a.M * a.N)), dim3(256), 0, st,
+                     (const float*)d->work, slices, a.M, a.N, d->gw, d->gb);
+  return hip_code(hipGetLastError());
+}
+
+extern "C" int rrin_tpool2_fwd(const float* x, float* y, int32_t nc, int32_t h, int32_t w, void* stream) {
+  if (!x || !y || nc < 1 || h < 2 || w < 2 || (h & 1) || (w & 1)) return RRIN_E_ARG;
+  const int64_t total = (int64_t)nc * (h / 2) * (w / 2);
+  hipLaunchKernelGGL(tpool2_fwd_kernel, dim3(grid_of(total)), dim3(256), 0, (hipStream_t)stream, x, y, h, w, total);
+  return hip_code(hipGetLastError());
+}
+
+extern "C" int rrin_tpool2_bwd(const float* gy, float* gx, int32_t nc, int32_t h, int32_t w, void* stream) {
+  if (!gy || !gx || nc < 1 || h < 2 || w < 2 || (h & 1) || (w & 1)) return RRIN_E_ARG;
+  const int64_t total = (int64_t)nc * h * w;
+  hipLaunchKernelGGL(tpool2_bwd_kernel, dim3(grid_of(total)), dim3(256), 0, (hipStream_t)stream, gy, gx, h, w,
+                     total);
+  return hip_code(hipGetLastError());
+}
+
+extern "C" int rrin_tup2_fwd(const float* x, float* y, int32_t nc, int32_t h, int32_t w, void* stream) {
+  if (!x || !y || nc < 1 || h < 1 || w < 1) return RRIN_E_ARG;
+  const int64_t total = (int64_t)nc * 4 * h * w;
+  hipLaunchKernelGGL(tup2_fwd_kernel, dim3(grid_of(total)), dim3(256), 0, (hipStream_t)stream, x, y, h, w, total);
+  return hip_code(hipGetLastError());
+}
+
+extern "C" int rrin_tup2_bwd(const float* gy, float* gx, int32_t nc, int32_t h, int32_t w, void* stream) {
+  if (!gy || !gx || nc < 1 || h < 1 || w < 1) return RRIN_E_ARG;
+  const int64_t total = (int64_t)nc * h * w;
+  hipLaunchKernelGGL(tup2_bwd_kernel, dim3(grid_of(total)), dim3(256), 0, (hipStream_t)stream, gy, gx, h, w, total);
+  return hip_code(hipGetLastError());
+}
+
+extern "C" int64_t rrin_twarp_bwd_work_bytes(int32_t n, int32_t c, int32_t h, int32_t w) {
+  if (n < 1 || c < 1 || h < 1 || w < 1) return RRIN_E_ARG;
+  return (int64_t)n * c * h * w * 8 + 256;
+}
+
+extern "C" int rrin_twarp_bwd(const float* img, const float* flow, const float* gout, float* gimg, float* gflow,
+                              void* work, int64_t work_bytes, int32_t n, int32_t c, int32_t h, int32_t w,
+                              void* stream) {
+  if (!img || !flow || !gout || !gimg || !gflow || !work || n < 1 || c < 1 || h < 1 || w < 1) return RRIN_E_ARG;
+  const int64_t total = (int64_t)n * c * h * w;
+  if (work_bytes < rrin_twarp_bwd_work_bytes(n, c, h, w)) return RRIN_E_WORKSPACE;
+  const hipStream_t st = (hipStream_t)stream;
+  unsigned long long* acc = static_cast<unsigned long long*>(work);
+  unsigned* mx = reinterpret_cast<unsigned*>(acc + total);
+  if (hipError_t e = hipMemsetAsync(work, 0, (size_t)total * 8 + 256, st)) return (int)e;
+  hipLaunchKernelGGL(tabsmax_kernel, dim3(grid_of(total)), dim3(256), 0, st, gout, total, mx);
+  const int64_t px = (int64_t)n * h * w;
+  hipLaunchKernelGGL(twarp_bwd_kernel, dim3(grid_of(px)), dim3(256), 0, st, img, flow, gout, acc, gflow,
+                     (const unsigned*)mx, c, h, w, px);
+  hipLaunchKernelGGL(tfix_to_float_kernel, dim3(grid_of(total)), dim3(256), 0, st, (const unsigned long long*)acc,
+                     (const unsigned*)mx, gimg, total);
+  return hip_code(hipGetLastError());
+}

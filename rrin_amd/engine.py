@@ -159,6 +159,12 @@ def size_class(pixels: int) -> str:
 # direct-form tables below.
 WINO = True
 WINO_SIZES = ("small", "medium", "large", "xlarge", "xxlarge")
+# ... except where the direct form wins: the 6-channel first conv (Flow down0.a,
+# unet.py:59 with in_channels 6) has one 8-channel K chunk, so a Winograd tile is
+# mostly its prologue and epilogue; the direct form's BM 32 x TH 16 persistent
+# tile (cfg 13) is 5-11 % faster (0.020 vs 0.021 ms at 640x368 x 1, 0.096 vs
+# 0.108 ms at 1280x720 x 2; profiles/r02/wino/tune_fp32r_*_v3.txt, line 2).
+WINO_DIRECT = {(6, 32, 0): 13}
 
 
 def wino_cfg() -> int:
@@ -174,6 +180,9 @@ def choose_cfg_h8(cin: int, cout: int, prec: int, level: int = 0, size: str = "l
     swept choice (H8_TUNED_BY_SIZE, H8_TUNED), else a level rule from the same
     sweep."""
     if prec == _lib.PREC_F32R and WINO and size in WINO_SIZES:
+        c = WINO_DIRECT.get((cin, cout, level))
+        if c is not None and _lib.lib().rrin_conv_h8_cfg_fits(c, prec, cin):
+            return c
         return wino_cfg()
     table = H8_TUNED_BY_SIZE.get(size, {}).get(prec) or H8_TUNED.get(prec, {})
     cfg = table.get((cin, cout, level))

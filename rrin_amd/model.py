@@ -15,11 +15,13 @@ is no PyTorch-operator path.  The HIP path requires:
   caller `convert.py:117`.
 
 With autograd on (the training caller `train.py:98`) ``forward``
-runs the reference math with PyTorch operators on the model's device instead
-(``_forward_autograd``, same op order as `model.py:32-65`), so that training
-keeps working through the drop-in; there are no HIP backward kernels.  That
-path is never taken for inference, and without autograd a missing or failing
-HIP library raises.
+runs the reference graph (`model.py:32-65`) on the HIP training kernels: on a
+ROCm device every conv3x3 (+ leaky), avg-pool, upsample and backwarp is an
+autograd Function whose forward and backward are HIP kernels
+(``rrin_amd.autograd``, ``csrc/train.hip``), the elementwise glue is PyTorch
+autograd; on a CPU device the same graph runs with PyTorch operators
+(``_forward_autograd``).  That path is never taken for inference, and a
+missing or failing HIP library raises.
 """
 from __future__ import annotations
 
@@ -110,6 +112,9 @@ class Net(nn.Module):
     def forward(self, input0, input1, t=0.5):
         if torch.is_grad_enabled() and (input0.requires_grad or input1.requires_grad or
                                         any(p.requires_grad for p in self.parameters())):
+            if input0.is_cuda:
+                from .autograd import net_forward
+                return net_forward(self, input0, input1, t)
             return self._forward_autograd(input0, input1, t)
         return self.engine().forward(input0, input1, t, streams=self.streams)
 
@@ -126,7 +131,7 @@ class Net(nn.Module):
         return F.grid_sample(img, grid, mode="bilinear", padding_mode="zeros", align_corners=False)
 
     def _forward_autograd(self, input0, input1, t=0.5):
-        """Training path (autograd on): model.py:32-65 with PyTorch operators."""
+        """Training path on a CPU device (autograd on): model.py:32-65 with PyTorch operators."""
         x = torch.cat((input0, input1), 1)
         flow = self.Flow(x)
         f01, f10 = flow[:, :2], flow[:, 2:4]

@@ -10,6 +10,8 @@ backend "nccl" on ROCm; gloo in the CPU tests).
 """
 from __future__ import annotations
 
+import zlib
+
 import torch
 import torch.distributed as dist
 
@@ -80,6 +82,38 @@ class GatherPipeline:
             if f is not None and f[0] is not None:
                 f[0].wait()
             self.inflight[i] = None
+
+
+def _crc(t: torch.Tensor) -> int:
+    return zlib.crc32(t.detach().contiguous().cpu().view(torch.uint8).numpy().tobytes()) & 0xFFFFFFFF
+
+
+def verify_gather(local: torch.Tensor, gathered: torch.Tensor, group=None) -> dict:
+    """Bitwise check of one all-gather: every rank's shard ``local`` [b,...] is the
+    rank-order slice of ``gathered`` [world*b,...] -- on every rank, its own slice
+    by exact equality, and every slice's CRC-32 against the CRC its owner computed
+    of its shard (exchanged with ``all_gather_object``).  The verdict is reduced
+    over the ranks, so every rank returns the same ``ok``."""
+    inited = dist.is_available() and dist.is_initialized()
+    world = dist.get_world_size(group) if inited else 1
+    rank = dist.get_rank(group) if inited else 0
+    b = local.shape[0]
+    own = bool(torch.equal(gathered[rank * b:(rank + 1) * b], local))
+    mine = _crc(local)
+    crcs = [mine]
+    if inited:
+        crcs = [None] * world
+        dist.all_gather_object(crcs, mine, group=group)
+    seen = [_crc(gathered[r * b:(r + 1) * b]) for r in range(world)]
+    ok = own and seen == crcs
+    if inited:
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32,
+                            device=gathered.device if dist.get_backend(group) != "gloo" else "cpu")
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+        ok = bool(flag.item())
+    return {"ok": ok, "shard_crc32": [f"{c:08x}" for c in crcs],
+            "what": "bitwise: each rank's own slice of the gathered output == its shard (torch.equal), and "
+                    "the CRC-32 of every slice == the CRC-32 its owner computed of its shard; reduced over ranks"}
 
 
 def interpolate_sharded(net, i0_local: torch.Tensor, i1_local: torch.Tensor, t=0.5, group=None,

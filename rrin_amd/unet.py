@@ -7,7 +7,8 @@ arithmetic is done by `rrin_amd.engine`, which walks the tree and launches HIP
 kernels with the packed weights: inside ``Net.forward`` for the whole Net, and
 for a ``UNet`` called on its own (``UNet.forward`` without autograd ->
 ``rrin_unet_fwd``, same kernels).  With autograd on, ``UNet.forward`` is the
-PyTorch-operator training path.  Attribute paths (the reference key layout):
+training path (HIP forward + backward kernels on a ROCm device,
+``rrin_amd.autograd``; PyTorch operators on a CPU device).  Attribute paths (the reference key layout):
 
     down_path.{i}.block.{0,2}.{weight,bias}          unet.py:23-28, 59-63
     midconv.{weight,bias}                            unet.py:29
@@ -112,10 +113,14 @@ class UNet(nn.Module):
     def forward(self, x):
         """Reference ``UNet.forward`` (unet.py:40-51).  Without autograd: the HIP
         kernels (``rrin_unet_fwd``; the input must be fp32 on a ROCm device, H
-        and W multiples of 16).  With autograd on (training): the same math with
-        PyTorch operators, differentiable."""
+        and W multiples of 16).  With autograd on (training): on a ROCm device
+        the HIP training Functions (``rrin_amd.autograd.unet_forward``), on a
+        CPU device the same math with PyTorch operators."""
         if not torch.is_grad_enabled() or not (x.requires_grad or any(p.requires_grad for p in self.parameters())):
             return self._hip_engine().unet_forward(x)
+        if x.is_cuda:  # training on the GPU: HIP forward + backward kernels (rrin_amd.autograd)
+            from .autograd import unet_forward
+            return unet_forward(self, x)
         bridges = []
         for i, d in enumerate(self.down_path):
             x = d.block(x)

@@ -112,3 +112,32 @@ def test_gather_pipeline_gloo(tmp_path):
     for k in range(3):
         ref = torch.cat([torch.full((2, 3, 4, 5), float(10 * k + r)) for r in range(world)])
         assert torch.equal(got[k], ref)
+
+
+def _verify_worker(rank, world, port, result_path):
+    """verify_gather: an honest gather passes on every rank; one flipped bit in
+    rank 0's slice of rank 1's gathered copy fails on every rank."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from rrin_amd.shard import gather_frames, verify_gather
+    local = torch.rand(2, 3, 8, 10, generator=torch.Generator().manual_seed(rank))
+    g = gather_frames(local)
+    ok1 = verify_gather(local, g)["ok"]
+    bad = g.clone()
+    if rank == 1:
+        bits = bad.view(torch.int32)
+        bits[0, 1, 2, 3] ^= 1  # rank 0's slice, as rank 1 received it
+    ok2 = verify_gather(local, bad)["ok"]
+    torch.save(torch.tensor([ok1, ok2]), f"{result_path}.{rank}")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_verify_gather_bitwise_gloo(tmp_path):
+    world = 2
+    path = str(tmp_path / "v")
+    mp.start_processes(_verify_worker, args=(world, _free_port(), path), nprocs=world, join=True,
+                       start_method="spawn")
+    for r in range(world):
+        ok1, ok2 = torch.load(f"{path}.{r}", weights_only=True).tolist()
+        assert ok1 and not ok2, (r, ok1, ok2)

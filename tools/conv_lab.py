@@ -473,9 +473,88 @@ def ablate32(args):
         json.dump(results, open(args.out, "w"), indent=1)
 
 
+def abconv(args):
+    """A/B of the record-layout conv of two library builds (--lib vs --lib-b) on
+    the shapes of --shapes (cin:cout:level:epi:cfg,...), interleaved rounds in one
+    process, outputs compared bitwise; median ms per build."""
+    from rrin_amd.pp import H8Tensor
+    from tests.test_gpu_h8 import pack_h8
+    dev = torch.device("cuda:0")
+    paths = [args.lib or _lib.LIB_PATH] + args.lib_b.split(",")
+    libs = [C.CDLL(os.path.abspath(p)) for p in paths]
+    for L_ in libs:
+        L_.rrin_conv3x3_h8_fwd.argtypes = [C.POINTER(_lib.ConvH8Desc), C.c_void_p]
+        L_.rrin_conv3x3_h8_fwd.restype = C.c_int
+    prec = _lib.PRECISIONS[args.precision]
+    st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    bad = 0
+    for spec in args.shapes.split(","):
+        cin, cout, L, epi, cfg = (int(v) for v in spec.split(":"))
+        n, h, w = args.batch, args.height >> L, args.width >> L
+        if epi == 4:  # sub-pixel: the conv runs on the low-res grid, 4 x cout phase rows
+            h, w = h // 2, w // 2
+        torch.manual_seed(0)
+        x = H8Tensor.from_nchw(torch.rand(n, cin, h, w, device=dev) * 2 - 1, prec)
+        wt = torch.randn(cout, cin, 3, 3) / (3 * cin ** 0.5)
+        whi, wlo, bp, inv = pack_h8(wt, torch.randn(cout) * 0.1, cfg, prec, dev)
+        outs, descs, keep = [], [], []
+        for _ in libs:
+            if epi == 4:
+                dst = H8Tensor(n, cout // 4, 2 * h, 2 * w, dev, prec)
+            else:
+                dst = H8Tensor(n, cout, h, w, dev, prec)
+            pool = H8Tensor(n, cout, h // 2, w // 2, dev, prec) if epi == 2 else None
+            d = _lib.ConvH8Desc()
+            d.n, d.cin, d.cout, d.cfg, d.prec, d.epi_mode, d.slope, d.inv_wscale = n, cin, cout, cfg, prec, epi, 0.1, inv
+            d.src, d.dst = x.view(0, cin), dst.view(0, cout // 4 if epi == 4 else cout)
+            if pool is not None:
+                d.pool = pool.view(0, cout)
+            if epi == 4:
+                ring = torch.zeros(n * (cout // 4) * (2 * (2 * w) + 2 * (2 * h - 2)), device=dev)
+                d.edge = ring.data_ptr()
+                keep.append(ring)
+            d.whi, d.wlo, d.bias = whi.data_ptr(), wlo.data_ptr(), bp.data_ptr()
+            outs.append((dst, pool))
+            descs.append(d)
+        times = [[] for _ in libs]
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        for i, L_ in enumerate(libs):
+            _lib.check(L_.rrin_conv3x3_h8_fwd(C.byref(descs[i]), st))
+        torch.cuda.synchronize()
+        same = True
+        for k in range(1, len(libs)):
+            same = same and torch.equal(outs[0][0].to_nchw(), outs[k][0].to_nchw())
+            if epi == 2:
+                same = same and torch.equal(outs[0][1].to_nchw(), outs[k][1].to_nchw())
+            if epi == 4:
+                same = same and torch.equal(keep[0], keep[k])
+        for _ in range(args.rounds):
+            for i, L_ in enumerate(libs):
+                e0.record()
+                for _ in range(args.reps):
+                    L_.rrin_conv3x3_h8_fwd(C.byref(descs[i]), st)
+                e1.record()
+                e1.synchronize()
+                times[i].append(e0.elapsed_time(e1) / args.reps)
+        med = [sorted(t)[len(t) // 2] for t in times]
+        wf = 2 * 4 * cin * cout * h * w * n  # Winograd work (4/9 of direct)
+        rel = "  ".join(f"{chr(66 + k)} {med[k + 1]:.4f} ({med[k + 1] / med[0]:.3f})" for k in range(len(libs) - 1))
+        print(f"{cin:4d}->{cout:4d} L{L} epi{epi} cfg{cfg} n{n}: A {med[0]:.4f} ms  {rel}  "
+              f"best {wf / (min(med) * 1e-3) / 1e12:.1f} TF(wino)  {'bitwise equal' if same else 'DIFFERENT'}",
+              flush=True)
+        bad += 0 if same else 1
+    if bad and args.check:
+        sys.exit(3)
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("mode", choices=["breakdown", "tune", "single", "ablate", "ablate32"])
+    ap.add_argument("mode", choices=["breakdown", "tune", "single", "ablate", "ablate32", "abconv"])
+    ap.add_argument("--lib", default=None, help="abconv: library A (default: the in-tree product library)")
+    ap.add_argument("--lib-b", default=None, help="abconv: libraries B, C, ... (comma-separated)")
+    ap.add_argument("--shapes", default="256:256:3:1:18,64:32:0:1:18,32:32:0:1:18,128:64:1:1:18",
+                    help="abconv: cin:cout:level:epi:cfg list")
+    ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--shape", type=int, nargs=5, default=[512, 256, 3, 1, 0],
                     help="single: cin cout level epi cfg")
     ap.add_argument("--check", action="store_true", help="single, lab: compare with the product kernel bitwise")
@@ -492,7 +571,8 @@ def main():
                     help="breakdown: run the first conv of every U-Net with this H8 config (same BM only)")
     ap.add_argument("--precision", default="fp32", choices=["fp32", "fp32_planar", "fp32_split16", "fp16"])
     args = ap.parse_args()
-    {"breakdown": breakdown, "tune": tune, "single": single, "ablate": ablate, "ablate32": ablate32}[args.mode](args)
+    {"breakdown": breakdown, "tune": tune, "single": single, "ablate": ablate, "ablate32": ablate32,
+     "abconv": abconv}[args.mode](args)
 
 
 if __name__ == "__main__":
