@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define RRIN_ABI_VERSION 8
+#define RRIN_ABI_VERSION 9
 
 #define RRIN_OK 0
 #define RRIN_E_SHAPE (-1)     /* H or W not a multiple of 16, or N < 1          */
@@ -209,8 +209,9 @@ int rrin_conv_h8_cfg_ok(int32_t cfg, int32_t prec); /* 1 if the config fits LDS 
  * every weight chunk resident in LDS needs them to fit) */
 int rrin_conv_h8_cfg_fits(int32_t cfg, int32_t prec, int32_t cin);
 int rrin_conv3x3_h8_fwd(const rrin_conv_h8_desc* d, void* stream);
-/* 1 if cfg is the Winograd F(2x2,3x3) exact-fp32 config (F32R only, BM 32 x TH 8):
- * its weights are packed by rrin_pack_conv3x3_wino, not rrin_pack_conv3x3_r32 */
+/* 1 if cfg is a Winograd F(2x2,3x3) exact-fp32 config (F32R only: BM 32 x TH 8,
+ * 4 waves; BM 64 x TH 8, 8 waves): its weights are packed by
+ * rrin_pack_conv3x3_wino_bm with the config's BM, not rrin_pack_conv3x3_r32 */
 int rrin_conv_h8_cfg_wino(int32_t cfg);
 
 /* F32R packing: [co_block][chunk of 8 ci][tap][half][bm][4] fp32 (half hh holds
@@ -220,11 +221,15 @@ int64_t rrin_pack_conv3x3_r32_floats(int32_t cout, int32_t cin, int32_t bm);
 int rrin_pack_conv3x3_r32(const float* w, const float* b, int32_t cout, int32_t cin, int32_t bm,
                           const int32_t* perm, float* wpack, float* bpack);
 
-/* Winograd packing (F32R, the rrin_conv_h8_cfg_wino config): U = G g G^T per
+/* Winograd packing (F32R, the rrin_conv_h8_cfg_wino configs): U = G g G^T per
  * (co, ci) computed in double and rounded once to fp32, laid out
- * [co_block of 32][chunk of 4 ci][xi 16][co 32][4 ci] (xi = 4*row + col of the
- * 4x4 transform, G = [1 0 0; .5 .5 .5; .5 -.5 .5; 0 0 1]).  bpack:
- * rrin_pack_bias_floats(cout, 32) floats. */
+ * [co_block of bm][chunk of 8 ci][xi 16][half 2][co bm][4 ci] (xi = 4*row + col
+ * of the 4x4 transform, G = [1 0 0; .5 .5 .5; .5 -.5 .5; 0 0 1]; half hh holds
+ * input channels chunk*8 + 4*hh .. +3); bm = 32 or 64 (the config's BM).
+ * bpack: rrin_pack_bias_floats(cout, bm) floats.  The un-suffixed pair is bm 32. */
+int64_t rrin_pack_conv3x3_wino_bm_floats(int32_t cout, int32_t cin, int32_t bm);
+int rrin_pack_conv3x3_wino_bm(const float* w, const float* b, int32_t cout, int32_t cin, int32_t bm,
+                              const int32_t* perm, float* wpack, float* bpack);
 int64_t rrin_pack_conv3x3_wino_floats(int32_t cout, int32_t cin);
 int rrin_pack_conv3x3_wino(const float* w, const float* b, int32_t cout, int32_t cin, const int32_t* perm,
                            float* wpack, float* bpack);
@@ -379,6 +384,7 @@ typedef struct rrin_unet_desc {
   void* workspace;
   int64_t workspace_bytes;
   rrin_prof* prof;                 /* nullable */
+  int32_t* status;                 /* optional device int32: the F16X3 / F16 range guard, as rrin_net_desc */
 } rrin_unet_desc;
 int64_t rrin_unet_conv_count(int32_t depth);
 int rrin_unet_fwd(const rrin_unet_desc* d, void* stream);

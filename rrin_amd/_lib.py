@@ -9,7 +9,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "librrin_hip.so")
 
 # enums (rrin_hip.h)
@@ -116,7 +116,7 @@ class UNetDesc(C.Structure):
     _fields_ = [("n", C.c_int32), ("h", C.c_int32), ("w", C.c_int32), ("in_ch", C.c_int32), ("out_ch", C.c_int32),
                 ("depth", C.c_int32), ("prec", C.c_int32), ("pad_", C.c_int32), ("x", C.c_void_p), ("y", C.c_void_p),
                 ("convs", C.POINTER(ConvWeights)), ("head", HeadWeights), ("workspace", C.c_void_p),
-                ("workspace_bytes", C.c_int64), ("prof", C.c_void_p)]
+                ("workspace_bytes", C.c_int64), ("prof", C.c_void_p), ("status", C.c_void_p)]
 
 
 # every symbol include/rrin_hip.h declares: name -> (restype, argtypes)
@@ -146,6 +146,9 @@ SIGNATURES = {
     "rrin_conv3x3_h8_fwd": (C.c_int, [C.POINTER(ConvH8Desc), C.c_void_p]),
     "rrin_conv_h8_cfg_wino": (C.c_int, [C.c_int32]),
     "rrin_pack_conv3x3_wino_floats": (C.c_int64, [C.c_int32, C.c_int32]),
+    "rrin_pack_conv3x3_wino_bm_floats": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32]),
+    "rrin_pack_conv3x3_wino_bm": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p,
+                                            C.c_void_p, C.c_void_p]),
     "rrin_pack_conv3x3_wino": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p,
                                          C.c_void_p]),
     "rrin_pack_conv3x3_h8_halves": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32]),

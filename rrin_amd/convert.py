@@ -194,7 +194,7 @@ def interpolate_folder(model, src, dest, sf, batch=4, resume=False, device=None,
         metas1 = [g[2] for g in group_items[1:]] if nloc else []
         if world > 1 and gather:
             outs, metas0, metas1, ks = _gather_step(outs, metas0, metas1, nloc, shards, s_, batch, sf, group,
-                                                    device)
+                                                    device, getattr(model, "check_range", None))
             if rank != 0:
                 continue
         else:
@@ -223,16 +223,28 @@ def interpolate_folder(model, src, dest, sf, batch=4, resume=False, device=None,
     return written[0]
 
 
-def _gather_step(outs, metas0, metas1, nloc, shards, s_, batch, sf, group, device):
+def _gather_step(outs, metas0, metas1, nloc, shards, s_, batch, sf, group, device, model_check=None):
     """All-gather of one step's interpolated frames of every rank (rank order).
     Every rank contributes a [batch, sf, 3, H, W] slot (zero-padded past its
     nloc pairs); frame metadata travels as a Python object gather.  Returns the
     frames per t, the metadata and the global pair index of every gathered pair."""
     import torch.distributed as dist
     world = dist.get_world_size(group)
+    # the fp16 range guard of every rank (fp32_split16 / fp16: an overflowed
+    # forward wrote NaN frames) travels with the metadata, so rank 0 never
+    # writes another rank's poisoned frames and every rank raises together
+    bad = None
+    if outs is not None and model_check is not None:
+        try:
+            model_check()
+        except RuntimeError as e:
+            bad = str(e)
     meta_all = [None] * world
     dist.all_gather_object(meta_all, (nloc, metas0, metas1, None if outs is None else tuple(outs[0].shape[1:]),
-                                      None if outs is None else outs[0].dtype), group=group)
+                                      None if outs is None else outs[0].dtype, bad), group=group)
+    errs = [(r, m[5]) for r, m in enumerate(meta_all) if m[5]]
+    if errs:
+        raise RuntimeError(f"rank {errs[0][0]}: {errs[0][1]}")
     shape = next(m[3] for m in meta_all if m[3] is not None)
     dtype = next(m[4] for m in meta_all if m[4] is not None)
     dev = device if device is not None else torch.device("cpu")
@@ -299,7 +311,8 @@ def convert(args):
     ``torchrun --nproc-per-node N`` (WORLD_SIZE > 1) every process drives its
     own GPU (LOCAL_RANK), the pairs are sharded and their frames all-gathered
     over RCCL (``interpolate_folder``); rank 0 does the ffmpeg steps and the
-    folder checks, the other ranks wait at a barrier."""
+    folder checks and broadcasts their outcome, so a failure there ends every
+    rank (same message / exit code as the reference, convert.py:67-82)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     if world > 1 and int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 8:
@@ -324,17 +337,33 @@ def convert(args):
     else:
         raise Exception("Missing arguments! Video or folder needs to be specified")
     inp, dest = os.path.join(temp, "input"), os.path.join(temp, "output")
+    # rank 0's folder checks and frame extraction; their outcome is broadcast so
+    # that a failure ends every rank (the others would otherwise wait at the
+    # next collective until its timeout)
+    failure = None  # (kind, message)
     if not args.resume and rank == 0:
-        if os.path.exists(dest) and os.listdir(dest):
-            raise Exception("Folder is already in use! Did you intend to resume the progress? Use the --resume flag")
-        if args.input_video is not None:
-            shutil.rmtree(temp, ignore_errors=True)
-            os.makedirs(inp)
-            if _ffmpeg(["ffmpeg", "-i", args.input_video, "-vsync", "0", os.path.join(inp, "%9d.png")]):
-                print("Failed to convert video to images.")
-                sys.exit(1)
+        try:
+            if os.path.exists(dest) and os.listdir(dest):
+                failure = ("raise", "Folder is already in use! Did you intend to resume the progress? "
+                                    "Use the --resume flag")
+            elif args.input_video is not None:
+                shutil.rmtree(temp, ignore_errors=True)
+                os.makedirs(inp)
+                if _ffmpeg(["ffmpeg", "-i", args.input_video, "-vsync", "0", os.path.join(inp, "%9d.png")]):
+                    failure = ("exit", "Failed to convert video to images.")
+        except Exception as e:  # noqa: BLE001 -- re-raised on every rank below
+            failure = ("raise", f"{type(e).__name__}: {e}")
     if world > 1:
-        dist.barrier()
+        box = [failure]
+        dist.broadcast_object_list(box, src=0)
+        failure = box[0]
+    if failure is not None:
+        if world > 1:
+            dist.destroy_process_group()
+        if failure[0] == "exit":
+            print(failure[1])
+            sys.exit(1)
+        raise Exception(failure[1])
     src = inp if args.input_video is not None else args.image_folder
     dev = torch.device("cuda", torch.cuda.current_device())
     net = load_net(args.model_name, dev, getattr(args, "precision", "fp32"))

@@ -215,6 +215,13 @@ __device__ inline void dma16(const uint4* src, uint4* lds_wave_base) {
 // the record-layout table (F32R only), its LDS bytes per block and launcher.
 constexpr size_t kWinoLds = (size_t)(2 * 704 + 2 * 16 * 2 * 32) * 16;
 int launch_wino(const ConvH8Args& a, int epi, hipStream_t st);
+// zero channels [c0, c1) of a record-layout view (conv_f16.hip)
+int clear_channels_h8(const rrin_h8* v, int32_t n, int32_t c0, int32_t c1, int32_t prec, hipStream_t st);
+// 64-channel tile (8 waves, one block per CU): two stages of raw tile + 64-co U slab
+constexpr size_t kWino64Lds = (size_t)2 * (704 + 16 * 2 * 64) * 16;
+int launch_wino64(const ConvH8Args& a, int epi, hipStream_t st);
+// cfg 18's tile on 8 waves of 4 accumulators (<= 128 VGPRs: 4 waves per SIMD)
+int launch_winoq(const ConvH8Args& a, int epi, hipStream_t st);
 #ifdef RRIN_LAB
 int launch_wino_lab(const ConvH8Args& a, int abl, hipStream_t st);  // ablation bits (conv_wino.hip)
 #endif

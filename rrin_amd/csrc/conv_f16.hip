@@ -1649,10 +1649,16 @@ static const CfgH8 kCfgH8[] = {
 #undef X
     // kWinoCfg: Winograd F(2x2,3x3) on fp32 records (conv_wino.hip), BM 32 x TH 8
     {32, 8, kWinoLds, (size_t)1 << 30, 0, true, 0, 0},
+    // kWino64Cfg: the same, BM 64 x TH 8, 8 waves (conv3x3_wino64_kernel)
+    {64, 8, kWino64Lds, (size_t)1 << 30, 0, true, 0, 0},
+    // kWinoQCfg: cfg 18's tile and packing, 8 waves of 4 accumulators (conv3x3_winoq_kernel)
+    {32, 8, kWinoLds, (size_t)1 << 30, 0, true, 0, 0},
 };
 static constexpr int kNumCfgH8 = sizeof(kCfgH8) / sizeof(kCfgH8[0]);
-static constexpr int kWinoCfg = kNumCfgH8 - 1;
-static inline bool is_wino(int cfg) { return cfg == kWinoCfg; }
+static constexpr int kWinoCfg = kNumCfgH8 - 3;
+static constexpr int kWino64Cfg = kNumCfgH8 - 2;
+static constexpr int kWinoQCfg = kNumCfgH8 - 1;
+static inline bool is_wino(int cfg) { return cfg == kWinoCfg || cfg == kWino64Cfg || cfg == kWinoQCfg; }
 static constexpr size_t kMaxLds = 160 * 1024;
 
 static int num_cus(int dev) {
@@ -1879,7 +1885,9 @@ extern "C" int rrin_conv3x3_h8_fwd(const rrin_conv_h8_desc* d, void* stream) {
   const int rc = h8_prepare(d, a);
   if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;
-  if (is_wino(d->cfg)) return launch_wino(a, d->epi_mode, st);
+  if (d->cfg == kWinoCfg) return launch_wino(a, d->epi_mode, st);
+  if (d->cfg == kWino64Cfg) return launch_wino64(a, d->epi_mode, st);
+  if (d->cfg == kWinoQCfg) return launch_winoq(a, d->epi_mode, st);
   switch (d->cfg) {
 #define X(id, nw, wm, wn, sc, pe) \
   case id:                        \
@@ -2150,6 +2158,47 @@ extern "C" int rrin_upsample2x_h8(const rrin_h8* src, const rrin_h8* dst, int32_
   }
   return hip_code(hipGetLastError());
 }
+
+namespace rrin {
+// zero channels [c0, c1) of every interior pixel of a record-layout view (H8 hi
+// and lo planes, or R32); rrin_unet_fwd clears the channels its PLAIN head
+// writes past in_ch so that the next call's first conv never stages them
+__global__ void clear_channels_kernel(_Float16* hi, _Float16* lo, float* r32, int64_t img_stride, int64_t gp, int wp,
+                                      int c0, int c, int h, int w, int64_t total) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int x = (int)(i % w);
+  int64_t t = i / w;
+  const int y = (int)(t % h);
+  t /= h;
+  const int ch = c0 + (int)(t % c);
+  const int n = (int)(t / c);
+  if (r32) {
+    r32[r32_elem_index(img_stride, gp, wp, n, ch, y, x)] = 0.f;
+    return;
+  }
+  const int64_t k = h8_half_index(img_stride, gp, wp, n, ch, y, x);
+  hi[k] = (_Float16)0.f;
+  if (lo) lo[k] = (_Float16)0.f;
+}
+
+int clear_channels_h8(const rrin_h8* v, int32_t n, int32_t c0, int32_t c1, int32_t prec, hipStream_t st) {
+  if (!v || n < 1 || c0 < 0 || c1 <= c0 || !rec_prec(prec) || c1 > chans_per_rec(prec) * v->groups) return RRIN_E_ARG;
+  const int64_t total = (int64_t)n * (c1 - c0) * v->g.h * v->g.w;
+  const int grid = (int)((total + 255) / 256);
+  if (prec == RRIN_PREC_F32R) {
+    hipLaunchKernelGGL(clear_channels_kernel, dim3(grid), dim3(256), 0, st, (_Float16*)nullptr, (_Float16*)nullptr,
+                       static_cast<float*>(v->hi) + (int64_t)v->g_off * v->g.plane * 4, v->img_stride, v->g.plane,
+                       v->g.wp, c0, c1 - c0, v->g.h, v->g.w, total);
+  } else {
+    const int64_t go = (int64_t)v->g_off * v->g.plane * 8;
+    hipLaunchKernelGGL(clear_channels_kernel, dim3(grid), dim3(256), 0, st, static_cast<_Float16*>(v->hi) + go,
+                       planes_of(prec) == 2 ? static_cast<_Float16*>(v->lo) + go : (_Float16*)nullptr,
+                       (float*)nullptr, v->img_stride, v->g.plane, v->g.wp, c0, c1 - c0, v->g.h, v->g.w, total);
+  }
+  return hip_code(hipGetLastError());
+}
+}  // namespace rrin
 
 extern "C" int rrin_nchw_to_h8(const float* src, int32_t n, int32_t c, int32_t ch_off, const rrin_h8* dst,
                                int32_t prec, void* stream) {

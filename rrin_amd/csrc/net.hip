@@ -486,6 +486,10 @@ extern "C" int rrin_unet_fwd(const rrin_unet_desc* d, void* stream) {
   if (d->workspace_bytes < p.bytes) return RRIN_E_WORKSPACE;
   p.prof = d->prof;
   hipStream_t st = (hipStream_t)stream;
+  if (d->status && (d->prec == RRIN_PREC_F16X3 || d->prec == RRIN_PREC_F16)) {
+    p.status = d->status;  // fp16 range guard, as rrin_net_fwd
+    if (hipError_t e = hipMemsetAsync(d->status, 0, sizeof(int32_t), st)) return (int)e;
+  }
   const UNetSpec u{d->in_ch, d->out_ch, d->depth, RRIN_HEAD_PLAIN};
   const HeadIO io{nullptr, nullptr, d->y};
   int rc;
@@ -497,6 +501,9 @@ extern "C" int rrin_unet_fwd(const rrin_unet_desc* d, void* stream) {
     } else {
       const rrin_h8 gx = hview(p.G, 0, 16);
       rc = rrin_nchw_to_h8(d->x, d->n, d->in_ch, 0, &gx, d->prec, st);
+      // the PLAIN head writes its out_ch channels into this buffer: past in_ch
+      // they would be staged (against zero weights) by the next call's first conv
+      if (!rc && d->out_ch > d->in_ch) rc = clear_channels_h8(&gx, d->n, d->in_ch, d->out_ch, d->prec, st);
     }
   }
   if (rc) return rc;

@@ -368,9 +368,9 @@ class RRINEngine:
                 bp = np.empty(L.rrin_pack_bias_floats(cout, bm), np.float32)
                 pa = perm_arr.ctypes.data if perm_arr is not None else None
                 if L.rrin_conv_h8_cfg_wino(cfg):  # Winograd F(2x2,3x3): transformed weights
-                    wp = np.empty(L.rrin_pack_conv3x3_wino_floats(cout, cin), np.float32)
-                    _lib.check(L.rrin_pack_conv3x3_wino(w.ctypes.data, b.ctypes.data, cout, cin, pa,
-                                                        wp.ctypes.data, bp.ctypes.data), "rrin_pack_conv3x3_wino")
+                    wp = np.empty(L.rrin_pack_conv3x3_wino_bm_floats(cout, cin, bm), np.float32)
+                    _lib.check(L.rrin_pack_conv3x3_wino_bm(w.ctypes.data, b.ctypes.data, cout, cin, bm, pa,
+                                                           wp.ctypes.data, bp.ctypes.data), "rrin_pack_conv3x3_wino_bm")
                 else:
                     wp = np.empty(L.rrin_pack_conv3x3_r32_floats(cout, cin, bm), np.float32)
                     _lib.check(L.rrin_pack_conv3x3_r32(w.ctypes.data, b.ctypes.data, cout, cin, bm, pa,
@@ -568,9 +568,17 @@ class RRINEngine:
         d.head = self.head_table[0]
         ws = self.workspace(n, h, w, slot=100)   # own workspace: its input channels [C, 16) stay zero
         d.workspace, d.workspace_bytes = ws.data_ptr(), ws.numel()
+        status = self._status_of(100) if self.prec in (_lib.PREC_F16X3, _lib.PREC_F16) else None
+        d.status = status.data_ptr() if status is not None else None
         with torch.cuda.device(self.device):
             st = torch.cuda.current_stream(self.device)
             _lib.check(self.lib.rrin_unet_fwd(C.byref(d), C.c_void_p(st.cuda_stream)), "rrin_unet_fwd")
+            if status is not None:  # the range guard, checked as the Net's (_poll_range)
+                host = torch.empty(1, dtype=torch.int32, pin_memory=True)
+                host.copy_(status, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(st)
+                self._pending_status.append((ev, host))
         return y
 
     def _forward_part(self, i0, i1, out, coef, slot, ws, stream, prof, reuse_flow, tapbuf=None):

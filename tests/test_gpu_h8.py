@@ -65,11 +65,11 @@ def pack_h8(w, b, cfg, prec, dev, perm=None):
     bm = lib.rrin_conv_h8_cfg_bm(cfg)
     pa = np.asarray(perm, np.int32) if perm is not None else None
     if prec == R32 and lib.rrin_conv_h8_cfg_wino(cfg):  # Winograd: U = G g G^T per point
-        wp = np.zeros(lib.rrin_pack_conv3x3_wino_floats(cout, cin), np.float32)
+        wp = np.zeros(lib.rrin_pack_conv3x3_wino_bm_floats(cout, cin, bm), np.float32)
         bp = np.zeros(lib.rrin_pack_bias_floats(cout, bm), np.float32)
-        _lib.check(lib.rrin_pack_conv3x3_wino(w.ctypes.data, b.ctypes.data, cout, cin,
-                                              pa.ctypes.data if pa is not None else None, wp.ctypes.data,
-                                              bp.ctypes.data))
+        _lib.check(lib.rrin_pack_conv3x3_wino_bm(w.ctypes.data, b.ctypes.data, cout, cin, bm,
+                                                 pa.ctypes.data if pa is not None else None, wp.ctypes.data,
+                                                 bp.ctypes.data))
         wt = torch.from_numpy(wp).to(dev)
         return wt, wt, torch.from_numpy(bp).to(dev), 1.0
     if prec == R32:  # fp32 records: unscaled fp32 weights, no lo blob

@@ -118,7 +118,14 @@ def test_backwarp(gpu, scale):
 @pytest.mark.parametrize("stress", [False, True])
 def test_net_gradients_match_oracle_autograd(gpu, stress):
     """d(sum of Net output) / d(inputs, every parameter) through the HIP training
-    path vs PyTorch-CPU autograd of the oracle (the reference op sequence)."""
+    path vs PyTorch-CPU autograd of the oracle (the reference op sequence),
+    within 1e-4 relative (max-abs error / max-abs gradient, per tensor).
+
+    With the stress weights (10-18 px flows) the gradient is ill-conditioned: the
+    bilinear sampler's derivative jumps where a sample position crosses an
+    integer, so the reference's OWN fp32 gradients move by up to ~4e-3 relative
+    when its weights are perturbed by 1e-6 relative.  Each tensor's bound is
+    therefore max(1e-4, 2 x that sensitivity of the oracle), measured here."""
     from oracle.ref_net import net_forward
     net = Net()
     sd = keyed_state_dict(net.state_dict(), stress=stress)
@@ -128,18 +135,27 @@ def test_net_gradients_match_oracle_autograd(gpu, stress):
     a0, a1 = i0.to(gpu).requires_grad_(), i1.to(gpu).requires_grad_()
     out = net(a0, a1, 0.5)
     out.sum().backward()
-    ref_sd = {k: v.clone().requires_grad_() for k, v in sd.items()}
-    r0, r1 = i0.clone().requires_grad_(), i1.clone().requires_grad_()
-    ref = net_forward(ref_sd, r0, r1, 0.5)
-    ref.sum().backward()
+
+    def oracle(weights):
+        p = {k: v.clone().requires_grad_() for k, v in weights.items()}
+        r0, r1 = i0.clone().requires_grad_(), i1.clone().requires_grad_()
+        o = net_forward(p, r0, r1, 0.5)
+        o.sum().backward()
+        return o, {k: v.grad for k, v in p.items()}, r0.grad, r1.grad
+
+    ref, gref, g0, g1 = oracle(sd)
+    g = torch.Generator().manual_seed(1)
+    _, gpert, p0, p1 = oracle({k: v * (1 + 1e-6 * torch.randn(v.shape, generator=g)) for k, v in sd.items()})
     assert rel(out, ref) < 1e-4
     bad = []
     for name, p in net.named_parameters():
-        e = rel(p.grad, ref_sd[name].grad)
-        if e > 1e-4:
-            bad.append((name, e))
+        tol = max(1e-4, 2 * rel(gpert[name], gref[name]))
+        e = rel(p.grad, gref[name])
+        if e > tol:
+            bad.append((name, e, tol))
     assert not bad, bad
-    assert rel(a0.grad, r0.grad) < 1e-4 and rel(a1.grad, r1.grad) < 1e-4
+    assert rel(a0.grad, g0) <= max(1e-4, 2 * rel(p0, g0))
+    assert rel(a1.grad, g1) <= max(1e-4, 2 * rel(p1, g1))
 
 
 def test_net_backward_is_deterministic(gpu):

@@ -87,10 +87,13 @@ def test_wino_packing_layout_and_perm():
 def test_wino_config_entry():
     lib = _lib.lib()
     ids = [c for c in range(lib.rrin_conv_h8_cfg_count()) if lib.rrin_conv_h8_cfg_wino(c)]
-    assert len(ids) == 1
+    assert len(ids) == 2  # BM 32 (4 waves) and BM 64 (8 waves), both TH 8
+    assert sorted(lib.rrin_conv_h8_cfg_bm(c) for c in ids) == [32, 64]
     for c in ids:
-        assert lib.rrin_conv_h8_cfg_bm(c) == 32 and lib.rrin_conv_h8_cfg_th(c) == 8
+        assert lib.rrin_conv_h8_cfg_th(c) == 8
         assert lib.rrin_conv_h8_cfg_ok(c, _lib.PREC_F32R) == 1
         assert lib.rrin_conv_h8_cfg_ok(c, _lib.PREC_F16X3) == 0 and lib.rrin_conv_h8_cfg_ok(c, _lib.PREC_F16) == 0
     assert lib.rrin_pack_conv3x3_wino_floats(33, 5) == 2 * 1 * 16 * 2 * 32 * 4
     assert lib.rrin_pack_conv3x3_wino_floats(0, 5) < 0
+    assert lib.rrin_pack_conv3x3_wino_bm_floats(65, 9, 64) == 2 * 2 * 16 * 2 * 64 * 4
+    assert lib.rrin_pack_conv3x3_wino_bm_floats(8, 8, 48) < 0

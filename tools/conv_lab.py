@@ -547,9 +547,77 @@ def abconv(args):
         sys.exit(3)
 
 
+def cfgab(args):
+    """Two tile configs of the product library on the same conv (each with its own
+    packing): outputs compared bitwise, interleaved timing (--cfgs A,B; shapes as
+    abconv without the cfg field: cin:cout:level:epi)."""
+    from rrin_amd.pp import H8Tensor
+    from tests.test_gpu_h8 import pack_h8
+    dev = torch.device("cuda:0")
+    L_ = _lib.lib()
+    prec = _lib.PRECISIONS[args.precision]
+    ca, cb = (int(c) for c in args.cfgs.split(","))
+    st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    bad = 0
+    for spec in args.shapes.split(","):
+        cin, cout, L, epi = (int(v) for v in spec.split(":")[:4])
+        n, h, w = args.batch, args.height >> L, args.width >> L
+        if epi == 4:
+            h, w = h // 2, w // 2
+        torch.manual_seed(0)
+        x = H8Tensor.from_nchw(torch.rand(n, cin, h, w, device=dev) * 2 - 1, prec)
+        wt = torch.randn(cout, cin, 3, 3) / (3 * cin ** 0.5)
+        bias = torch.randn(cout) * 0.1
+        outs, descs, keep = [], [], []
+        for cfg in (ca, cb):
+            whi, wlo, bp, inv = pack_h8(wt, bias, cfg, prec, dev)
+            dst = H8Tensor(n, cout // 4, 2 * h, 2 * w, dev, prec) if epi == 4 else H8Tensor(n, cout, h, w, dev, prec)
+            pool = H8Tensor(n, cout, h // 2, w // 2, dev, prec) if epi == 2 else None
+            d = _lib.ConvH8Desc()
+            d.n, d.cin, d.cout, d.cfg, d.prec, d.epi_mode, d.slope, d.inv_wscale = n, cin, cout, cfg, prec, epi, 0.1, inv
+            d.src, d.dst = x.view(0, cin), dst.view(0, cout // 4 if epi == 4 else cout)
+            if pool is not None:
+                d.pool = pool.view(0, cout)
+            ring = None
+            if epi == 4:
+                ring = torch.zeros(n * (cout // 4) * (2 * (2 * w) + 2 * (2 * h - 2)), device=dev)
+                d.edge = ring.data_ptr()
+            d.whi, d.wlo, d.bias = whi.data_ptr(), wlo.data_ptr(), bp.data_ptr()
+            keep.append((whi, wlo, bp, ring))
+            outs.append((dst, pool, ring))
+            descs.append(d)
+        for d in descs:
+            _lib.check(L_.rrin_conv3x3_h8_fwd(C.byref(d), st))
+        torch.cuda.synchronize()
+        same = torch.equal(outs[0][0].to_nchw(), outs[1][0].to_nchw())
+        if epi == 2:
+            same = same and torch.equal(outs[0][1].to_nchw(), outs[1][1].to_nchw())
+        if epi == 4:
+            same = same and torch.equal(outs[0][2], outs[1][2])
+        times = [[], []]
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        for _ in range(args.rounds):
+            for i, d in enumerate(descs):
+                e0.record()
+                for _ in range(args.reps):
+                    L_.rrin_conv3x3_h8_fwd(C.byref(d), st)
+                e1.record()
+                e1.synchronize()
+                times[i].append(e0.elapsed_time(e1) / args.reps)
+        med = [sorted(t)[len(t) // 2] for t in times]
+        wf = 2 * 4 * cin * cout * h * w * n
+        print(f"{cin:4d}->{cout:4d} L{L} epi{epi} n{n}: cfg{ca} {med[0]:.4f} ms ({wf / (med[0] * 1e-3) / 1e12:.1f} TF)  "
+              f"cfg{cb} {med[1]:.4f} ms ({wf / (med[1] * 1e-3) / 1e12:.1f} TF)  B/A {med[1] / med[0]:.3f}  "
+              f"{'bitwise equal' if same else 'DIFFERENT'}", flush=True)
+        bad += 0 if same else 1
+    if bad and args.check:
+        sys.exit(3)
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("mode", choices=["breakdown", "tune", "single", "ablate", "ablate32", "abconv"])
+    ap.add_argument("mode", choices=["breakdown", "tune", "single", "ablate", "ablate32", "abconv", "cfgab"])
+    ap.add_argument("--cfgs", default="18,19", help="cfgab: the two tile configs")
     ap.add_argument("--lib", default=None, help="abconv: library A (default: the in-tree product library)")
     ap.add_argument("--lib-b", default=None, help="abconv: libraries B, C, ... (comma-separated)")
     ap.add_argument("--shapes", default="256:256:3:1:18,64:32:0:1:18,32:32:0:1:18,128:64:1:1:18",
@@ -572,7 +640,7 @@ def main():
     ap.add_argument("--precision", default="fp32", choices=["fp32", "fp32_planar", "fp32_split16", "fp16"])
     args = ap.parse_args()
     {"breakdown": breakdown, "tune": tune, "single": single, "ablate": ablate, "ablate32": ablate32,
-     "abconv": abconv}[args.mode](args)
+     "abconv": abconv, "cfgab": cfgab}[args.mode](args)
 
 
 if __name__ == "__main__":
