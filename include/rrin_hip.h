@@ -209,9 +209,11 @@ int rrin_conv_h8_cfg_ok(int32_t cfg, int32_t prec); /* 1 if the config fits LDS 
  * every weight chunk resident in LDS needs them to fit) */
 int rrin_conv_h8_cfg_fits(int32_t cfg, int32_t prec, int32_t cin);
 int rrin_conv3x3_h8_fwd(const rrin_conv_h8_desc* d, void* stream);
-/* 1 if cfg is a Winograd F(2x2,3x3) exact-fp32 config (F32R only: BM 32 x TH 8,
- * 4 waves; BM 64 x TH 8, 8 waves): its weights are packed by
- * rrin_pack_conv3x3_wino_bm with the config's BM, not rrin_pack_conv3x3_r32 */
+/* Nonzero if cfg is a Winograd F(2x2,3x3) exact-fp32 config (F32R only; its
+ * weights are packed by rrin_pack_conv3x3_wino_bm with the config's BM, not
+ * rrin_pack_conv3x3_r32): the tile kind, 1 = BM 32 x TH 8 on 4 waves, 2 = BM 64
+ * x TH 8 on 8 waves, 3 = BM 32 x TH 8 on 8 waves of 4 accumulators (4 waves per
+ * SIMD); all three give bitwise-equal outputs.  0: direct form. */
 int rrin_conv_h8_cfg_wino(int32_t cfg);
 
 /* F32R packing: [co_block][chunk of 8 ci][tap][half][bm][4] fp32 (half hh holds

@@ -220,7 +220,10 @@ int clear_channels_h8(const rrin_h8* v, int32_t n, int32_t c0, int32_t c1, int32
 // 64-channel tile (8 waves, one block per CU): two stages of raw tile + 64-co U slab
 constexpr size_t kWino64Lds = (size_t)2 * (704 + 16 * 2 * 64) * 16;
 int launch_wino64(const ConvH8Args& a, int epi, hipStream_t st);
-// cfg 18's tile on 8 waves of 4 accumulators (<= 128 VGPRs: 4 waves per SIMD)
+// cfg 18's tile on 8 waves of 4 accumulators (<= 128 VGPRs: 4 waves per SIMD),
+// two stages of [raw 680 | U 1024] records (three in A/B builds: two blocks per
+// CU would fill 163,584 B)
+constexpr size_t kWinoQLds = (size_t)3 * (680 + 1024) * 16;
 int launch_winoq(const ConvH8Args& a, int epi, hipStream_t st);
 #ifdef RRIN_LAB
 int launch_wino_lab(const ConvH8Args& a, int abl, hipStream_t st);  // ablation bits (conv_wino.hip)

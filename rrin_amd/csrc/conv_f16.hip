@@ -1652,7 +1652,7 @@ static const CfgH8 kCfgH8[] = {
     // kWino64Cfg: the same, BM 64 x TH 8, 8 waves (conv3x3_wino64_kernel)
     {64, 8, kWino64Lds, (size_t)1 << 30, 0, true, 0, 0},
     // kWinoQCfg: cfg 18's tile and packing, 8 waves of 4 accumulators (conv3x3_winoq_kernel)
-    {32, 8, kWinoLds, (size_t)1 << 30, 0, true, 0, 0},
+    {32, 8, (size_t)2 * (680 + 1024) * 16, (size_t)1 << 30, 0, true, 0, 0},
 };
 static constexpr int kNumCfgH8 = sizeof(kCfgH8) / sizeof(kCfgH8[0]);
 static constexpr int kWinoCfg = kNumCfgH8 - 3;
@@ -1862,7 +1862,10 @@ extern "C" int rrin_conv_h8_cfg_bm(int32_t cfg) {
 extern "C" int rrin_conv_h8_cfg_th(int32_t cfg) {
   return (cfg >= 0 && cfg < kNumCfgH8) ? kCfgH8[cfg].th : RRIN_E_CONFIG;
 }
-extern "C" int rrin_conv_h8_cfg_wino(int32_t cfg) { return is_wino(cfg) ? 1 : 0; }
+// 0: direct form; Winograd tile kind: 1 BM 32 / 4 waves, 2 BM 64 / 8 waves, 3 BM 32 / 8 waves
+extern "C" int rrin_conv_h8_cfg_wino(int32_t cfg) {
+  return cfg == kWinoCfg ? 1 : cfg == kWino64Cfg ? 2 : cfg == kWinoQCfg ? 3 : 0;
+}
 extern "C" int rrin_conv_h8_cfg_ok(int32_t cfg, int32_t prec) {
   if (cfg < 0 || cfg >= kNumCfgH8) return 0;
   if (!rec_prec(prec)) return 0;

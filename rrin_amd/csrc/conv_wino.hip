@@ -771,11 +771,18 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wino64_kernel(ConvH8Args a) {
 // others wait on LDS, barriers or their transform, instead of a deeper
 // per-wave pipeline.  The output transform meets through LDS as in cfg 19.
 // ============================================================================
+#ifndef RRIN_WINOQ_STAGES
+#define RRIN_WINOQ_STAGES 2
+#endif
+constexpr int kWqStages = RRIN_WINOQ_STAGES;
+constexpr int kWqStage = kWnRaw + kWnU;  // records per stage (raw 680 + U 1024)
+static_assert(kWinoQLds >= (size_t)kWqStages * kWqStage * 16, "LDS size");
+static_assert(2 * kWinoQLds <= 160 * 1024, "two blocks per CU");
+
 template <int EPI>
 __global__ __launch_bounds__(512, 2) void conv3x3_winoq_kernel(ConvH8Args a) {
   extern __shared__ __attribute__((aligned(16))) uint4 smem4[];
-  uint4* s_raw = smem4;                   // [2][kWnRawStride]
-  uint4* s_u = smem4 + 2 * kWnRawStride;  // [2][kWnU]
+  // kWqStages stages of [raw 680 | U 1024] records
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int yw = wv & 3, pt = wv >> 2, j = lane & 31, hh = lane >> 5;
   int bid;
@@ -814,16 +821,17 @@ __global__ __launch_bounds__(512, 2) void conv3x3_winoq_kernel(ConvH8Args a) {
     p_zero[it] = col - y0 * a.src_wp;
   }
   auto issue = [&](int c, int b) {
+    uint4* base = smem4 + b * kWqStage;
 #pragma unroll
     for (int it = 0; it < 2; ++it) {
       if (it == 0 || tid < kWnRaw - 512) {
         const int gg = 2 * c + p_g[it];
         const int64_t off = gg * 4 < a.cin ? (int64_t)(2 * c) * a.src_gp + p_off[it] : (int64_t)p_zero[it];
-        dma16(tsrc + off, s_raw + b * kWnRawStride + 512 * it + (tid & ~63));
+        dma16(tsrc + off, base + 512 * it + (tid & ~63));
       }
     }
 #pragma unroll
-    for (int it = 0; it < 2; ++it) dma16(wsrc + (int64_t)c * kWnU + 512 * it, s_u + b * kWnU + 512 * it + (tid & ~63));
+    for (int it = 0; it < 2; ++it) dma16(wsrc + (int64_t)c * kWnU + 512 * it, base + kWnRaw + 512 * it + (tid & ~63));
   };
   const int pr = 2 * pt + (j >> 4), jx = (j + 12 * (j >> 4)) & 15;
   const int ra = yw == 0 ? 0 : (yw == 2 ? 2 : 1);
@@ -840,7 +848,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_winoq_kernel(ConvH8Args a) {
   // one chunk in buffer b: window reads -> B^T row -> 4 points, then per point
   // its U record and 4 MFMAs (point-major, the cfg 18 accumulation order)
   auto chunk = [&](int b, bool first) {
-    const uint4* rw = s_raw + b * kWnRawStride + rw0;
+    const uint4* rw = smem4 + b * kWqStage + rw0;
     wfloatx4 t[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -854,7 +862,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_winoq_kernel(ConvH8Args a) {
     v[1] = t[1] + t[2];
     v[2] = t[2] - t[1];
     v[3] = t[1] - t[3];
-    const uint4* su = s_u + b * kWnU + su0;
+    const uint4* su = smem4 + b * kWqStage + kWnRaw + su0;
 #pragma unroll
     for (int x = 0; x < 4; ++x) {
       const wfloatx4 u = __builtin_bit_cast(wfloatx4, su[x * 64]);
@@ -865,12 +873,37 @@ __global__ __launch_bounds__(512, 2) void conv3x3_winoq_kernel(ConvH8Args a) {
       }
     }
   };
+  // kWqStages = 3 (A/B builds; 1-10 % slower than 2 stages on every shape,
+  // profiles/r03/ab_winoq_stages.txt): the DMA of chunk c + 2 is issued at the
+  // top of chunk c, so a chunk has two chunk-times to land.  At the top of chunk c a wave waits for
+  // its own pieces of chunk c (leaving chunk c + 1's in flight: 4 pieces for
+  // waves 0-2, which also stage the raw tile's 168-record tail, 3 for the rest),
+  // then the barrier makes every wave's pieces visible and ends every read of
+  // chunk c - 1, whose stage takes chunk c + 2.
+  const bool tail_wave = __builtin_amdgcn_readfirstlane(wv) < 3;
+  auto wait_chunk = [&](bool next_in_flight) {
+    if (!next_in_flight) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if (tail_wave) {
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    }
+  };
   issue(0, 0);
+  if (kWqStages == 3 && nch > 1) issue(1, 1);
   for (int c = 0; c < nch; ++c) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();  // chunk c landed everywhere; buffers (c + 1) & 1 were last read in chunk c - 1
-    if (c + 1 < nch) issue(c + 1, (c + 1) & 1);
-    chunk(c & 1, c == 0);
+    if constexpr (kWqStages == 3) {
+      wait_chunk(c + 1 < nch);
+      __syncthreads();
+      if (c + 2 < nch) issue(c + 2, (c + 2) % 3);
+      chunk(c % 3, c == 0);
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();  // chunk c landed everywhere; stage (c + 1) & 1 was last read in chunk c - 1
+      if (c + 1 < nch) issue(c + 1, (c + 1) & 1);
+      chunk(c & 1, c == 0);
+    }
   }
   __syncthreads();  // every read done before the exchange reuses the LDS
 
@@ -991,9 +1024,10 @@ template <int EPI>
 static int launch_winoq_k(const ConvH8Args& a, hipStream_t st) {
   auto k = conv3x3_winoq_kernel<EPI>;
   static LdsAttr attr;
-  if (int e = attr.ensure((const void*)k, (int)kWinoLds, st)) return e;
+  constexpr size_t lds = (size_t)kWqStages * kWqStage * 16;
+  if (int e = attr.ensure((const void*)k, (int)lds, st)) return e;
   const int64_t grid = (int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n;
-  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(512), kWinoLds, st, a);
+  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(512), lds, st, a);
   return hip_code(hipGetLastError());
 }
 

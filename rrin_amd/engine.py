@@ -167,9 +167,16 @@ WINO_SIZES = ("small", "medium", "large", "xlarge", "xxlarge")
 WINO_DIRECT = {(6, 32, 0): 13}
 
 
+# Winograd tile kind (rrin_conv_h8_cfg_wino): 3 = BM 32 x TH 8 on 8 waves of 4
+# accumulators (4 waves per SIMD) -- 1-9 % faster than kind 1
+# (4 waves of 8 accumulators) on every conv shape of the Net, bitwise equal
+# (profiles/r03/cfgab_18_20.txt)
+WINO_KIND = 3
+
+
 def wino_cfg() -> int:
     lib = _lib.lib()
-    return next(c for c in range(lib.rrin_conv_h8_cfg_count()) if lib.rrin_conv_h8_cfg_wino(c))
+    return next(c for c in range(lib.rrin_conv_h8_cfg_count()) if lib.rrin_conv_h8_cfg_wino(c) == WINO_KIND)
 
 
 def choose_cfg_h8(cin: int, cout: int, prec: int, level: int = 0, size: str = "large") -> int:

@@ -87,8 +87,9 @@ def test_wino_packing_layout_and_perm():
 def test_wino_config_entry():
     lib = _lib.lib()
     ids = [c for c in range(lib.rrin_conv_h8_cfg_count()) if lib.rrin_conv_h8_cfg_wino(c)]
-    assert len(ids) == 2  # BM 32 (4 waves) and BM 64 (8 waves), both TH 8
-    assert sorted(lib.rrin_conv_h8_cfg_bm(c) for c in ids) == [32, 64]
+    # kinds 1 (BM 32, 4 waves), 2 (BM 64, 8 waves), 3 (BM 32, 8 waves of 4 accumulators), all TH 8
+    assert sorted(lib.rrin_conv_h8_cfg_wino(c) for c in ids) == [1, 2, 3]
+    assert {lib.rrin_conv_h8_cfg_wino(c): lib.rrin_conv_h8_cfg_bm(c) for c in ids} == {1: 32, 2: 64, 3: 32}
     for c in ids:
         assert lib.rrin_conv_h8_cfg_th(c) == 8
         assert lib.rrin_conv_h8_cfg_ok(c, _lib.PREC_F32R) == 1
