@@ -67,8 +67,9 @@ KERNEL = {"fp32": "conv3x3_h8_kernel on fp32 records (77 body convs, v_mfma_f32_
           "fp32_planar": "conv3x3_mfma_kernel, planar fp32 (77 body convs, v_mfma_f32_32x32x2_f32)",
           "fp32_split16": "conv3x3_h8_kernel (77 body convs, v_mfma_f32_32x32x16_f16 x3)",
           "fp16": "conv3x3_h8_kernel (77 body convs, v_mfma_f32_32x32x16_f16)"}
-KERNEL_WINO = ("conv3x3_wino_kernel: Winograd F(2x2,3x3) on fp32 records (77 body convs; fp32 input/output "
-               "transforms, v_mfma_f32_32x32x2_f32 contraction per transform point)")
+KERNEL_WINO = ("conv3x3_winoq_kernel: Winograd F(2x2,3x3) on fp32 records (76 of the 77 body convs; fp32 "
+               "input/output transforms, v_mfma_f32_32x32x2_f32 contraction per transform point; 8 waves of 4 "
+               "accumulators per 32 co x 32 px x 8 row tile, 4 waves per SIMD)")
 DTYPE = {"fp32": "f32", "fp32_planar": "f32",
          "fp32_split16": "f16x3 (fp32-emulated: fp16 hi+lo split, 3 f16 MFMA products, f32 accumulate)",
          "fp16": "f16"}

@@ -442,22 +442,6 @@ static int launch_wino_k(const ConvH8Args& a, hipStream_t st) {
   return hip_code(hipGetLastError());
 }
 
-#ifdef RRIN_LAB
-// kernel lab (librrin_lab.so only): the LEAKY conv with ablation bits
-int launch_wino_lab(const ConvH8Args& a, int abl, hipStream_t st) {
-  switch (abl) {
-    case 0: return launch_wino_k<RRIN_EPI_LEAKY, 0>(a, st);
-    case 1: return launch_wino_k<RRIN_EPI_LEAKY, 1>(a, st);
-    case 2: return launch_wino_k<RRIN_EPI_LEAKY, 2>(a, st);
-    case 3: return launch_wino_k<RRIN_EPI_LEAKY, 3>(a, st);
-    case 4: return launch_wino_k<RRIN_EPI_LEAKY, 4>(a, st);
-    case 8: return launch_wino_k<RRIN_EPI_LEAKY, 8>(a, st);
-    case 11: return launch_wino_k<RRIN_EPI_LEAKY, 11>(a, st);
-    case 15: return launch_wino_k<RRIN_EPI_LEAKY, 15>(a, st);
-  }
-  return RRIN_E_CONFIG;
-}
-#endif
 
 int launch_wino(const ConvH8Args& a, int epi, hipStream_t st) {
   switch (epi) {
@@ -779,7 +763,10 @@ constexpr int kWqStage = kWnRaw + kWnU;  // records per stage (raw 680 + U 1024)
 static_assert(kWinoQLds >= (size_t)kWqStages * kWqStage * 16, "LDS size");
 static_assert(2 * kWinoQLds <= 160 * 1024, "two blocks per CU");
 
-template <int EPI>
+// ABL (lab builds only, librrin_lab.so): 1 no U DMA after chunk 0, 2 no raw DMA
+// after chunk 0, 4 no MFMAs, 8 no transform arithmetic, 16 no window reads after
+// chunk 0 (registers reused), 32 no U reads after chunk 0, 64 no epilogue stores
+template <int EPI, int ABL = 0>
 __global__ __launch_bounds__(512, 2) void conv3x3_winoq_kernel(ConvH8Args a) {
   extern __shared__ __attribute__((aligned(16))) uint4 smem4[];
   // kWqStages stages of [raw 680 | U 1024] records
@@ -824,14 +811,15 @@ __global__ __launch_bounds__(512, 2) void conv3x3_winoq_kernel(ConvH8Args a) {
     uint4* base = smem4 + b * kWqStage;
 #pragma unroll
     for (int it = 0; it < 2; ++it) {
-      if (it == 0 || tid < kWnRaw - 512) {
+      if ((it == 0 || tid < kWnRaw - 512) && !((ABL & 2) && c > 0)) {
         const int gg = 2 * c + p_g[it];
         const int64_t off = gg * 4 < a.cin ? (int64_t)(2 * c) * a.src_gp + p_off[it] : (int64_t)p_zero[it];
         dma16(tsrc + off, base + 512 * it + (tid & ~63));
       }
     }
 #pragma unroll
-    for (int it = 0; it < 2; ++it) dma16(wsrc + (int64_t)c * kWnU + 512 * it, base + kWnRaw + 512 * it + (tid & ~63));
+    for (int it = 0; it < 2; ++it)
+      if (!((ABL & 1) && c > 0)) dma16(wsrc + (int64_t)c * kWnU + 512 * it, base + kWnRaw + 512 * it + (tid & ~63));
   };
   const int pr = 2 * pt + (j >> 4), jx = (j + 12 * (j >> 4)) & 15;
   const int ra = yw == 0 ? 0 : (yw == 2 ? 2 : 1);
@@ -845,6 +833,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_winoq_kernel(ConvH8Args a) {
   const int su0 = (4 * yw) * 64 + hh * 32 + j;  // U of point 4 yw + x: + x * 64 (layout [xi][half][32 co])
 
   wfloatx16 acc[4];
+  wfloatx4 dk[8], uk[4];  // ABL 16 / 32: chunk 0's reads kept
   // one chunk in buffer b: window reads -> B^T row -> 4 points, then per point
   // its U record and 4 MFMAs (point-major, the cfg 18 accumulation order)
   auto chunk = [&](int b, bool first) {
@@ -852,24 +841,51 @@ __global__ __launch_bounds__(512, 2) void conv3x3_winoq_kernel(ConvH8Args a) {
     wfloatx4 t[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const wfloatx4 d0 = __builtin_bit_cast(wfloatx4, rw[oa + pc[k]]);
-      const wfloatx4 d1 = __builtin_bit_cast(wfloatx4, rw[ob + pc[k]]);
+      wfloatx4 d0, d1;
+      if (!(ABL & 16) || first) {
+        d0 = __builtin_bit_cast(wfloatx4, rw[oa + pc[k]]);
+        d1 = __builtin_bit_cast(wfloatx4, rw[ob + pc[k]]);
+        if constexpr ((ABL & 16) != 0) dk[2 * k] = d0, dk[2 * k + 1] = d1;
+      } else {
+        d0 = dk[2 * k];
+        d1 = dk[2 * k + 1];
+      }
+      if constexpr ((ABL & 8) != 0) {
+        t[k] = d0;
+        asm volatile("" ::"v"(d1));
+      } else {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) t[k][e] = fmaf(sg, d1[e], d0[e]);
+        for (int e = 0; e < 4; ++e) t[k][e] = fmaf(sg, d1[e], d0[e]);
+      }
     }
     wfloatx4 v[4];
-    v[0] = t[0] - t[2];
-    v[1] = t[1] + t[2];
-    v[2] = t[2] - t[1];
-    v[3] = t[1] - t[3];
+    if constexpr ((ABL & 8) != 0) {
+#pragma unroll
+      for (int x = 0; x < 4; ++x) v[x] = t[x];
+    } else {
+      v[0] = t[0] - t[2];
+      v[1] = t[1] + t[2];
+      v[2] = t[2] - t[1];
+      v[3] = t[1] - t[3];
+    }
     const uint4* su = smem4 + b * kWqStage + kWnRaw + su0;
 #pragma unroll
     for (int x = 0; x < 4; ++x) {
-      const wfloatx4 u = __builtin_bit_cast(wfloatx4, su[x * 64]);
+      wfloatx4 u;
+      if (!(ABL & 32) || first) {
+        u = __builtin_bit_cast(wfloatx4, su[x * 64]);
+        if constexpr ((ABL & 32) != 0) uk[x] = u;
+      } else {
+        u = uk[x];
+      }
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const wfloatx16 c = (first && e == 0) ? wfloatx16{} : acc[x];
-        acc[x] = __builtin_amdgcn_mfma_f32_32x32x2f32(u[e], v[x][e], c, 0, 0, 0);
+        if constexpr ((ABL & 4) != 0) {
+          asm volatile("" ::"v"(u[e]), "v"(v[x][e]));
+        } else {
+          const wfloatx16 c = (first && e == 0) ? wfloatx16{} : acc[x];
+          acc[x] = __builtin_amdgcn_mfma_f32_32x32x2f32(u[e], v[x][e], c, 0, 0, 0);
+        }
       }
     }
   };
@@ -890,6 +906,10 @@ __global__ __launch_bounds__(512, 2) void conv3x3_winoq_kernel(ConvH8Args a) {
       asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
     }
   };
+  if constexpr ((ABL & 4) != 0) {
+#pragma unroll
+    for (int x = 0; x < 4; ++x) acc[x] = wfloatx16{};
+  }
   issue(0, 0);
   if (kWqStages == 3 && nch > 1) issue(1, 1);
   for (int c = 0; c < nch; ++c) {
@@ -916,6 +936,10 @@ __global__ __launch_bounds__(512, 2) void conv3x3_winoq_kernel(ConvH8Args a) {
   const int y = y0 + 2 * pr + r, x = x0 + 2 * jx + cc;
   uint4* dst = a.dst_hi + (int64_t)img * a.dst_img;
   auto store4 = [&](int64_t rec, const float* vv) {
+    if constexpr ((ABL & 64) != 0) {
+      asm volatile("" ::"v"(vv[0]), "v"(vv[1]), "v"(vv[2]), "v"(vv[3]));
+      if (vv[0] != 12345.f) return;  // keeps the values live; never stores in practice
+    }
     dst[rec] = make_uint4(__float_as_uint(vv[0]), __float_as_uint(vv[1]), __float_as_uint(vv[2]), __float_as_uint(vv[3]));
   };
   // two passes (column c = 0, 1): the Q records of one column are 32 KB
@@ -1020,9 +1044,9 @@ __global__ __launch_bounds__(512, 2) void conv3x3_winoq_kernel(ConvH8Args a) {
   }
 }
 
-template <int EPI>
+template <int EPI, int ABL = 0>
 static int launch_winoq_k(const ConvH8Args& a, hipStream_t st) {
-  auto k = conv3x3_winoq_kernel<EPI>;
+  auto k = conv3x3_winoq_kernel<EPI, ABL>;
   static LdsAttr attr;
   constexpr size_t lds = (size_t)kWqStages * kWqStage * 16;
   if (int e = attr.ensure((const void*)k, (int)lds, st)) return e;
@@ -1062,6 +1086,34 @@ int launch_wino64(const ConvH8Args& a, int epi, hipStream_t st) {
   }
   return RRIN_E_ARG;
 }
+
+#ifdef RRIN_LAB
+// kernel lab (librrin_lab.so only): the LEAKY conv with ablation bits
+int launch_wino_lab(const ConvH8Args& a, int abl, hipStream_t st) {
+  switch (abl) {  // 1024 + bits: the 4-waves-per-SIMD tile (cfg 20)
+    case 1024 + 0: return launch_winoq_k<RRIN_EPI_LEAKY, 0>(a, st);
+    case 1024 + 3: return launch_winoq_k<RRIN_EPI_LEAKY, 3>(a, st);
+    case 1024 + 4: return launch_winoq_k<RRIN_EPI_LEAKY, 4>(a, st);
+    case 1024 + 8: return launch_winoq_k<RRIN_EPI_LEAKY, 8>(a, st);
+    case 1024 + 16: return launch_winoq_k<RRIN_EPI_LEAKY, 16>(a, st);
+    case 1024 + 32: return launch_winoq_k<RRIN_EPI_LEAKY, 32>(a, st);
+    case 1024 + 48: return launch_winoq_k<RRIN_EPI_LEAKY, 48>(a, st);
+    case 1024 + 56: return launch_winoq_k<RRIN_EPI_LEAKY, 56>(a, st);
+    case 1024 + 59: return launch_winoq_k<RRIN_EPI_LEAKY, 59>(a, st);
+    case 1024 + 64: return launch_winoq_k<RRIN_EPI_LEAKY, 64>(a, st);
+    case 1024 + 123: return launch_winoq_k<RRIN_EPI_LEAKY, 123>(a, st);
+    case 0: return launch_wino_k<RRIN_EPI_LEAKY, 0>(a, st);
+    case 1: return launch_wino_k<RRIN_EPI_LEAKY, 1>(a, st);
+    case 2: return launch_wino_k<RRIN_EPI_LEAKY, 2>(a, st);
+    case 3: return launch_wino_k<RRIN_EPI_LEAKY, 3>(a, st);
+    case 4: return launch_wino_k<RRIN_EPI_LEAKY, 4>(a, st);
+    case 8: return launch_wino_k<RRIN_EPI_LEAKY, 8>(a, st);
+    case 11: return launch_wino_k<RRIN_EPI_LEAKY, 11>(a, st);
+    case 15: return launch_wino_k<RRIN_EPI_LEAKY, 15>(a, st);
+  }
+  return RRIN_E_CONFIG;
+}
+#endif
 
 }  // namespace rrin
 
