@@ -112,6 +112,8 @@ def parse():
     ap.add_argument("--no-wino", action="store_true",
                     help="A/B: exact fp32 on the direct-form conv (v_mfma_f32_32x32x2_f32 per tap) instead of "
                          "Winograd F(2x2,3x3)")
+    ap.add_argument("--no-wino-th4", action="store_true",
+                    help="A/B: no TH-4 Winograd tiles on the deep convs (engine.WINO_TH4)")
     ap.add_argument("--split", default=None,
                     help="explicit pairs per stream, e.g. 1,3 (overrides --streams' even split)")
     return ap.parse_args()
@@ -250,6 +252,8 @@ def main():
 
     if args.no_wino:
         engine_mod.WINO = False
+    if args.no_wino_th4:
+        engine_mod.WINO_TH4 = {}
     net = Net()
     sd = keyed_state_dict(net.state_dict())
     net.load_state_dict(sd, strict=True)

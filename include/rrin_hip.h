@@ -209,11 +209,14 @@ int rrin_conv_h8_cfg_ok(int32_t cfg, int32_t prec); /* 1 if the config fits LDS 
  * every weight chunk resident in LDS needs them to fit) */
 int rrin_conv_h8_cfg_fits(int32_t cfg, int32_t prec, int32_t cin);
 int rrin_conv3x3_h8_fwd(const rrin_conv_h8_desc* d, void* stream);
-/* Nonzero if cfg is a Winograd F(2x2,3x3) exact-fp32 config (F32R only; its
- * weights are packed by rrin_pack_conv3x3_wino_bm with the config's BM, not
- * rrin_pack_conv3x3_r32): the tile kind, 1 = BM 32 x TH 8 on 4 waves, 2 = BM 64
- * x TH 8 on 8 waves, 3 = BM 32 x TH 8 on 8 waves of 4 accumulators (4 waves per
- * SIMD); all three give bitwise-equal outputs.  0: direct form. */
+/* Nonzero if cfg is a Winograd exact-fp32 config (F32R only, not packed by
+ * rrin_pack_conv3x3_r32): the tile kind.  F(2x2,3x3), packed by
+ * rrin_pack_conv3x3_wino_bm with the config's BM: 1 = BM 32 x TH 8 on 4 waves,
+ * 2 = BM 64 x TH 8 on 8 waves, 3 = BM 32 x TH 8 on 8 waves of 4 accumulators
+ * (4 waves per SIMD), 4 = kind 3 on TH 4 tiles (4 waves); all four give
+ * bitwise-equal outputs.  5 = F(4x4,3x3), BM 32 x TH 16 on 6 waves, packed by
+ * rrin_pack_conv3x3_wino4 (a different rounding: 36 transform points).
+ * 0: direct form. */
 int rrin_conv_h8_cfg_wino(int32_t cfg);
 
 /* F32R packing: [co_block][chunk of 8 ci][tap][half][bm][4] fp32 (half hh holds
@@ -235,6 +238,15 @@ int rrin_pack_conv3x3_wino_bm(const float* w, const float* b, int32_t cout, int3
 int64_t rrin_pack_conv3x3_wino_floats(int32_t cout, int32_t cin);
 int rrin_pack_conv3x3_wino(const float* w, const float* b, int32_t cout, int32_t cin, const int32_t* perm,
                            float* wpack, float* bpack);
+/* Winograd F(4x4,3x3) packing (kind 5): U = G g G^T, G = [1/2 0 0; 1/6 1/6 1/6;
+ * 1/6 -1/6 1/6; 16/15 8/15 4/15; 1/30 -1/15 2/15; 0 0 1/2] (interpolation points
+ * 0, 1, -1, 1/2, -2, inf with B^T scaled to integers), in double, rounded once,
+ * laid out [co_block of 32][chunk of 4 ci][xi 36][half 2][co 32][2 ci] (xi =
+ * 6*row + col; half hh holds channels chunk*4 + 2*hh, +1).  bpack:
+ * rrin_pack_bias_floats(cout, 32) floats. */
+int64_t rrin_pack_conv3x3_wino4_floats(int32_t cout, int32_t cin);
+int rrin_pack_conv3x3_wino4(const float* w, const float* b, int32_t cout, int32_t cin, const int32_t* perm,
+                            float* wpack, float* bpack);
 
 /* Host packing: [co_block][chunk of 16 ci][tap][half][bm][8] halves, weights
  * pre-scaled by a power of two so max|w| lands in [2^12, 2^13) (keeps lo

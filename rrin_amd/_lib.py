@@ -147,6 +147,9 @@ SIGNATURES = {
     "rrin_conv_h8_cfg_wino": (C.c_int, [C.c_int32]),
     "rrin_pack_conv3x3_wino_floats": (C.c_int64, [C.c_int32, C.c_int32]),
     "rrin_pack_conv3x3_wino_bm_floats": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32]),
+    "rrin_pack_conv3x3_wino4_floats": (C.c_int64, [C.c_int32, C.c_int32]),
+    "rrin_pack_conv3x3_wino4": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p,
+                                          C.c_void_p]),
     "rrin_pack_conv3x3_wino_bm": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p,
                                             C.c_void_p, C.c_void_p]),
     "rrin_pack_conv3x3_wino": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p,

@@ -224,7 +224,14 @@ int launch_wino64(const ConvH8Args& a, int epi, hipStream_t st);
 // two stages of [raw 680 | U 1024] records (three in A/B builds: two blocks per
 // CU would fill 163,584 B)
 constexpr size_t kWinoQLds = (size_t)3 * (680 + 1024) * 16;
-int launch_winoq(const ConvH8Args& a, int epi, hipStream_t st);
+// th = 8 (cfg 20: 8 waves) or 4 (cfg 21: 4 waves, the same arithmetic on half-height tiles)
+int launch_winoq(const ConvH8Args& a, int epi, int th, hipStream_t st);
+// Winograd F(4x4,3x3) (conv_wino4.hip): BM 32 x TH 16, 6 waves, 4-channel K chunks
+constexpr size_t kWino4Lds = (size_t)2 * (612 + 1152) * 16;
+int launch_wino4(const ConvH8Args& a, int epi, hipStream_t st);
+#ifdef RRIN_LAB
+int launch_wino4_lab(const ConvH8Args& a, int abl, hipStream_t st);
+#endif
 #ifdef RRIN_LAB
 int launch_wino_lab(const ConvH8Args& a, int abl, hipStream_t st);  // ablation bits (conv_wino.hip)
 #endif

@@ -1653,12 +1653,20 @@ static const CfgH8 kCfgH8[] = {
     {64, 8, kWino64Lds, (size_t)1 << 30, 0, true, 0, 0},
     // kWinoQCfg: cfg 18's tile and packing, 8 waves of 4 accumulators (conv3x3_winoq_kernel)
     {32, 8, (size_t)2 * (680 + 1024) * 16, (size_t)1 << 30, 0, true, 0, 0},
+    // kWinoQ4Cfg: the same on half-height tiles (TH 4, 4 waves): twice the tiles
+    {32, 4, (size_t)2 * (408 + 1024) * 16, (size_t)1 << 30, 0, true, 0, 0},
+    // kWino4Cfg: Winograd F(4x4,3x3), BM 32 x TH 16, 6 waves (conv_wino4.hip)
+    {32, 16, kWino4Lds, (size_t)1 << 30, 0, true, 0, 0},
 };
 static constexpr int kNumCfgH8 = sizeof(kCfgH8) / sizeof(kCfgH8[0]);
-static constexpr int kWinoCfg = kNumCfgH8 - 3;
-static constexpr int kWino64Cfg = kNumCfgH8 - 2;
-static constexpr int kWinoQCfg = kNumCfgH8 - 1;
-static inline bool is_wino(int cfg) { return cfg == kWinoCfg || cfg == kWino64Cfg || cfg == kWinoQCfg; }
+static constexpr int kWinoCfg = kNumCfgH8 - 5;
+static constexpr int kWino64Cfg = kNumCfgH8 - 4;
+static constexpr int kWinoQCfg = kNumCfgH8 - 3;
+static constexpr int kWinoQ4Cfg = kNumCfgH8 - 2;
+static constexpr int kWino4Cfg = kNumCfgH8 - 1;
+static inline bool is_wino(int cfg) {
+  return cfg == kWinoCfg || cfg == kWino64Cfg || cfg == kWinoQCfg || cfg == kWinoQ4Cfg || cfg == kWino4Cfg;
+}
 static constexpr size_t kMaxLds = 160 * 1024;
 
 static int num_cus(int dev) {
@@ -1838,7 +1846,8 @@ static int h8_prepare(const rrin_conv_h8_desc* d, ConvH8Args& a) {
   if (is_wino(d->cfg)) {
     if (d->prec != RRIN_PREC_F32R) return RRIN_E_CONFIG;
     if ((d->cin & 3) && !d->tail_finite) return RRIN_E_CONFIG;  // stages whole records only
-    a.nchunks = (d->cin + 7) / 8;  // two record groups per K chunk
+    // two record groups per K chunk; F(4x4): one
+    a.nchunks = d->cfg == kWino4Cfg ? (d->cin + 3) / 4 : (d->cin + 7) / 8;
   }
   a.n = d->n;
   if ((int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n > 0x7fffffff) return RRIN_E_SHAPE;
@@ -1862,9 +1871,16 @@ extern "C" int rrin_conv_h8_cfg_bm(int32_t cfg) {
 extern "C" int rrin_conv_h8_cfg_th(int32_t cfg) {
   return (cfg >= 0 && cfg < kNumCfgH8) ? kCfgH8[cfg].th : RRIN_E_CONFIG;
 }
-// 0: direct form; Winograd tile kind: 1 BM 32 / 4 waves, 2 BM 64 / 8 waves, 3 BM 32 / 8 waves
+// 0: direct form; Winograd tile kind: 1 BM 32 / 4 waves, 2 BM 64 / 8 waves, 3 BM 32 / 8 waves,
+// 4 BM 32 x TH 4 / 4 waves; 5 Winograd F(4x4,3x3), BM 32 x TH 16 / 6 waves (its own packing,
+// rrin_pack_conv3x3_wino4)
 extern "C" int rrin_conv_h8_cfg_wino(int32_t cfg) {
-  return cfg == kWinoCfg ? 1 : cfg == kWino64Cfg ? 2 : cfg == kWinoQCfg ? 3 : 0;
+  return cfg == kWinoCfg     ? 1
+         : cfg == kWino64Cfg ? 2
+         : cfg == kWinoQCfg  ? 3
+         : cfg == kWinoQ4Cfg ? 4
+         : cfg == kWino4Cfg  ? 5
+                             : 0;
 }
 extern "C" int rrin_conv_h8_cfg_ok(int32_t cfg, int32_t prec) {
   if (cfg < 0 || cfg >= kNumCfgH8) return 0;
@@ -1890,7 +1906,9 @@ extern "C" int rrin_conv3x3_h8_fwd(const rrin_conv_h8_desc* d, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (d->cfg == kWinoCfg) return launch_wino(a, d->epi_mode, st);
   if (d->cfg == kWino64Cfg) return launch_wino64(a, d->epi_mode, st);
-  if (d->cfg == kWinoQCfg) return launch_winoq(a, d->epi_mode, st);
+  if (d->cfg == kWinoQCfg) return launch_winoq(a, d->epi_mode, 8, st);
+  if (d->cfg == kWinoQ4Cfg) return launch_winoq(a, d->epi_mode, 4, st);
+  if (d->cfg == kWino4Cfg) return launch_wino4(a, d->epi_mode, st);
   switch (d->cfg) {
 #define X(id, nw, wm, wn, sc, pe) \
   case id:                        \
@@ -1923,7 +1941,9 @@ extern "C" int rrin_conv3x3_h8_lab(const rrin_conv_h8_desc* d, int32_t sched, in
   if (d && is_wino(d->cfg) && d->epi_mode == RRIN_EPI_LEAKY) {  // Winograd: sched = ablation bits
     ConvH8Args a;
     const int rc = h8_prepare(d, a);
-    return rc ? rc : launch_wino_lab(a, sched, (hipStream_t)stream);
+    if (rc) return rc;
+    if (d->cfg == kWino4Cfg) return launch_wino4_lab(a, sched, (hipStream_t)stream);
+    return launch_wino_lab(a, sched, (hipStream_t)stream);
   }
   if (!d || (d->prec != RRIN_PREC_F16X3 && d->prec != RRIN_PREC_F32R) || d->epi_mode != RRIN_EPI_LEAKY ||
       (d->cin % 8))

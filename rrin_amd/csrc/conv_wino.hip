@@ -759,17 +759,24 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wino64_kernel(ConvH8Args a) {
 #define RRIN_WINOQ_STAGES 2
 #endif
 constexpr int kWqStages = RRIN_WINOQ_STAGES;
-constexpr int kWqStage = kWnRaw + kWnU;  // records per stage (raw 680 + U 1024)
+constexpr int kWqStage = kWnRaw + kWnU;  // records per stage of the 8-wave tile (raw 680 + U 1024)
 static_assert(kWinoQLds >= (size_t)kWqStages * kWqStage * 16, "LDS size");
 static_assert(2 * kWinoQLds <= 160 * 1024, "two blocks per CU");
 
 // ABL (lab builds only, librrin_lab.so): 1 no U DMA after chunk 0, 2 no raw DMA
 // after chunk 0, 4 no MFMAs, 8 no transform arithmetic, 16 no window reads after
 // chunk 0 (registers reused), 32 no U reads after chunk 0, 64 no epilogue stores
-template <int EPI, int ABL = 0>
-__global__ __launch_bounds__(512, 2) void conv3x3_winoq_kernel(ConvH8Args a) {
+// PT: patch-row pairs per tile -- 2: 8 waves, TH 8 (cfg 20); 1: 4 waves, TH 4
+// (cfg 21, twice the tiles for the few-tile deep levels of small workloads).
+template <int EPI, int ABL = 0, int PT = 2>
+__global__ __launch_bounds__(256 * PT, 2) void conv3x3_winoq_kernel(ConvH8Args a) {
+  constexpr int NT = 256 * PT, TH = 4 * PT;
+  constexpr int RG = (TH + 2) * kWnRawCols, RAW = 2 * RG, STAGE = RAW + kWnU;
+  static_assert(RAW > NT && RAW <= 2 * NT && kWnU % NT == 0, "two raw pieces, whole U pieces");
+  constexpr int NS = PT == 2 ? kWqStages : 2;  // the 3-stage A/B ring is built for the 8-wave tile
+  constexpr int UP = kWnU / NT;  // U pieces per thread
   extern __shared__ __attribute__((aligned(16))) uint4 smem4[];
-  // kWqStages stages of [raw 680 | U 1024] records
+  // kWqStages stages of [raw RAW | U 1024] records
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int yw = wv & 3, pt = wv >> 2, j = lane & 31, hh = lane >> 5;
   int bid;
@@ -788,19 +795,19 @@ __global__ __launch_bounds__(512, 2) void conv3x3_winoq_kernel(ConvH8Args a) {
     t /= a.co_blocks;
     x0 = (t % a.tiles_x) * 32;
     t /= a.tiles_x;
-    y0 = (t % a.tiles_y) * 8;
+    y0 = (t % a.tiles_y) * TH;
     img = t / a.tiles_y;
   }
   const uint4* tsrc = a.src_hi + (int64_t)img * a.src_img + (int64_t)y0 * a.src_wp + x0 + (kH8PadLeft - 1);
   const uint4* wsrc = a.w_hi + (int64_t)cob * nch * kWnU + tid;
-  // staging: raw 680 records = 512 + 168, U 1024 = 2 x 512
+  // staging: raw RAW records = NT + the rest, U 1024 = UP x NT
   int64_t p_off[2];
   int p_g[2], p_zero[2];
 #pragma unroll
   for (int it = 0; it < 2; ++it) {
-    const int idx = tid + 512 * it;
-    const int g = idx >= kWnRawG ? 1 : 0;
-    const int rem = idx - g * kWnRawG;
+    const int idx = tid + NT * it;
+    const int g = idx >= RG ? 1 : 0;
+    const int rem = idx - g * RG;
     const int r = rem / kWnRawCols, pos = rem - r * kWnRawCols;
     const int col = pos < 17 ? 2 * pos : 2 * (pos - 17) + 1;
     p_g[it] = g;
@@ -808,24 +815,24 @@ __global__ __launch_bounds__(512, 2) void conv3x3_winoq_kernel(ConvH8Args a) {
     p_zero[it] = col - y0 * a.src_wp;
   }
   auto issue = [&](int c, int b) {
-    uint4* base = smem4 + b * kWqStage;
+    uint4* base = smem4 + b * STAGE;
 #pragma unroll
     for (int it = 0; it < 2; ++it) {
-      if ((it == 0 || tid < kWnRaw - 512) && !((ABL & 2) && c > 0)) {
+      if ((it == 0 || tid < RAW - NT) && !((ABL & 2) && c > 0)) {
         const int gg = 2 * c + p_g[it];
         const int64_t off = gg * 4 < a.cin ? (int64_t)(2 * c) * a.src_gp + p_off[it] : (int64_t)p_zero[it];
-        dma16(tsrc + off, base + 512 * it + (tid & ~63));
+        dma16(tsrc + off, base + NT * it + (tid & ~63));
       }
     }
 #pragma unroll
-    for (int it = 0; it < 2; ++it)
-      if (!((ABL & 1) && c > 0)) dma16(wsrc + (int64_t)c * kWnU + 512 * it, base + kWnRaw + 512 * it + (tid & ~63));
+    for (int it = 0; it < UP; ++it)
+      if (!((ABL & 1) && c > 0)) dma16(wsrc + (int64_t)c * kWnU + NT * it, base + RAW + NT * it + (tid & ~63));
   };
   const int pr = 2 * pt + (j >> 4), jx = (j + 12 * (j >> 4)) & 15;
   const int ra = yw == 0 ? 0 : (yw == 2 ? 2 : 1);
   const int rb = yw == 0 ? 2 : (yw == 1 ? 2 : (yw == 2 ? 1 : 3));
   const float sg = yw == 1 ? 1.f : -1.f;
-  const int rw0 = hh * kWnRawG + (2 * pr) * kWnRawCols;
+  const int rw0 = hh * RG + (2 * pr) * kWnRawCols;
   const int oa = ra * kWnRawCols, ob = rb * kWnRawCols;
   int pc[4];
 #pragma unroll
@@ -837,7 +844,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_winoq_kernel(ConvH8Args a) {
   // one chunk in buffer b: window reads -> B^T row -> 4 points, then per point
   // its U record and 4 MFMAs (point-major, the cfg 18 accumulation order)
   auto chunk = [&](int b, bool first) {
-    const uint4* rw = smem4 + b * kWqStage + rw0;
+    const uint4* rw = smem4 + b * STAGE + rw0;
     wfloatx4 t[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -868,7 +875,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_winoq_kernel(ConvH8Args a) {
       v[2] = t[2] - t[1];
       v[3] = t[1] - t[3];
     }
-    const uint4* su = smem4 + b * kWqStage + kWnRaw + su0;
+    const uint4* su = smem4 + b * STAGE + RAW + su0;
 #pragma unroll
     for (int x = 0; x < 4; ++x) {
       wfloatx4 u;
@@ -911,9 +918,9 @@ __global__ __launch_bounds__(512, 2) void conv3x3_winoq_kernel(ConvH8Args a) {
     for (int x = 0; x < 4; ++x) acc[x] = wfloatx16{};
   }
   issue(0, 0);
-  if (kWqStages == 3 && nch > 1) issue(1, 1);
+  if (NS == 3 && nch > 1) issue(1, 1);
   for (int c = 0; c < nch; ++c) {
-    if constexpr (kWqStages == 3) {
+    if constexpr (NS == 3) {
       wait_chunk(c + 1 < nch);
       __syncthreads();
       if (c + 2 < nch) issue(c + 2, (c + 2) % 3);
@@ -1044,18 +1051,28 @@ __global__ __launch_bounds__(512, 2) void conv3x3_winoq_kernel(ConvH8Args a) {
   }
 }
 
-template <int EPI, int ABL = 0>
+template <int EPI, int ABL = 0, int PT = 2>
 static int launch_winoq_k(const ConvH8Args& a, hipStream_t st) {
-  auto k = conv3x3_winoq_kernel<EPI, ABL>;
+  auto k = conv3x3_winoq_kernel<EPI, ABL, PT>;
   static LdsAttr attr;
-  constexpr size_t lds = (size_t)kWqStages * kWqStage * 16;
+  constexpr size_t lds = (size_t)(PT == 2 ? kWqStages : 2) * (2 * (4 * PT + 2) * kWnRawCols + kWnU) * 16;
   if (int e = attr.ensure((const void*)k, (int)lds, st)) return e;
   const int64_t grid = (int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n;
-  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(512), lds, st, a);
+  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256 * PT), lds, st, a);
   return hip_code(hipGetLastError());
 }
 
-int launch_winoq(const ConvH8Args& a, int epi, hipStream_t st) {
+int launch_winoq(const ConvH8Args& a, int epi, int th, hipStream_t st) {
+  if (th == 4) {
+    switch (epi) {
+      case RRIN_EPI_LINEAR: return launch_winoq_k<RRIN_EPI_LINEAR, 0, 1>(a, st);
+      case RRIN_EPI_LEAKY: return launch_winoq_k<RRIN_EPI_LEAKY, 0, 1>(a, st);
+      case RRIN_EPI_LEAKY_POOL: return launch_winoq_k<RRIN_EPI_LEAKY_POOL, 0, 1>(a, st);
+      case RRIN_EPI_LEAKY_REP: return launch_winoq_k<RRIN_EPI_LEAKY_REP, 0, 1>(a, st);
+      case RRIN_EPI_SUBPIXEL: return launch_winoq_k<RRIN_EPI_SUBPIXEL, 0, 1>(a, st);
+    }
+    return RRIN_E_ARG;
+  }
   switch (epi) {
     case RRIN_EPI_LINEAR: return launch_winoq_k<RRIN_EPI_LINEAR>(a, st);
     case RRIN_EPI_LEAKY: return launch_winoq_k<RRIN_EPI_LEAKY>(a, st);

@@ -172,11 +172,24 @@ WINO_DIRECT = {(6, 32, 0): 13}
 # (4 waves of 8 accumulators) on every conv shape of the Net, bitwise equal
 # (profiles/r03/cfgab_18_20.txt)
 WINO_KIND = 3
+# ... and kind 4 (the same arithmetic on TH 4 tiles of 4 waves: twice the
+# workgroups) on the few-tile deep convs where that wins, (cin, cout rows, grid
+# level) per size class as in WINO_DIRECT (a sub-pixel up conv: 4 x cout, the
+# low-res grid).  cfg 20 vs 21 on every conv shape of the Net
+# (profiles/r03/cfgab_20_21_*.txt): 0.71-0.72 at level 4 and 0.84 for the level-2
+# up conv at 640x368 x 1; 0.90-0.97 on the level-4 grid at 1280x720 x 2; 1.00-1.10
+# on the rest (more tiles than CUs already: the 8-wave tile's shared U stage wins).
+# Whole forward (profiles/r03/bench_th4_ab.txt): 640x368 x 1 +2.8 %, 1280x720 x 1
+# +0.8 %; 1280x720 x 4 on two streams (class "large") -0.2 %, noise -- the other
+# stream already fills the CUs there, so that class keeps the 8-wave tile.
+WINO_TH4 = {"small": {(256, 512, 4), (512, 512, 4), (256, 512, 3)},
+            "medium": {(256, 512, 4), (512, 512, 4), (512, 1024, 4)}}
 
 
-def wino_cfg() -> int:
+def wino_cfg(kind: int = None) -> int:
     lib = _lib.lib()
-    return next(c for c in range(lib.rrin_conv_h8_cfg_count()) if lib.rrin_conv_h8_cfg_wino(c) == WINO_KIND)
+    kind = WINO_KIND if kind is None else kind
+    return next(c for c in range(lib.rrin_conv_h8_cfg_count()) if lib.rrin_conv_h8_cfg_wino(c) == kind)
 
 
 def choose_cfg_h8(cin: int, cout: int, prec: int, level: int = 0, size: str = "large") -> int:
@@ -190,7 +203,7 @@ def choose_cfg_h8(cin: int, cout: int, prec: int, level: int = 0, size: str = "l
         c = WINO_DIRECT.get((cin, cout, level))
         if c is not None and _lib.lib().rrin_conv_h8_cfg_fits(c, prec, cin):
             return c
-        return wino_cfg()
+        return wino_cfg(4 if (cin, cout, level) in WINO_TH4.get(size, ()) else None)
     table = H8_TUNED_BY_SIZE.get(size, {}).get(prec) or H8_TUNED.get(prec, {})
     cfg = table.get((cin, cout, level))
     if cfg is not None and _lib.lib().rrin_conv_h8_cfg_fits(cfg, prec, cin):
@@ -374,7 +387,11 @@ class RRINEngine:
             if f32:  # fp32 records: unscaled fp32 weights (offsets in floats)
                 bp = np.empty(L.rrin_pack_bias_floats(cout, bm), np.float32)
                 pa = perm_arr.ctypes.data if perm_arr is not None else None
-                if L.rrin_conv_h8_cfg_wino(cfg):  # Winograd F(2x2,3x3): transformed weights
+                if L.rrin_conv_h8_cfg_wino(cfg) == 5:  # Winograd F(4x4,3x3): 36-point transformed weights
+                    wp = np.empty(L.rrin_pack_conv3x3_wino4_floats(cout, cin), np.float32)
+                    _lib.check(L.rrin_pack_conv3x3_wino4(w.ctypes.data, b.ctypes.data, cout, cin, pa,
+                                                         wp.ctypes.data, bp.ctypes.data), "rrin_pack_conv3x3_wino4")
+                elif L.rrin_conv_h8_cfg_wino(cfg):  # Winograd F(2x2,3x3): transformed weights
                     wp = np.empty(L.rrin_pack_conv3x3_wino_bm_floats(cout, cin, bm), np.float32)
                     _lib.check(L.rrin_pack_conv3x3_wino_bm(w.ctypes.data, b.ctypes.data, cout, cin, bm, pa,
                                                            wp.ctypes.data, bp.ctypes.data), "rrin_pack_conv3x3_wino_bm")

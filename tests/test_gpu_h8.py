@@ -2,7 +2,9 @@
 (R32, the default "fp32" precision), split-fp16 (fp32_split16) and fp16.
 
 R32 is exact fp32 arithmetic (fp32 storage, v_mfma_f32_32x32x2_f32 products,
-fp32 accumulation): held to 1e-5 against float64.
+fp32 accumulation): held to 1e-5 against float64; the Winograd F(4x4,3x3)
+config (tile kind 5) to 5e-5 -- its 6x6 transforms carry about 6x the rounding
+error of F(2x2) (still every operation an IEEE fp32 operation).
 
 fp32_split16 holds each fp32 value as fp16 hi+lo and forms each product from
 three exact fp16 products with fp32 accumulation (error ~2^-21 relative per
@@ -26,6 +28,12 @@ pytestmark = pytest.mark.gpu
 X3, F16, R32 = _lib.PREC_F16X3, _lib.PREC_F16, _lib.PREC_F32R
 PRECS = [R32, X3, F16]
 TOL = {X3: dict(rtol=1e-4, atol=1e-4), F16: dict(rtol=2e-2, atol=2e-2), R32: dict(rtol=1e-5, atol=1e-5)}
+TOL_W4 = dict(rtol=5e-5, atol=5e-5)
+
+
+def tol(prec, cfg):
+    """Tolerance of config cfg at prec (the F(4x4) Winograd tile: TOL_W4)."""
+    return TOL_W4 if prec == R32 and _lib.lib().rrin_conv_h8_cfg_wino(cfg) == 5 else TOL[prec]
 
 
 def ref_conv(x, w, b, slope=None):
@@ -44,7 +52,7 @@ NO_POOL_CFGS = (4, 16)
 
 
 def wino_cfgs():
-    """Ids of the Winograd F(2x2,3x3) exact-fp32 configs (R32 only)."""
+    """Ids of the Winograd exact-fp32 configs (R32 only): F(2x2,3x3) kinds 1-4, F(4x4,3x3) kind 5."""
     lib = _lib.lib()
     return tuple(c for c in range(lib.rrin_conv_h8_cfg_count()) if lib.rrin_conv_h8_cfg_wino(c))
 
@@ -64,6 +72,14 @@ def pack_h8(w, b, cfg, prec, dev, perm=None):
     cout, cin = w.shape[:2]
     bm = lib.rrin_conv_h8_cfg_bm(cfg)
     pa = np.asarray(perm, np.int32) if perm is not None else None
+    if prec == R32 and lib.rrin_conv_h8_cfg_wino(cfg) == 5:  # Winograd F(4x4): 36 points
+        wp = np.zeros(lib.rrin_pack_conv3x3_wino4_floats(cout, cin), np.float32)
+        bp = np.zeros(lib.rrin_pack_bias_floats(cout, 32), np.float32)
+        _lib.check(lib.rrin_pack_conv3x3_wino4(w.ctypes.data, b.ctypes.data, cout, cin,
+                                               pa.ctypes.data if pa is not None else None, wp.ctypes.data,
+                                               bp.ctypes.data))
+        wt = torch.from_numpy(wp).to(dev)
+        return wt, wt, torch.from_numpy(bp).to(dev), 1.0
     if prec == R32 and lib.rrin_conv_h8_cfg_wino(cfg):  # Winograd: U = G g G^T per point
         wp = np.zeros(lib.rrin_pack_conv3x3_wino_bm_floats(cout, cin, bm), np.float32)
         bp = np.zeros(lib.rrin_pack_bias_floats(cout, bm), np.float32)
@@ -137,7 +153,7 @@ def test_h8_conv_golden(gpu, golden, prec, cin, cout):
     x = torch.from_numpy(g[f"conv_{cin}_{cout}_in"]).to(gpu)
     for cfg in cfgs(prec, cout, cin):
         dst, _ = conv_h8(H8Tensor.from_nchw(x, prec), w, b, cfg, prec)
-        np.testing.assert_allclose(dst.to_nchw().cpu().numpy(), g[f"conv_{cin}_{cout}_out"], **TOL[prec],
+        np.testing.assert_allclose(dst.to_nchw().cpu().numpy(), g[f"conv_{cin}_{cout}_out"], **tol(prec, cfg),
                                    err_msg=f"cfg {cfg}")
 
 
@@ -154,9 +170,9 @@ def test_h8_conv_pool(gpu, prec, n, cin, cout, h, w):
             continue  # WN == 1: no pool epilogue (rejected with RRIN_E_CONFIG, see test below)
         dst, pool = conv_h8(H8Tensor.from_nchw(x, prec), wt, b, cfg, prec, epi=_lib.EPI_LEAKY_POOL, dst_off=cout,
                             dst=H8Tensor(n, 2 * cout, h, w, gpu, prec))
-        np.testing.assert_allclose(dst.to_nchw(cout, cout).cpu().double().numpy(), ref.numpy(), **TOL[prec])
+        np.testing.assert_allclose(dst.to_nchw(cout, cout).cpu().double().numpy(), ref.numpy(), **tol(prec, cfg))
         assert not dst.to_nchw(0, cout).any()
-        np.testing.assert_allclose(pool.to_nchw().cpu().double().numpy(), refp.numpy(), **TOL[prec],
+        np.testing.assert_allclose(pool.to_nchw().cpu().double().numpy(), refp.numpy(), **tol(prec, cfg),
                                    err_msg=f"cfg {cfg}")
 
 
@@ -203,7 +219,7 @@ def test_h8_conv_dma_finite_tail(gpu, prec, cin):
     ref = ref_conv(x[:, :cin], wt, b)
     for cfg in (1, 6) + (wino_cfgs() if prec == R32 else ()):
         dst, _ = conv_h8(H8Tensor.from_nchw(x, prec), wt, b, cfg, prec, cin=cin, tail_finite=1)
-        np.testing.assert_allclose(dst.to_nchw().cpu().double().numpy(), ref.numpy(), **TOL[prec])
+        np.testing.assert_allclose(dst.to_nchw().cpu().double().numpy(), ref.numpy(), **tol(prec, cfg))
 
 
 @pytest.mark.parametrize("prec", PRECS)
@@ -243,7 +259,7 @@ def test_h8_leaky_rep_writes_replicated_ring(gpu, prec):
     ref = ref_conv(x, wt, b, 0.1)
     for cfg in (0, 6) + (wino_cfgs() if prec == R32 else ()):
         dst, _ = conv_h8(H8Tensor.from_nchw(x, prec), wt, b, cfg, prec, epi=_lib.EPI_LEAKY_REP)
-        np.testing.assert_allclose(dst.to_nchw().cpu().double().numpy(), ref.numpy(), **TOL[prec])
+        np.testing.assert_allclose(dst.to_nchw().cpu().double().numpy(), ref.numpy(), **tol(prec, cfg))
         # the ring must equal the replicated border; everything else in the padding stays zero
         want = SimpleNamespace(h=dst.h, w=dst.w, hi=dst.hi.clone(), lo=dst.lo.clone() if dst.lo is not None else None)
         for a in (want.hi, want.lo):
@@ -306,7 +322,7 @@ def test_h8_subpixel_upconv(gpu, prec, n, cin, cout, sh, sw):
     replicate_ring(src)
     for cfg in cfgs(prec, 4 * cout, cin):
         dst = subpixel_upconv(src, wt, b, cfg, prec, dst=H8Tensor(n, 2 * cout, 2 * sh, 2 * sw, gpu, prec))
-        np.testing.assert_allclose(dst.to_nchw(0, cout).cpu().double().numpy(), ref.numpy(), **TOL[prec],
+        np.testing.assert_allclose(dst.to_nchw(0, cout).cpu().double().numpy(), ref.numpy(), **tol(prec, cfg),
                                    err_msg=f"cfg {cfg}")
         assert not dst.to_nchw(cout, cout).any()           # the bridge half of CAT is untouched
         assert not dst.hi[:, :, 0].any() and not dst.hi[:, :, :, :8].any()  # zero padding kept
@@ -327,10 +343,10 @@ def test_h8_conv_many_tiles_per_block(gpu, prec, cin, epi):
         if epi == _lib.EPI_LEAKY_POOL and cfg in NO_POOL_CFGS:
             continue
         dst, pool = conv_h8(H8Tensor.from_nchw(x, prec), wt, b, cfg, prec, epi=epi)
-        np.testing.assert_allclose(dst.to_nchw().cpu().double().numpy(), ref.numpy(), **TOL[prec],
+        np.testing.assert_allclose(dst.to_nchw().cpu().double().numpy(), ref.numpy(), **tol(prec, cfg),
                                    err_msg=f"cfg {cfg}")
         if pool is not None:
-            np.testing.assert_allclose(pool.to_nchw().cpu().double().numpy(), refp.numpy(), **TOL[prec],
+            np.testing.assert_allclose(pool.to_nchw().cpu().double().numpy(), refp.numpy(), **tol(prec, cfg),
                                        err_msg=f"cfg {cfg} pool")
 
 
@@ -347,7 +363,7 @@ def test_h8_subpixel_many_tiles_per_block(gpu, prec):
     replicate_ring(src)
     for cfg in cfgs(prec, 4 * cout, cin):
         dst = subpixel_upconv(src, wt, b, cfg, prec, dst=H8Tensor(n, 2 * cout, 2 * sh, 2 * sw, gpu, prec))
-        np.testing.assert_allclose(dst.to_nchw(0, cout).cpu().double().numpy(), ref.numpy(), **TOL[prec],
+        np.testing.assert_allclose(dst.to_nchw(0, cout).cpu().double().numpy(), ref.numpy(), **tol(prec, cfg),
                                    err_msg=f"cfg {cfg}")
 
 
