@@ -29,7 +29,7 @@
 // (one record group): lanes 0-31 carry channels 0-1 of the record, lanes 32-63
 // channels 2-3 (8-byte LDS reads), 2 MFMAs per point.  Per chunk, double
 // buffered in LDS (LDS-DMA, one chunk ahead): the raw tile (18 rows x 34 cols,
-// even columns first) and U [xi][half][co][2]; 55 KB per block, so two blocks
+// columns by phase col % 4) and U [xi][half][co][2]; 55 KB per block, so two blocks
 // share a CU (12 waves, 3 per SIMD).  The output transform meets through LDS
 // in two column passes.
 #include <type_traits>
@@ -58,7 +58,11 @@ static_assert(kW4Raw > kW4NT && kW4Raw <= 2 * kW4NT && kW4U % kW4NT == 0, "stagi
 constexpr float kBT4[6][6] = {{2, -3, -4, 3, 2, 0},  {0, -2, 1, 5, 2, 0},  {0, -2, 5, -1, -2, 0},
                               {0, 2, 1, -2, -1, 0}, {0, 1, -2, -1, 2, 0}, {0, 2, -3, -4, 3, 2}};
 
-__device__ inline int w4_col(int col) { return (col & 1) * 17 + (col >> 1); }
+// LDS position of raw column col (0..33) within its row: four phases by col % 4
+// (9, 9, 8, 8 columns), so the 8 patches of a row (columns 4 pc + k) read
+// consecutive records and, with the 34-record row stride, the tile's 32 patches
+// cover every LDS bank once per read
+__device__ inline int w4_col(int col) { return (col & 3) * 9 - ((col & 3) == 3 ? 1 : 0) + (col >> 2); }
 
 // A^T rows applied to six values (Q = M A or Y = A^T Q), fixed order
 __device__ inline w4x4 w4_at(int r, const w4x4* m) {
@@ -106,7 +110,7 @@ __global__ __launch_bounds__(kW4NT) __attribute__((amdgpu_waves_per_eu(3))) void
   for (int it = 0; it < 2; ++it) {
     const int idx = tid + kW4NT * it;
     const int r = idx / kW4Cols, pos = idx - r * kW4Cols;
-    const int col = pos < 17 ? 2 * pos : 2 * (pos - 17) + 1;
+    const int col = pos < 9 ? 4 * pos : pos < 18 ? 4 * (pos - 9) + 1 : pos < 26 ? 4 * (pos - 18) + 2 : 4 * (pos - 26) + 3;
     p_off[it] = (int64_t)r * a.src_wp + col;
   }
   auto issue = [&](int c, int b) {
