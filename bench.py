@@ -112,6 +112,9 @@ def parse():
     ap.add_argument("--no-wino", action="store_true",
                     help="A/B: exact fp32 on the direct-form conv (v_mfma_f32_32x32x2_f32 per tap) instead of "
                          "Winograd F(2x2,3x3)")
+    ap.add_argument("--wino-kind", type=int, default=None,
+                    help="A/B: Winograd tile kind of the exact-fp32 body convs (rrin_conv_h8_cfg_wino; "
+                         "default engine.WINO_KIND)")
     ap.add_argument("--no-wino-th4", action="store_true",
                     help="A/B: no TH-4 Winograd tiles on the deep convs (engine.WINO_TH4)")
     ap.add_argument("--split", default=None,
@@ -252,6 +255,8 @@ def main():
 
     if args.no_wino:
         engine_mod.WINO = False
+    if args.wino_kind is not None:
+        engine_mod.WINO_KIND = args.wino_kind
     if args.no_wino_th4:
         engine_mod.WINO_TH4 = {}
     net = Net()

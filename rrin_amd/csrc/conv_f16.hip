@@ -1657,15 +1657,19 @@ static const CfgH8 kCfgH8[] = {
     {32, 4, (size_t)2 * (408 + 1024) * 16, (size_t)1 << 30, 0, true, 0, 0},
     // kWino4Cfg: Winograd F(4x4,3x3), BM 32 x TH 16, 6 waves (conv_wino4.hip)
     {32, 16, kWino4Lds, (size_t)1 << 30, 0, true, 0, 0},
+    // kWinoPCfg: cfg 20's tile and packing with the ping-pong main loop (conv3x3_winoq_kernel<.., PP>)
+    {32, 8, (size_t)2 * (680 + 1024) * 16, (size_t)1 << 30, 0, true, 0, 0},
 };
 static constexpr int kNumCfgH8 = sizeof(kCfgH8) / sizeof(kCfgH8[0]);
-static constexpr int kWinoCfg = kNumCfgH8 - 5;
-static constexpr int kWino64Cfg = kNumCfgH8 - 4;
-static constexpr int kWinoQCfg = kNumCfgH8 - 3;
-static constexpr int kWinoQ4Cfg = kNumCfgH8 - 2;
-static constexpr int kWino4Cfg = kNumCfgH8 - 1;
+static constexpr int kWinoCfg = kNumCfgH8 - 6;
+static constexpr int kWino64Cfg = kNumCfgH8 - 5;
+static constexpr int kWinoQCfg = kNumCfgH8 - 4;
+static constexpr int kWinoQ4Cfg = kNumCfgH8 - 3;
+static constexpr int kWino4Cfg = kNumCfgH8 - 2;
+static constexpr int kWinoPCfg = kNumCfgH8 - 1;
 static inline bool is_wino(int cfg) {
-  return cfg == kWinoCfg || cfg == kWino64Cfg || cfg == kWinoQCfg || cfg == kWinoQ4Cfg || cfg == kWino4Cfg;
+  return cfg == kWinoCfg || cfg == kWino64Cfg || cfg == kWinoQCfg || cfg == kWinoQ4Cfg || cfg == kWino4Cfg ||
+         cfg == kWinoPCfg;
 }
 static constexpr size_t kMaxLds = 160 * 1024;
 
@@ -1873,13 +1877,14 @@ extern "C" int rrin_conv_h8_cfg_th(int32_t cfg) {
 }
 // 0: direct form; Winograd tile kind: 1 BM 32 / 4 waves, 2 BM 64 / 8 waves, 3 BM 32 / 8 waves,
 // 4 BM 32 x TH 4 / 4 waves; 5 Winograd F(4x4,3x3), BM 32 x TH 16 / 6 waves (its own packing,
-// rrin_pack_conv3x3_wino4)
+// rrin_pack_conv3x3_wino4); 6 kind 3's tile with the ping-pong main loop
 extern "C" int rrin_conv_h8_cfg_wino(int32_t cfg) {
   return cfg == kWinoCfg     ? 1
          : cfg == kWino64Cfg ? 2
          : cfg == kWinoQCfg  ? 3
          : cfg == kWinoQ4Cfg ? 4
          : cfg == kWino4Cfg  ? 5
+         : cfg == kWinoPCfg  ? 6
                              : 0;
 }
 extern "C" int rrin_conv_h8_cfg_ok(int32_t cfg, int32_t prec) {
@@ -1909,6 +1914,7 @@ extern "C" int rrin_conv3x3_h8_fwd(const rrin_conv_h8_desc* d, void* stream) {
   if (d->cfg == kWinoQCfg) return launch_winoq(a, d->epi_mode, 8, st);
   if (d->cfg == kWinoQ4Cfg) return launch_winoq(a, d->epi_mode, 4, st);
   if (d->cfg == kWino4Cfg) return launch_wino4(a, d->epi_mode, st);
+  if (d->cfg == kWinoPCfg) return launch_winop(a, d->epi_mode, st);
   switch (d->cfg) {
 #define X(id, nw, wm, wn, sc, pe) \
   case id:                        \

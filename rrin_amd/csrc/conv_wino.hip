@@ -768,8 +768,25 @@ static_assert(2 * kWinoQLds <= 160 * 1024, "two blocks per CU");
 // chunk 0 (registers reused), 32 no U reads after chunk 0, 64 no epilogue stores
 // PT: patch-row pairs per tile -- 2: 8 waves, TH 8 (cfg 20); 1: 4 waves, TH 4
 // (cfg 21, twice the tiles for the few-tile deep levels of small workloads).
-template <int EPI, int ABL = 0, int PT = 2>
-__global__ __launch_bounds__(256 * PT, 2) void conv3x3_winoq_kernel(ConvH8Args a) {
+//
+// PP (cfg 23, kind 6; PT 2 only): ping-pong main loop.  The two patch-row halves
+// of the block (waves 0-3: pt 0 = group A, waves 4-7: pt 1 = group B; wave w and
+// w + 4 share a SIMD) alternate between a matrix segment (the chunk's 16 MFMAs
+// from operands already in registers) and a memory segment (LDS-DMA issue,
+// window reads, B^T transform of the next chunk), one s_barrier per segment, so
+// each SIMD always has one wave of the block feeding its matrix pipe while its
+// partner stages -- instead of all eight waves reading and transforming after
+// each barrier and then all issuing MFMAs.  Chunk c is read by A in segment 2c
+// and by B in segment 2c + 1; its stage (c & 1) then takes chunk c + 2: the raw
+// tile issued by A in segment 2c + 2 (its memory segment), the U slab by B in
+// segment 2c + 3; both land before the barrier that ends segment 2c + 3.  The
+// barriers are bare s_barrier (no vmcnt(0) drain of __syncthreads): each wave
+// waits only for what the next segment needs.  Same products in the same order
+// per accumulator as cfg 20: bitwise equal outputs.
+template <int EPI, int ABL = 0, int PT = 2, int PP = 0>
+__global__ __launch_bounds__(256 * PT, 2) __attribute__((amdgpu_waves_per_eu(4)))
+void conv3x3_winoq_kernel(ConvH8Args a) {
+  static_assert(!PP || PT == 2, "ping-pong needs the two patch-row halves");
   constexpr int NT = 256 * PT, TH = 4 * PT;
   constexpr int RG = (TH + 2) * kWnRawCols, RAW = 2 * RG, STAGE = RAW + kWnU;
   static_assert(RAW > NT && RAW <= 2 * NT && kWnU % NT == 0, "two raw pieces, whole U pieces");
@@ -913,10 +930,114 @@ __global__ __launch_bounds__(256 * PT, 2) void conv3x3_winoq_kernel(ConvH8Args a
       asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
     }
   };
-  if constexpr ((ABL & 4) != 0) {
+  if constexpr ((ABL & 4) != 0 || PP) {
 #pragma unroll
     for (int x = 0; x < 4; ++x) acc[x] = wfloatx16{};
   }
+  if constexpr (PP) {
+    const bool grp_b = __builtin_amdgcn_readfirstlane(wv) >= 4;
+    const int gt = tid & 255;
+    // group-local staging (256 threads): raw tile 680 = 256 + 256 + 168 records, U 1024 = 4 x 256
+    int64_t q_off[3];
+    int q_zero[3], q_g[3];
+#pragma unroll
+    for (int it = 0; it < 3; ++it) {
+      const int idx = gt + 256 * it;
+      const int g = idx >= RG ? 1 : 0;
+      const int rem = idx - g * RG;
+      const int r = rem / kWnRawCols, pos = rem - r * kWnRawCols;
+      const int col = pos < 17 ? 2 * pos : 2 * (pos - 17) + 1;
+      q_g[it] = g;
+      q_off[it] = (int64_t)g * a.src_gp + r * a.src_wp + col;
+      q_zero[it] = col - y0 * a.src_wp;
+    }
+    auto issue_raw_g = [&](int c, int b) {
+      uint4* base = smem4 + b * STAGE;
+#pragma unroll
+      for (int it = 0; it < 3; ++it) {
+        if (it < 2 || gt < RAW - 512) {
+          const int gg = 2 * c + q_g[it];
+          const int64_t off = gg * 4 < a.cin ? (int64_t)(2 * c) * a.src_gp + q_off[it] : (int64_t)q_zero[it];
+          dma16(tsrc + off, base + 256 * it + (gt & ~63));
+        }
+      }
+    };
+    const uint4* wsrc_g = a.w_hi + (int64_t)cob * nch * kWnU + gt;
+    auto issue_u_g = [&](int c, int b) {
+      uint4* base = smem4 + b * STAGE + RAW;
+#pragma unroll
+      for (int it = 0; it < 4; ++it) dma16(wsrc_g + (int64_t)c * kWnU + 256 * it, base + 256 * it + (gt & ~63));
+    };
+    // memory segment: window reads + B^T row of the chunk in stage b -> v
+    wfloatx4 v[4];
+    auto prep = [&](int b) {
+      const uint4* rw = smem4 + b * STAGE + rw0;
+      wfloatx4 t[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const wfloatx4 d0 = __builtin_bit_cast(wfloatx4, rw[oa + pc[k]]);
+        const wfloatx4 d1 = __builtin_bit_cast(wfloatx4, rw[ob + pc[k]]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) t[k][e] = fmaf(sg, d1[e], d0[e]);
+      }
+      v[0] = t[0] - t[2];
+      v[1] = t[1] + t[2];
+      v[2] = t[2] - t[1];
+      v[3] = t[1] - t[3];
+      // the transform belongs to this segment: keep it ahead of the segment's barrier
+#pragma unroll
+      for (int x = 0; x < 4; ++x) asm volatile("" : "+v"(v[x]));
+    };
+    // matrix segment: the U records of the chunk in stage b, then its 16 MFMAs
+    // (product e of the four points in turn: each accumulator still takes e = 0..3 in order)
+    auto mma = [&](int b) {
+      const uint4* su = smem4 + b * STAGE + RAW + su0;
+      wfloatx4 u[4];
+#pragma unroll
+      for (int x = 0; x < 4; ++x) u[x] = __builtin_bit_cast(wfloatx4, su[x * 64]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int x = 0; x < 4; ++x) acc[x] = __builtin_amdgcn_mfma_f32_32x32x2f32(u[x][e], v[x][e], acc[x], 0, 0, 0);
+    };
+    // segment boundary: nothing (MFMAs included) crosses it
+    auto seg_end = [&](bool drain_dma) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (drain_dma)
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    // prologue: chunks 0 and 1 staged by all eight waves.  Then every wave runs the
+    // same loop, {memory segment of chunk k; matrix segment of chunk k}, group B one
+    // segment behind group A (B's extra barrier up front, A's at the end), so A's
+    // matrix segments meet B's memory segments and the other way round.  In its
+    // memory segment of chunk k >= 1 a wave first stages its share of chunk k + 1
+    // (A the raw tile, B the U slab) into stage (k + 1) & 1, whose last reader (B's
+    // matrix segment of chunk k - 1) has passed the previous barrier.  Chunk k + 1
+    // is complete at the barrier that ends B's memory segment of chunk k (= A's
+    // matrix segment): both drain their DMA there.
+    issue(0, 0);
+    if (nch > 1) issue(1, 1);
+    seg_end(true);
+    if (grp_b) seg_end(false);
+#pragma clang loop unroll(disable)
+    for (int k = 0; k < nch; ++k) {
+      const int b = k & 1;
+      if (k >= 1 && k + 1 < nch) {
+        if (grp_b)
+          issue_u_g(k + 1, b ^ 1);
+        else
+          issue_raw_g(k + 1, b ^ 1);
+      }
+      prep(b);
+      seg_end(grp_b);
+      mma(b);
+      seg_end(true);
+    }
+    if (!grp_b) seg_end(false);
+  } else {
   issue(0, 0);
   if (NS == 3 && nch > 1) issue(1, 1);
   for (int c = 0; c < nch; ++c) {
@@ -931,6 +1052,7 @@ __global__ __launch_bounds__(256 * PT, 2) void conv3x3_winoq_kernel(ConvH8Args a
       if (c + 1 < nch) issue(c + 1, (c + 1) & 1);
       chunk(c & 1, c == 0);
     }
+  }
   }
   __syncthreads();  // every read done before the exchange reuses the LDS
 
@@ -1051,9 +1173,9 @@ __global__ __launch_bounds__(256 * PT, 2) void conv3x3_winoq_kernel(ConvH8Args a
   }
 }
 
-template <int EPI, int ABL = 0, int PT = 2>
+template <int EPI, int ABL = 0, int PT = 2, int PP = 0>
 static int launch_winoq_k(const ConvH8Args& a, hipStream_t st) {
-  auto k = conv3x3_winoq_kernel<EPI, ABL, PT>;
+  auto k = conv3x3_winoq_kernel<EPI, ABL, PT, PP>;
   static LdsAttr attr;
   constexpr size_t lds = (size_t)(PT == 2 ? kWqStages : 2) * (2 * (4 * PT + 2) * kWnRawCols + kWnU) * 16;
   if (int e = attr.ensure((const void*)k, (int)lds, st)) return e;
@@ -1079,6 +1201,17 @@ int launch_winoq(const ConvH8Args& a, int epi, int th, hipStream_t st) {
     case RRIN_EPI_LEAKY_POOL: return launch_winoq_k<RRIN_EPI_LEAKY_POOL>(a, st);
     case RRIN_EPI_LEAKY_REP: return launch_winoq_k<RRIN_EPI_LEAKY_REP>(a, st);
     case RRIN_EPI_SUBPIXEL: return launch_winoq_k<RRIN_EPI_SUBPIXEL>(a, st);
+  }
+  return RRIN_E_ARG;
+}
+
+int launch_winop(const ConvH8Args& a, int epi, hipStream_t st) {
+  switch (epi) {
+    case RRIN_EPI_LINEAR: return launch_winoq_k<RRIN_EPI_LINEAR, 0, 2, 1>(a, st);
+    case RRIN_EPI_LEAKY: return launch_winoq_k<RRIN_EPI_LEAKY, 0, 2, 1>(a, st);
+    case RRIN_EPI_LEAKY_POOL: return launch_winoq_k<RRIN_EPI_LEAKY_POOL, 0, 2, 1>(a, st);
+    case RRIN_EPI_LEAKY_REP: return launch_winoq_k<RRIN_EPI_LEAKY_REP, 0, 2, 1>(a, st);
+    case RRIN_EPI_SUBPIXEL: return launch_winoq_k<RRIN_EPI_SUBPIXEL, 0, 2, 1>(a, st);
   }
   return RRIN_E_ARG;
 }

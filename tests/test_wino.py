@@ -88,10 +88,11 @@ def test_wino_config_entry():
     lib = _lib.lib()
     ids = [c for c in range(lib.rrin_conv_h8_cfg_count()) if lib.rrin_conv_h8_cfg_wino(c)]
     # kinds 1 (BM 32, 4 waves), 2 (BM 64, 8 waves), 3 (BM 32, 8 waves of 4 accumulators), TH 8;
-    # 4 (kind 3's arithmetic on TH 4 tiles, 4 waves); 5 F(4x4,3x3) on TH 16 tiles
-    assert sorted(lib.rrin_conv_h8_cfg_wino(c) for c in ids) == [1, 2, 3, 4, 5]
+    # 4 (kind 3's arithmetic on TH 4 tiles, 4 waves); 5 F(4x4,3x3) on TH 16 tiles; 6 kind 3's tile
+    # with the ping-pong main loop
+    assert sorted(lib.rrin_conv_h8_cfg_wino(c) for c in ids) == [1, 2, 3, 4, 5, 6]
     assert {lib.rrin_conv_h8_cfg_wino(c): lib.rrin_conv_h8_cfg_bm(c) for c in ids} == {1: 32, 2: 64, 3: 32, 4: 32,
-                                                                                        5: 32}
+                                                                                        5: 32, 6: 32}
     for c in ids:
         assert lib.rrin_conv_h8_cfg_th(c) == {4: 4, 5: 16}.get(lib.rrin_conv_h8_cfg_wino(c), 8)
         assert lib.rrin_conv_h8_cfg_ok(c, _lib.PREC_F32R) == 1
