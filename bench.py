@@ -115,6 +115,9 @@ def parse():
     ap.add_argument("--wino-kind", type=int, default=None,
                     help="A/B: Winograd tile kind of the exact-fp32 body convs (rrin_conv_h8_cfg_wino; "
                          "default engine.WINO_KIND)")
+    ap.add_argument("--wino-split", default=None,
+                    help="A/B: split-K slices per grid level for every Winograd conv, e.g. '2:2,3:4,4:8' "
+                         "(engine.WINO_SPLIT_LEVELS); 'none' disables the tuned splits")
     ap.add_argument("--no-wino-th4", action="store_true",
                     help="A/B: no TH-4 Winograd tiles on the deep convs (engine.WINO_TH4)")
     ap.add_argument("--split", default=None,
@@ -257,6 +260,11 @@ def main():
         engine_mod.WINO = False
     if args.wino_kind is not None:
         engine_mod.WINO_KIND = args.wino_kind
+    if args.wino_split == "none":
+        engine_mod.WINO_SPLIT = {}
+    elif args.wino_split:
+        engine_mod.WINO_SPLIT_LEVELS.update({int(k): int(v) for k, v in
+                                             (kv.split(":") for kv in args.wino_split.split(","))})
     if args.no_wino_th4:
         engine_mod.WINO_TH4 = {}
     net = Net()

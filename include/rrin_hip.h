@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define RRIN_ABI_VERSION 9
+#define RRIN_ABI_VERSION 10
 
 #define RRIN_OK 0
 #define RRIN_E_SHAPE (-1)     /* H or W not a multiple of 16, or N < 1          */
@@ -199,6 +199,16 @@ typedef struct rrin_conv_h8_desc {
   float* edge;                 /* EPI_SUBPIXEL: [n][cout/4][rrin_ring_pixels(H,W)] fp32 */
   int32_t* status;             /* optional (F16X3 / F16): set to 1 when a stored value does not
                                   fit fp16 (|v| > 65504, inf or NaN) -- see rrin_net_desc.status */
+  int32_t ksplit;              /* Winograd kinds 3, 4: > 1 splits the input channels into
+                                  ksplit slices of whole 8-channel chunks (fewer if a slice would
+                                  be empty), one workgroup per tile and slice; the last slice of a
+                                  tile sums the slices' pre-bias outputs in slice order.  0 / 1:
+                                  no split.  A fixed split per conv keeps batch == per-sample
+                                  outputs bitwise; a different split rounds differently */
+  int32_t pad2_;
+  float* part;                 /* ksplit > 1: rrin_conv_h8_split_floats() floats, any contents */
+  int32_t* cnt;                /* ksplit > 1: one int per tile, zero before the first call; every
+                                  call leaves it zero again (one call at a time per cnt) */
 } rrin_conv_h8_desc;
 
 int rrin_conv_h8_cfg_count(void);
@@ -209,13 +219,17 @@ int rrin_conv_h8_cfg_ok(int32_t cfg, int32_t prec); /* 1 if the config fits LDS 
  * every weight chunk resident in LDS needs them to fit) */
 int rrin_conv_h8_cfg_fits(int32_t cfg, int32_t prec, int32_t cin);
 int rrin_conv3x3_h8_fwd(const rrin_conv_h8_desc* d, void* stream);
+/* Scratch of a split-K conv (d->ksplit > 1): returns the floats of d->part and
+ * stores the ints of d->cnt (0 and 0 without a split); < 0: the error code */
+int64_t rrin_conv_h8_split_floats(const rrin_conv_h8_desc* d, int64_t* cnt_ints);
 /* Nonzero if cfg is a Winograd exact-fp32 config (F32R only, not packed by
  * rrin_pack_conv3x3_r32): the tile kind.  F(2x2,3x3), packed by
  * rrin_pack_conv3x3_wino_bm with the config's BM: 1 = BM 32 x TH 8 on 4 waves,
  * 2 = BM 64 x TH 8 on 8 waves, 3 = BM 32 x TH 8 on 8 waves of 4 accumulators
  * (4 waves per SIMD), 4 = kind 3 on TH 4 tiles (4 waves); all four give
  * bitwise-equal outputs.  5 = F(4x4,3x3), BM 32 x TH 16 on 6 waves, packed by
- * rrin_pack_conv3x3_wino4 (a different rounding: 36 transform points).
+ * rrin_pack_conv3x3_wino4 (a different rounding: 36 transform points).  Kinds
+ * 3 and 4 take a split-K (rrin_conv_h8_desc.ksplit).
  * 0: direct form. */
 int rrin_conv_h8_cfg_wino(int32_t cfg);
 
@@ -326,7 +340,8 @@ typedef struct rrin_conv_weights {
   const void* wlo;      /* F16X3: packed lo halves                            */
   int32_t subpixel;     /* F16*, up convs: 1 = whi/wlo/bias hold the sub-pixel
                            weights (4*cout rows) and the upsample pass is skipped */
-  int32_t pad_;
+  int32_t ksplit;       /* F32R Winograd kinds 3, 4: rrin_conv_h8_desc.ksplit (0: none);
+                           the forward's workspace holds the split scratch */
   const float* wedge;   /* subpixel: original weights [cin][9][cout] fp32      */
   const float* bias_raw;/* subpixel: original bias [cout]                      */
 } rrin_conv_weights;

@@ -9,7 +9,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "librrin_hip.so")
 
 # enums (rrin_hip.h)
@@ -54,7 +54,7 @@ class HeadDesc(C.Structure):
 
 class ConvWeights(C.Structure):
     _fields_ = [("wpack", C.c_void_p), ("bias", C.c_void_p), ("cfg", C.c_int32), ("inv_wscale", C.c_float),
-                ("whi", C.c_void_p), ("wlo", C.c_void_p), ("subpixel", C.c_int32), ("pad_", C.c_int32),
+                ("whi", C.c_void_p), ("wlo", C.c_void_p), ("subpixel", C.c_int32), ("ksplit", C.c_int32),
                 ("wedge", C.c_void_p), ("bias_raw", C.c_void_p)]
 
 
@@ -67,7 +67,8 @@ class ConvH8Desc(C.Structure):
     _fields_ = [("n", C.c_int32), ("cin", C.c_int32), ("cout", C.c_int32), ("cfg", C.c_int32),
                 ("prec", C.c_int32), ("epi_mode", C.c_int32), ("slope", C.c_float), ("inv_wscale", C.c_float),
                 ("tail_finite", C.c_int32), ("pad_", C.c_int32), ("src", H8), ("dst", H8), ("pool", H8), ("whi", C.c_void_p), ("wlo", C.c_void_p),
-                ("bias", C.c_void_p), ("edge", C.c_void_p), ("status", C.c_void_p)]
+                ("bias", C.c_void_p), ("edge", C.c_void_p), ("status", C.c_void_p), ("ksplit", C.c_int32),
+                ("pad2_", C.c_int32), ("part", C.c_void_p), ("cnt", C.c_void_p)]
 
 
 class EdgeFixDesc(C.Structure):
@@ -145,6 +146,7 @@ SIGNATURES = {
     "rrin_conv_h8_cfg_fits": (C.c_int, [C.c_int32, C.c_int32, C.c_int32]),
     "rrin_conv3x3_h8_fwd": (C.c_int, [C.POINTER(ConvH8Desc), C.c_void_p]),
     "rrin_conv_h8_cfg_wino": (C.c_int, [C.c_int32]),
+    "rrin_conv_h8_split_floats": (C.c_int64, [C.c_void_p, C.c_void_p]),
     "rrin_pack_conv3x3_wino_floats": (C.c_int64, [C.c_int32, C.c_int32]),
     "rrin_pack_conv3x3_wino_bm_floats": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32]),
     "rrin_pack_conv3x3_wino4_floats": (C.c_int64, [C.c_int32, C.c_int32]),

@@ -191,6 +191,12 @@ struct ConvH8Args {
   float* edge;  // EPI_SUBPIXEL: [n][cout/4][ring] pre-bias values of the 2h x 2w ring
   int64_t ring;
   int* status;  // optional fp16 range flag (F16X3 / F16)
+  // Winograd split-K (ksplit > 1): slice ks of a tile runs chunks [ks * kper, ..), writes its
+  // pre-bias outputs to part and counts itself in cnt[tile]; the last slice sums all of them
+  // in slice order and runs the epilogue (cnt is reset to 0 by that slice)
+  int ksplit, kper;
+  float* part;
+  int* cnt;
 };
 
 // Ring index of pixel (y, x) of an H x W image (rrin_ring_pixels order: top
@@ -226,9 +232,6 @@ int launch_wino64(const ConvH8Args& a, int epi, hipStream_t st);
 constexpr size_t kWinoQLds = (size_t)3 * (680 + 1024) * 16;
 // th = 8 (cfg 20: 8 waves) or 4 (cfg 21: 4 waves, the same arithmetic on half-height tiles)
 int launch_winoq(const ConvH8Args& a, int epi, int th, hipStream_t st);
-// cfg 23 (kind 6): cfg 20's tile with the ping-pong main loop (the two patch-row
-// halves alternate matrix and memory segments; bitwise equal to cfg 20)
-int launch_winop(const ConvH8Args& a, int epi, hipStream_t st);
 // Winograd F(4x4,3x3) (conv_wino4.hip): BM 32 x TH 16, 6 waves, 4-channel K chunks
 constexpr size_t kWino4Lds = (size_t)2 * (612 + 1152) * 16;
 int launch_wino4(const ConvH8Args& a, int epi, hipStream_t st);

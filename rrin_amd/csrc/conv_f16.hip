@@ -1657,21 +1657,18 @@ static const CfgH8 kCfgH8[] = {
     {32, 4, (size_t)2 * (408 + 1024) * 16, (size_t)1 << 30, 0, true, 0, 0},
     // kWino4Cfg: Winograd F(4x4,3x3), BM 32 x TH 16, 6 waves (conv_wino4.hip)
     {32, 16, kWino4Lds, (size_t)1 << 30, 0, true, 0, 0},
-    // kWinoPCfg: cfg 20's tile and packing with the ping-pong main loop (conv3x3_winoq_kernel<.., PP>)
-    {32, 8, (size_t)2 * (680 + 1024) * 16, (size_t)1 << 30, 0, true, 0, 0},
 };
 static constexpr int kNumCfgH8 = sizeof(kCfgH8) / sizeof(kCfgH8[0]);
-static constexpr int kWinoCfg = kNumCfgH8 - 6;
-static constexpr int kWino64Cfg = kNumCfgH8 - 5;
-static constexpr int kWinoQCfg = kNumCfgH8 - 4;
-static constexpr int kWinoQ4Cfg = kNumCfgH8 - 3;
-static constexpr int kWino4Cfg = kNumCfgH8 - 2;
-static constexpr int kWinoPCfg = kNumCfgH8 - 1;
+static constexpr int kWinoCfg = kNumCfgH8 - 5;
+static constexpr int kWino64Cfg = kNumCfgH8 - 4;
+static constexpr int kWinoQCfg = kNumCfgH8 - 3;
+static constexpr int kWinoQ4Cfg = kNumCfgH8 - 2;
+static constexpr int kWino4Cfg = kNumCfgH8 - 1;
 static inline bool is_wino(int cfg) {
-  return cfg == kWinoCfg || cfg == kWino64Cfg || cfg == kWinoQCfg || cfg == kWinoQ4Cfg || cfg == kWino4Cfg ||
-         cfg == kWinoPCfg;
+  return cfg == kWinoCfg || cfg == kWino64Cfg || cfg == kWinoQCfg || cfg == kWinoQ4Cfg || cfg == kWino4Cfg;
 }
 static constexpr size_t kMaxLds = 160 * 1024;
+static constexpr int kMaxKSplit = 16;
 
 static int num_cus(int dev) {
   static std::atomic<int> n[kMaxDevices] = {};
@@ -1782,7 +1779,7 @@ static inline bool rec_prec(int prec) {
 static inline int chans_per_rec(int prec) { return prec == RRIN_PREC_F32R ? 4 : 8; }
 
 // Validate a conv descriptor and turn it into kernel arguments.
-static int h8_prepare(const rrin_conv_h8_desc* d, ConvH8Args& a) {
+static int h8_prepare(const rrin_conv_h8_desc* d, ConvH8Args& a, bool need_scratch = true) {
   if (!d || !d->whi || !d->bias) return RRIN_E_ARG;
   if (!rec_prec(d->prec)) return RRIN_E_ARG;
   if (d->prec == RRIN_PREC_F16X3 && !d->wlo) return RRIN_E_ARG;
@@ -1855,7 +1852,27 @@ static int h8_prepare(const rrin_conv_h8_desc* d, ConvH8Args& a) {
   }
   a.n = d->n;
   if ((int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n > 0x7fffffff) return RRIN_E_SHAPE;
+  a.ksplit = 1;
+  if (d->ksplit > 1) {  // Winograd split-K: kinds 3 and 4 only
+    if (d->cfg != kWinoQCfg && d->cfg != kWinoQ4Cfg) return RRIN_E_CONFIG;
+    if (d->ksplit > kMaxKSplit || (need_scratch && (!d->part || !d->cnt))) return RRIN_E_ARG;
+    a.kper = (a.nchunks + d->ksplit - 1) / d->ksplit;
+    a.ksplit = (a.nchunks + a.kper - 1) / a.kper;  // every slice non-empty
+    if ((int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n * a.ksplit > 0x7fffffff) return RRIN_E_SHAPE;
+    a.part = d->part;
+    a.cnt = d->cnt;
+  }
   return 0;
+}
+
+// floats of rrin_conv_h8_desc.part and ints of .cnt a split-K conv needs (0 without a split)
+extern "C" int64_t rrin_conv_h8_split_floats(const rrin_conv_h8_desc* d, int64_t* cnt_ints) {
+  ConvH8Args a;
+  const int rc = h8_prepare(d, a, false);
+  if (rc) return rc;
+  const int64_t tiles = (int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n;
+  if (cnt_ints) *cnt_ints = a.ksplit > 1 ? tiles : 0;
+  return a.ksplit > 1 ? tiles * a.ksplit * 32 * 32 * kCfgH8[d->cfg].th : 0;  // 16 floats per thread of 64 x th threads
 }
 
 }  // namespace rrin
@@ -1877,14 +1894,13 @@ extern "C" int rrin_conv_h8_cfg_th(int32_t cfg) {
 }
 // 0: direct form; Winograd tile kind: 1 BM 32 / 4 waves, 2 BM 64 / 8 waves, 3 BM 32 / 8 waves,
 // 4 BM 32 x TH 4 / 4 waves; 5 Winograd F(4x4,3x3), BM 32 x TH 16 / 6 waves (its own packing,
-// rrin_pack_conv3x3_wino4); 6 kind 3's tile with the ping-pong main loop
+// rrin_pack_conv3x3_wino4)
 extern "C" int rrin_conv_h8_cfg_wino(int32_t cfg) {
   return cfg == kWinoCfg     ? 1
          : cfg == kWino64Cfg ? 2
          : cfg == kWinoQCfg  ? 3
          : cfg == kWinoQ4Cfg ? 4
          : cfg == kWino4Cfg  ? 5
-         : cfg == kWinoPCfg  ? 6
                              : 0;
 }
 extern "C" int rrin_conv_h8_cfg_ok(int32_t cfg, int32_t prec) {
@@ -1914,7 +1930,6 @@ extern "C" int rrin_conv3x3_h8_fwd(const rrin_conv_h8_desc* d, void* stream) {
   if (d->cfg == kWinoQCfg) return launch_winoq(a, d->epi_mode, 8, st);
   if (d->cfg == kWinoQ4Cfg) return launch_winoq(a, d->epi_mode, 4, st);
   if (d->cfg == kWino4Cfg) return launch_wino4(a, d->epi_mode, st);
-  if (d->cfg == kWinoPCfg) return launch_winop(a, d->epi_mode, st);
   switch (d->cfg) {
 #define X(id, nw, wm, wn, sc, pe) \
   case id:                        \

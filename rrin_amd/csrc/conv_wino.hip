@@ -769,24 +769,16 @@ static_assert(2 * kWinoQLds <= 160 * 1024, "two blocks per CU");
 // PT: patch-row pairs per tile -- 2: 8 waves, TH 8 (cfg 20); 1: 4 waves, TH 4
 // (cfg 21, twice the tiles for the few-tile deep levels of small workloads).
 //
-// PP (cfg 23, kind 6; PT 2 only): ping-pong main loop.  The two patch-row halves
-// of the block (waves 0-3: pt 0 = group A, waves 4-7: pt 1 = group B; wave w and
-// w + 4 share a SIMD) alternate between a matrix segment (the chunk's 16 MFMAs
-// from operands already in registers) and a memory segment (LDS-DMA issue,
-// window reads, B^T transform of the next chunk), one s_barrier per segment, so
-// each SIMD always has one wave of the block feeding its matrix pipe while its
-// partner stages -- instead of all eight waves reading and transforming after
-// each barrier and then all issuing MFMAs.  Chunk c is read by A in segment 2c
-// and by B in segment 2c + 1; its stage (c & 1) then takes chunk c + 2: the raw
-// tile issued by A in segment 2c + 2 (its memory segment), the U slab by B in
-// segment 2c + 3; both land before the barrier that ends segment 2c + 3.  The
-// barriers are bare s_barrier (no vmcnt(0) drain of __syncthreads): each wave
-// waits only for what the next segment needs.  Same products in the same order
-// per accumulator as cfg 20: bitwise equal outputs.
-template <int EPI, int ABL = 0, int PT = 2, int PP = 0>
-__global__ __launch_bounds__(256 * PT, 2) __attribute__((amdgpu_waves_per_eu(4)))
-void conv3x3_winoq_kernel(ConvH8Args a) {
-  static_assert(!PP || PT == 2, "ping-pong needs the two patch-row halves");
+// SK (split-K, a.ksplit > 1): the grid has a.ksplit blocks per tile, slice ks running
+// chunks [ks * a.kper, ..).  After its output transform a slice stores its pre-bias
+// outputs (16 floats per lane) to a.part and counts itself in a.cnt[tile]
+// (agent-scope release / acquire: the slices may run on different XCDs); the slice that
+// counts last reads the tile's slices back, sums them in slice order (so the result
+// does not depend on which slice finished last), resets the counter and runs the
+// epilogue.  A different association of the K sum than one slice (not bitwise equal to
+// cfg 20), fixed per conv: batch and per-sample outputs stay bitwise equal.
+template <int EPI, int ABL = 0, int PT = 2, int SK = 0>
+__global__ __launch_bounds__(256 * PT, 2) void conv3x3_winoq_kernel(ConvH8Args a) {
   constexpr int NT = 256 * PT, TH = 4 * PT;
   constexpr int RG = (TH + 2) * kWnRawCols, RAW = 2 * RG, STAGE = RAW + kWnU;
   static_assert(RAW > NT && RAW <= 2 * NT && kWnU % NT == 0, "two raw pieces, whole U pieces");
@@ -803,11 +795,17 @@ void conv3x3_winoq_kernel(ConvH8Args a) {
     bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
   }
   const int ntiles = a.co_blocks * a.tiles_x * a.tiles_y * a.n;
-  if (bid >= ntiles) return;
-  const int nch = a.nchunks;
+  const int ksn = SK ? a.ksplit : 1;  // K slices per tile
+  if (bid >= ntiles * ksn) return;
+  const int tile = SK ? bid / ksn : bid, ks = SK ? bid - tile * ksn : 0;
+  // this slice's chunks [c0, c0 + nch) of the conv's a.nchunks; staging below counts chunks
+  // from c0 (source and weight bases moved by c0 chunks, cin_loc channels from there)
+  const int c0 = SK ? ks * a.kper : 0;
+  const int nch = SK ? min(a.nchunks - c0, a.kper) : a.nchunks;
+  const int cin_loc = a.cin - 8 * c0;
   int cob, x0, y0, img;
   {
-    int t = bid;
+    int t = tile;
     cob = t % a.co_blocks;
     t /= a.co_blocks;
     x0 = (t % a.tiles_x) * 32;
@@ -815,8 +813,9 @@ void conv3x3_winoq_kernel(ConvH8Args a) {
     y0 = (t % a.tiles_y) * TH;
     img = t / a.tiles_y;
   }
-  const uint4* tsrc = a.src_hi + (int64_t)img * a.src_img + (int64_t)y0 * a.src_wp + x0 + (kH8PadLeft - 1);
-  const uint4* wsrc = a.w_hi + (int64_t)cob * nch * kWnU + tid;
+  const uint4* tsrc =
+      a.src_hi + (int64_t)img * a.src_img + (int64_t)(2 * c0) * a.src_gp + (int64_t)y0 * a.src_wp + x0 + (kH8PadLeft - 1);
+  const uint4* wsrc = a.w_hi + ((int64_t)cob * a.nchunks + c0) * kWnU + tid;
   // staging: raw RAW records = NT + the rest, U 1024 = UP x NT
   int64_t p_off[2];
   int p_g[2], p_zero[2];
@@ -837,7 +836,7 @@ void conv3x3_winoq_kernel(ConvH8Args a) {
     for (int it = 0; it < 2; ++it) {
       if ((it == 0 || tid < RAW - NT) && !((ABL & 2) && c > 0)) {
         const int gg = 2 * c + p_g[it];
-        const int64_t off = gg * 4 < a.cin ? (int64_t)(2 * c) * a.src_gp + p_off[it] : (int64_t)p_zero[it];
+        const int64_t off = gg * 4 < cin_loc ? (int64_t)(2 * c) * a.src_gp + p_off[it] : (int64_t)p_zero[it];
         dma16(tsrc + off, base + NT * it + (tid & ~63));
       }
     }
@@ -930,114 +929,11 @@ void conv3x3_winoq_kernel(ConvH8Args a) {
       asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
     }
   };
-  if constexpr ((ABL & 4) != 0 || PP) {
+  if constexpr ((ABL & 4) != 0) {
 #pragma unroll
     for (int x = 0; x < 4; ++x) acc[x] = wfloatx16{};
   }
-  if constexpr (PP) {
-    const bool grp_b = __builtin_amdgcn_readfirstlane(wv) >= 4;
-    const int gt = tid & 255;
-    // group-local staging (256 threads): raw tile 680 = 256 + 256 + 168 records, U 1024 = 4 x 256
-    int64_t q_off[3];
-    int q_zero[3], q_g[3];
-#pragma unroll
-    for (int it = 0; it < 3; ++it) {
-      const int idx = gt + 256 * it;
-      const int g = idx >= RG ? 1 : 0;
-      const int rem = idx - g * RG;
-      const int r = rem / kWnRawCols, pos = rem - r * kWnRawCols;
-      const int col = pos < 17 ? 2 * pos : 2 * (pos - 17) + 1;
-      q_g[it] = g;
-      q_off[it] = (int64_t)g * a.src_gp + r * a.src_wp + col;
-      q_zero[it] = col - y0 * a.src_wp;
-    }
-    auto issue_raw_g = [&](int c, int b) {
-      uint4* base = smem4 + b * STAGE;
-#pragma unroll
-      for (int it = 0; it < 3; ++it) {
-        if (it < 2 || gt < RAW - 512) {
-          const int gg = 2 * c + q_g[it];
-          const int64_t off = gg * 4 < a.cin ? (int64_t)(2 * c) * a.src_gp + q_off[it] : (int64_t)q_zero[it];
-          dma16(tsrc + off, base + 256 * it + (gt & ~63));
-        }
-      }
-    };
-    const uint4* wsrc_g = a.w_hi + (int64_t)cob * nch * kWnU + gt;
-    auto issue_u_g = [&](int c, int b) {
-      uint4* base = smem4 + b * STAGE + RAW;
-#pragma unroll
-      for (int it = 0; it < 4; ++it) dma16(wsrc_g + (int64_t)c * kWnU + 256 * it, base + 256 * it + (gt & ~63));
-    };
-    // memory segment: window reads + B^T row of the chunk in stage b -> v
-    wfloatx4 v[4];
-    auto prep = [&](int b) {
-      const uint4* rw = smem4 + b * STAGE + rw0;
-      wfloatx4 t[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const wfloatx4 d0 = __builtin_bit_cast(wfloatx4, rw[oa + pc[k]]);
-        const wfloatx4 d1 = __builtin_bit_cast(wfloatx4, rw[ob + pc[k]]);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) t[k][e] = fmaf(sg, d1[e], d0[e]);
-      }
-      v[0] = t[0] - t[2];
-      v[1] = t[1] + t[2];
-      v[2] = t[2] - t[1];
-      v[3] = t[1] - t[3];
-      // the transform belongs to this segment: keep it ahead of the segment's barrier
-#pragma unroll
-      for (int x = 0; x < 4; ++x) asm volatile("" : "+v"(v[x]));
-    };
-    // matrix segment: the U records of the chunk in stage b, then its 16 MFMAs
-    // (product e of the four points in turn: each accumulator still takes e = 0..3 in order)
-    auto mma = [&](int b) {
-      const uint4* su = smem4 + b * STAGE + RAW + su0;
-      wfloatx4 u[4];
-#pragma unroll
-      for (int x = 0; x < 4; ++x) u[x] = __builtin_bit_cast(wfloatx4, su[x * 64]);
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-#pragma unroll
-        for (int x = 0; x < 4; ++x) acc[x] = __builtin_amdgcn_mfma_f32_32x32x2f32(u[x][e], v[x][e], acc[x], 0, 0, 0);
-    };
-    // segment boundary: nothing (MFMAs included) crosses it
-    auto seg_end = [&](bool drain_dma) {
-      __builtin_amdgcn_sched_barrier(0);
-      if (drain_dma)
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      else
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-    };
-    // prologue: chunks 0 and 1 staged by all eight waves.  Then every wave runs the
-    // same loop, {memory segment of chunk k; matrix segment of chunk k}, group B one
-    // segment behind group A (B's extra barrier up front, A's at the end), so A's
-    // matrix segments meet B's memory segments and the other way round.  In its
-    // memory segment of chunk k >= 1 a wave first stages its share of chunk k + 1
-    // (A the raw tile, B the U slab) into stage (k + 1) & 1, whose last reader (B's
-    // matrix segment of chunk k - 1) has passed the previous barrier.  Chunk k + 1
-    // is complete at the barrier that ends B's memory segment of chunk k (= A's
-    // matrix segment): both drain their DMA there.
-    issue(0, 0);
-    if (nch > 1) issue(1, 1);
-    seg_end(true);
-    if (grp_b) seg_end(false);
-#pragma clang loop unroll(disable)
-    for (int k = 0; k < nch; ++k) {
-      const int b = k & 1;
-      if (k >= 1 && k + 1 < nch) {
-        if (grp_b)
-          issue_u_g(k + 1, b ^ 1);
-        else
-          issue_raw_g(k + 1, b ^ 1);
-      }
-      prep(b);
-      seg_end(grp_b);
-      mma(b);
-      seg_end(true);
-    }
-    if (!grp_b) seg_end(false);
-  } else {
+  {
   issue(0, 0);
   if (NS == 3 && nch > 1) issue(1, 1);
   for (int c = 0; c < nch; ++c) {
@@ -1099,6 +995,57 @@ void conv3x3_winoq_kernel(ConvH8Args a) {
       }
     }
     __syncthreads();
+  }
+  if constexpr (SK) {
+    // slice partial: plane q of the slice = NT lanes x 4 floats (coalesced per wave).
+    // Split-K seam (cdna_hip_programming.md, split-K reduction recipe, sc1 form): the slice
+    // drawing ksn - 1 reduces after ONE agent-scope acquire.  Correct for any placement of
+    // a tile's slices over CUs / XCDs.
+    // The slab stores are write-through (sc1), so no release fence: every wave drains, the
+    // barrier, then lane 0's relaxed ticket.
+    float4* pp = reinterpret_cast<float4*>(a.part) + (int64_t)(tile * ksn) * 4 * NT + tid;
+    {
+      float* slab = a.part + (int64_t)(tile * ksn) * 4 * NT * 4;  // block-uniform base
+      const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(slab, 0, ksn * 4 * NT * 16, 0x00020000);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 v = {__float_as_uint(yv[4 * q]), __float_as_uint(yv[4 * q + 1]), __float_as_uint(yv[4 * q + 2]),
+                         __float_as_uint(yv[4 * q + 3])};
+        __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, ((ks * 4 + q) * NT + tid) * 16, 0, 16 /* sc1 */);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    // "last slice" flag in the dynamic LDS array (right past the exchange records: 2048 of TH 8, 1024 of TH 4)
+    int* s_last = reinterpret_cast<int*>(smem4 + 2048);
+    if (tid == 0) {
+      const int old = __hip_atomic_fetch_add(a.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = old == ksn - 1;
+      if (last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(a.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+      }
+      *s_last = last;
+    }
+    __syncthreads();
+    if (!*s_last) return;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float4 sum = pp[(int64_t)q * NT];
+      for (int k = 1; k < ksn; ++k) {
+        const float4 v = pp[(int64_t)(k * 4 + q) * NT];
+        sum.x += v.x;
+        sum.y += v.y;
+        sum.z += v.z;
+        sum.w += v.w;
+      }
+      yv[4 * q] = sum.x;
+      yv[4 * q + 1] = sum.y;
+      yv[4 * q + 2] = sum.z;
+      yv[4 * q + 3] = sum.w;
+    }
   }
   if constexpr (EPI == RRIN_EPI_SUBPIXEL) {
     const int HH = 2 * a.h, WW = 2 * a.w, creal = a.cout >> 2;
@@ -1173,18 +1120,31 @@ void conv3x3_winoq_kernel(ConvH8Args a) {
   }
 }
 
-template <int EPI, int ABL = 0, int PT = 2, int PP = 0>
+template <int EPI, int ABL = 0, int PT = 2, int SK = 0>
 static int launch_winoq_k(const ConvH8Args& a, hipStream_t st) {
-  auto k = conv3x3_winoq_kernel<EPI, ABL, PT, PP>;
+  auto k = conv3x3_winoq_kernel<EPI, ABL, PT, SK>;
   static LdsAttr attr;
   constexpr size_t lds = (size_t)(PT == 2 ? kWqStages : 2) * (2 * (4 * PT + 2) * kWnRawCols + kWnU) * 16;
   if (int e = attr.ensure((const void*)k, (int)lds, st)) return e;
-  const int64_t grid = (int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n;
+  const int64_t grid = (int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n * (SK ? a.ksplit : 1);
   hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256 * PT), lds, st, a);
   return hip_code(hipGetLastError());
 }
 
+template <int PT>
+static int launch_winoq_sk(const ConvH8Args& a, int epi, hipStream_t st) {
+  switch (epi) {
+    case RRIN_EPI_LINEAR: return launch_winoq_k<RRIN_EPI_LINEAR, 0, PT, 1>(a, st);
+    case RRIN_EPI_LEAKY: return launch_winoq_k<RRIN_EPI_LEAKY, 0, PT, 1>(a, st);
+    case RRIN_EPI_LEAKY_POOL: return launch_winoq_k<RRIN_EPI_LEAKY_POOL, 0, PT, 1>(a, st);
+    case RRIN_EPI_LEAKY_REP: return launch_winoq_k<RRIN_EPI_LEAKY_REP, 0, PT, 1>(a, st);
+    case RRIN_EPI_SUBPIXEL: return launch_winoq_k<RRIN_EPI_SUBPIXEL, 0, PT, 1>(a, st);
+  }
+  return RRIN_E_ARG;
+}
+
 int launch_winoq(const ConvH8Args& a, int epi, int th, hipStream_t st) {
+  if (a.ksplit > 1) return th == 4 ? launch_winoq_sk<1>(a, epi, st) : launch_winoq_sk<2>(a, epi, st);
   if (th == 4) {
     switch (epi) {
       case RRIN_EPI_LINEAR: return launch_winoq_k<RRIN_EPI_LINEAR, 0, 1>(a, st);
@@ -1201,17 +1161,6 @@ int launch_winoq(const ConvH8Args& a, int epi, int th, hipStream_t st) {
     case RRIN_EPI_LEAKY_POOL: return launch_winoq_k<RRIN_EPI_LEAKY_POOL>(a, st);
     case RRIN_EPI_LEAKY_REP: return launch_winoq_k<RRIN_EPI_LEAKY_REP>(a, st);
     case RRIN_EPI_SUBPIXEL: return launch_winoq_k<RRIN_EPI_SUBPIXEL>(a, st);
-  }
-  return RRIN_E_ARG;
-}
-
-int launch_winop(const ConvH8Args& a, int epi, hipStream_t st) {
-  switch (epi) {
-    case RRIN_EPI_LINEAR: return launch_winoq_k<RRIN_EPI_LINEAR, 0, 2, 1>(a, st);
-    case RRIN_EPI_LEAKY: return launch_winoq_k<RRIN_EPI_LEAKY, 0, 2, 1>(a, st);
-    case RRIN_EPI_LEAKY_POOL: return launch_winoq_k<RRIN_EPI_LEAKY_POOL, 0, 2, 1>(a, st);
-    case RRIN_EPI_LEAKY_REP: return launch_winoq_k<RRIN_EPI_LEAKY_REP, 0, 2, 1>(a, st);
-    case RRIN_EPI_SUBPIXEL: return launch_winoq_k<RRIN_EPI_SUBPIXEL, 0, 2, 1>(a, st);
   }
   return RRIN_E_ARG;
 }

@@ -61,8 +61,15 @@ struct Plan {
                           // edge-replicate padding by its producer (EPI_LEAKY_REP)
   float* EDGE;            // F16*: pre-bias ring values of the current sub-pixel up conv
   Buf FLOWRAW;            // raw 4-ch Flow output, kept for reuse across t (skip_flow)
+  float* PART;            // F32R: split-K slice outputs of the current conv (kPartFloats)
+  int32_t* CNT;           // F32R: split-K tile counters (kPartTiles; zero between convs)
   int64_t bytes;
 };
+
+// split-K scratch of an F32R plan: a split conv may have up to kPartFloats slice
+// outputs (8192 per TH 8 tile and slice: 4096 slices) and kPartTiles tiles
+constexpr int64_t kPartFloats = (int64_t)4096 * 8192;
+constexpr int64_t kPartTiles = 4096;
 
 int64_t align256(int64_t b) { return (b + 255) & ~(int64_t)255; }
 
@@ -117,6 +124,14 @@ void make_plan(int n, int h, int w, int prec, char* base, Plan& p) {
     off += align256(edge_floats * 4);
   }
   p.FLOWRAW = take(f32 ? 4 : cpr, p.g[0]);
+  p.PART = nullptr;
+  p.CNT = nullptr;
+  if (prec == RRIN_PREC_F32R) {
+    p.PART = base ? reinterpret_cast<float*>(base + off) : nullptr;
+    off += align256(kPartFloats * 4);
+    p.CNT = base ? reinterpret_cast<int32_t*>(base + off) : nullptr;
+    off += align256(kPartTiles * 4);
+  }
   p.bytes = off;
 }
 
@@ -290,6 +305,16 @@ int conv_h8(const Plan& p, const rrin_conv_weights& cw, int cin, int cout, int e
   d.bias = cw.bias;
   d.edge = edge;
   d.status = p.status;
+  if (cw.ksplit > 1) {
+    if (!p.PART) return RRIN_E_CONFIG;
+    d.ksplit = cw.ksplit;
+    d.part = p.PART;
+    d.cnt = p.CNT;
+    int64_t cnt = 0;
+    const int64_t need = rrin_conv_h8_split_floats(&d, &cnt);
+    if (need < 0) return (int)need;
+    if (need > kPartFloats || cnt > kPartTiles) return RRIN_E_CONFIG;
+  }
   return rrin_conv3x3_h8_fwd(&d, st);
 }
 

@@ -186,6 +186,27 @@ WINO_TH4 = {"small": {(256, 512, 4), (512, 512, 4), (256, 512, 3)},
             "medium": {(256, 512, 4), (512, 512, 4), (512, 1024, 4)}}
 
 
+# Split-K of the Winograd convs (rrin_conv_h8_desc.ksplit; kinds 3, 4) per size
+# class, grid level -> slices: the few-tile deep convs of small forward parts, where a
+# tile per workgroup leaves most CUs idle.  A split conv sums its K slices in slice
+# order (a different rounding from the unsplit conv, fixed per conv and class: batch
+# == per-sample stays bitwise within a class).  640x368 x 1 (profiles/r03/split_ab.txt):
+# none 272.7 pairs/s, L4 / 4 277.6, L3 / 2 + L4 / 4 279.1, L2 / 2 + L3 / 4 + L4 / 8
+# 274.6; 1280x720 x 1 loses with L3 / 2 + L4 / 4 (110.0 -> 108.7), so only "small".
+WINO_SPLIT = {"small": {3: 2, 4: 4}}
+# A/B override: grid level -> slices for every Winograd conv at that level, all classes
+WINO_SPLIT_LEVELS = {}
+
+
+def choose_split(cin: int, cout: int, level: int, size: str, cfg: int) -> int:
+    """Slices of the split-K for this conv (0: none)."""
+    if _lib.lib().rrin_conv_h8_cfg_wino(cfg) not in (3, 4):
+        return 0
+    if level in WINO_SPLIT_LEVELS:
+        return WINO_SPLIT_LEVELS[level]
+    return WINO_SPLIT.get(size, {}).get(level, 0)
+
+
 def wino_cfg(kind: int = None) -> int:
     lib = _lib.lib()
     kind = WINO_KIND if kind is None else kind
@@ -377,8 +398,8 @@ class RRINEngine:
         key = tuple(cfgs)
         p = self._packs_by_cfgs.get(key)
         if p is not None:
-            self._packs[size] = p
-            return p
+            self._packs[size] = self._with_splits(p, size)
+            return self._packs[size]
         halves, biases, meta = [], [], []
         hoff = boff = 0
         f32 = self.prec == _lib.PREC_F32R
@@ -442,8 +463,24 @@ class RRINEngine:
                 e.bias_raw = edge[1].data_ptr()
         p = (blob, bias_blob, table, cfgs)
         self._packs_by_cfgs[key] = p
-        self._packs[size] = p
-        return p
+        self._packs[size] = self._with_splits(p, size)
+        return self._packs[size]
+
+    def _with_splits(self, p, size: str):
+        """The packing p of class ``size`` with that class's split-K slices set in a copy
+        of its ConvWeights table (the weight blobs stay shared)."""
+        if self.prec != _lib.PREC_F32R:
+            return p
+        blob, bias_blob, table, cfgs = p
+        ks = [choose_split(cin, cout, level, size, cfg)
+              for (_, _, cin, cout, level, _, _), cfg in zip(self._h8_convs, cfgs)]
+        if not any(ks):
+            return p
+        t2 = (_lib.ConvWeights * len(table))()
+        C.memmove(t2, table, C.sizeof(table))
+        for i, k in enumerate(ks):
+            t2[i].ksplit = k
+        return (blob, bias_blob, t2, cfgs)
 
     force_size_class = None  # A/B knob: use this tile-table class for every forward part
 

@@ -108,8 +108,23 @@ def pack_h8(w, b, cfg, prec, dev, perm=None):
     return t(whi), t(wlo), torch.from_numpy(bp).to(dev), inv.value
 
 
+def set_split(d, ksplit, dev, keep):
+    """Give desc d a split-K of ksplit slices (Winograd kinds 3, 4) with fresh scratch;
+    keep collects the scratch tensors (the counters are checked by test_gpu_split)."""
+    if not ksplit:
+        return
+    d.ksplit = ksplit
+    nc = C.c_int64()
+    nf = _lib.lib().rrin_conv_h8_split_floats(C.byref(d), C.byref(nc))
+    assert nf > 0 and nc.value > 0, nf
+    part = torch.full((nf,), float("nan"), device=dev)
+    cnt = torch.zeros(nc.value, dtype=torch.int32, device=dev)
+    d.part, d.cnt = part.data_ptr(), cnt.data_ptr()
+    keep.extend([part, cnt])
+
+
 def conv_h8(src: H8Tensor, w, b, cfg, prec, epi=_lib.EPI_LINEAR, dst=None, dst_off=0, pool=None, perm=None,
-            cin=None, tail_finite=0):
+            cin=None, tail_finite=0, ksplit=0, keep=None):
     dev = src.hi.device
     cout, cin_w = w.shape[:2]
     cin = cin or cin_w
@@ -126,6 +141,7 @@ def conv_h8(src: H8Tensor, w, b, cfg, prec, epi=_lib.EPI_LINEAR, dst=None, dst_o
     if pool is not None:
         d.pool = pool.view(0, cout)
     d.whi, d.wlo, d.bias = whi.data_ptr(), wlo.data_ptr() if prec == X3 else None, bp.data_ptr()
+    set_split(d, ksplit, dev, keep if keep is not None else [])
     _lib.check(_lib.lib().rrin_conv3x3_h8_fwd(C.byref(d), H.stream(dev)), "rrin_conv3x3_h8_fwd")
     torch.cuda.synchronize(dev)
     return dst, pool
@@ -275,7 +291,7 @@ def test_h8_leaky_rep_writes_replicated_ring(gpu, prec):
         assert dst.hi[:, :, 0, 7:9 + dst.w].any() and dst.hi[:, :, 1:dst.h + 1, 7].any()
 
 
-def subpixel_upconv(src: H8Tensor, w, b, cfg, prec, dst=None):
+def subpixel_upconv(src: H8Tensor, w, b, cfg, prec, dst=None, ksplit=0, keep=None):
     """EPI_SUBPIXEL conv + ring fix-up through the C ABI (the Net's up.1 conv)."""
     lib = _lib.lib()
     dev = src.hi.device
@@ -296,6 +312,7 @@ def subpixel_upconv(src: H8Tensor, w, b, cfg, prec, dst=None):
     d.src, d.dst = src.view(0, cin), dst.view(0, cout)
     d.whi, d.wlo, d.bias = whi.data_ptr(), wlo.data_ptr() if prec == X3 else None, bp.data_ptr()
     d.edge = edge.data_ptr()
+    set_split(d, ksplit, dev, keep if keep is not None else [])
     _lib.check(lib.rrin_conv3x3_h8_fwd(C.byref(d), H.stream(dev)), "rrin_conv3x3_h8_fwd(subpixel)")
     wedge = torch.from_numpy(np.ascontiguousarray(wn.transpose(1, 2, 3, 0))).to(dev)
     braw = torch.from_numpy(bn.copy()).to(dev)

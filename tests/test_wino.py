@@ -88,11 +88,10 @@ def test_wino_config_entry():
     lib = _lib.lib()
     ids = [c for c in range(lib.rrin_conv_h8_cfg_count()) if lib.rrin_conv_h8_cfg_wino(c)]
     # kinds 1 (BM 32, 4 waves), 2 (BM 64, 8 waves), 3 (BM 32, 8 waves of 4 accumulators), TH 8;
-    # 4 (kind 3's arithmetic on TH 4 tiles, 4 waves); 5 F(4x4,3x3) on TH 16 tiles; 6 kind 3's tile
-    # with the ping-pong main loop
-    assert sorted(lib.rrin_conv_h8_cfg_wino(c) for c in ids) == [1, 2, 3, 4, 5, 6]
+    # 4 (kind 3's arithmetic on TH 4 tiles, 4 waves); 5 F(4x4,3x3) on TH 16 tiles
+    assert sorted(lib.rrin_conv_h8_cfg_wino(c) for c in ids) == [1, 2, 3, 4, 5]
     assert {lib.rrin_conv_h8_cfg_wino(c): lib.rrin_conv_h8_cfg_bm(c) for c in ids} == {1: 32, 2: 64, 3: 32, 4: 32,
-                                                                                        5: 32, 6: 32}
+                                                                                        5: 32}
     for c in ids:
         assert lib.rrin_conv_h8_cfg_th(c) == {4: 4, 5: 16}.get(lib.rrin_conv_h8_cfg_wino(c), 8)
         assert lib.rrin_conv_h8_cfg_ok(c, _lib.PREC_F32R) == 1
@@ -152,3 +151,32 @@ def test_pack_wino4_layout():
     np.testing.assert_array_equal(bp[:cout], b)
     assert not bp[cout:].any()
     assert lib.rrin_pack_conv3x3_wino4_floats(0, 3) < 0
+
+
+def test_split_scratch_size():
+    """rrin_conv_h8_split_floats: 16 floats per thread of every (tile, slice) workgroup
+    (64 x TH threads), one counter per tile; slices are whole chunks and never empty."""
+    import ctypes as C
+
+    import torch
+
+    from rrin_amd.pp import H8Tensor
+    lib = _lib.lib()
+    q8 = next(c for c in range(lib.rrin_conv_h8_cfg_count()) if lib.rrin_conv_h8_cfg_wino(c) == 3)
+    q4 = next(c for c in range(lib.rrin_conv_h8_cfg_count()) if lib.rrin_conv_h8_cfg_wino(c) == 4)
+    n, cin, cout, h, w = 2, 96, 64, 46, 80
+    src = H8Tensor(n, cin, h, w, torch.device("cpu"), _lib.PREC_F32R)
+    dst = H8Tensor(n, cout, h, w, torch.device("cpu"), _lib.PREC_F32R)
+    for cfg, th in ((q8, 8), (q4, 4)):
+        for ks, eff in ((0, 0), (1, 0), (2, 2), (5, 4), (8, 6), (12, 12)):  # 12 chunks: 5 -> 4 slices of 3
+            d = _lib.ConvH8Desc()
+            d.n, d.cin, d.cout, d.cfg, d.prec, d.epi_mode, d.slope = n, cin, cout, cfg, _lib.PREC_F32R, 1, 0.1
+            d.src, d.dst, d.whi, d.bias, d.ksplit = src.view(), dst.view(), 1, 1, ks
+            cnt = C.c_int64(-1)
+            tiles = 2 * 3 * -(-h // th) * n   # co blocks x tiles_x x tiles_y x n
+            assert lib.rrin_conv_h8_split_floats(C.byref(d), C.byref(cnt)) == tiles * eff * 64 * th * 16
+            assert cnt.value == (tiles if eff else 0)
+    d.cfg = next(c for c in range(lib.rrin_conv_h8_cfg_count()) if lib.rrin_conv_h8_cfg_wino(c) == 1)
+    d.ksplit = 2
+    assert lib.rrin_conv_h8_split_floats(C.byref(d), None) == _lib.RRIN_E_CONFIG if hasattr(_lib, "RRIN_E_CONFIG") \
+        else lib.rrin_conv_h8_split_floats(C.byref(d), None) < 0
