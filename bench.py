@@ -118,6 +118,8 @@ def parse():
     ap.add_argument("--wino-split", default=None,
                     help="A/B: split-K slices per grid level for every Winograd conv, e.g. '2:2,3:4,4:8' "
                          "(engine.WINO_SPLIT_LEVELS); 'none' disables the tuned splits")
+    ap.add_argument("--no-ring-fold", action="store_true",
+                    help="A/B: run the sub-pixel ring fix-up as its own launch (engine.RING_FOLD = False)")
     ap.add_argument("--no-wino-th4", action="store_true",
                     help="A/B: no TH-4 Winograd tiles on the deep convs (engine.WINO_TH4)")
     ap.add_argument("--split", default=None,
@@ -265,6 +267,8 @@ def main():
     elif args.wino_split:
         engine_mod.WINO_SPLIT_LEVELS.update({int(k): int(v) for k, v in
                                              (kv.split(":") for kv in args.wino_split.split(","))})
+    if args.no_ring_fold:
+        engine_mod.RING_FOLD = False
     if args.no_wino_th4:
         engine_mod.WINO_TH4 = {}
     net = Net()

@@ -209,6 +209,16 @@ typedef struct rrin_conv_h8_desc {
   float* part;                 /* ksplit > 1: rrin_conv_h8_split_floats() floats, any contents */
   int32_t* cnt;                /* ksplit > 1: one int per tile, zero before the first call; every
                                   call leaves it zero again (one call at a time per cnt) */
+  /* EPI_SUBPIXEL ring fold (Winograd kind 3, no split): with ring_w set, the launch
+     also writes the 1-pixel ring of the 2h x 2w output (the work of
+     rrin_subpixel_edge_fix_h8, which is then not called): correction workgroups at
+     the head of the grid, one per ring segment, and the segment's conv tile meet
+     through ring_cnt; edge still receives the phase values */
+  const float* ring_w;         /* original weights [cin][9][cout/4] fp32 (NULL: no fold) */
+  const float* ring_bias;      /* original bias [cout/4] */
+  float* ring_corr;            /* rrin_conv_h8_ring_floats() floats, any contents */
+  int32_t* ring_cnt;           /* rrin_conv_h8_ring_floats() ints, zero before the first call;
+                                  every call leaves it zero again */
 } rrin_conv_h8_desc;
 
 int rrin_conv_h8_cfg_count(void);
@@ -222,6 +232,10 @@ int rrin_conv3x3_h8_fwd(const rrin_conv_h8_desc* d, void* stream);
 /* Scratch of a split-K conv (d->ksplit > 1): returns the floats of d->part and
  * stores the ints of d->cnt (0 and 0 without a split); < 0: the error code */
 int64_t rrin_conv_h8_split_floats(const rrin_conv_h8_desc* d, int64_t* cnt_ints);
+/* Scratch of a ring-folding sub-pixel conv (d->ring_w set): returns the floats of
+ * d->ring_corr and stores the ints of d->ring_cnt; < 0: the error code (RRIN_E_CONFIG:
+ * the config cannot fold -- run rrin_subpixel_edge_fix_h8 instead) */
+int64_t rrin_conv_h8_ring_floats(const rrin_conv_h8_desc* d, int64_t* cnt_ints);
 /* Nonzero if cfg is a Winograd exact-fp32 config (F32R only, not packed by
  * rrin_pack_conv3x3_r32): the tile kind.  F(2x2,3x3), packed by
  * rrin_pack_conv3x3_wino_bm with the config's BM: 1 = BM 32 x TH 8 on 4 waves,
@@ -339,7 +353,9 @@ typedef struct rrin_conv_weights {
   const void* whi;      /* F16*: packed halves                                */
   const void* wlo;      /* F16X3: packed lo halves                            */
   int32_t subpixel;     /* F16*, up convs: 1 = whi/wlo/bias hold the sub-pixel
-                           weights (4*cout rows) and the upsample pass is skipped */
+                           weights (4*cout rows) and the upsample pass is skipped;
+                           2 = the same with the ring fix-up folded into the conv
+                           launch (F32R Winograd kind 3, ksplit <= 1) */
   int32_t ksplit;       /* F32R Winograd kinds 3, 4: rrin_conv_h8_desc.ksplit (0: none);
                            the forward's workspace holds the split scratch */
   const float* wedge;   /* subpixel: original weights [cin][9][cout] fp32      */

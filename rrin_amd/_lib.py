@@ -68,7 +68,8 @@ class ConvH8Desc(C.Structure):
                 ("prec", C.c_int32), ("epi_mode", C.c_int32), ("slope", C.c_float), ("inv_wscale", C.c_float),
                 ("tail_finite", C.c_int32), ("pad_", C.c_int32), ("src", H8), ("dst", H8), ("pool", H8), ("whi", C.c_void_p), ("wlo", C.c_void_p),
                 ("bias", C.c_void_p), ("edge", C.c_void_p), ("status", C.c_void_p), ("ksplit", C.c_int32),
-                ("pad2_", C.c_int32), ("part", C.c_void_p), ("cnt", C.c_void_p)]
+                ("pad2_", C.c_int32), ("part", C.c_void_p), ("cnt", C.c_void_p), ("ring_w", C.c_void_p),
+                ("ring_bias", C.c_void_p), ("ring_corr", C.c_void_p), ("ring_cnt", C.c_void_p)]
 
 
 class EdgeFixDesc(C.Structure):
@@ -147,6 +148,7 @@ SIGNATURES = {
     "rrin_conv3x3_h8_fwd": (C.c_int, [C.POINTER(ConvH8Desc), C.c_void_p]),
     "rrin_conv_h8_cfg_wino": (C.c_int, [C.c_int32]),
     "rrin_conv_h8_split_floats": (C.c_int64, [C.c_void_p, C.c_void_p]),
+    "rrin_conv_h8_ring_floats": (C.c_int64, [C.c_void_p, C.c_void_p]),
     "rrin_pack_conv3x3_wino_floats": (C.c_int64, [C.c_int32, C.c_int32]),
     "rrin_pack_conv3x3_wino_bm_floats": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32]),
     "rrin_pack_conv3x3_wino4_floats": (C.c_int64, [C.c_int32, C.c_int32]),

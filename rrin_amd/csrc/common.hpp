@@ -197,6 +197,15 @@ struct ConvH8Args {
   int ksplit, kper;
   float* part;
   int* cnt;
+  // EPI_SUBPIXEL ring fold (Winograd kind 3, conv_wino.hip): nring correction blocks at
+  // the head of the grid compute the out-of-image taps of every ring segment (nseg per
+  // image and co block) into corr; the segment's conv tile and its correction block
+  // each count themselves in rcnt, and the later one writes the ring pixels
+  int nring, nseg, rstride;  // rstride: workgroups per ring group of 8 (a multiple of 8)
+  const float* wedge;     // [cin][9][cout/4] original weights
+  const float* bias_raw;  // [cout/4]
+  float* corr;            // [n][co_blocks][nseg][512]
+  int* rcnt;              // [n][co_blocks][nseg], zero between launches
 };
 
 // Ring index of pixel (y, x) of an H x W image (rrin_ring_pixels order: top

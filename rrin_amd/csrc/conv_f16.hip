@@ -1862,7 +1862,32 @@ static int h8_prepare(const rrin_conv_h8_desc* d, ConvH8Args& a, bool need_scrat
     a.part = d->part;
     a.cnt = d->cnt;
   }
+  if (d->ring_w) {  // sub-pixel ring fold (kind 3, unsplit): no separate edge fix-up launch
+    if (!sub || d->cfg != kWinoQCfg || a.ksplit > 1) return RRIN_E_CONFIG;
+    if ((d->cin & 7) || !d->ring_bias || (need_scratch && (!d->ring_corr || !d->ring_cnt))) return RRIN_E_ARG;
+    a.nseg = 2 * a.tiles_x + 2 * a.tiles_y;
+    const int64_t rb = (int64_t)a.n * a.co_blocks * a.nseg;
+    if (rb + (int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n > 0x7fffffff) return RRIN_E_SHAPE;
+    a.nring = (int)((rb + 7) & ~(int64_t)7);  // keeps the tiles' XCD remap aligned
+    const int64_t grid = (int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n + a.nring;
+    a.rstride = 8 * (int)(grid / a.nring);    // ring groups spread over the whole grid
+    a.wedge = d->ring_w;
+    a.bias_raw = d->ring_bias;
+    a.corr = d->ring_corr;
+    a.rcnt = d->ring_cnt;
+  }
   return 0;
+}
+
+// floats of rrin_conv_h8_desc.ring_corr and ints of .ring_cnt a ring-folding sub-pixel conv
+// needs (0 and 0 when d->ring_w is NULL)
+extern "C" int64_t rrin_conv_h8_ring_floats(const rrin_conv_h8_desc* d, int64_t* cnt_ints) {
+  ConvH8Args a;
+  const int rc = h8_prepare(d, a, false);
+  if (rc) return rc;
+  const int64_t segs = a.nring > 0 ? (int64_t)a.n * a.co_blocks * a.nseg : 0;
+  if (cnt_ints) *cnt_ints = segs;
+  return segs * 512;
 }
 
 // floats of rrin_conv_h8_desc.part and ints of .cnt a split-K conv needs (0 without a split)

@@ -768,6 +768,172 @@ static_assert(2 * kWinoQLds <= 160 * 1024, "two blocks per CU");
 // chunk 0 (registers reused), 32 no U reads after chunk 0, 64 no epilogue stores
 // PT: patch-row pairs per tile -- 2: 8 waves, TH 8 (cfg 20); 1: 4 waves, TH 4
 // (cfg 21, twice the tiles for the few-tile deep levels of small workloads).
+// ---- sub-pixel ring fold (RF) ---------------------------------------------------
+// A sub-pixel up conv computes conv3x3(upsample_x2(x)) from phase weights over the
+// edge-replicated low-res x; on the 1-pixel ring of the 2h x 2w output the true conv
+// reads zero padding where the phase form read the clamped upsample, so the ring
+// pixels take  y = (phase value - corr) + bias  with corr = sum over ci of the
+// out-of-image taps w[c][ci][ky][kx] * up(ci, clamp(Y + ky - 1), clamp(X + kx - 1))
+// (the arithmetic of edge_fix_h8_kernel, conv_f16.hip, which runs as a separate
+// launch for the other configs).  Ring segment seg of (image, co block): top / bottom
+// row under tile column tx (seg tx / tiles_x + tx: X in [64 tx, 64 tx + 64)), left /
+// right column beside tile row ty (2 tiles_x + ty / 2 tiles_x + tiles_y + ty:
+// Y in [16 ty, 16 ty + 16) within [1, H - 2]); 8 real channels (the co block).
+struct RingSeg {
+  int line, idx, np;  // line 0 top 1 bottom 2 left 3 right; tile column / row; pixels (64 / 16)
+  int Y0, X0;         // first pixel
+  int lo, hi;         // valid pixel positions [lo, hi) along the line
+};
+__device__ inline RingSeg ring_seg(const ConvH8Args& a, int seg) {
+  RingSeg r;
+  const int H = 2 * a.h, W = 2 * a.w;
+  if (seg < 2 * a.tiles_x) {
+    r.line = seg < a.tiles_x ? 0 : 1;
+    r.idx = seg - r.line * a.tiles_x;
+    r.np = 64;
+    r.X0 = 64 * r.idx;
+    r.Y0 = r.line == 0 ? 0 : H - 1;
+    r.lo = 0;
+    r.hi = min(64, W - r.X0);
+  } else {
+    const int t = seg - 2 * a.tiles_x;
+    r.line = t < a.tiles_y ? 2 : 3;
+    r.idx = t - (r.line - 2) * a.tiles_y;
+    r.np = 16;
+    r.Y0 = 16 * r.idx;
+    r.X0 = r.line == 2 ? 0 : W - 1;
+    r.lo = max(0, 1 - r.Y0);
+    r.hi = max(r.lo, min(16, H - 1 - r.Y0));
+  }
+  return r;
+}
+// bilinear x2 upsample (align_corners = False, edge clamp) of channel ci of image img
+// at output pixel (Y, X), in upsample_bilinear2d's order (edge_fix_h8_kernel's Up8)
+__device__ inline float ring_up(const ConvH8Args& a, int img, int ci, int Y, int X) {
+  int ra, rb, ca, cb;
+  float wa, wc;
+  if (Y & 1) { ra = Y >> 1; rb = min(ra + 1, a.h - 1); wa = 0.75f; }
+  else { rb = Y >> 1; ra = max(rb - 1, 0); wa = 0.25f; }
+  if (X & 1) { ca = X >> 1; cb = min(ca + 1, a.w - 1); wc = 0.75f; }
+  else { cb = X >> 1; ca = max(cb - 1, 0); wc = 0.25f; }
+  const float* src = reinterpret_cast<const float*>(a.src_hi + (int64_t)img * a.src_img + (int64_t)(ci >> 2) * a.src_gp +
+                                                    kH8PadLeft) + (ci & 3);
+  const float v0 = src[((int64_t)(ra + 1) * a.src_wp + ca) * 4], v1 = src[((int64_t)(ra + 1) * a.src_wp + cb) * 4];
+  const float v2 = src[((int64_t)(rb + 1) * a.src_wp + ca) * 4], v3 = src[((int64_t)(rb + 1) * a.src_wp + cb) * 4];
+  const float wb = 1.0f - wa, wd = 1.0f - wc;
+  const float top = wc * v0 + wd * v1;
+  const float bot = wc * v2 + wd * v3;
+  return wa * top + wb * bot;
+}
+// segment (img, cob, seg) done by both of its writers: the later one writes its ring
+// pixels, (phase value - corr) + bias, from the edge and corr scratch (after the
+// caller's agent-scope acquire)
+__device__ inline void ring_combine(const ConvH8Args& a, int img, int cob, int seg, int tid) {
+  const RingSeg r = ring_seg(a, seg);
+  const int p = tid & (r.np - 1), c = tid / r.np;
+  if (c >= 8 || p < r.lo || p >= r.hi) return;
+  const int H = 2 * a.h, W = 2 * a.w, creal = a.cout >> 2;
+  const int Y = r.line < 2 ? r.Y0 : r.Y0 + p, X = r.line < 2 ? r.X0 + p : r.X0;
+  const int ch = cob * 8 + c;
+  // sc1 loads (write-through stores of other workgroups, possibly on other XCDs)
+  const auto er = __builtin_amdgcn_make_buffer_rsrc(a.edge, 0, 0x7fffffff, 0x00020000);
+  const float e = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+      er, (int)((((int64_t)img * creal + ch) * a.ring + ring_index(Y, X, H, W)) * 4), 0, 16));
+  float* slab = a.corr + ((int64_t)(img * a.co_blocks + cob) * a.nseg + seg) * 512;
+  const auto cr = __builtin_amdgcn_make_buffer_rsrc(slab, 0, 512 * 4, 0x00020000);
+  const float corr = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(cr, (c * r.np + p) * 4, 0, 16));
+  float* dst = reinterpret_cast<float*>(a.dst_hi);
+  dst[(((int64_t)img * a.dst_img + (int64_t)(ch >> 2) * a.dst_gp + (int64_t)(Y + 1) * a.dst_wp + X + kH8PadLeft) << 2) +
+      (ch & 3)] = (e - corr) + a.bias_raw[ch];
+}
+// one ticket of segment (img, cob, seg) by lane 0 (after every wave drained its
+// write-through stores and the barrier); returns on every thread whether this
+// workgroup was the segment's second writer (then after an agent-scope acquire)
+__device__ inline bool ring_ticket(const ConvH8Args& a, int img, int cob, int seg, int tid, int* s_flag) {
+  if (tid == 0) {
+    int* cnt = a.rcnt + (img * a.co_blocks + cob) * a.nseg + seg;
+    const int last = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1;
+    if (last) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+    *s_flag = last;
+  }
+  __syncthreads();
+  const bool last = *s_flag != 0;
+  __syncthreads();  // s_flag reusable
+  // every load of the handed-off values is an sc1 load (ring_combine): no agent-scope
+  // acquire (it would drop this CU's cached lines), only the compiler-ordering fence
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  return last;
+}
+// correction workgroup rb (< n * co_blocks * nseg; 512 threads): corr of its segment,
+// 64 input channels per LDS stage (the segment's upsampled line +-1 and the two corner
+// values, the 9 taps x 8 channels of weights: 36 KB), so a stage is one round of loads
+__device__ inline void ring_block(const ConvH8Args& a, int rb, float* sm) {
+  const int tid = threadIdx.x;
+  const int seg = rb % a.nseg, t = rb / a.nseg, cob = t % a.co_blocks, img = t / a.co_blocks;
+  const RingSeg r = ring_seg(a, seg);
+  if (r.lo >= r.hi) return;  // an empty column segment (its conv tile does not count it either)
+  const int H = 2 * a.h, W = 2 * a.w, creal = a.cout >> 2;
+  const bool row = r.line < 2;
+  const int nl = r.np + 2;           // staged line: positions -1 .. np
+  constexpr int RC = 64;             // input channels per LDS stage (one load round per stage)
+  float* s_l = sm;                   // [RC][nl]
+  float* s_e = sm + RC * 66;         // [RC][2] corner extras (row lines)
+  float* s_w = s_e + RC * 2;         // [RC ci][9 taps][8 c]
+  const int p = tid & (r.np - 1), c = tid / r.np;
+  const bool act = c < 8 && p >= r.lo && p < r.hi;
+  const int X = row ? r.X0 + p : r.X0;
+  // extras: the second row in (top: 1, bottom: H - 2) at the corner columns
+  const int Ye = r.line == 0 ? min(1, H - 1) : max(H - 2, 0);
+  float acc = 0.f;
+  for (int c0 = 0; c0 < a.cin; c0 += RC) {
+    const int nc = min(RC, a.cin - c0);
+    for (int i = tid; i < nc * nl; i += 512) {
+      const int ci = i / nl, j = i - ci * nl;
+      const int Yv = row ? r.Y0 : min(max(r.Y0 - 1 + j, 0), H - 1);
+      const int Xv = row ? min(max(r.X0 - 1 + j, 0), W - 1) : r.X0;
+      s_l[ci * nl + j] = ring_up(a, img, c0 + ci, Yv, Xv);
+    }
+    if (row && tid < 2 * nc) s_e[tid] = ring_up(a, img, c0 + (tid >> 1), Ye, (tid & 1) ? W - 1 : 0);
+    for (int i = tid; i < nc * 72; i += 512) {
+      const int ci = i / 72, tap = (i / 8) % 9, cc = i & 7;
+      s_w[i] = cob * 8 + cc < creal ? a.wedge[((int64_t)(c0 + ci) * 9 + tap) * creal + cob * 8 + cc] : 0.f;
+    }
+    __syncthreads();
+    if (act) {
+      for (int ci = 0; ci < nc; ++ci) {
+        const float* l = s_l + ci * nl;
+        const float* w = s_w + ci * 72 + c;
+        if (r.line == 0 || r.line == 1) {  // the outside kernel row ky (0 top, 2 bottom), then the corners
+          const int ky = r.line == 0 ? 0 : 2;
+#pragma unroll
+          for (int kx = 0; kx < 3; ++kx) acc = fmaf(w[(ky * 3 + kx) * 8], l[p + kx], acc);
+          if (X == 0) {
+            acc = fmaf(w[((r.line == 0 ? 1 : 0) * 3) * 8], r.line == 0 ? l[p] : s_e[ci * 2], acc);
+            acc = fmaf(w[((r.line == 0 ? 2 : 1) * 3) * 8], r.line == 0 ? s_e[ci * 2] : l[p], acc);
+          }
+          if (X == W - 1) {
+            acc = fmaf(w[((r.line == 0 ? 1 : 0) * 3 + 2) * 8], r.line == 0 ? l[p + 2] : s_e[ci * 2 + 1], acc);
+            acc = fmaf(w[((r.line == 0 ? 2 : 1) * 3 + 2) * 8], r.line == 0 ? s_e[ci * 2 + 1] : l[p + 2], acc);
+          }
+        } else {  // the outside kernel column kx (0 left, 2 right)
+          const int kx = r.line == 2 ? 0 : 2;
+#pragma unroll
+          for (int ky = 0; ky < 3; ++ky) acc = fmaf(w[(ky * 3 + kx) * 8], l[p + ky], acc);
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (act) {
+    float* slab = a.corr + ((int64_t)(img * a.co_blocks + cob) * a.nseg + seg) * 512;
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(slab, 0, 512 * 4, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc), rsrc, (c * r.np + p) * 4, 0, 16 /* sc1 */);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (ring_ticket(a, img, cob, seg, tid, reinterpret_cast<int*>(sm + 9216))) ring_combine(a, img, cob, seg, tid);
+}
+
 //
 // SK (split-K, a.ksplit > 1): the grid has a.ksplit blocks per tile, slice ks running
 // chunks [ks * a.kper, ..).  After its output transform a slice stores its pre-bias
@@ -777,8 +943,14 @@ static_assert(2 * kWinoQLds <= 160 * 1024, "two blocks per CU");
 // does not depend on which slice finished last), resets the counter and runs the
 // epilogue.  A different association of the K sum than one slice (not bitwise equal to
 // cfg 20), fixed per conv: batch and per-sample outputs stay bitwise equal.
-template <int EPI, int ABL = 0, int PT = 2, int SK = 0>
+//
+// RF (EPI_SUBPIXEL, PT 2, no split): the ring fold -- the first a.nring workgroups of the
+// grid are ring correction blocks (ring_block), the rest the conv tiles; a tile on the
+// image border stores its ring values write-through and counts itself in the ticket of
+// each ring segment it covers (ring_combine by the later writer).
+template <int EPI, int ABL = 0, int PT = 2, int SK = 0, int RF = 0>
 __global__ __launch_bounds__(256 * PT, 2) void conv3x3_winoq_kernel(ConvH8Args a) {
+  static_assert(!RF || (EPI == RRIN_EPI_SUBPIXEL && PT == 2 && !SK), "ring fold: 8-wave sub-pixel conv");
   constexpr int NT = 256 * PT, TH = 4 * PT;
   constexpr int RG = (TH + 2) * kWnRawCols, RAW = 2 * RG, STAGE = RAW + kWnU;
   static_assert(RAW > NT && RAW <= 2 * NT && kWnU % NT == 0, "two raw pieces, whole U pieces");
@@ -788,10 +960,22 @@ __global__ __launch_bounds__(256 * PT, 2) void conv3x3_winoq_kernel(ConvH8Args a
   // kWqStages stages of [raw RAW | U 1024] records
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int yw = wv & 3, pt = wv >> 2, j = lane & 31, hh = lane >> 5;
+  // RF: groups of 8 ring blocks (one per XCD) at the head of every a.rstride workgroups,
+  // so the dispatcher interleaves them with the tiles; the tiles' index space skips them
+  int cidx = blockIdx.x;
+  if constexpr (RF) {
+    const int g = blockIdx.x / a.rstride, off = blockIdx.x - g * a.rstride, ng = a.nring >> 3;
+    if (g < ng && off < 8) {
+      const int rb = 8 * g + off;
+      if (rb < a.n * a.co_blocks * a.nseg) ring_block(a, rb, reinterpret_cast<float*>(smem4));
+      return;
+    }
+    cidx -= 8 * min(g + 1, ng);
+  }
   int bid;
   {
-    const int nwg = gridDim.x, q = nwg >> 3, r = nwg & 7;
-    const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+    const int nwg = gridDim.x - (RF ? a.nring : 0), q = nwg >> 3, r = nwg & 7;
+    const int xcd = cidx & 7, slot = cidx >> 3;
     bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
   }
   const int ntiles = a.co_blocks * a.tiles_x * a.tiles_y * a.n;
@@ -939,7 +1123,8 @@ __global__ __launch_bounds__(256 * PT, 2) void conv3x3_winoq_kernel(ConvH8Args a
   for (int c = 0; c < nch; ++c) {
     if constexpr (NS == 3) {
       wait_chunk(c + 1 < nch);
-      __syncthreads();
+      // bare barrier: __syncthreads() would drain vmcnt to 0 and wait for chunk c + 1 too
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       if (c + 2 < nch) issue(c + 2, (c + 2) % 3);
       chunk(c % 3, c == 0);
     } else {
@@ -999,11 +1184,10 @@ __global__ __launch_bounds__(256 * PT, 2) void conv3x3_winoq_kernel(ConvH8Args a
   if constexpr (SK) {
     // slice partial: plane q of the slice = NT lanes x 4 floats (coalesced per wave).
     // Split-K seam (cdna_hip_programming.md, split-K reduction recipe, sc1 form): the slice
-    // drawing ksn - 1 reduces after ONE agent-scope acquire.  Correct for any placement of
-    // a tile's slices over CUs / XCDs.
+    // drawing ksn - 1 reduces, reading every slab with sc1 loads.  Correct for any
+    // placement of a tile's slices over CUs / XCDs.
     // The slab stores are write-through (sc1), so no release fence: every wave drains, the
     // barrier, then lane 0's relaxed ticket.
-    float4* pp = reinterpret_cast<float4*>(a.part) + (int64_t)(tile * ksn) * 4 * NT + tid;
     {
       float* slab = a.part + (int64_t)(tile * ksn) * 4 * NT * 4;  // block-uniform base
       const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(slab, 0, ksn * 4 * NT * 16, 0x00020000);
@@ -1022,20 +1206,26 @@ __global__ __launch_bounds__(256 * PT, 2) void conv3x3_winoq_kernel(ConvH8Args a
     if (tid == 0) {
       const int old = __hip_atomic_fetch_add(a.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const int last = old == ksn - 1;
-      if (last) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(a.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
-      }
+      if (last) __hip_atomic_store(a.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
       *s_last = last;
     }
     __syncthreads();
     if (!*s_last) return;
+    // the slabs are read with sc1 loads (no agent-scope acquire, which would drop this
+    // CU's cached lines); the wavefront fence only keeps the loads below the ticket
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const auto srs = __builtin_amdgcn_make_buffer_rsrc(a.part + (int64_t)(tile * ksn) * 4 * NT * 4, 0,
+                                                       ksn * 4 * NT * 16, 0x00020000);
+    auto ld = [&](int k, int q) {
+      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(srs, ((k * 4 + q) * NT + tid) * 16, 0, 16);
+      return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
+    };
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      float4 sum = pp[(int64_t)q * NT];
+      float4 sum = ld(0, q);
       for (int k = 1; k < ksn; ++k) {
-        const float4 v = pp[(int64_t)(k * 4 + q) * NT];
+        const float4 v = ld(k, q);
         sum.x += v.x;
         sum.y += v.y;
         sum.z += v.z;
@@ -1056,12 +1246,39 @@ __global__ __launch_bounds__(256 * PT, 2) void conv3x3_winoq_kernel(ConvH8Args a
         const int64_t ri = ring_index(Y, XX, HH, WW);
         if (ri >= 0) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) a.edge[((int64_t)img * creal + cob * 8 + 4 * hh + e) * a.ring + ri] = yv[4 * qq + e];
+          for (int e = 0; e < 4; ++e) {
+            const int64_t k = ((int64_t)img * creal + cob * 8 + 4 * hh + e) * a.ring + ri;
+            if constexpr (RF) {  // write-through: the segment's other writer may combine it
+              const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(a.edge, 0, 0x7fffffff, 0x00020000);
+              __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(yv[4 * qq + e]), rsrc, (int)(k * 4), 0, 16);
+            } else {
+              a.edge[k] = yv[4 * qq + e];
+            }
+          }
         } else {
           float vv[4];
 #pragma unroll
           for (int e = 0; e < 4; ++e) vv[e] = yv[4 * qq + e] + a.bias[cob * 32 + 8 * qq + 4 * hh + e];
           store4((int64_t)(2 * cob + hh) * a.dst_gp + (int64_t)(Y + 1) * a.dst_wp + XX + kH8PadLeft, vv);
+        }
+      }
+    }
+    if constexpr (RF) {
+      // the ring segments this tile writes (its tile column's top / bottom row, its tile
+      // row's left / right column): one ticket each, the later writer combines
+      const int tx = x0 >> 5, ty = y0 / TH;
+      const bool on[4] = {ty == 0, ty == a.tiles_y - 1, tx == 0, tx == a.tiles_x - 1};
+      if (on[0] || on[1] || on[2] || on[3]) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        int* s_flag = reinterpret_cast<int*>(smem4 + 2048);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (!on[k]) continue;
+          const int seg = k == 0 ? tx : k == 1 ? a.tiles_x + tx : k == 2 ? 2 * a.tiles_x + ty : 2 * a.tiles_x + a.tiles_y + ty;
+          const RingSeg rs = ring_seg(a, seg);
+          if (rs.lo >= rs.hi) continue;  // empty column segment: no ring block counts it either
+          if (ring_ticket(a, img, cob, seg, tid, s_flag)) ring_combine(a, img, cob, seg, tid);
         }
       }
     }
@@ -1120,13 +1337,13 @@ __global__ __launch_bounds__(256 * PT, 2) void conv3x3_winoq_kernel(ConvH8Args a
   }
 }
 
-template <int EPI, int ABL = 0, int PT = 2, int SK = 0>
+template <int EPI, int ABL = 0, int PT = 2, int SK = 0, int RF = 0>
 static int launch_winoq_k(const ConvH8Args& a, hipStream_t st) {
-  auto k = conv3x3_winoq_kernel<EPI, ABL, PT, SK>;
+  auto k = conv3x3_winoq_kernel<EPI, ABL, PT, SK, RF>;
   static LdsAttr attr;
   constexpr size_t lds = (size_t)(PT == 2 ? kWqStages : 2) * (2 * (4 * PT + 2) * kWnRawCols + kWnU) * 16;
   if (int e = attr.ensure((const void*)k, (int)lds, st)) return e;
-  const int64_t grid = (int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n * (SK ? a.ksplit : 1);
+  const int64_t grid = (int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n * (SK ? a.ksplit : 1) + (RF ? a.nring : 0);
   hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256 * PT), lds, st, a);
   return hip_code(hipGetLastError());
 }
@@ -1145,6 +1362,10 @@ static int launch_winoq_sk(const ConvH8Args& a, int epi, hipStream_t st) {
 
 int launch_winoq(const ConvH8Args& a, int epi, int th, hipStream_t st) {
   if (a.ksplit > 1) return th == 4 ? launch_winoq_sk<1>(a, epi, st) : launch_winoq_sk<2>(a, epi, st);
+  if (a.nring > 0) {
+    if (th != 8 || epi != RRIN_EPI_SUBPIXEL) return RRIN_E_CONFIG;
+    return launch_winoq_k<RRIN_EPI_SUBPIXEL, 0, 2, 0, 1>(a, st);
+  }
   if (th == 4) {
     switch (epi) {
       case RRIN_EPI_LINEAR: return launch_winoq_k<RRIN_EPI_LINEAR, 0, 1>(a, st);

@@ -63,6 +63,9 @@ struct Plan {
   Buf FLOWRAW;            // raw 4-ch Flow output, kept for reuse across t (skip_flow)
   float* PART;            // F32R: split-K slice outputs of the current conv (kPartFloats)
   int32_t* CNT;           // F32R: split-K tile counters (kPartTiles; zero between convs)
+  float* RCORR;           // F32R: ring-fold corrections of the current sub-pixel conv
+  int32_t* RCNT;          // F32R: ring-fold segment tickets (zero between convs)
+  int64_t rcorr_floats, rcnt_ints;
   int64_t bytes;
 };
 
@@ -126,7 +129,22 @@ void make_plan(int n, int h, int w, int prec, char* base, Plan& p) {
   p.FLOWRAW = take(f32 ? 4 : cpr, p.g[0]);
   p.PART = nullptr;
   p.CNT = nullptr;
+  p.RCORR = nullptr;
+  p.RCNT = nullptr;
+  p.rcorr_floats = p.rcnt_ints = 0;
   if (prec == RRIN_PREC_F32R) {
+    // ring fold of the sub-pixel up conv into level L (runs on level L + 1's grid, 4 C_L
+    // phase rows): 512 floats and one ticket per ring segment, co block and image
+    for (int L = 0; L < kMaxDepth - 1; ++L) {
+      const int64_t hl = h >> (L + 1), wl = w >> (L + 1);
+      const int64_t segs = (int64_t)n * (4 * chans(L) / 32) * (2 * ((wl + 31) / 32) + 2 * ((hl + 7) / 8));
+      p.rcnt_ints = segs > p.rcnt_ints ? segs : p.rcnt_ints;
+    }
+    p.rcorr_floats = 512 * p.rcnt_ints;
+    p.RCORR = base ? reinterpret_cast<float*>(base + off) : nullptr;
+    off += align256(p.rcorr_floats * 4);
+    p.RCNT = base ? reinterpret_cast<int32_t*>(base + off) : nullptr;
+    off += align256(p.rcnt_ints * 4);
     p.PART = base ? reinterpret_cast<float*>(base + off) : nullptr;
     off += align256(kPartFloats * 4);
     p.CNT = base ? reinterpret_cast<int32_t*>(base + off) : nullptr;
@@ -279,7 +297,7 @@ int run_unet(const Plan& p, const UNetSpec& u, const rrin_conv_weights* cw, cons
 }
 
 int conv_h8(const Plan& p, const rrin_conv_weights& cw, int cin, int cout, int epi, const rrin_h8& src,
-            const rrin_h8& dst, const rrin_h8* pool, hipStream_t st, float* edge = nullptr) {
+            const rrin_h8& dst, const rrin_h8* pool, hipStream_t st, float* edge = nullptr, bool ring_fold = false) {
   // algorithmic FLOPs of the conv (a sub-pixel conv has 4 phase rows per real channel): 9
   // multiply-adds per output and input channel in the direct form, 4 in Winograd F(2x2,3x3)
   // (16 per 2x2 patch)
@@ -305,6 +323,16 @@ int conv_h8(const Plan& p, const rrin_conv_weights& cw, int cin, int cout, int e
   d.bias = cw.bias;
   d.edge = edge;
   d.status = p.status;
+  if (ring_fold) {
+    d.ring_w = cw.wedge;
+    d.ring_bias = cw.bias_raw;
+    d.ring_corr = p.RCORR;
+    d.ring_cnt = p.RCNT;
+    int64_t cnt = 0;
+    const int64_t need = rrin_conv_h8_ring_floats(&d, &cnt);
+    if (need < 0) return (int)need;
+    if (need > p.rcorr_floats || cnt > p.rcnt_ints) return RRIN_E_CONFIG;
+  }
   if (cw.ksplit > 1) {
     if (!p.PART) return RRIN_E_CONFIG;
     d.ksplit = cw.ksplit;
@@ -322,6 +350,10 @@ int conv_h8(const Plan& p, const rrin_conv_weights& cw, int cin, int cout, int e
 // edge-replicated) -> CAT[L][0, C), then the ring fix-up.
 int upconv_subpixel(const Plan& p, const rrin_conv_weights& cw, int C, const rrin_h8& x, const rrin_h8& up,
                     hipStream_t st) {
+  if (cw.subpixel == 2) {  // ring folded into the conv (Winograd kind 3, no split)
+    if (!p.RCORR || rrin_conv_h8_cfg_wino(cw.cfg) != 3 || cw.ksplit > 1) return RRIN_E_CONFIG;
+    return conv_h8(p, cw, 2 * C, 4 * C, RRIN_EPI_SUBPIXEL, x, up, nullptr, st, p.EDGE, true);
+  }
   RRIN_TRY(conv_h8(p, cw, 2 * C, 4 * C, RRIN_EPI_SUBPIXEL, x, up, nullptr, st, p.EDGE));
   rrin_edge_fix_desc e;
   memset(&e, 0, sizeof(e));

@@ -198,6 +198,16 @@ WINO_SPLIT = {"small": {3: 2, 4: 4}}
 WINO_SPLIT_LEVELS = {}
 
 
+# Sub-pixel ring fold (rrin_conv_weights.subpixel = 2): the ring fix-up of an
+# exact-fp32 sub-pixel up conv runs inside its Winograd launch (kind 3, no split)
+# instead of as rrin_subpixel_edge_fix_h8.  Correct (tests/test_gpu_ringfold.py) but
+# slower (profiles/r03/ringfold_ab.txt: 1280x720 x 4 121.6-122.0 vs 128.8-129.3
+# pairs/s, conv busy +2 ms per step; 1280x720 x 1 108.2 vs 110.4; 640x368 x 1 equal):
+# the correction workgroups hold full conv slots for latency-bound ring work that the
+# separate launch runs beside the other stream's convs.  Off; the A/B knob stays.
+RING_FOLD = False
+
+
 def choose_split(cin: int, cout: int, level: int, size: str, cfg: int) -> int:
     """Slices of the split-K for this conv (0: none)."""
     if _lib.lib().rrin_conv_h8_cfg_wino(cfg) not in (3, 4):
@@ -475,12 +485,22 @@ class RRINEngine:
         ks = [choose_split(cin, cout, level, size, cfg)
               for (_, _, cin, cout, level, _, _), cfg in zip(self._h8_convs, cfgs)]
         if not any(ks):
+            self._set_fold(table, cfgs)
             return p
         t2 = (_lib.ConvWeights * len(table))()
         C.memmove(t2, table, C.sizeof(table))
         for i, k in enumerate(ks):
             t2[i].ksplit = k
+        self._set_fold(t2, cfgs)
         return (blob, bias_blob, t2, cfgs)
+
+    def _set_fold(self, table, cfgs):
+        """subpixel = 2 (ring folded into the conv) where the conv can fold, else 1."""
+        for i, cfg in enumerate(cfgs):
+            if table[i].subpixel:
+                fold = (RING_FOLD and self.prec == _lib.PREC_F32R and table[i].ksplit <= 1
+                        and self.lib.rrin_conv_h8_cfg_wino(cfg) == 3)
+                table[i].subpixel = 2 if fold else 1
 
     force_size_class = None  # A/B knob: use this tile-table class for every forward part
 

@@ -291,8 +291,10 @@ def test_h8_leaky_rep_writes_replicated_ring(gpu, prec):
         assert dst.hi[:, :, 0, 7:9 + dst.w].any() and dst.hi[:, :, 1:dst.h + 1, 7].any()
 
 
-def subpixel_upconv(src: H8Tensor, w, b, cfg, prec, dst=None, ksplit=0, keep=None):
-    """EPI_SUBPIXEL conv + ring fix-up through the C ABI (the Net's up.1 conv)."""
+def subpixel_upconv(src: H8Tensor, w, b, cfg, prec, dst=None, ksplit=0, keep=None, fold=False):
+    """EPI_SUBPIXEL conv + ring fix-up through the C ABI (the Net's up.1 conv); fold: the
+    ring in the conv launch (rrin_conv_h8_desc.ring_w, Winograd kind 3) instead of
+    rrin_subpixel_edge_fix_h8."""
     lib = _lib.lib()
     dev = src.hi.device
     cout, cin = w.shape[:2]
@@ -312,10 +314,23 @@ def subpixel_upconv(src: H8Tensor, w, b, cfg, prec, dst=None, ksplit=0, keep=Non
     d.src, d.dst = src.view(0, cin), dst.view(0, cout)
     d.whi, d.wlo, d.bias = whi.data_ptr(), wlo.data_ptr() if prec == X3 else None, bp.data_ptr()
     d.edge = edge.data_ptr()
-    set_split(d, ksplit, dev, keep if keep is not None else [])
-    _lib.check(lib.rrin_conv3x3_h8_fwd(C.byref(d), H.stream(dev)), "rrin_conv3x3_h8_fwd(subpixel)")
+    keep = keep if keep is not None else []
+    set_split(d, ksplit, dev, keep)
     wedge = torch.from_numpy(np.ascontiguousarray(wn.transpose(1, 2, 3, 0))).to(dev)
     braw = torch.from_numpy(bn.copy()).to(dev)
+    if fold:
+        d.ring_w, d.ring_bias = wedge.data_ptr(), braw.data_ptr()
+        nc = C.c_int64()
+        nf = lib.rrin_conv_h8_ring_floats(C.byref(d), C.byref(nc))
+        assert nf > 0 and nc.value > 0, nf
+        corr = torch.full((nf,), float("nan"), device=dev)
+        cnt = torch.zeros(nc.value, dtype=torch.int32, device=dev)
+        d.ring_corr, d.ring_cnt = corr.data_ptr(), cnt.data_ptr()
+        keep.extend([corr, cnt])
+        _lib.check(lib.rrin_conv3x3_h8_fwd(C.byref(d), H.stream(dev)), "rrin_conv3x3_h8_fwd(subpixel, fold)")
+        torch.cuda.synchronize(dev)
+        return dst
+    _lib.check(lib.rrin_conv3x3_h8_fwd(C.byref(d), H.stream(dev)), "rrin_conv3x3_h8_fwd(subpixel)")
     e = _lib.EdgeFixDesc()
     e.n, e.cin, e.cout, e.prec, e.epi_mode, e.slope = src.n, cin, cout, prec, _lib.EPI_LINEAR, 0.1
     e.src, e.dst = src.view(0, cin), dst.view(0, cout)
