@@ -758,6 +758,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wino64_kernel(ConvH8Args a) {
 #ifndef RRIN_WINOQ_STAGES
 #define RRIN_WINOQ_STAGES 2
 #endif
+#ifndef RRIN_WINOQ_PRIO
+#define RRIN_WINOQ_PRIO 0  // A/B builds only: 1 s_setprio around each MFMA cluster, 2 static for waves 4-7
+#endif
 constexpr int kWqStages = RRIN_WINOQ_STAGES;
 constexpr int kWqStage = kWnRaw + kWnU;  // records per stage of the 8-wave tile (raw 680 + U 1024)
 static_assert(kWinoQLds >= (size_t)kWqStages * kWqStage * 16, "LDS size");
@@ -1076,6 +1079,9 @@ __global__ __launch_bounds__(256 * PT, 2) void conv3x3_winoq_kernel(ConvH8Args a
       v[3] = t[1] - t[3];
     }
     const uint4* su = smem4 + b * STAGE + RAW + su0;
+#if RRIN_WINOQ_PRIO == 1
+    __builtin_amdgcn_s_setprio(1);  // A/B: priority around the MFMA cluster (guide T5)
+#endif
 #pragma unroll
     for (int x = 0; x < 4; ++x) {
       wfloatx4 u;
@@ -1095,7 +1101,14 @@ __global__ __launch_bounds__(256 * PT, 2) void conv3x3_winoq_kernel(ConvH8Args a
         }
       }
     }
+#if RRIN_WINOQ_PRIO == 1
+    __builtin_amdgcn_s_setprio(0);
+#endif
   };
+#if RRIN_WINOQ_PRIO == 2
+  // A/B: static priority for the younger half of the workgroup (guide T5, static form)
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
+#endif
   // kWqStages = 3 (A/B builds; 1-10 % slower than 2 stages on every shape,
   // profiles/r03/ab_winoq_stages.txt): the DMA of chunk c + 2 is issued at the
   // top of chunk c, so a chunk has two chunk-times to land.  At the top of chunk c a wave waits for
