@@ -64,15 +64,3 @@ clean:
 	rm -rf build $(LIB) $(LAB) $(LAB32) $(PKV)
 
 .PHONY: all lab clean resource pk-variants
-
-# Persistent-grid threshold A/B (tools/gpu_pers_ab.sh): tiles per block slot from
-# which the Winograd grid is persistent (product: never)
-PERSV := rrin_amd/librrin_hip_pers3.so rrin_amd/librrin_hip_pers8.so
-pers-variants: $(PERSV)
-
-rrin_amd/librrin_hip_pers%.so: $(SRCS) $(SRC_DIR)/common.hpp include/rrin_hip.h
-	$(HIPCC) $(CXXFLAGS) -DRRIN_WINO_PERS_MIN=$* -shared -o $@ $(SRCS)
-
-# persistent with 1 block per CU per launch (the other stream's launch holds the other slot)
-rrin_amd/librrin_hip_pers%b1.so: $(SRCS) $(SRC_DIR)/common.hpp include/rrin_hip.h
-	$(HIPCC) $(CXXFLAGS) -DRRIN_WINO_PERS_MIN=$* -DRRIN_WINO_PERS_BPC=1 -shared -o $@ $(SRCS)
