@@ -60,11 +60,15 @@ H8_TUNED = {
                       (128, 64, 1): 10, (128, 128, 2): 11, (128, 256, 2): 10, (128, 256, 3): 11,
                       (256, 128, 2): 11, (256, 256, 3): 11, (256, 512, 3): 11, (256, 512, 4): 1,
                       (512, 256, 3): 11, (512, 512, 4): 1},
-    _lib.PREC_F16: {(6, 32, 0): 15, (9, 32, 0): 13, (10, 32, 0): 15, (16, 32, 0): 9, (32, 32, 0): 9,
-                    (32, 64, 1): 10, (64, 32, 0): 9, (64, 64, 1): 9, (64, 128, 1): 10, (64, 128, 2): 11,
-                    (128, 64, 1): 0, (128, 128, 2): 11, (128, 256, 2): 11, (128, 256, 3): 10,
-                    (256, 128, 2): 11, (256, 256, 3): 10, (256, 512, 3): 11, (256, 512, 4): 4,
-                    (512, 256, 3): 5, (512, 512, 4): 4},
+    # fp16: re-swept in round 3 at the BASELINE C3 part size, 1280x736 x 2
+    # (profiles/r03/tune_fp16_1280x736x2.json: schedule sum 4.413 -> 4.283 ms; the 512->256
+    # L3 up conv 0.222 -> 0.141 ms); C3 bench 466.6-469.1 -> 470.6-477.7 pairs/s in
+    # interleaved runs (profiles/r03/fp16_table_ab.txt)
+    _lib.PREC_F16: {(6, 32, 0): 9, (9, 32, 0): 9, (10, 32, 0): 9, (16, 32, 0): 13, (32, 32, 0): 9,
+                    (32, 64, 1): 10, (64, 32, 0): 9, (64, 64, 1): 10, (64, 128, 1): 11, (64, 128, 2): 10,
+                    (128, 64, 1): 11, (128, 128, 2): 11, (128, 256, 2): 11, (128, 256, 3): 11,
+                    (256, 128, 2): 10, (256, 256, 3): 11, (256, 512, 3): 10, (256, 512, 4): 4,
+                    (512, 256, 3): 10, (512, 512, 4): 4},
 }
 
 # Smaller work per forward part leaves the deep levels with a few dozen BM 64 x
