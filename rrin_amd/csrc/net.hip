@@ -11,10 +11,17 @@
 using namespace rrin;
 
 struct rrin_prof {
-  std::vector<hipEvent_t> ev;  // 2 per launch
+  std::vector<hipEvent_t> ev;  // 2 per launch: start (recorded or shared), end
+  std::vector<int32_t> start;  // per launch: index in ev of its start event
   std::vector<int32_t> kind;
   std::vector<double> flops;
   int count = 0;
+  // within one rrin_net_fwd / rrin_unet_fwd call every launch on its stream is
+  // bracketed, so a launch that directly follows the previous one on the same
+  // stream starts at that launch's end event: one event record per launch
+  bool chain = false;  // last_st / last_slot describe the call's previous launch
+  hipStream_t last_st = nullptr;
+  int last_slot = -1;
 };
 
 namespace {
@@ -188,11 +195,21 @@ struct ProfScope {
       slot = p->count++;
       p->kind[slot] = kind;
       p->flops[slot] = flops;
-      (void)hipEventRecord(p->ev[2 * slot], st);
+      if (p->chain && slot > 0 && p->last_st == st && p->last_slot == slot - 1) {
+        p->start[slot] = 2 * (slot - 1) + 1;  // the previous launch's end on this stream
+      } else {
+        p->start[slot] = 2 * slot;
+        (void)hipEventRecord(p->ev[2 * slot], st);
+      }
     }
   }
   ~ProfScope() {
-    if (slot >= 0) (void)hipEventRecord(p->ev[2 * slot + 1], st);
+    if (slot >= 0) {
+      (void)hipEventRecord(p->ev[2 * slot + 1], st);
+      p->chain = true;
+      p->last_st = st;
+      p->last_slot = slot;
+    }
   }
 };
 
@@ -475,6 +492,7 @@ extern "C" int rrin_net_fwd(const rrin_net_desc* d, void* stream) {
   make_plan(d->n, d->h, d->w, d->prec, reinterpret_cast<char*>(d->workspace), p);
   if (d->workspace_bytes < p.bytes) return RRIN_E_WORKSPACE;
   p.prof = d->prof;  // per call: concurrent calls never share launch state
+  if (p.prof) p.prof->chain = false;  // the call's first launch records its own start
   hipStream_t st = (hipStream_t)stream;
   if (d->status && (d->prec == RRIN_PREC_F16X3 || d->prec == RRIN_PREC_F16)) {
     p.status = d->status;
@@ -542,6 +560,7 @@ extern "C" int rrin_unet_fwd(const rrin_unet_desc* d, void* stream) {
   make_plan(d->n, d->h, d->w, d->prec, reinterpret_cast<char*>(d->workspace), p);
   if (d->workspace_bytes < p.bytes) return RRIN_E_WORKSPACE;
   p.prof = d->prof;
+  if (p.prof) p.prof->chain = false;
   hipStream_t st = (hipStream_t)stream;
   if (d->status && (d->prec == RRIN_PREC_F16X3 || d->prec == RRIN_PREC_F16)) {
     p.status = d->status;  // fp16 range guard, as rrin_net_fwd
@@ -572,6 +591,7 @@ extern "C" int rrin_prof_create(int32_t capacity, rrin_prof** out) {
   if (!out || capacity < 1) return RRIN_E_ARG;
   rrin_prof* p = new rrin_prof();
   p->ev.resize(2 * (size_t)capacity);
+  p->start.resize(capacity);
   p->kind.resize(capacity);
   p->flops.resize(capacity);
   // timing-only events: no system-scope fence (a default event record writes
@@ -598,6 +618,7 @@ extern "C" int rrin_prof_destroy(rrin_prof* p) {
 extern "C" int rrin_prof_reset(rrin_prof* p) {
   if (!p) return RRIN_E_ARG;
   p->count = 0;
+  p->chain = false;
   return 0;
 }
 
@@ -609,7 +630,7 @@ extern "C" int rrin_prof_read(rrin_prof* p, int32_t* kinds, float* ms, double* f
     if (kinds) kinds[i] = p->kind[i];
     if (flops) flops[i] = p->flops[i];
     if (ms) {
-      hipError_t r = hipEventElapsedTime(&ms[i], p->ev[2 * i], p->ev[2 * i + 1]);
+      hipError_t r = hipEventElapsedTime(&ms[i], p->ev[p->start[i]], p->ev[2 * i + 1]);
       if (r != hipSuccess) return (int)r;
     }
   }
@@ -621,7 +642,7 @@ extern "C" int rrin_prof_read_spans(rrin_prof* p, float* t0_ms, float* t1_ms, in
   if (!p || !count || !t0_ms || !t1_ms) return RRIN_E_ARG;
   const int n = p->count < cap ? p->count : cap;
   for (int i = 0; i < n; ++i) {
-    hipError_t r = hipEventElapsedTime(&t0_ms[i], p->ev[0], p->ev[2 * i]);
+    hipError_t r = hipEventElapsedTime(&t0_ms[i], p->ev[0], p->ev[p->start[i]]);
     if (r == hipSuccess) r = hipEventElapsedTime(&t1_ms[i], p->ev[0], p->ev[2 * i + 1]);
     if (r != hipSuccess) return (int)r;
   }

@@ -575,6 +575,7 @@ def cfgab(args):
             pool = H8Tensor(n, cout, h // 2, w // 2, dev, prec) if epi == 2 else None
             d = _lib.ConvH8Desc()
             d.n, d.cin, d.cout, d.cfg, d.prec, d.epi_mode, d.slope, d.inv_wscale = n, cin, cout, cfg, prec, epi, 0.1, inv
+            d.tail_finite = 1  # channels past cin are zero (as the Net's g16 buffer)
             d.src, d.dst = x.view(0, cin), dst.view(0, cout // 4 if epi == 4 else cout)
             if pool is not None:
                 d.pool = pool.view(0, cout)
