@@ -758,6 +758,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wino64_kernel(ConvH8Args a) {
 #ifndef RRIN_WINOQ_STAGES
 #define RRIN_WINOQ_STAGES 2
 #endif
+#ifndef RRIN_WINOQ_ORDER
+#define RRIN_WINOQ_ORDER 0  // A/B builds only: tile order of the workgroup index
+#endif
 #ifndef RRIN_WINOQ_PRIO
 #define RRIN_WINOQ_PRIO 0  // A/B builds only: 1 s_setprio around each MFMA cluster, 2 static for waves 4-7
 #endif
@@ -993,10 +996,25 @@ __global__ __launch_bounds__(256 * PT, 2) void conv3x3_winoq_kernel(ConvH8Args a
   int cob, x0, y0, img;
   {
     int t = tile;
+#if RRIN_WINOQ_ORDER == 1  // A/B: tile column fastest, then the co block
+    x0 = (t % a.tiles_x) * 32;
+    t /= a.tiles_x;
+    cob = t % a.co_blocks;
+    t /= a.co_blocks;
+#elif RRIN_WINOQ_ORDER == 2  // A/B: the co block outermost within an image
+    x0 = (t % a.tiles_x) * 32;
+    t /= a.tiles_x;
+    const int ty_ = t % a.tiles_y;
+    t /= a.tiles_y;
+    cob = t % a.co_blocks;
+    t /= a.co_blocks;
+    t = t * a.tiles_y + ty_;
+#else  // the co blocks of a tile position on consecutive workgroups (they share its raw tile)
     cob = t % a.co_blocks;
     t /= a.co_blocks;
     x0 = (t % a.tiles_x) * 32;
     t /= a.tiles_x;
+#endif
     y0 = (t % a.tiles_y) * TH;
     img = t / a.tiles_y;
   }
