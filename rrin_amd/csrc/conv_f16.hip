@@ -817,6 +817,7 @@ __global__ void RRIN_PK_EDGE_ATTR __launch_bounds__(256 * KS) edge_fix_h8_kernel
   // per-thread staging work of one ci chunk, fetched one chunk ahead
   constexpr int kItems = GPC * (kFixPx + 2);  // U: record groups x line positions
   constexpr int kUIt = (kItems + 255) / 256;
+  constexpr int kFixB = KS == 4 ? 1 : 4;  // channels per batch of LDS reads (KS 4: 128 VGPRs)
   Up8<PLANES, F32> ru[kUIt], rx;
   float4 rw[7];
   const int w_ci = tid >> 3, w_cq = (tid & 7) * 4;
@@ -864,49 +865,91 @@ __global__ void RRIN_PK_EDGE_ATTR __launch_bounds__(256 * KS) edge_fix_h8_kernel
       if (sl < nslot) *reinterpret_cast<float4*>(&s_w[sl][w_ci][w_cq]) = rw[sl];
   };
 
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  // acc: the 3 line taps; accx: a corner pixel's 2 extra taps, kept apart so the
+  // line-tap loop has no per-thread branch (a branch per ci split the loop into
+  // blocks that each waited out their own LDS reads: one wave per SIMD, nothing
+  // else to hide the latency) and added once at the end
+  float acc[4] = {0.f, 0.f, 0.f, 0.f}, accx[4] = {0.f, 0.f, 0.f, 0.f};
 #if defined(RRIN_PK_EDGE_ASM)
-  f32x2 a01 = {0.f, 0.f}, a23 = {0.f, 0.f};
-#define FIX_FMA(w, u) pk_fma4(a01, a23, w, u)
+  f32x2 acc01 = {0.f, 0.f}, acc23 = {0.f, 0.f}, accx01 = {0.f, 0.f}, accx23 = {0.f, 0.f};
+#define FIX_FMA(A, W_, U_) pk_fma4(A##01, A##23, W_, U_)
 #else
-#define FIX_FMA(w, u)                  \
-  acc[0] = fmaf(w.x, u, acc[0]);       \
-  acc[1] = fmaf(w.y, u, acc[1]);       \
-  acc[2] = fmaf(w.z, u, acc[2]);       \
-  acc[3] = fmaf(w.w, u, acc[3])
+#define FIX_FMA(A, W_, U_)             \
+  A[0] = fmaf((W_).x, U_, A[0]);       \
+  A[1] = fmaf((W_).y, U_, A[1]);       \
+  A[2] = fmaf((W_).z, U_, A[2]);       \
+  A[3] = fmaf((W_).w, U_, A[3])
 #endif
   const int pos = pos0 + px;
   const bool cl = has_l && pos == 0, cr = has_r && pos == W - 1;
+  const int sb = cl ? 0 : 2;  // corner extra slots of this thread (used by cl / cr only)
+  // the conv's pre-fix ring values and the bias, loaded up front: their latency
+  // overlaps the first chunk's instead of following the last one
+  const bool live = ks == 0 && pos - first < count;
+  const int Y = row ? fixed : pos, X = row ? pos : fixed;
+  float pre[4] = {0.f, 0.f, 0.f, 0.f}, bco[4] = {0.f, 0.f, 0.f, 0.f};
+  auto load_pre = [&]() {
+    const int64_t e = ring_index(Y, X, H, W);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int co = co0 + cg * 4 + i;
+      if (co < a.cout) {
+        pre[i] = a.edge[((int64_t)img * a.cout + co) * a.ring + e];
+        bco[i] = a.bias[co];
+      }
+    }
+  };
+  // (KS 4 runs at 128 VGPRs: the 8 registers would spill there)
+  if constexpr (KS < 4)
+    if (live) load_pre();
   // every K group runs the same number of chunks (launch: cin % (KS * kFixCi) == 0)
   fetch(ks * kFixCi);
   for (int c0 = ks * kFixCi; c0 < a.cin; c0 += KS * kFixCi) {
     stage();
     __syncthreads();
     if (c0 + KS * kFixCi < a.cin) fetch(c0 + KS * kFixCi);  // in flight during the FMAs below
-#pragma unroll 4
-    for (int ci = 0; ci < kFixCi; ++ci) {
+    // batches of kFixB channels: every LDS read of a batch issued before its
+    // FMAs (the scheduler otherwise waits out each read on its own)
+#pragma clang loop unroll(disable)
+    for (int cb = 0; cb < kFixCi; cb += kFixB) {
+      float u[kFixB][3];
+      float4 w[kFixB][3];
 #pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const float u = s_u[ci][px + k];
-        const float4 w = *reinterpret_cast<const float4*>(&s_w[k][ci][cg * 4]);
-        FIX_FMA(w, u);
-      }
-      if (cl || cr) {
-        const int sb = cl ? 0 : 2;
+      for (int j = 0; j < kFixB; ++j)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          u[j][k] = s_u[cb + j][px + k];
+          w[j][k] = *reinterpret_cast<const float4*>(&s_w[k][cb + j][cg * 4]);
+        }
+      //SB __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < kFixB; ++j)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          FIX_FMA(acc, w[j][k], u[j][k]);
+        }
+      //SB __builtin_amdgcn_sched_barrier(0);
+    }
+    if (corners) {  // block-uniform; every thread runs it, cl / cr keep the result
+#pragma unroll 2
+      for (int ci = 0; ci < kFixCi; ++ci)
 #pragma unroll
         for (int m = 0; m < 2; ++m) {
           const float u = s_ux[ci][sb + m];
           const float4 w = *reinterpret_cast<const float4*>(&s_w[3 + sb + m][ci][cg * 4]);
-          FIX_FMA(w, u);
+          FIX_FMA(accx, w, u);
         }
-      }
     }
     __syncthreads();
   }
 #undef FIX_FMA
 #if defined(RRIN_PK_EDGE_ASM)
-  acc[0] = a01.x; acc[1] = a01.y; acc[2] = a23.x; acc[3] = a23.y;
+  acc[0] = acc01.x; acc[1] = acc01.y; acc[2] = acc23.x; acc[3] = acc23.y;
+  accx[0] = accx01.x; accx[1] = accx01.y; accx[2] = accx23.x; accx[3] = accx23.y;
 #endif
+  if (cl || cr)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i] += accx[i];
   if constexpr (KS > 1) {
     // groups 1.. park their sums in their own (now idle) staging region
     if (ks > 0) {
@@ -920,14 +963,13 @@ __global__ void RRIN_PK_EDGE_ATTR __launch_bounds__(256 * KS) edge_fix_h8_kernel
 #pragma unroll
       for (int i = 0; i < 4; ++i) acc[i] += s_fix[k * kFixSubFloats + i * 256 + tid];
   }
-  if (pos - first >= count) return;
-  const int Y = row ? fixed : pos, X = row ? pos : fixed;
-  const int64_t e = ring_index(Y, X, H, W);
+  if (!live) return;
+  if constexpr (KS == 4) load_pre();
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int co = co0 + cg * 4 + i;
     if (co >= a.cout) break;
-    float v = (a.edge[((int64_t)img * a.cout + co) * a.ring + e] - acc[i]) + a.bias[co];
+    float v = (pre[i] - acc[i]) + bco[i];
     if (a.leaky) v = v > 0.f ? v : v * a.slope;
     const int64_t k = (((int64_t)img * a.d_img + (int64_t)(co / CPR) * a.d_gp + (int64_t)(Y + 1) * a.d_wp + X +
                         kH8PadLeft) * CPR) + (co % CPR);
@@ -2185,13 +2227,12 @@ extern "C" int rrin_subpixel_edge_fix_h8(const rrin_edge_fix_desc* d, void* stre
   // 128 VGPRs: the two-plane kernel spills there)
   int ks = d->cin % (2 * kFixCi) == 0 && d->cin >= 4 * kFixCi ? 2 : 1;
   if (planes == 1 && d->cin % (4 * kFixCi) == 0 && d->cin >= 8 * kFixCi) ks = 4;
+  // fp32 records: 2 groups from cin 64 on, never 4 (4 x 256 threads cap a thread
+  // at 128 VGPRs and the fp32 kernel spills there: 31.6 vs 15.7 us per launch)
+  if (d->prec == RRIN_PREC_F32R) ks = d->cin % (2 * kFixCi) == 0 ? 2 : 1;
   hipStream_t st = (hipStream_t)stream;
   if (d->prec == RRIN_PREC_F32R) {
-    switch (ks) {
-      case 4: return edge_fix_launch<1, 4, true>(a, grid, st);
-      case 2: return edge_fix_launch<1, 2, true>(a, grid, st);
-      default: return edge_fix_launch<1, 1, true>(a, grid, st);
-    }
+    return ks == 2 ? edge_fix_launch<1, 2, true>(a, grid, st) : edge_fix_launch<1, 1, true>(a, grid, st);
   }
   switch (planes * 8 + ks) {
     case 2 * 8 + 2: return edge_fix_launch<2, 2>(a, grid, st);
