@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define RRIN_ABI_VERSION 10
+#define RRIN_ABI_VERSION 11
 
 #define RRIN_OK 0
 #define RRIN_E_SHAPE (-1)     /* H or W not a multiple of 16, or N < 1          */
@@ -307,8 +307,21 @@ typedef struct rrin_edge_fix_desc {
   const float* wedge;          /* original weights as [cin][9][cout] fp32       */
   const float* bias;           /* original bias [cout]                          */
   int32_t* status;             /* optional: fp16 range flag, as rrin_conv_h8_desc */
+  /* ABI 11, optional (zero = one workgroup per tile loops over the K runs; the
+   * result is the same bit for bit): scratch for the cross-workgroup K split of
+   * fp32 records (cin / 64 runs of 64 channels, one workgroup each; the last one
+   * of a tile, by a ticket in cnt, adds the runs in run order).  Used when
+   * part_floats / cnt_len cover rrin_edge_fix_split_floats; cnt starts at zero
+   * and is left at zero. */
+  float* part;
+  int32_t* cnt;
+  int64_t part_floats;
+  int32_t cnt_len, pad_;
 } rrin_edge_fix_desc;
 int rrin_subpixel_edge_fix_h8(const rrin_edge_fix_desc* d, void* stream);
+/* Scratch floats (return; 0 = this cin / precision does not split) and tickets
+ * (*cnt) of the ring fix-up's cross-workgroup K split for d's shapes. */
+int64_t rrin_edge_fix_split_floats(const rrin_edge_fix_desc* d, int64_t* cnt);
 
 /* nn.Upsample(bilinear, x2) (unet.py:77) of an H8 view into another H8 view. */
 int rrin_upsample2x_h8(const rrin_h8* src, const rrin_h8* dst, int32_t n, int32_t prec, void* stream);

@@ -9,7 +9,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "librrin_hip.so")
 
 # enums (rrin_hip.h)
@@ -75,7 +75,9 @@ class ConvH8Desc(C.Structure):
 class EdgeFixDesc(C.Structure):
     _fields_ = [("n", C.c_int32), ("cin", C.c_int32), ("cout", C.c_int32), ("prec", C.c_int32),
                 ("epi_mode", C.c_int32), ("slope", C.c_float), ("src", H8), ("dst", H8),
-                ("edge", C.c_void_p), ("wedge", C.c_void_p), ("bias", C.c_void_p), ("status", C.c_void_p)]
+                ("edge", C.c_void_p), ("wedge", C.c_void_p), ("bias", C.c_void_p), ("status", C.c_void_p),
+                ("part", C.c_void_p), ("cnt", C.c_void_p), ("part_floats", C.c_int64), ("cnt_len", C.c_int32),
+                ("pad_", C.c_int32)]
 
 
 class HeadH8Desc(C.Structure):
@@ -149,6 +151,7 @@ SIGNATURES = {
     "rrin_conv_h8_cfg_wino": (C.c_int, [C.c_int32]),
     "rrin_conv_h8_split_floats": (C.c_int64, [C.c_void_p, C.c_void_p]),
     "rrin_conv_h8_ring_floats": (C.c_int64, [C.c_void_p, C.c_void_p]),
+    "rrin_edge_fix_split_floats": (C.c_int64, [C.c_void_p, C.c_void_p]),
     "rrin_pack_conv3x3_wino_floats": (C.c_int64, [C.c_int32, C.c_int32]),
     "rrin_pack_conv3x3_wino_bm_floats": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32]),
     "rrin_pack_conv3x3_wino4_floats": (C.c_int64, [C.c_int32, C.c_int32]),

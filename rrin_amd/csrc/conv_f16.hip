@@ -722,6 +722,14 @@ struct EdgeFixArgs {
   int leaky;
   int tiles_row, tiles_col;  // tiles per row line / per column line
   int* status;               // optional fp16 range flag
+  // K slices: the cin chunks in nslices runs of KS chunks (one per K group) or,
+  // fp16, one run; a run's group sums are added in group order, the runs' sums
+  // in run order.  cross: one workgroup per (tile, run), partial sums through
+  // part (1024 floats per run) and the last workgroup (cnt ticket) adds them in
+  // run order -- the same arithmetic as one workgroup looping over the runs.
+  int nslices, cross;
+  float* part;
+  int* cnt;
 };
 
 // The 4 low-res records (8 halves / 4 floats, both planes) that bilinear x2
@@ -792,7 +800,9 @@ __global__ void RRIN_PK_EDGE_ATTR __launch_bounds__(256 * KS) edge_fix_h8_kernel
   // slots 0-2 line taps, 3-6 corner extras
   float(*s_w)[kFixCi][kFixCo] = reinterpret_cast<float(*)[kFixCi][kFixCo]>(s_base + kFixCi * (kFixPx + 2) + kFixCi * 4);
   const int tid = threadIdx.x & 255, px = tid & (kFixPx - 1), cg = tid / kFixPx;  // 8 groups of 4 channels
-  const int img = blockIdx.z, co0 = blockIdx.y * kFixCo;
+  const int nsl = a.nslices, img = a.cross ? blockIdx.z / nsl : blockIdx.z, co0 = blockIdx.y * kFixCo;
+  const int sl0 = a.cross ? blockIdx.z - img * nsl : 0, sl1 = a.cross ? sl0 + 1 : nsl;
+  const int csl = a.cin / nsl;  // channels per run (a multiple of KS * kFixCi)
   const int H = 2 * a.sh, W = 2 * a.sw;
   // line of this tile: 0 top, 1 bottom, 2 left, 3 right
   int t = blockIdx.x, line;
@@ -868,10 +878,10 @@ __global__ void RRIN_PK_EDGE_ATTR __launch_bounds__(256 * KS) edge_fix_h8_kernel
   // acc: the 3 line taps; accx: a corner pixel's 2 extra taps, kept apart so the
   // line-tap loop has no per-thread branch (a branch per ci split the loop into
   // blocks that each waited out their own LDS reads: one wave per SIMD, nothing
-  // else to hide the latency) and added once at the end
-  float acc[4] = {0.f, 0.f, 0.f, 0.f}, accx[4] = {0.f, 0.f, 0.f, 0.f};
+  // else to hide the latency) and added at the end of each run
+  float acc[4], accx[4], tot[4] = {0.f, 0.f, 0.f, 0.f};
 #if defined(RRIN_PK_EDGE_ASM)
-  f32x2 acc01 = {0.f, 0.f}, acc23 = {0.f, 0.f}, accx01 = {0.f, 0.f}, accx23 = {0.f, 0.f};
+  f32x2 acc01, acc23, accx01, accx23;
 #define FIX_FMA(A, W_, U_) pk_fma4(A##01, A##23, W_, U_)
 #else
 #define FIX_FMA(A, W_, U_)             \
@@ -902,67 +912,115 @@ __global__ void RRIN_PK_EDGE_ATTR __launch_bounds__(256 * KS) edge_fix_h8_kernel
   // (KS 4 runs at 128 VGPRs: the 8 registers would spill there)
   if constexpr (KS < 4)
     if (live) load_pre();
-  // every K group runs the same number of chunks (launch: cin % (KS * kFixCi) == 0)
-  fetch(ks * kFixCi);
-  for (int c0 = ks * kFixCi; c0 < a.cin; c0 += KS * kFixCi) {
-    stage();
-    __syncthreads();
-    if (c0 + KS * kFixCi < a.cin) fetch(c0 + KS * kFixCi);  // in flight during the FMAs below
-    // batches of kFixB channels: every LDS read of a batch issued before its
-    // FMAs (the scheduler otherwise waits out each read on its own)
+  // every K group runs the same number of chunks per run (launch: csl % (KS * kFixCi) == 0)
+  fetch(sl0 * csl + ks * kFixCi);
+  for (int sl = sl0; sl < sl1; ++sl) {
+#if defined(RRIN_PK_EDGE_ASM)
+    acc01 = acc23 = accx01 = accx23 = f32x2{0.f, 0.f};
+#else
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i] = accx[i] = 0.f;
+#endif
+    const int cend = (sl + 1) * csl;
+    for (int c0 = sl * csl + ks * kFixCi; c0 < cend; c0 += KS * kFixCi) {
+      stage();
+      __syncthreads();
+      // the next chunk of this group, in this run or the next one, is in flight during the FMAs below
+      const int nxt = c0 + KS * kFixCi < cend ? c0 + KS * kFixCi : (sl + 1 < sl1 ? cend + ks * kFixCi : -1);
+      if (nxt >= 0) fetch(nxt);
+      // batches of kFixB channels: every LDS read of a batch issued before its
+      // FMAs (the scheduler otherwise waits out each read on its own)
 #pragma clang loop unroll(disable)
-    for (int cb = 0; cb < kFixCi; cb += kFixB) {
-      float u[kFixB][3];
-      float4 w[kFixB][3];
+      for (int cb = 0; cb < kFixCi; cb += kFixB) {
+        float u[kFixB][3];
+        float4 w[kFixB][3];
 #pragma unroll
-      for (int j = 0; j < kFixB; ++j)
+        for (int j = 0; j < kFixB; ++j)
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          u[j][k] = s_u[cb + j][px + k];
-          w[j][k] = *reinterpret_cast<const float4*>(&s_w[k][cb + j][cg * 4]);
-        }
-      //SB __builtin_amdgcn_sched_barrier(0);
+          for (int k = 0; k < 3; ++k) {
+            u[j][k] = s_u[cb + j][px + k];
+            w[j][k] = *reinterpret_cast<const float4*>(&s_w[k][cb + j][cg * 4]);
+          }
 #pragma unroll
-      for (int j = 0; j < kFixB; ++j)
+        for (int j = 0; j < kFixB; ++j)
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          FIX_FMA(acc, w[j][k], u[j][k]);
-        }
-      //SB __builtin_amdgcn_sched_barrier(0);
-    }
-    if (corners) {  // block-uniform; every thread runs it, cl / cr keep the result
+          for (int k = 0; k < 3; ++k) {
+            FIX_FMA(acc, w[j][k], u[j][k]);
+          }
+      }
+      if (corners) {  // block-uniform; every thread runs it, cl / cr keep the result
 #pragma unroll 2
-      for (int ci = 0; ci < kFixCi; ++ci)
+        for (int ci = 0; ci < kFixCi; ++ci)
 #pragma unroll
-        for (int m = 0; m < 2; ++m) {
-          const float u = s_ux[ci][sb + m];
-          const float4 w = *reinterpret_cast<const float4*>(&s_w[3 + sb + m][ci][cg * 4]);
-          FIX_FMA(accx, w, u);
-        }
+          for (int m = 0; m < 2; ++m) {
+            const float u = s_ux[ci][sb + m];
+            const float4 w = *reinterpret_cast<const float4*>(&s_w[3 + sb + m][ci][cg * 4]);
+            FIX_FMA(accx, w, u);
+          }
+      }
+      __syncthreads();
     }
-    __syncthreads();
+#if defined(RRIN_PK_EDGE_ASM)
+    acc[0] = acc01.x; acc[1] = acc01.y; acc[2] = acc23.x; acc[3] = acc23.y;
+    accx[0] = accx01.x; accx[1] = accx01.y; accx[2] = accx23.x; accx[3] = accx23.y;
+#endif
+    if (cl || cr)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i] += accx[i];
+    if constexpr (KS > 1) {
+      // groups 1.. park their run sums in their own (now idle) staging region
+      if (ks > 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) s_base[i * 256 + tid] = acc[i];
+      }
+      __syncthreads();
+      if (ks == 0) {
+#pragma unroll
+        for (int k = 1; k < KS; ++k)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[i] += s_fix[k * kFixSubFloats + i * 256 + tid];
+      }
+      __syncthreads();  // the next run's staging overwrites the parked sums
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) tot[i] = sl == sl0 ? acc[i] : tot[i] + acc[i];
   }
 #undef FIX_FMA
-#if defined(RRIN_PK_EDGE_ASM)
-  acc[0] = acc01.x; acc[1] = acc01.y; acc[2] = acc23.x; acc[3] = acc23.y;
-  accx[0] = accx01.x; accx[1] = accx01.y; accx[2] = accx23.x; accx[3] = accx23.y;
-#endif
-  if (cl || cr)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) acc[i] += accx[i];
-  if constexpr (KS > 1) {
-    // groups 1.. park their sums in their own (now idle) staging region
-    if (ks > 0) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) s_base[i * 256 + tid] = acc[i];
+  if (a.cross) {
+    // split-K seam, sc1 form (as conv3x3_winoq_kernel's SK path): write-through run
+    // sums, drain, barrier, one relaxed ticket; the last workgroup reads every run's
+    // sums with sc1 loads and adds them in run order
+    const int64_t tile = ((int64_t)img * gridDim.x + blockIdx.x) * gridDim.y + blockIdx.y;
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(a.part + tile * nsl * 1024, 0, nsl * 1024 * 4, 0x00020000);
+    if (ks == 0) {
+      const u32x4 v = {__float_as_uint(tot[0]), __float_as_uint(tot[1]), __float_as_uint(tot[2]),
+                       __float_as_uint(tot[3])};
+      __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, (sl0 * 256 + tid) * 16, 0, 16 /* sc1 */);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* s_last = reinterpret_cast<int*>(s_fix);  // group 0's staging region is idle now
+    if (threadIdx.x == 0) {
+      const int old = __hip_atomic_fetch_add(a.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = old == nsl - 1;
+      if (last) __hip_atomic_store(a.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+      *s_last = last;
     }
     __syncthreads();
-    if (ks > 0) return;
+    if (!*s_last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (live) {
+#pragma unroll 1
+      for (int k = 0; k < nsl; ++k) {
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (k * 256 + tid) * 16, 0, 16);
 #pragma unroll
-    for (int k = 1; k < KS; ++k)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) acc[i] += s_fix[k * kFixSubFloats + i * 256 + tid];
+        for (int i = 0; i < 4; ++i) tot[i] = k == 0 ? __uint_as_float(v[i]) : tot[i] + __uint_as_float(v[i]);
+      }
+    }
   }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i] = tot[i];
   if (!live) return;
   if constexpr (KS == 4) load_pre();
 #pragma unroll
@@ -2179,6 +2237,23 @@ static int edge_fix_launch(const EdgeFixArgs& a, dim3 grid, hipStream_t st) {
   return hip_code(hipGetLastError());
 }
 
+// K groups and K runs of the ring fix-up, by cin and precision only (the
+// summation order never depends on batch, size or scratch).  fp32 records: 2
+// groups from cin 64 on, never 4 (4 x 256 threads cap a thread at 128 VGPRs and
+// the fp32 kernel spills there: 31.6 vs 15.7 us per launch), runs of one chunk per
+// group (cin / 64 runs).  fp16: split16 stops at 2 groups (the two-plane kernel
+// spills at 4), one run.
+static void edge_fix_split(int cin, int prec, int* ks, int* nsl) {
+  *nsl = 1;
+  if (prec == RRIN_PREC_F32R) {
+    *ks = cin % (2 * kFixCi) == 0 ? 2 : 1;
+    if (cin % (*ks * kFixCi) == 0) *nsl = cin / (*ks * kFixCi);
+    return;
+  }
+  *ks = cin % (2 * kFixCi) == 0 && cin >= 4 * kFixCi ? 2 : 1;
+  if (planes_of(prec) == 1 && cin % (4 * kFixCi) == 0 && cin >= 8 * kFixCi) *ks = 4;
+}
+
 extern "C" int rrin_subpixel_edge_fix_h8(const rrin_edge_fix_desc* d, void* stream) {
   if (!d || !d->edge || !d->wedge || !d->bias) return RRIN_E_ARG;
   if (!rec_prec(d->prec)) return RRIN_E_ARG;
@@ -2222,25 +2297,41 @@ extern "C" int rrin_subpixel_edge_fix_h8(const rrin_edge_fix_desc* d, void* stre
   a.tiles_col = (H - 2 + kFixPx - 1) / kFixPx;
   const dim3 grid((unsigned)(2 * a.tiles_row + 2 * a.tiles_col), (unsigned)((d->cout + kFixCo - 1) / kFixCo),
                   (unsigned)d->n);
-  // K split by cin and precision only (the summation order never depends on
-  // batch or size); split16 stops at 2 groups (4 x 256 threads cap a thread at
-  // 128 VGPRs: the two-plane kernel spills there)
-  int ks = d->cin % (2 * kFixCi) == 0 && d->cin >= 4 * kFixCi ? 2 : 1;
-  if (planes == 1 && d->cin % (4 * kFixCi) == 0 && d->cin >= 8 * kFixCi) ks = 4;
-  // fp32 records: 2 groups from cin 64 on, never 4 (4 x 256 threads cap a thread
-  // at 128 VGPRs and the fp32 kernel spills there: 31.6 vs 15.7 us per launch)
-  if (d->prec == RRIN_PREC_F32R) ks = d->cin % (2 * kFixCi) == 0 ? 2 : 1;
+  int ks, nsl;
+  edge_fix_split(d->cin, d->prec, &ks, &nsl);
+  a.nslices = nsl;
+  a.cross = 0;
+  dim3 g = grid;
+  const int64_t tiles = (int64_t)grid.x * grid.y * d->n;
+  if (nsl > 1 && d->part && d->cnt && tiles * nsl * 1024 <= d->part_floats && tiles <= d->cnt_len) {
+    a.cross = 1;  // one workgroup per K run (same arithmetic as the loop over runs)
+    a.part = d->part;
+    a.cnt = d->cnt;
+    g.z = (unsigned)(d->n * nsl);
+  }
   hipStream_t st = (hipStream_t)stream;
   if (d->prec == RRIN_PREC_F32R) {
-    return ks == 2 ? edge_fix_launch<1, 2, true>(a, grid, st) : edge_fix_launch<1, 1, true>(a, grid, st);
+    return ks == 2 ? edge_fix_launch<1, 2, true>(a, g, st) : edge_fix_launch<1, 1, true>(a, g, st);
   }
   switch (planes * 8 + ks) {
-    case 2 * 8 + 2: return edge_fix_launch<2, 2>(a, grid, st);
-    case 2 * 8 + 1: return edge_fix_launch<2, 1>(a, grid, st);
-    case 1 * 8 + 4: return edge_fix_launch<1, 4>(a, grid, st);
-    case 1 * 8 + 2: return edge_fix_launch<1, 2>(a, grid, st);
-    default: return edge_fix_launch<1, 1>(a, grid, st);
+    case 2 * 8 + 2: return edge_fix_launch<2, 2>(a, g, st);
+    case 2 * 8 + 1: return edge_fix_launch<2, 1>(a, g, st);
+    case 1 * 8 + 4: return edge_fix_launch<1, 4>(a, g, st);
+    case 1 * 8 + 2: return edge_fix_launch<1, 2>(a, g, st);
+    default: return edge_fix_launch<1, 1>(a, g, st);
   }
+}
+
+extern "C" int64_t rrin_edge_fix_split_floats(const rrin_edge_fix_desc* d, int64_t* cnt) {
+  if (!d || d->n < 1 || d->cin < 8 || (d->cin & 7) || d->cout < 8 || !rec_prec(d->prec)) return RRIN_E_ARG;
+  int ks, nsl;
+  edge_fix_split(d->cin, d->prec, &ks, &nsl);
+  const int H = d->dst.g.h, W = d->dst.g.w;
+  if (H < 2 || W < 1) return RRIN_E_SHAPE;
+  const int64_t tiles = (int64_t)(2 * ((W + kFixPx - 1) / kFixPx) + 2 * ((H - 2 + kFixPx - 1) / kFixPx)) *
+                        ((d->cout + kFixCo - 1) / kFixCo) * d->n;
+  if (cnt) *cnt = nsl > 1 ? tiles : 0;
+  return nsl > 1 ? tiles * nsl * 1024 : 0;
 }
 
 extern "C" int rrin_upsample2x_h8(const rrin_h8* src, const rrin_h8* dst, int32_t n, int32_t prec, void* stream) {

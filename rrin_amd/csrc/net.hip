@@ -80,6 +80,8 @@ struct Plan {
 // outputs (8192 per TH 8 tile and slice: 4096 slices) and kPartTiles tiles
 constexpr int64_t kPartFloats = (int64_t)4096 * 8192;
 constexpr int64_t kPartTiles = 4096;
+// ring fix-up: cross-workgroup K split up to this many workgroups (one per CU)
+constexpr int64_t kEdgeCrossMaxGroups = 256;
 
 int64_t align256(int64_t b) { return (b + 255) & ~(int64_t)255; }
 
@@ -385,6 +387,21 @@ int upconv_subpixel(const Plan& p, const rrin_conv_weights& cw, int C, const rri
   e.wedge = cw.wedge;
   e.bias = cw.bias_raw;
   e.status = p.status;
+  // F32R plans: the cross-workgroup K split (the same result bit for bit) where the
+  // split grid is at most one workgroup per CU -- the latency-bound small grids
+  // (640x368 x 1: fix-up 195 -> 129 us per forward); larger grids keep one
+  // workgroup per tile, whose extra workgroups only queue behind the other
+  // stream's convs (720p x 4 on 2 streams: fix-up span 1.4 -> 3.5 ms per step)
+  if (p.PART && p.CNT) {
+    int64_t tk = 0;
+    const int64_t nf = rrin_edge_fix_split_floats(&e, &tk);
+    if (nf > 0 && nf / 1024 <= kEdgeCrossMaxGroups) {
+      e.part = p.PART;
+      e.cnt = p.CNT;
+      e.part_floats = kPartFloats;
+      e.cnt_len = (int32_t)kPartTiles;
+    }
+  }
   ProfScope ps(p.prof, st, RRIN_KIND_EDGE, 0.0);
   return rrin_subpixel_edge_fix_h8(&e, st);
 }

@@ -291,7 +291,7 @@ def test_h8_leaky_rep_writes_replicated_ring(gpu, prec):
         assert dst.hi[:, :, 0, 7:9 + dst.w].any() and dst.hi[:, :, 1:dst.h + 1, 7].any()
 
 
-def subpixel_upconv(src: H8Tensor, w, b, cfg, prec, dst=None, ksplit=0, keep=None, fold=False):
+def subpixel_upconv(src: H8Tensor, w, b, cfg, prec, dst=None, ksplit=0, keep=None, fold=False, edge_split=False):
     """EPI_SUBPIXEL conv + ring fix-up through the C ABI (the Net's up.1 conv); fold: the
     ring in the conv launch (rrin_conv_h8_desc.ring_w, Winograd kind 3) instead of
     rrin_subpixel_edge_fix_h8."""
@@ -335,6 +335,15 @@ def subpixel_upconv(src: H8Tensor, w, b, cfg, prec, dst=None, ksplit=0, keep=Non
     e.n, e.cin, e.cout, e.prec, e.epi_mode, e.slope = src.n, cin, cout, prec, _lib.EPI_LINEAR, 0.1
     e.src, e.dst = src.view(0, cin), dst.view(0, cout)
     e.edge, e.wedge, e.bias = edge.data_ptr(), wedge.data_ptr(), braw.data_ptr()
+    if edge_split:  # cross-workgroup K split of the fix-up (fp32 records)
+        nc = C.c_int64(-1)
+        nf = lib.rrin_edge_fix_split_floats(C.byref(e), C.byref(nc))
+        assert nf >= 0 and nc.value >= 0, nf
+        if nf:
+            part = torch.full((nf,), float("nan"), device=dev)
+            cnt = torch.zeros(nc.value, dtype=torch.int32, device=dev)
+            e.part, e.cnt, e.part_floats, e.cnt_len = part.data_ptr(), cnt.data_ptr(), nf, nc.value
+            keep.extend([part, cnt])
     _lib.check(lib.rrin_subpixel_edge_fix_h8(C.byref(e), H.stream(dev)), "rrin_subpixel_edge_fix_h8")
     torch.cuda.synchronize(dev)
     return dst
@@ -358,6 +367,31 @@ def test_h8_subpixel_upconv(gpu, prec, n, cin, cout, sh, sw):
                                    err_msg=f"cfg {cfg}")
         assert not dst.to_nchw(cout, cout).any()           # the bridge half of CAT is untouched
         assert not dst.hi[:, :, 0].any() and not dst.hi[:, :, :, :8].any()  # zero padding kept
+
+
+@pytest.mark.parametrize("n,cin,cout,sh,sw", [(2, 128, 64, 20, 36), (1, 256, 128, 5, 7), (2, 512, 256, 3, 5),
+                                              (1, 256, 128, 1, 1), (1, 64, 32, 9, 17)])
+def test_h8_subpixel_edge_split(gpu, n, cin, cout, sh, sw):
+    """fp32 ring fix-up with its cross-workgroup K split (one workgroup per 64-channel
+    run, the last one of a tile adds the runs in run order): bit for bit the
+    one-workgroup result, tickets back at zero, and within 1e-5 of float64."""
+    x = torch.rand(n, cin, sh, sw, device=gpu) * 2 - 1
+    wt, b = keyed_conv(cin, cout, "sub")
+    up = F.interpolate(x.double().cpu(), scale_factor=2, mode="bilinear", align_corners=False)
+    ref = F.conv2d(up, wt.double().cpu(), b.double().cpu(), padding=1)
+    src = H8Tensor.from_nchw(x, _lib.PREC_F32R)
+    replicate_ring(src)
+    cfg = next(c for c in cfgs(_lib.PREC_F32R, 4 * cout, cin) if _lib.lib().rrin_conv_h8_cfg_wino(c) == 3)
+    plain = subpixel_upconv(src, wt, b, cfg, _lib.PREC_F32R, dst=H8Tensor(n, cout, 2 * sh, 2 * sw, gpu, _lib.PREC_F32R))
+    keep = []
+    split = subpixel_upconv(src, wt, b, cfg, _lib.PREC_F32R, keep=keep, edge_split=True,
+                            dst=H8Tensor(n, cout, 2 * sh, 2 * sw, gpu, _lib.PREC_F32R))
+    assert torch.equal(plain.hi, split.hi)
+    if cin > 64:
+        assert len(keep) == 2 and not keep[1].any()  # scratch was used; every ticket back at zero
+    else:
+        assert not keep                               # cin 64: one run, no scratch
+    np.testing.assert_allclose(split.to_nchw(0, cout).cpu().double().numpy(), ref.numpy(), rtol=1e-5, atol=1e-5)
 
 
 @pytest.mark.parametrize("prec", PRECS)

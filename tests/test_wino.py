@@ -180,3 +180,30 @@ def test_split_scratch_size():
     d.ksplit = 2
     assert lib.rrin_conv_h8_split_floats(C.byref(d), None) == _lib.RRIN_E_CONFIG if hasattr(_lib, "RRIN_E_CONFIG") \
         else lib.rrin_conv_h8_split_floats(C.byref(d), None) < 0
+
+
+def test_edge_fix_split_scratch_size():
+    """rrin_edge_fix_split_floats: fp32 ring fix-up runs of 64 channels (cin / 64 of
+    them), 1024 floats per (tile, co block, image, run), one ticket per (tile, co
+    block, image); one run (cin 64, fp16) needs no scratch."""
+    import ctypes as C
+
+    import torch
+
+    from rrin_amd.pp import H8Tensor
+    lib = _lib.lib()
+    n, h, w = 2, 23, 40
+    for prec, cin, cout, runs in ((_lib.PREC_F32R, 256, 128, 4), (_lib.PREC_F32R, 128, 64, 2),
+                                  (_lib.PREC_F32R, 64, 32, 1), (_lib.PREC_F16, 256, 128, 1)):
+        src = H8Tensor(n, cin, h, w, torch.device("cpu"), prec)
+        dst = H8Tensor(n, cout, 2 * h, 2 * w, torch.device("cpu"), prec)
+        e = _lib.EdgeFixDesc()
+        e.n, e.cin, e.cout, e.prec = n, cin, cout, prec
+        e.src, e.dst = src.view(0, cin), dst.view(0, cout)
+        tiles = (2 * -(-2 * w // 32) + 2 * -(-(2 * h - 2) // 32)) * -(-cout // 32) * n
+        cnt = C.c_int64(-1)
+        nf = lib.rrin_edge_fix_split_floats(C.byref(e), C.byref(cnt))
+        assert nf == (tiles * runs * 1024 if runs > 1 else 0), (prec, cin)
+        assert cnt.value == (tiles if runs > 1 else 0)
+    e.cin = 4
+    assert lib.rrin_edge_fix_split_floats(C.byref(e), None) < 0
