@@ -3,7 +3,7 @@
 # the N>1 bench (bitwise gather check, parity + CPU baseline at N>1), kernel-trace
 # stats and PMC counters (SQ, FETCH, WRITE) of the default forward.
 set -u
-O=gpurun_out/r03final; mkdir -p $O; export TMPDIR=/tmp
+O=${O:-gpurun_out/r03final}; mkdir -p $O; export TMPDIR=/tmp
 STEPS=${STEPS:-tests,smoke,bench,c2,gloo,prof,pmc}
 run() {  # name limit cmd...
   local name=$1 lim=$2; shift 2
