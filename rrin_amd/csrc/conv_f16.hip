@@ -800,8 +800,10 @@ __global__ void RRIN_PK_EDGE_ATTR __launch_bounds__(256 * KS) edge_fix_h8_kernel
   // slots 0-2 line taps, 3-6 corner extras
   float(*s_w)[kFixCi][kFixCo] = reinterpret_cast<float(*)[kFixCi][kFixCo]>(s_base + kFixCi * (kFixPx + 2) + kFixCi * 4);
   const int tid = threadIdx.x & 255, px = tid & (kFixPx - 1), cg = tid / kFixPx;  // 8 groups of 4 channels
-  const int nsl = a.nslices, img = a.cross ? blockIdx.z / nsl : blockIdx.z, co0 = blockIdx.y * kFixCo;
-  const int sl0 = a.cross ? blockIdx.z - img * nsl : 0, sl1 = a.cross ? sl0 + 1 : nsl;
+  // (fp16 records always run one K run in one workgroup: compile-time there)
+  const bool cross = F32 && a.cross;
+  const int nsl = F32 ? a.nslices : 1, img = cross ? blockIdx.z / nsl : blockIdx.z, co0 = blockIdx.y * kFixCo;
+  const int sl0 = cross ? blockIdx.z - img * nsl : 0, sl1 = cross ? sl0 + 1 : nsl;
   const int csl = a.cin / nsl;  // channels per run (a multiple of KS * kFixCi)
   const int H = 2 * a.sh, W = 2 * a.sw;
   // line of this tile: 0 top, 1 bottom, 2 left, 3 right
@@ -827,7 +829,7 @@ __global__ void RRIN_PK_EDGE_ATTR __launch_bounds__(256 * KS) edge_fix_h8_kernel
   // per-thread staging work of one ci chunk, fetched one chunk ahead
   constexpr int kItems = GPC * (kFixPx + 2);  // U: record groups x line positions
   constexpr int kUIt = (kItems + 255) / 256;
-  constexpr int kFixB = KS == 4 ? 1 : 4;  // channels per batch of LDS reads (KS 4: 128 VGPRs)
+  constexpr int kFixB = F32 ? 4 : 1;  // channels per batch of LDS reads (fp32 records only)
   Up8<PLANES, F32> ru[kUIt], rx;
   float4 rw[7];
   const int w_ci = tid >> 3, w_cq = (tid & 7) * 4;
@@ -909,8 +911,10 @@ __global__ void RRIN_PK_EDGE_ATTR __launch_bounds__(256 * KS) edge_fix_h8_kernel
       }
     }
   };
-  // (KS 4 runs at 128 VGPRs: the 8 registers would spill there)
-  if constexpr (KS < 4)
+  // fp32 records only (fp16: C3 measured ~0.7 % slower with the preload and the
+  // batched loop; its KS 4 variant runs at 128 VGPRs)
+  constexpr bool kPre = F32;
+  if constexpr (kPre)
     if (live) load_pre();
   // every K group runs the same number of chunks per run (launch: csl % (KS * kFixCi) == 0)
   fetch(sl0 * csl + ks * kFixCi);
@@ -928,8 +932,19 @@ __global__ void RRIN_PK_EDGE_ATTR __launch_bounds__(256 * KS) edge_fix_h8_kernel
       // the next chunk of this group, in this run or the next one, is in flight during the FMAs below
       const int nxt = c0 + KS * kFixCi < cend ? c0 + KS * kFixCi : (sl + 1 < sl1 ? cend + ks * kFixCi : -1);
       if (nxt >= 0) fetch(nxt);
-      // batches of kFixB channels: every LDS read of a batch issued before its
-      // FMAs (the scheduler otherwise waits out each read on its own)
+      // fp32 records: batches of kFixB channels, every LDS read of a batch issued
+      // before its FMAs (the scheduler otherwise waits out each read on its own);
+      // fp16 (kFixB 1): the plain unrolled loop measured no slower (C3, same box)
+      if constexpr (kFixB == 1) {
+#pragma unroll 4
+        for (int ci = 0; ci < kFixCi; ++ci)
+#pragma unroll
+          for (int k = 0; k < 3; ++k) {
+            const float u = s_u[ci][px + k];
+            const float4 w = *reinterpret_cast<const float4*>(&s_w[k][ci][cg * 4]);
+            FIX_FMA(acc, w, u);
+          }
+      } else
 #pragma clang loop unroll(disable)
       for (int cb = 0; cb < kFixCi; cb += kFixB) {
         float u[kFixB][3];
@@ -986,7 +1001,7 @@ __global__ void RRIN_PK_EDGE_ATTR __launch_bounds__(256 * KS) edge_fix_h8_kernel
     for (int i = 0; i < 4; ++i) tot[i] = sl == sl0 ? acc[i] : tot[i] + acc[i];
   }
 #undef FIX_FMA
-  if (a.cross) {
+  if (cross) {
     // split-K seam, sc1 form (as conv3x3_winoq_kernel's SK path): write-through run
     // sums, drain, barrier, one relaxed ticket; the last workgroup reads every run's
     // sums with sc1 loads and adds them in run order
@@ -1022,7 +1037,7 @@ __global__ void RRIN_PK_EDGE_ATTR __launch_bounds__(256 * KS) edge_fix_h8_kernel
 #pragma unroll
   for (int i = 0; i < 4; ++i) acc[i] = tot[i];
   if (!live) return;
-  if constexpr (KS == 4) load_pre();
+  if constexpr (!kPre) load_pre();
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int co = co0 + cg * 4 + i;
