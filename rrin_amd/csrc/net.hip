@@ -80,8 +80,12 @@ struct Plan {
 // outputs (8192 per TH 8 tile and slice: 4096 slices) and kPartTiles tiles
 constexpr int64_t kPartFloats = (int64_t)4096 * 8192;
 constexpr int64_t kPartTiles = 4096;
-// ring fix-up: cross-workgroup K split up to this many workgroups (one per CU)
-constexpr int64_t kEdgeCrossMaxGroups = 256;
+// ring fix-up: cross-workgroup K split up to this many workgroups (one per CU;
+// RRIN_EDGE_CROSS_MAX: A/B builds)
+#ifndef RRIN_EDGE_CROSS_MAX
+#define RRIN_EDGE_CROSS_MAX 256
+#endif
+constexpr int64_t kEdgeCrossMaxGroups = RRIN_EDGE_CROSS_MAX;
 
 int64_t align256(int64_t b) { return (b + 255) & ~(int64_t)255; }
 
