@@ -124,7 +124,15 @@ def parse():
                     help="A/B: no TH-4 Winograd tiles on the deep convs (engine.WINO_TH4)")
     ap.add_argument("--split", default=None,
                     help="explicit pairs per stream, e.g. 1,3 (overrides --streams' even split)")
-    return ap.parse_args()
+    ap.add_argument("--train", action="store_true",
+                    help="training step instead (SURVEY §8f f4, train.py:98,142-145): Net.forward under "
+                         "autograd on the HIP training kernels + charbonnier loss + backward + AdamW step; "
+                         "default size 640x368 x 2 pairs")
+    a = ap.parse_args()
+    a.batch_given = "--batch" in sys.argv
+    a.height_given = "--height" in sys.argv
+    a.width_given = "--width" in sys.argv
+    return a
 
 
 def host_cpu_share():
@@ -236,8 +244,80 @@ def read_prof(lib, prof, cap):
     return union_ms([(t0s[i], t1s[i]) for i in conv]), sum(fl[i] for i in conv), len(conv)
 
 
+def train_main(args):
+    """One training step per iteration (train.py:98-145 without its VGG perceptual loss,
+    whose weights need the network): forward of the rank's pairs under autograd on the
+    HIP training kernels (rrin_amd.autograd), charbonnier loss (losses.py:39-42) against
+    a synthetic target frame, backward, AdamW (lr 1e-4, train.py:49).  Prints one JSON
+    line: pairs/s and the conv work of the step (forward, dgrad and wgrad) over the
+    whole step time -- a lower bound on the conv kernels' rate; their own launch times
+    come from the rocprofv3 family summary (profiles/)."""
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    B = args.batch if args.batch_given else 2
+    H = args.height if args.height_given else 368
+    W = args.width if args.width_given else 640
+    net = Net()
+    sd = keyed_state_dict(net.state_dict())
+    net.load_state_dict(sd, strict=True)
+    net = net.to(dev).train()
+    i0, i1 = synthetic_batch(B, H, W, first_index=0)
+    i0, i1, tgt = i0.to(dev), i1.to(dev), (0.5 * (i0 + i1)).to(dev)
+    opt = torch.optim.AdamW(net.parameters(), lr=1e-4)
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        out = net(i0, i1, args.t)
+        loss = torch.sum(torch.sqrt((out - tgt).pow(2) + 1e-6)) / B  # charbonnierLoss, losses.py:39-42
+        loss.backward()
+        opt.step()
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    units = ("Flow", "refine_flow", "Mask", "final")
+    fwd = B * sum(fl for u in units for _, fl, _, _ in conv_work(getattr(net, u), H, W))
+    # dgrad of every body conv except Flow's first (its input, cat(I0, I1), needs no
+    # gradient: autograd skips it); wgrad of every body conv (the heads, 1 % of the
+    # FLOPs, are left out of all three)
+    first_flow = B * conv_work(net.Flow, H, W)[0][1]
+    step_fl = 3 * fwd - first_flow
+    ach = step_fl / (el / args.steps) / 1e12
+    res = {
+        "metric": f"training steps at {W}x{H} fp32 (Net forward + backward + AdamW, frame pairs/s)",
+        "value": round(B * args.steps / el, 3), "unit": "pairs/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(1e3 * el / args.steps, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (key-seeded weights, randint/255 frame pairs, target = their mean)",
+        "config": {"workload": f"RRIN training step {W}x{H} fp32, {B} pairs: forward under autograd (HIP training "
+                               "kernels), charbonnierLoss, backward, AdamW lr 1e-4 (train.py:98,142-145; no VGG loss)",
+                   "global_batch": B, "height": H, "width": W, "parallelism": "single GPU"},
+        "roofline": {"bound": "mfma", "achieved": round(ach, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(ach / FP32_PEAK_TFLOPS, 4), "traffic": None,
+                     "kernel": "rrin_amd.autograd over csrc/train.hip (conv forward / dgrad / wgrad on "
+                               "v_mfma_f32_32x32x2_f32, direct form)",
+                     "flops_basis": "direct-form conv FLOPs of forward + dgrad + wgrad of the 77 body convs "
+                                    "(Flow's first conv has no dgrad)",
+                     "conv_tflop_per_step": round(step_fl / 1e12, 4),
+                     "frac_basis": "conv FLOPs / whole step time (includes the glue, loss and optimizer: a "
+                                   "lower bound on the conv kernels' own rate)"},
+        "loss": float(loss.item()),
+        "cpu_baseline": None,
+    }
+    print(json.dumps(res), flush=True)
+
+
 def main():
     args = parse()
+    if args.train:
+        train_main(args)
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -422,8 +502,15 @@ def main():
         # exact fp32: "fp32" = the Winograd kernel, "fp32-direct" = the direct form (--no-wino)
         kp = args.precision + ("-direct" if args.precision == "fp32" and roofline["conv_algorithm"] == "direct" else "")
         key = f"{kp}@{W}x{H}x{B}" + (f"s{args.streams}" if args.streams > 1 else "")
+        build = _lib.build_id()
+        roofline["traffic_build"] = build
         if os.path.exists(tab):
             ent = json.load(open(tab)).get(key)
+            if ent is not None and ent.get("build") != build:
+                # measured on another build of the kernels: no stale figure in the line
+                roofline["traffic_note"] = (f"profiles/pmc_traffic.json[{key}] is from build {ent.get('build')}, "
+                                            f"this library is {build}: traffic not measured for this build")
+                ent = None
             if ent is not None:
                 roofline["traffic"] = round(ent["hbm_bytes_per_launch"])
                 roofline["traffic_unit"] = "bytes/launch"
@@ -432,7 +519,7 @@ def main():
                 alg = sum(sum(conv_bytes(getattr(net, u), H, W, bpv))
                           for u in ("Flow", "refine_flow", "Mask", "final"))
                 roofline["algorithmic_bytes_per_step_gb"] = round(B * alg / 1e9, 2)
-                roofline["traffic_source"] = "profiles/pmc_traffic.json[" + key + "]"
+                roofline["traffic_source"] = f"profiles/pmc_traffic.json[{key}], build {build}"
 
     eng.check_range()  # fp16-stored precisions: no activation left the fp16 range (raises otherwise)
     gather_check = None

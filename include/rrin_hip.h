@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define RRIN_ABI_VERSION 11
+#define RRIN_ABI_VERSION 12
 
 #define RRIN_OK 0
 #define RRIN_E_SHAPE (-1)     /* H or W not a multiple of 16, or N < 1          */
@@ -420,7 +420,18 @@ typedef struct rrin_net_desc {
                            of the forward, set to 1 if any activation stored as fp16 overflows
                            (|v| > 65504, inf, NaN); the output is then all NaN (poisoned) instead
                            of silently wrong.  fp32 paths never set it. */
+  void* scratch;        /* nullable (ABI 12): device, rrin_net_scratch_bytes(d) bytes, zero-filled
+                           once (its ticket words are left zero by every call); F32R split-K
+                           slabs of convs with ksplit > 1 (required for them: RRIN_E_WORKSPACE
+                           without) and the ring fix-up's cross-workgroup K split (used only
+                           when present; the same bits either way).  Kept out of the workspace
+                           so plans without splits pay nothing for it. */
+  int64_t scratch_bytes;
 } rrin_net_desc;
+
+/* Bytes of rrin_net_desc.scratch the forward of d needs with its conv table
+ * (0: none; only n, h, w, prec and convs are read).  One forward at a time per scratch. */
+int64_t rrin_net_scratch_bytes(const rrin_net_desc* d);
 
 int rrin_net_conv_count(void);                 /* 77 = 81 convs - 4 heads      */
 
@@ -443,8 +454,11 @@ typedef struct rrin_unet_desc {
   int64_t workspace_bytes;
   rrin_prof* prof;                 /* nullable */
   int32_t* status;                 /* optional device int32: the F16X3 / F16 range guard, as rrin_net_desc */
+  void* scratch;                   /* nullable (ABI 12): as rrin_net_desc.scratch, rrin_unet_scratch_bytes */
+  int64_t scratch_bytes;
 } rrin_unet_desc;
 int64_t rrin_unet_conv_count(int32_t depth);
+int64_t rrin_unet_scratch_bytes(const rrin_unet_desc* d);
 int rrin_unet_fwd(const rrin_unet_desc* d, void* stream);
 int64_t rrin_net_workspace_bytes(int32_t n, int32_t h, int32_t w, int32_t prec);
 int rrin_net_fwd(const rrin_net_desc* d, void* stream);

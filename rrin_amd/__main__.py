@@ -1,8 +1,11 @@
 """``python -m rrin_amd --model_name M convert --sf S --fps F --image_folder D``
 
 Same command line as the reference (`/root/reference/__main__.py:33-72`).
-``train`` is accepted for compatibility but is out of scope (no backward
-kernels)."""
+``train`` is parsed for compatibility but refused: the training loop and its
+losses (reference ``train.py`` / ``losses.py``: AdamW, the VGG19 perceptual loss
+whose weights come from the network) are out of scope.  The
+model's own forward and backward do run on the HIP training kernels
+(``rrin_amd.autograd``): call ``Net`` under autograd from your loop."""
 import argparse
 import warnings
 
@@ -14,7 +17,7 @@ def build_parser():
     p.add_argument("--rm", action="store_true", default=False, help="Removed temp folder on proper finish.")
     sub = p.add_subparsers(dest="mode")
     sub.required = True
-    tr = sub.add_parser("train", help="Train the model (not supported by rrin_amd)")
+    tr = sub.add_parser("train", help="Train the model (the loop is not shipped by rrin_amd)")
     tr.add_argument("--train_folder", type=str, required=True)
     tr.add_argument("--resume", action="store_true", default=False)
     tr.add_argument("--batch_size", type=int, default=2)
@@ -35,8 +38,9 @@ def build_parser():
 def main(argv=None):
     args = build_parser().parse_args(argv)
     if args.mode == "train":
-        raise SystemExit("rrin_amd is an inference implementation: training needs backward kernels "
-                         "(out of scope, SURVEY §8f f4); use the reference train.py")
+        raise SystemExit("rrin_amd does not ship the training loop (AdamW, VGG19 perceptual loss: out of "
+                         "scope, SURVEY §2 rows 11-12); Net.forward / backward run on the HIP training "
+                         "kernels under autograd, so drive them from your own loop or the reference train.py")
     from .convert import convert
     with warnings.catch_warnings():
         warnings.simplefilter("ignore", category=UserWarning)

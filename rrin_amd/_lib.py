@@ -9,7 +9,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-ABI_VERSION = 11
+ABI_VERSION = 12
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "librrin_hip.so")
 
 # enums (rrin_hip.h)
@@ -97,7 +97,7 @@ class NetDesc(C.Structure):
                 ("convs", C.POINTER(ConvWeights)), ("heads", C.POINTER(HeadWeights)),
                 ("workspace", C.c_void_p), ("workspace_bytes", C.c_int64),
                 ("skip_flow", C.c_int32), ("prec", C.c_int32), ("prof", C.c_void_p), ("taps", C.c_void_p),
-                ("status", C.c_void_p)]
+                ("status", C.c_void_p), ("scratch", C.c_void_p), ("scratch_bytes", C.c_int64)]
 
 
 class TConvDesc(C.Structure):
@@ -120,7 +120,8 @@ class UNetDesc(C.Structure):
     _fields_ = [("n", C.c_int32), ("h", C.c_int32), ("w", C.c_int32), ("in_ch", C.c_int32), ("out_ch", C.c_int32),
                 ("depth", C.c_int32), ("prec", C.c_int32), ("pad_", C.c_int32), ("x", C.c_void_p), ("y", C.c_void_p),
                 ("convs", C.POINTER(ConvWeights)), ("head", HeadWeights), ("workspace", C.c_void_p),
-                ("workspace_bytes", C.c_int64), ("prof", C.c_void_p), ("status", C.c_void_p)]
+                ("workspace_bytes", C.c_int64), ("prof", C.c_void_p), ("status", C.c_void_p),
+                ("scratch", C.c_void_p), ("scratch_bytes", C.c_int64)]
 
 
 # every symbol include/rrin_hip.h declares: name -> (restype, argtypes)
@@ -141,6 +142,8 @@ SIGNATURES = {
                                 C.c_int32, C.c_int32, C.c_void_p]),
     "rrin_net_conv_count": (C.c_int, []),
     "rrin_net_workspace_bytes": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32, C.c_int32]),
+    "rrin_net_scratch_bytes": (C.c_int64, [C.POINTER(NetDesc)]),
+    "rrin_unet_scratch_bytes": (C.c_int64, [C.POINTER(UNetDesc)]),
     "rrin_make_geom_h8": (C.c_int, [C.c_int32, C.c_int32, C.POINTER(Geom)]),
     "rrin_conv_h8_cfg_count": (C.c_int, []),
     "rrin_conv_h8_cfg_bm": (C.c_int, [C.c_int32]),
@@ -210,6 +213,18 @@ _LIB = None
 
 class RRINError(RuntimeError):
     pass
+
+
+def build_id(path: str = LIB_PATH) -> str:
+    """First 16 hex digits of the SHA-256 of the library file: names the build a
+    measurement came from (profiles/pmc_traffic.json entries carry it; bench.py only
+    reports a PMC traffic figure measured on the library it runs)."""
+    import hashlib
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for blk in iter(lambda: f.read(1 << 20), b""):
+            h.update(blk)
+    return h.hexdigest()[:16]
 
 
 def lib():

@@ -32,8 +32,10 @@ from . import _lib
 LEAKY_SLOPE = 0.1
 
 
-def _stream():
-    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+def _stream(device: torch.device):
+    """The current stream of the tensors' device (not the thread's current device: a
+    model on cuda:1 without set_device must not launch on device 0's stream)."""
+    return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 
 def _f32(t: torch.Tensor) -> torch.Tensor:
@@ -55,7 +57,7 @@ class _Conv3x3(torch.autograd.Function):
         d = _lib.TConvDesc(n=n, cin=cin, cout=cout, h=h, w=w, mode=_lib.TCONV_FWD, leaky=int(leaky),
                            slope=LEAKY_SLOPE, x=x.data_ptr(), y=None, wt=weight.data_ptr(),
                            bias=bias.data_ptr() if bias is not None else None, out=y.data_ptr())
-        _lib.check(_lib.lib().rrin_tconv3x3(C.byref(d), _stream()), "rrin_tconv3x3 (forward)")
+        _lib.check(_lib.lib().rrin_tconv3x3(C.byref(d), _stream(x.device)), "rrin_tconv3x3 (forward)")
         ctx.leaky = bool(leaky)
         ctx.has_bias = bias is not None
         ctx.save_for_backward(x, weight, y if leaky else None)
@@ -68,7 +70,7 @@ class _Conv3x3(torch.autograd.Function):
         n, cin, h, w = x.shape
         cout = weight.shape[0]
         L = _lib.lib()
-        st = _stream()
+        st = _stream(x.device)
         gx = gw = gb = None
         if ctx.needs_input_grad[0]:
             gx = torch.empty_like(x)
@@ -96,7 +98,7 @@ class _AvgPool2(torch.autograd.Function):
         x = _f32(x)
         n, c, h, w = x.shape
         y = torch.empty((n, c, h // 2, w // 2), dtype=torch.float32, device=x.device)
-        _lib.check(_lib.lib().rrin_tpool2_fwd(x.data_ptr(), y.data_ptr(), n * c, h, w, _stream()), "rrin_tpool2_fwd")
+        _lib.check(_lib.lib().rrin_tpool2_fwd(x.data_ptr(), y.data_ptr(), n * c, h, w, _stream(x.device)), "rrin_tpool2_fwd")
         ctx.shape = x.shape
         return y
 
@@ -105,7 +107,7 @@ class _AvgPool2(torch.autograd.Function):
         gy = _f32(gy)
         n, c, h, w = ctx.shape
         gx = torch.empty(ctx.shape, dtype=torch.float32, device=gy.device)
-        _lib.check(_lib.lib().rrin_tpool2_bwd(gy.data_ptr(), gx.data_ptr(), n * c, h, w, _stream()),
+        _lib.check(_lib.lib().rrin_tpool2_bwd(gy.data_ptr(), gx.data_ptr(), n * c, h, w, _stream(gy.device)),
                    "rrin_tpool2_bwd")
         return gx
 
@@ -116,7 +118,7 @@ class _Upsample2(torch.autograd.Function):
         x = _f32(x)
         n, c, h, w = x.shape
         y = torch.empty((n, c, 2 * h, 2 * w), dtype=torch.float32, device=x.device)
-        _lib.check(_lib.lib().rrin_tup2_fwd(x.data_ptr(), y.data_ptr(), n * c, h, w, _stream()), "rrin_tup2_fwd")
+        _lib.check(_lib.lib().rrin_tup2_fwd(x.data_ptr(), y.data_ptr(), n * c, h, w, _stream(x.device)), "rrin_tup2_fwd")
         ctx.shape = x.shape
         return y
 
@@ -125,7 +127,7 @@ class _Upsample2(torch.autograd.Function):
         gy = _f32(gy)
         n, c, h, w = ctx.shape
         gx = torch.empty(ctx.shape, dtype=torch.float32, device=gy.device)
-        _lib.check(_lib.lib().rrin_tup2_bwd(gy.data_ptr(), gx.data_ptr(), n * c, h, w, _stream()), "rrin_tup2_bwd")
+        _lib.check(_lib.lib().rrin_tup2_bwd(gy.data_ptr(), gx.data_ptr(), n * c, h, w, _stream(gy.device)), "rrin_tup2_bwd")
         return gx
 
 
@@ -137,7 +139,7 @@ class _Backwarp(torch.autograd.Function):
         if flow.shape != (n, 2, h, w):
             raise ValueError(f"flow {tuple(flow.shape)} for image {tuple(img.shape)}")
         out = torch.empty_like(img)
-        _lib.check(_lib.lib().rrin_warp_fwd(img.data_ptr(), flow.data_ptr(), out.data_ptr(), n, c, h, w, _stream()),
+        _lib.check(_lib.lib().rrin_warp_fwd(img.data_ptr(), flow.data_ptr(), out.data_ptr(), n, c, h, w, _stream(img.device)),
                    "rrin_warp_fwd")
         ctx.save_for_backward(img, flow)
         return out
@@ -155,7 +157,7 @@ class _Backwarp(torch.autograd.Function):
         gimg = torch.empty_like(img)
         gflow = torch.empty_like(flow)
         _lib.check(L.rrin_twarp_bwd(img.data_ptr(), flow.data_ptr(), gout.data_ptr(), gimg.data_ptr(),
-                                    gflow.data_ptr(), work.data_ptr(), nb, n, c, h, w, _stream()), "rrin_twarp_bwd")
+                                    gflow.data_ptr(), work.data_ptr(), nb, n, c, h, w, _stream(img.device)), "rrin_twarp_bwd")
         return gimg, gflow
 
 

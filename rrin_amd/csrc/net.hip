@@ -50,6 +50,16 @@ struct Buf {
   rrin_geom g;
 };
 
+// What a schedule needs of the caller's scratch (size query, rrin_net_scratch_bytes):
+// split-K slabs and tickets of the split convs, the ring fix-up's cross-workgroup K split.
+struct ScratchNeed {
+  int64_t part_floats = 0, cnt_ints = 0;
+  void add(int64_t f, int64_t c) {
+    part_floats = f > part_floats ? f : part_floats;
+    cnt_ints = c > cnt_ints ? c : cnt_ints;
+  }
+};
+
 // Workspace plan: offsets are identical in size query and forward.
 struct Plan {
   int n, prec;
@@ -68,18 +78,21 @@ struct Plan {
                           // edge-replicate padding by its producer (EPI_LEAKY_REP)
   float* EDGE;            // F16*: pre-bias ring values of the current sub-pixel up conv
   Buf FLOWRAW;            // raw 4-ch Flow output, kept for reuse across t (skip_flow)
-  float* PART;            // F32R: split-K slice outputs of the current conv (kPartFloats)
-  int32_t* CNT;           // F32R: split-K tile counters (kPartTiles; zero between convs)
+  // split-K / ring fix-up K-split scratch: the caller's (rrin_net_desc.scratch), not the
+  // workspace, so a plan without splits pays nothing for it
+  float* PART;            // F32R: split-K slice outputs of the current conv (part_floats)
+  int32_t* CNT;           // F32R: split-K tile counters (cnt_ints; zero between convs)
+  int64_t part_floats, cnt_ints;
+  ScratchNeed* dry;       // non-null: size query only -- record the scratch the schedule
+                          // needs, launch nothing (rrin_net_scratch_bytes)
   float* RCORR;           // F32R: ring-fold corrections of the current sub-pixel conv
   int32_t* RCNT;          // F32R: ring-fold segment tickets (zero between convs)
   int64_t rcorr_floats, rcnt_ints;
   int64_t bytes;
 };
 
-// split-K scratch of an F32R plan: a split conv may have up to kPartFloats slice
-// outputs (8192 per TH 8 tile and slice: 4096 slices) and kPartTiles tiles
-constexpr int64_t kPartFloats = (int64_t)4096 * 8192;
-constexpr int64_t kPartTiles = 4096;
+// Caller-provided scratch (rrin_net_desc.scratch): [cnt_ints tickets | part floats]
+constexpr int64_t kScratchTickets = 4096;  // ints at the head of the scratch (16 KB)
 // ring fix-up: cross-workgroup K split up to this many workgroups (one per CU;
 // RRIN_EDGE_CROSS_MAX: A/B builds)
 #ifndef RRIN_EDGE_CROSS_MAX
@@ -158,12 +171,19 @@ void make_plan(int n, int h, int w, int prec, char* base, Plan& p) {
     off += align256(p.rcorr_floats * 4);
     p.RCNT = base ? reinterpret_cast<int32_t*>(base + off) : nullptr;
     off += align256(p.rcnt_ints * 4);
-    p.PART = base ? reinterpret_cast<float*>(base + off) : nullptr;
-    off += align256(kPartFloats * 4);
-    p.CNT = base ? reinterpret_cast<int32_t*>(base + off) : nullptr;
-    off += align256(kPartTiles * 4);
   }
+  p.part_floats = p.cnt_ints = 0;
+  p.dry = nullptr;
   p.bytes = off;
+}
+
+// The caller's scratch into the plan (F32R only; null / too small: no splits).
+void attach_scratch(Plan& p, void* scratch, int64_t bytes) {
+  if (p.prec != RRIN_PREC_F32R || !scratch || bytes < kScratchTickets * 4) return;
+  p.CNT = reinterpret_cast<int32_t*>(scratch);
+  p.cnt_ints = kScratchTickets;
+  p.PART = reinterpret_cast<float*>(reinterpret_cast<char*>(scratch) + kScratchTickets * 4);
+  p.part_floats = (bytes - kScratchTickets * 4) / 4;
 }
 
 // H8 view of channels [ch_off, ch_off+channels) of a buffer, at geometry g
@@ -356,16 +376,20 @@ int conv_h8(const Plan& p, const rrin_conv_weights& cw, int cin, int cout, int e
     if (need < 0) return (int)need;
     if (need > p.rcorr_floats || cnt > p.rcnt_ints) return RRIN_E_CONFIG;
   }
-  if (cw.ksplit > 1) {
-    if (!p.PART) return RRIN_E_CONFIG;
+  if (cw.ksplit > 1 && p.prec == RRIN_PREC_F32R) {
     d.ksplit = cw.ksplit;
     d.part = p.PART;
     d.cnt = p.CNT;
     int64_t cnt = 0;
     const int64_t need = rrin_conv_h8_split_floats(&d, &cnt);
     if (need < 0) return (int)need;
-    if (need > kPartFloats || cnt > kPartTiles) return RRIN_E_CONFIG;
+    if (p.dry) {
+      p.dry->add(need, cnt);
+    } else if (!p.PART || need > p.part_floats || cnt > p.cnt_ints) {
+      return RRIN_E_WORKSPACE;  // scratch smaller than rrin_net_scratch_bytes
+    }
   }
+  if (p.dry) return 0;
   return rrin_conv3x3_h8_fwd(&d, st);
 }
 
@@ -396,16 +420,21 @@ int upconv_subpixel(const Plan& p, const rrin_conv_weights& cw, int C, const rri
   // (640x368 x 1: fix-up 195 -> 129 us per forward); larger grids keep one
   // workgroup per tile, whose extra workgroups only queue behind the other
   // stream's convs (720p x 4 on 2 streams: fix-up span 1.4 -> 3.5 ms per step)
-  if (p.PART && p.CNT) {
+  if (p.prec == RRIN_PREC_F32R) {
     int64_t tk = 0;
     const int64_t nf = rrin_edge_fix_split_floats(&e, &tk);
     if (nf > 0 && nf / 1024 <= kEdgeCrossMaxGroups) {
-      e.part = p.PART;
-      e.cnt = p.CNT;
-      e.part_floats = kPartFloats;
-      e.cnt_len = (int32_t)kPartTiles;
+      if (p.dry) {
+        p.dry->add(nf, tk);
+      } else if (p.PART && nf <= p.part_floats && tk <= p.cnt_ints) {
+        e.part = p.PART;
+        e.cnt = p.CNT;
+        e.part_floats = p.part_floats;
+        e.cnt_len = (int32_t)p.cnt_ints;
+      }
     }
   }
+  if (p.dry) return 0;
   ProfScope ps(p.prof, st, RRIN_KIND_EDGE, 0.0);
   return rrin_subpixel_edge_fix_h8(&e, st);
 }
@@ -447,7 +476,7 @@ int run_unet_h8(const Plan& p, const UNetSpec& u, const rrin_conv_weights* cw, c
       RRIN_TRY(upconv_subpixel(p, cu, C, x, up, st));
     } else {
       const rrin_h8 upin = hview(p.UPT[L], 0, 2 * C);
-      {
+      if (!p.dry) {
         ProfScope ps(p.prof, st, RRIN_KIND_LAYOUT, 0.0);
         RRIN_TRY(rrin_upsample2x_h8(&x, &upin, p.n, p.prec, st));
       }
@@ -478,6 +507,7 @@ int run_unet_h8(const Plan& p, const UNetSpec& u, const rrin_conv_weights* cw, c
   hd.raw_out = io.raw;
   hd.status = p.status;
   if (u.head_mode == RRIN_HEAD_FLOW) hd.flow_raw = hview(p.FLOWRAW, 0, 4);
+  if (p.dry) return 0;
   ProfScope ps(p.prof, st, RRIN_KIND_HEAD, 2.0 * 9 * 32 * u.out_ch * (double)x.g.h * x.g.w * p.n);
   return rrin_head_h8_fwd(&hd, st);
 }
@@ -504,6 +534,35 @@ extern "C" int64_t rrin_net_workspace_bytes(int32_t n, int32_t h, int32_t w, int
   return p.bytes;
 }
 
+// Scratch the schedule of d needs (F32R: the split convs' slabs and tickets, the ring
+// fix-up's cross-workgroup K split; other precisions 0): the schedule walked with every
+// launch skipped.
+static int64_t scratch_bytes_of(int n, int h, int w, int prec, const rrin_conv_weights* convs, const UNetSpec* us,
+                                int nu) {
+  if (prec != RRIN_PREC_F32R) return 0;
+  Plan p;
+  // a stand-in base so the views pass the descriptor checks; never dereferenced
+  make_plan(n, h, w, prec, reinterpret_cast<char*>((uintptr_t)1 << 30), p);
+  ScratchNeed need;
+  p.dry = &need;
+  const rrin_head_weights hw{};
+  int k = 0;
+  for (int u = 0; u < nu; ++u) {
+    RRIN_TRY(run_unet_h8(p, us[u], convs + k, hw, HeadIO{nullptr, nullptr, nullptr}, nullptr));
+    k += convs_of(us[u].depth);
+  }
+  if (need.part_floats == 0 && need.cnt_ints == 0) return 0;
+  if (need.cnt_ints > kScratchTickets) return RRIN_E_CONFIG;
+  return kScratchTickets * 4 + need.part_floats * 4;
+}
+
+extern "C" int64_t rrin_net_scratch_bytes(const rrin_net_desc* d) {
+  if (!d || !d->convs) return RRIN_E_ARG;
+  if (d->n < 1 || d->h < 16 || d->w < 16 || (d->h % 16) || (d->w % 16)) return RRIN_E_SHAPE;
+  if (d->prec < RRIN_PREC_F32 || d->prec > RRIN_PREC_F32R) return RRIN_E_ARG;
+  return scratch_bytes_of(d->n, d->h, d->w, d->prec, d->convs, kUNets, 4);
+}
+
 extern "C" int rrin_net_fwd(const rrin_net_desc* d, void* stream) {
   if (!d || !d->i0 || !d->i1 || !d->out || !d->coef || !d->convs || !d->heads || !d->workspace)
     return RRIN_E_ARG;
@@ -512,6 +571,7 @@ extern "C" int rrin_net_fwd(const rrin_net_desc* d, void* stream) {
   Plan p;
   make_plan(d->n, d->h, d->w, d->prec, reinterpret_cast<char*>(d->workspace), p);
   if (d->workspace_bytes < p.bytes) return RRIN_E_WORKSPACE;
+  attach_scratch(p, d->scratch, d->scratch_bytes);
   p.prof = d->prof;  // per call: concurrent calls never share launch state
   if (p.prof) p.prof->chain = false;  // the call's first launch records its own start
   hipStream_t st = (hipStream_t)stream;
@@ -571,6 +631,16 @@ extern "C" int64_t rrin_unet_conv_count(int32_t depth) {
   return (depth < 2 || depth > kMaxDepth) ? RRIN_E_ARG : convs_of(depth);
 }
 
+extern "C" int64_t rrin_unet_scratch_bytes(const rrin_unet_desc* d) {
+  if (!d || !d->convs) return RRIN_E_ARG;
+  if (d->n < 1 || d->h < 16 || d->w < 16 || (d->h % 16) || (d->w % 16)) return RRIN_E_SHAPE;
+  if (d->in_ch < 1 || d->in_ch > 16 || d->out_ch < 2 || d->out_ch > 4 || d->depth < 2 || d->depth > kMaxDepth)
+    return RRIN_E_ARG;
+  if (d->prec < RRIN_PREC_F32 || d->prec > RRIN_PREC_F32R) return RRIN_E_ARG;
+  const UNetSpec u{d->in_ch, d->out_ch, d->depth, RRIN_HEAD_PLAIN};
+  return scratch_bytes_of(d->n, d->h, d->w, d->prec, d->convs, &u, 1);
+}
+
 extern "C" int rrin_unet_fwd(const rrin_unet_desc* d, void* stream) {
   if (!d || !d->x || !d->y || !d->convs || !d->head.w || !d->head.bias || !d->workspace) return RRIN_E_ARG;
   if (d->n < 1 || d->h < 16 || d->w < 16 || (d->h % 16) || (d->w % 16)) return RRIN_E_SHAPE;
@@ -580,6 +650,7 @@ extern "C" int rrin_unet_fwd(const rrin_unet_desc* d, void* stream) {
   Plan p;
   make_plan(d->n, d->h, d->w, d->prec, reinterpret_cast<char*>(d->workspace), p);
   if (d->workspace_bytes < p.bytes) return RRIN_E_WORKSPACE;
+  attach_scratch(p, d->scratch, d->scratch_bytes);
   p.prof = d->prof;
   if (p.prof) p.prof->chain = false;
   hipStream_t st = (hipStream_t)stream;
@@ -721,7 +792,8 @@ extern "C" const char* rrin_strerror(int code) {
     case RRIN_E_ARG:
       return "rrin: invalid argument (null pointer, mode or channel range)";
     case RRIN_E_WORKSPACE:
-      return "rrin: workspace smaller than rrin_net_workspace_bytes()";
+      return "rrin: workspace smaller than rrin_net_workspace_bytes() (or scratch smaller than "
+             "rrin_net_scratch_bytes())";
     case RRIN_E_CONFIG:
       return "rrin: unknown conv tile config";
   }

@@ -269,13 +269,19 @@ __global__ void tabsmax_kernel(const float* __restrict__ g, int64_t total, unsig
   if ((threadIdx.x & 63) == 0) atomicMax(mx, __float_as_uint(v));
 }
 
-// 2^e such that max|g| * 2^e ~ 2^40 (room for 2^23 contributions per pixel)
-__device__ inline float fx_scale(const unsigned* mx) {
+// 2^s with max|g| * 2^s < 2^(62 - hb), hb = ceil(log2(h w)): a source pixel receives at
+// most one tap from each of the image's h w output pixels (weight <= 1), so its signed
+// 64-bit sum cannot overflow at any size; the ulp stays 2^-(62 - hb) of max|g| (2^-39 at
+// 4K).  s is capped at 126 so the scale stays finite for tiny gradients (those that fall
+// below the ulp then count as zero, as they would in fp32 against max|g|).
+__device__ inline float fx_scale(const unsigned* mx, int64_t hw) {
   const float m = __uint_as_float(*mx);
   if (!(m > 0.f)) return 1.f;
   int e;
   frexpf(m, &e);  // m = f * 2^e, f in [0.5, 1)
-  return ldexpf(1.f, 40 - e);
+  int hb = 0;
+  while (((int64_t)1 << hb) < hw) ++hb;
+  return ldexpf(1.f, min(62 - hb - e, 126));
 }
 
 __global__ void twarp_bwd_kernel(const float* __restrict__ img, const float* __restrict__ flow,
@@ -291,7 +297,7 @@ __global__ void twarp_bwd_kernel(const float* __restrict__ img, const float* __r
   const float u = flow[(int64_t)n * 2 * hw + (int64_t)y * w + x];
   const float v = flow[(int64_t)n * 2 * hw + hw + (int64_t)y * w + x];
   const WarpTaps tp = warp_taps(x, y, u, v, h, w);
-  const float sc = fx_scale(mx);
+  const float sc = fx_scale(mx, hw);
   float gix = 0.f, giy = 0.f;
   // tap weights nw = s e, ne = s we, sw = n e, se = n we (common.hpp warp_taps)
   const float we_ = tp.wx, e_ = 1.0f - tp.wx, n_ = tp.wy, s_ = 1.0f - tp.wy;
@@ -308,7 +314,7 @@ __global__ void twarp_bwd_kernel(const float* __restrict__ img, const float* __r
     giy += go * ((cc - a) * e_ + (d - b) * we_);
     unsigned long long* q = acc + ((int64_t)n * c + ch) * hw + (int64_t)tp.y0 * w + tp.x0;
     auto add = [&](bool ok, int64_t off, float wgt) {
-      if (ok) atomicAdd(q + off, (unsigned long long)(long long)llrintf(go * wgt * sc));
+      if (ok && wgt != 0.f) atomicAdd(q + off, (unsigned long long)(long long)llrintf(go * wgt * sc));
     };
     add(tp.vy0 && tp.vx0, 0, tp.nw);
     add(tp.vy0 && tp.vx1, 1, tp.ne);
@@ -321,10 +327,10 @@ __global__ void twarp_bwd_kernel(const float* __restrict__ img, const float* __r
 }
 
 __global__ void tfix_to_float_kernel(const unsigned long long* __restrict__ acc, const unsigned* mx, float* out,
-                                     int64_t total) {
+                                     int64_t total, int64_t hw) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
-  out[i] = (float)((double)(long long)acc[i] / (double)fx_scale(mx));
+  out[i] = (float)((double)(long long)acc[i] / (double)fx_scale(mx, hw));
 }
 
 inline int grid_of(int64_t total) { return (int)((total + 255) / 256); }
@@ -453,6 +459,6 @@ extern "C" int rrin_twarp_bwd(const float* img, const float* flow, const float* 
   hipLaunchKernelGGL(twarp_bwd_kernel, dim3(grid_of(px)), dim3(256), 0, st, img, flow, gout, acc, gflow,
                      (const unsigned*)mx, c, h, w, px);
   hipLaunchKernelGGL(tfix_to_float_kernel, dim3(grid_of(total)), dim3(256), 0, st, (const unsigned long long*)acc,
-                     (const unsigned*)mx, gimg, total);
+                     (const unsigned*)mx, gimg, total, (int64_t)h * w);
   return hip_code(hipGetLastError());
 }

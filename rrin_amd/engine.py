@@ -193,11 +193,15 @@ WINO_TH4 = {"small": {(256, 512, 4), (512, 512, 4), (256, 512, 3)},
 # Split-K of the Winograd convs (rrin_conv_h8_desc.ksplit; kinds 3, 4) per size
 # class, grid level -> slices: the few-tile deep convs of small forward parts, where a
 # tile per workgroup leaves most CUs idle.  A split conv sums its K slices in slice
-# order (a different rounding from the unsplit conv, fixed per conv and class: batch
-# == per-sample stays bitwise within a class).  640x368 x 1 (profiles/r03/split_ab.txt):
-# none 272.7 pairs/s, L4 / 4 277.6, L3 / 2 + L4 / 4 279.1, L2 / 2 + L3 / 4 + L4 / 8
-# 274.6; 1280x720 x 1 loses with L3 / 2 + L4 / 4 (110.0 -> 108.7), so only "small".
-WINO_SPLIT = {"small": {3: 2, 4: 4}}
+# order, a different rounding from the unsplit conv.  640x368 x 1
+# (profiles/r03/split_ab.txt): none 272.7 pairs/s, L4 / 4 277.6, L3 / 2 + L4 / 4 279.1,
+# L2 / 2 + L3 / 4 + L4 / 8 274.6 -- within the box-to-box spread; 1280x720 x 1 loses.
+# Off by default since round 4: the size class follows n*h*w, so a split class would
+# make a pair's bits depend on its batch size, stream split or shard (DESIGN §6/§7
+# promise batch == per-sample and sharded == unsharded bitwise at every n).  Every
+# class now rounds identically (tests/test_gpu_net.py::test_batch_size_bitwise_640x368);
+# the machinery stays for A/B (WINO_SPLIT_LEVELS, bench.py --wino-split).
+WINO_SPLIT = {}
 # A/B override: grid level -> slices for every Winograd conv at that level, all classes
 WINO_SPLIT_LEVELS = {}
 
@@ -347,6 +351,7 @@ class RRINEngine:
             self.head_table[i].w = w.data_ptr()
             self.head_table[i].bias = b.data_ptr()
         self.cfgs = [m[2] for m in meta]
+        self._scratch = {}
         self._ws = OrderedDict()
         self._flow_valid = {}
         self._sides = []
@@ -395,6 +400,7 @@ class RRINEngine:
         self._packs = {}          # size class -> packing
         self._packs_by_cfgs = {}  # tuple of per-conv configs -> packing (shared between classes)
         _, _, self.conv_table, self.cfgs = self._pack_h8("large")
+        self._scratch = {}
         self._ws = OrderedDict()
         self._flow_valid = {}
         self._sides = []
@@ -549,12 +555,28 @@ class RRINEngine:
             while len(self._ws) >= self.MAX_WORKSPACES:
                 old, _ = self._ws.popitem(last=False)
                 self._flow_valid.pop(old, None)
+                for sk in [k for k in self._scratch if k[0] == old]:
+                    del self._scratch[sk]
             ws = torch.zeros(int(nbytes), dtype=torch.uint8, device=self.device)
             self._ws[key] = ws
             self._flow_valid[key] = False
         else:
             self._ws.move_to_end(key)
         return ws
+
+    def scratch(self, key, desc, query) -> torch.Tensor | None:
+        """Split-K / ring fix-up scratch of workspace ``key`` for the conv table of ``desc``
+        (rrin_net_scratch_bytes / rrin_unet_scratch_bytes; None when the schedule needs none),
+        zero-filled once, cached per workspace and table."""
+        sk = (key, C.addressof(desc.convs.contents))
+        if sk in self._scratch:
+            return self._scratch[sk]
+        nbytes = int(query(C.byref(desc)))
+        if nbytes < 0:
+            _lib.check(nbytes, "rrin_net_scratch_bytes")
+        sc = torch.zeros(nbytes, dtype=torch.uint8, device=self.device) if nbytes > 0 else None
+        self._scratch[sk] = sc
+        return sc
 
     side_priority = 0  # torch.cuda.Stream priority of the side streams (-1: high)
 
@@ -653,6 +675,9 @@ class RRINEngine:
         d.head = self.head_table[0]
         ws = self.workspace(n, h, w, slot=100)   # own workspace: its input channels [C, 16) stay zero
         d.workspace, d.workspace_bytes = ws.data_ptr(), ws.numel()
+        sc = self.scratch((n, h, w, 100), d, self.lib.rrin_unet_scratch_bytes)
+        if sc is not None:
+            d.scratch, d.scratch_bytes = sc.data_ptr(), sc.numel()
         status = self._status_of(100) if self.prec in (_lib.PREC_F16X3, _lib.PREC_F16) else None
         d.status = status.data_ptr() if status is not None else None
         with torch.cuda.device(self.device):
@@ -681,6 +706,9 @@ class RRINEngine:
         d.prec = self.prec
         d.prof = prof
         d.taps = tapbuf.data_ptr() if tapbuf is not None else None
+        sc = self.scratch(key, d, self.lib.rrin_net_scratch_bytes)
+        if sc is not None:
+            d.scratch, d.scratch_bytes = sc.data_ptr(), sc.numel()
         st = self._status_of(slot) if self.prec in (_lib.PREC_F16X3, _lib.PREC_F16) else None
         d.status = st.data_ptr() if st is not None else None
         _lib.check(self.lib.rrin_net_fwd(C.byref(d), C.c_void_p(stream.cuda_stream)), "rrin_net_fwd")

@@ -83,6 +83,28 @@ def test_batch_equals_per_sample_and_deterministic(gpu, nets):
     assert torch.equal(full, parts)
 
 
+@pytest.mark.parametrize("precision", ["fp32", "fp16"])
+def test_batch_size_bitwise_640x368(gpu, nets, precision):
+    """at 640x368 (BASELINE C2) a pair's bits must not depend on how it is
+    batched -- one pair alone (the "small" size class) vs three in one call ("medium")
+    vs a 2-stream split -- since the size class follows n*h*w and sharding relies on
+    batch == per-sample.  No class may pick a different K association (split-K)."""
+    net = nets["stress"]
+    net.precision = precision
+    try:
+        i0, i1 = synthetic_batch(3, 368, 640, first_index=40)
+        i0, i1 = i0.to(gpu), i1.to(gpu)
+        eng = net.engine()
+        with torch.no_grad():
+            three = eng.forward(i0, i1, 0.5)
+            two_streams = eng.forward(i0, i1, 0.5, streams=2)
+            ones = torch.cat([eng.forward(i0[k:k + 1], i1[k:k + 1], 0.5) for k in range(3)])
+        assert torch.equal(three, ones)
+        assert torch.equal(two_streams, three)
+    finally:
+        net.precision = "fp32"
+
+
 @pytest.mark.parametrize("precision", ["fp32_split16", "fp16", "fp32", "fp32_planar"])
 def test_streams_split_is_bitwise(gpu, nets, precision):
     """The batch split over several HIP streams (engine.forward(streams=k)) gives the

@@ -151,3 +151,23 @@ def test_size_class_tables():
     assert engine.size_class(2 * 1280 * 720) == "large"
     assert engine.size_class(4 * 1280 * 720) == "xlarge"
     assert engine.size_class(3840 * 2176) == "xxlarge"
+
+
+def test_autograd_stream_follows_tensor_device(monkeypatch):
+    """the training kernels launch on the current stream of the tensors'
+    device, not of the thread's current device (a model on cuda:1 without set_device)."""
+    import torch
+
+    from rrin_amd import autograd as ag
+    seen = []
+
+    class _S:
+        cuda_stream = 1234
+
+    def fake_current_stream(device=None):
+        seen.append(device)
+        return _S()
+
+    monkeypatch.setattr(torch.cuda, "current_stream", fake_current_stream)
+    st = ag._stream(torch.device("cuda", 1))
+    assert st.value == 1234 and seen == [torch.device("cuda", 1)]

@@ -207,3 +207,52 @@ def test_edge_fix_split_scratch_size():
         assert cnt.value == (tiles if runs > 1 else 0)
     e.cin = 4
     assert lib.rrin_edge_fix_split_floats(C.byref(e), None) < 0
+
+
+def _net_table(lib, ksplit_at=None):
+    """A 77-entry exact-fp32 Winograd conv table in rrin_net_fwd's schedule order (per
+    U-Net: down a/b per level, mid, up/a/b per level), sub-pixel up convs at levels 0-2
+    (the engine's default), ksplit_at: grid level -> slices."""
+    import ctypes as C
+    wq = next(c for c in range(lib.rrin_conv_h8_cfg_count()) if lib.rrin_conv_h8_cfg_wino(c) == 3)
+    rows = []
+    for depth in (5, 4, 4, 4):  # Flow, refine_flow, Mask, final (model.py:27-30)
+        for L in range(depth):
+            rows += [(L, 0), (L, 0)]
+        rows.append((depth - 1, 0))
+        for L in range(depth - 2, -1, -1):
+            sub = L <= 2
+            rows += [(L + 1 if sub else L, int(sub)), (L, 0), (L, 0)]
+    t = (_lib.ConvWeights * len(rows))()
+    for i, (grid_level, sub) in enumerate(rows):
+        t[i].cfg, t[i].subpixel = wq, sub
+        t[i].whi, t[i].bias = 1, 1  # never dereferenced by the size query
+        if sub:
+            t[i].wedge, t[i].bias_raw = 1, 1
+        t[i].ksplit = (ksplit_at or {}).get(grid_level, 0)
+    return t, C.cast(t, C.POINTER(_lib.ConvWeights))
+
+
+def test_net_scratch_bytes():
+    """rrin_net_scratch_bytes (ABI 12): the split-K / ring fix-up scratch lives outside the
+    workspace, sized by the conv table -- none for an unsplit 720p x 4 forward (its ring
+    fix-up grids exceed the cross-split limit), the ring fix-up's K split alone for
+    640x368 x 1, more with split-K convs; zero for the other precisions."""
+    import ctypes as C
+    lib = _lib.lib()
+    assert lib.rrin_net_conv_count() == 77
+
+    def need(n, h, w, prec=_lib.PREC_F32R, ks=None):
+        t, ptr = _net_table(lib, ks)
+        d = _lib.NetDesc()
+        d.n, d.h, d.w, d.prec, d.convs = n, h, w, prec, ptr
+        return lib.rrin_net_scratch_bytes(C.byref(d))
+
+    assert need(4, 720, 1280) == 0
+    base = need(1, 368, 640)
+    assert base > 16 * 1024 and base <= 16 * 1024 + 256 * 1024 * 4
+    split = need(1, 368, 640, ks={3: 2, 4: 4})
+    assert split > base
+    assert need(3, 368, 640, ks={3: 2, 4: 4}) > split  # the slabs scale with the batch
+    assert need(1, 368, 640, prec=_lib.PREC_F16) == 0
+    assert need(1, 72, 80) < 0  # not /16

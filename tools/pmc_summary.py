@@ -13,6 +13,7 @@ import argparse
 import csv
 import glob
 import json
+import sys
 import os
 import re
 from collections import defaultdict
@@ -34,6 +35,12 @@ def load(dirname, counter):
 def family(name):
     m = re.search(r"rrin::(\w+?)(<|\()", name)
     return m.group(1) if m else name[:40]
+
+
+def build_id():
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from rrin_amd._lib import build_id as bid
+    return bid()
 
 
 def main():
@@ -79,7 +86,9 @@ def main():
             "kernel_family": fam_name, "hbm_bytes_per_launch": r["hbm_bytes_per_dispatch"],
             "hbm_bytes_per_step": r["hbm_bytes_per_step"], "launches_per_step": r["dispatches_per_step"],
             "correction": "hbm = (2*FETCH_SIZE + WRITE_SIZE) KiB, separate --pmc passes",
-            "source": os.path.basename(os.path.normpath(a.fetch)) + " + " + os.path.basename(os.path.normpath(a.write))}
+            "source": os.path.basename(os.path.normpath(a.fetch)) + " + " + os.path.basename(os.path.normpath(a.write)),
+            # the library the profiled runs loaded (bench.py reports this entry only for that build)
+            "build": build_id()}
         json.dump(tab, open(a.table, "w"), indent=1, sort_keys=True)
 
 
