@@ -247,6 +247,12 @@ int launch_wino4(const ConvH8Args& a, int epi, hipStream_t st);
 #ifdef RRIN_LAB
 int launch_wino4_lab(const ConvH8Args& a, int abl, hipStream_t st);
 #endif
+// register-U Winograd tiles (conv_winoc.hip): 4 waves, two blocks per CU, the U operands
+// loaded straight into registers; ct = 2: BM 64 x TH 4 (kind 6), ct = 1: BM 32 x TH 8 (kind 7).
+// LDS: max(3 raw stages, the output-transform exchange)
+constexpr size_t kWinoCLds1 = (size_t)2048 * 16;  // TH 4: 3 x 512 stage records < 2048 exchange
+constexpr size_t kWinoCLds2 = (size_t)4096 * 16;  // TH 8: 3 x 768 < 4096
+int launch_winoc(const ConvH8Args& a, int epi, int ct, hipStream_t st);
 #ifdef RRIN_LAB
 int launch_wino_lab(const ConvH8Args& a, int abl, hipStream_t st);  // ablation bits (conv_wino.hip)
 #endif

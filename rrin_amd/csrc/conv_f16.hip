@@ -1772,15 +1772,23 @@ static const CfgH8 kCfgH8[] = {
     {32, 4, (size_t)2 * (408 + 1024) * 16, (size_t)1 << 30, 0, true, 0, 0},
     // kWino4Cfg: Winograd F(4x4,3x3), BM 32 x TH 16, 6 waves (conv_wino4.hip)
     {32, 16, kWino4Lds, (size_t)1 << 30, 0, true, 0, 0},
+    // kWinoC2Cfg: register-U tile, BM 64 x TH 4, 4 waves of 2 co tiles (conv_winoc.hip)
+    {64, 4, kWinoCLds1, (size_t)1 << 30, 0, true, 0, 0},
+    // kWinoC1Cfg: register-U tile, BM 32 x TH 8, 4 waves of 2 patch tiles
+    {32, 8, kWinoCLds2, (size_t)1 << 30, 0, true, 0, 0},
 };
 static constexpr int kNumCfgH8 = sizeof(kCfgH8) / sizeof(kCfgH8[0]);
-static constexpr int kWinoCfg = kNumCfgH8 - 5;
-static constexpr int kWino64Cfg = kNumCfgH8 - 4;
-static constexpr int kWinoQCfg = kNumCfgH8 - 3;
-static constexpr int kWinoQ4Cfg = kNumCfgH8 - 2;
-static constexpr int kWino4Cfg = kNumCfgH8 - 1;
+static constexpr int kWinoCfg = kNumCfgH8 - 7;
+static constexpr int kWino64Cfg = kNumCfgH8 - 6;
+static constexpr int kWinoQCfg = kNumCfgH8 - 5;
+static constexpr int kWinoQ4Cfg = kNumCfgH8 - 4;
+static constexpr int kWino4Cfg = kNumCfgH8 - 3;
+static constexpr int kWinoC2Cfg = kNumCfgH8 - 2;
+static constexpr int kWinoC1Cfg = kNumCfgH8 - 1;
+static inline bool is_winoc(int cfg) { return cfg == kWinoC2Cfg || cfg == kWinoC1Cfg; }
 static inline bool is_wino(int cfg) {
-  return cfg == kWinoCfg || cfg == kWino64Cfg || cfg == kWinoQCfg || cfg == kWinoQ4Cfg || cfg == kWino4Cfg;
+  return cfg == kWinoCfg || cfg == kWino64Cfg || cfg == kWinoQCfg || cfg == kWinoQ4Cfg || cfg == kWino4Cfg ||
+         is_winoc(cfg);
 }
 static constexpr size_t kMaxLds = 160 * 1024;
 static constexpr int kMaxKSplit = 16;
@@ -1962,6 +1970,8 @@ static int h8_prepare(const rrin_conv_h8_desc* d, ConvH8Args& a, bool need_scrat
   if (is_wino(d->cfg)) {
     if (d->prec != RRIN_PREC_F32R) return RRIN_E_CONFIG;
     if ((d->cin & 3) && !d->tail_finite) return RRIN_E_CONFIG;  // stages whole records only
+    // the register-U tiles stage both record groups of every chunk: they must exist
+    if (is_winoc(d->cfg) && (d->cin & 7) && !d->tail_finite) return RRIN_E_CONFIG;
     // two record groups per K chunk; F(4x4): one
     a.nchunks = d->cfg == kWino4Cfg ? (d->cin + 3) / 4 : (d->cin + 7) / 8;
   }
@@ -2034,13 +2044,15 @@ extern "C" int rrin_conv_h8_cfg_th(int32_t cfg) {
 }
 // 0: direct form; Winograd tile kind: 1 BM 32 / 4 waves, 2 BM 64 / 8 waves, 3 BM 32 / 8 waves,
 // 4 BM 32 x TH 4 / 4 waves; 5 Winograd F(4x4,3x3), BM 32 x TH 16 / 6 waves (its own packing,
-// rrin_pack_conv3x3_wino4)
+// rrin_pack_conv3x3_wino4); 6 BM 64 x TH 4 and 7 BM 32 x TH 8, register-U tiles (conv_winoc.hip)
 extern "C" int rrin_conv_h8_cfg_wino(int32_t cfg) {
   return cfg == kWinoCfg     ? 1
          : cfg == kWino64Cfg ? 2
          : cfg == kWinoQCfg  ? 3
          : cfg == kWinoQ4Cfg ? 4
          : cfg == kWino4Cfg  ? 5
+         : cfg == kWinoC2Cfg ? 6
+         : cfg == kWinoC1Cfg ? 7
                              : 0;
 }
 extern "C" int rrin_conv_h8_cfg_ok(int32_t cfg, int32_t prec) {
@@ -2070,6 +2082,8 @@ extern "C" int rrin_conv3x3_h8_fwd(const rrin_conv_h8_desc* d, void* stream) {
   if (d->cfg == kWinoQCfg) return launch_winoq(a, d->epi_mode, 8, st);
   if (d->cfg == kWinoQ4Cfg) return launch_winoq(a, d->epi_mode, 4, st);
   if (d->cfg == kWino4Cfg) return launch_wino4(a, d->epi_mode, st);
+  if (d->cfg == kWinoC2Cfg) return launch_winoc(a, d->epi_mode, 2, st);
+  if (d->cfg == kWinoC1Cfg) return launch_winoc(a, d->epi_mode, 1, st);
   switch (d->cfg) {
 #define X(id, nw, wm, wn, sc, pe) \
   case id:                        \

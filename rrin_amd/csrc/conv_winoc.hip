@@ -1,0 +1,408 @@
+// Exact-fp32 3x3 conv as Winograd F(2x2,3x3) on fp32 records (R32): the
+// "register-U" tiles, Winograd kinds 6 and 7 of the record-layout conv table.
+// Same arithmetic, in the same order, as conv3x3_winoq_kernel (conv_wino.hip):
+// the outputs are bitwise those of configs 18-21.
+//
+// Replaces nn.Conv2d(3, pad=1) + LeakyReLU(0.1) (unet.py:29,59-63), the fused
+// avg_pool2d output (unet.py:46), the cat by channel offset (unet.py:93) and the
+// sub-pixel form of Upsample + up conv (unet.py:77-78).
+//
+// Why this shape (tools/coissue_probe*.py): on gfx950 a wave's
+// v_mfma_f32_32x32x2_f32 stream does not overlap the other waves' VALU, LDS-read or
+// LDS-DMA instructions on the same SIMD -- their issue cycles add to the MFMA cycles.
+// The kernel time is therefore the MFMA cycles plus every other instruction's
+// price, whatever the occupancy, and what pays is fewer non-MFMA instructions per
+// MFMA:
+//   * the A operands (transformed weights U) go straight from L2 into registers
+//     (buffer_load_dwordx4: one per 4 MFMAs of a co tile, each record holding 4
+//     K steps), loaded a chunk ahead: no LDS-DMA pieces and no LDS reads for U;
+//   * only the raw input tile goes through LDS (buffer_load ... lds, 3 stages, one
+//     barrier per 8-channel chunk); a wave turns its window records into the B
+//     operands of its B^T row (one transform per lane, as kinds 1-4) and feeds them
+//     to CT co tiles (kind 6: CT 2) or uses each U record on NT patch tiles
+//     (kind 7: NT 2);
+//   * 4 waves of 8 accumulators (128 registers) per block, two blocks per CU, so
+//     one block's barrier, prologue and epilogue run beside the other's MFMAs.
+// Per wave and 8-channel chunk: 32 MFMAs, 4 CT U loads, 8 NT LDS reads, 32 NT VALU,
+// 2-3 LDS-DMA pieces (kind 3: 16 MFMAs, 4 + 8 LDS reads, 32 VALU, 3-4 pieces).
+//
+// Tile: BM = 32 CT output channels x 32 px x TH = 4 NT rows (16 x 2 NT patches).
+// Wave yw (0-3) owns B^T row yw (points 4 yw .. 4 yw + 3) of every patch; lane
+// (j, hh): patch j of a 32-patch MFMA tile, record half hh (channels 4 hh .. + 3
+// of the chunk; MFMA product e contracts channels e and 4 + e).
+#include "common.hpp"
+
+namespace rrin {
+
+typedef float cfloatx16 __attribute__((ext_vector_type(16)));
+typedef float cfloatx4 __attribute__((ext_vector_type(4)));
+typedef unsigned int cu32x4 __attribute__((ext_vector_type(4)));
+
+// LDS position of raw column col (0..33) within its row: even columns first (the
+// stride-2 window reads of 16 lanes fall on distinct banks), as kinds 1-4
+__device__ inline int wc_col(int col) { return (col & 1) * 17 + (col >> 1); }
+
+// buffer_load_dwordx4 ... lds: one 16-B record per lane at byte offset voff of rsrc into
+// the lane-linear LDS image at the wave-uniform base
+__device__ inline void buf_dma16(__amdgpu_buffer_rsrc_t rs, uint4* lds_wave_base, uint32_t voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)lds_wave_base, 16, voff, 0, 0,
+                                           0);
+}
+__device__ inline __amdgpu_buffer_rsrc_t buf_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
+}
+__device__ inline cfloatx4 buf_load16(__amdgpu_buffer_rsrc_t rs, uint32_t voff, int soff) {
+  return __builtin_bit_cast(cfloatx4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0));
+}
+
+template <int NT>
+struct WinoC {
+  static constexpr int TH = 4 * NT;
+  static constexpr int RG = (TH + 2) * 34;          // raw records per group
+  static constexpr int RAW = 2 * RG;                // per chunk (2 groups)
+  static constexpr int PIECES = (RAW + 255) / 256;  // DMA pieces per thread (every wave issues all)
+  static constexpr int STAGE = PIECES * 256;        // records per LDS stage (the tail is a dummy)
+  static constexpr int NS = 3;                      // stages: chunk c + 2 lands while c computes
+  static constexpr int XREC = NT * 4 * 8 * 64;      // output-transform exchange, one co tile
+  static constexpr size_t LDS = (size_t)(NS * STAGE > XREC ? NS * STAGE : XREC) * 16;
+};
+static_assert(WinoC<1>::LDS == kWinoCLds1 && WinoC<2>::LDS == kWinoCLds2, "LDS sizes (common.hpp)");
+static_assert(2 * WinoC<2>::LDS <= 160 * 1024, "two blocks per CU");
+
+template <int EPI, int CT, int NT>
+__global__ __launch_bounds__(256, 2) void conv3x3_winoc_kernel(ConvH8Args a) {
+  using G = WinoC<NT>;
+  constexpr int BM = 32 * CT, TH = G::TH, RG = G::RG, STAGE = G::STAGE, P = G::PIECES;
+  extern __shared__ __attribute__((aligned(16))) uint4 smem4[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int yw = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int j = lane & 31, hh = lane >> 5;
+  int bid;
+  {  // XCD-aware bijective remap (conv_mfma.hip): an XCD's workgroups are consecutive tiles
+    const int nwg = gridDim.x, q = nwg >> 3, r = nwg & 7;
+    const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+  }
+  const int ntiles = a.co_blocks * a.tiles_x * a.tiles_y * a.n;
+  if (bid >= ntiles) return;
+  const int nch = a.nchunks;
+  int cob, x0, y0, img;
+  {  // the co blocks of a tile position on consecutive workgroups (they share its raw tile)
+    int t = bid;
+    cob = t % a.co_blocks;
+    t /= a.co_blocks;
+    x0 = (t % a.tiles_x) * 32;
+    t /= a.tiles_x;
+    y0 = (t % a.tiles_y) * TH;
+    img = t / a.tiles_y;
+  }
+
+  // ---- raw tile: rows y0 - 1 .. y0 + TH, cols x0 - 1 .. x0 + 32 of the chunk's two
+  // record groups, by buffer_load ... lds from a per-chunk base (byte offsets per lane
+  // fixed; a lane past the tile re-reads record 0 into the stage's dummy tail)
+  const uint4* tbase = a.src_hi + (int64_t)img * a.src_img + (int64_t)y0 * a.src_wp + x0 + (kH8PadLeft - 1);
+  uint32_t voff[P];
+#pragma unroll
+  for (int it = 0; it < P; ++it) {
+    const int idx = tid + 256 * it;
+    const int g = idx >= RG ? 1 : 0;
+    const int rem = idx < G::RAW ? idx - g * RG : 0;
+    const int r = rem / 34, pos = rem - r * 34;
+    const int col = pos < 17 ? 2 * pos : 2 * (pos - 17) + 1;
+    voff[it] = (uint32_t)((idx < G::RAW ? (int64_t)g * a.src_gp : 0) + (int64_t)r * a.src_wp + col) * 16u;
+  }
+  auto issue_raw = [&](int c, int s) {
+    const auto rs = buf_rsrc(tbase + (int64_t)(2 * c) * a.src_gp);
+#pragma unroll
+    for (int it = 0; it < P; ++it) buf_dma16(rs, smem4 + s * STAGE + 256 * it + 64 * yw, voff[it]);
+  };
+
+  // ---- U (A operands) straight into registers: packing [cob][chunk][xi][hh][BM co][4 ch]
+  // (rrin_pack_conv3x3_wino_bm, bm = BM); wave yw reads points 4 yw .. + 3, both halves
+  const auto ur = buf_rsrc(a.w_hi + (int64_t)cob * nch * 32 * BM);
+  const uint32_t uvoff = (uint32_t)(hh * BM + j) * 16u;
+  auto load_u = [&](int c, int x, int t) {
+    // byte offset of record (xi = 4 yw + x, hh, co = 32 t + j) of chunk c: the chunk and
+    // point part in the scalar offset, the rest < 4 KB in the instruction's offset
+    const int soff = c * (32 * BM * 16) + (4 * yw + (CT == 2 ? (x & 2) : 0)) * (2 * BM * 16);
+    const int imm = (CT == 2 ? (x & 1) * 2048 : x * 1024) + t * 512;
+    return buf_load16(ur, uvoff + imm, soff);
+  };
+
+  // ---- B operands: lane (j, hh) of N tile nt is patch (pr = 2 nt + (j >> 4), jx), the
+  // second patch row's columns rotated by 12 (distinct banks per ds_read_b128 lane group)
+  const int jx = (j + 12 * (j >> 4)) & 15;
+  const int ra = yw == 0 ? 0 : (yw == 2 ? 2 : 1);
+  const int rb = yw == 0 ? 2 : (yw == 1 ? 2 : (yw == 2 ? 1 : 3));
+  const float sg = yw == 1 ? 1.f : -1.f;
+  int pcol[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) pcol[k] = hh * RG + (2 * (j >> 4)) * 34 + wc_col(2 * jx + k);
+  const int oa = ra * 34, ob = rb * 34;
+
+  cfloatx16 acc[CT][NT][4];
+#pragma unroll
+  for (int t = 0; t < CT; ++t)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int x = 0; x < 4; ++x) acc[t][nt][x] = cfloatx16{};
+  cfloatx4 u[CT][4];              // U of the chunk being computed (point x reloaded after its MFMAs)
+  cfloatx4 v[NT][4];              // B operands of the chunk being computed
+  cfloatx4 d[8];                  // window records of one N tile of the next chunk
+
+  // window records of N tile nt of the chunk in stage s -> d; B^T row yw -> its 4
+  // points' B operands v[nt]
+  auto read_raw = [&](int s, int nt) {
+    const uint4* rw = smem4 + s * STAGE + nt * 4 * 34;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      d[2 * k] = __builtin_bit_cast(cfloatx4, rw[oa + pcol[k]]);
+      d[2 * k + 1] = __builtin_bit_cast(cfloatx4, rw[ob + pcol[k]]);
+    }
+  };
+  auto transform = [&](int nt) {
+    cfloatx4 tr[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) tr[k][e] = fmaf(sg, d[2 * k + 1][e], d[2 * k][e]);
+    v[nt][0] = tr[0] - tr[2];
+    v[nt][1] = tr[1] + tr[2];
+    v[nt][2] = tr[2] - tr[1];
+    v[nt][3] = tr[1] - tr[3];
+  };
+  auto mfma_point = [&](int x, int nt) {
+#pragma unroll
+    for (int t = 0; t < CT; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        acc[t][nt][x] = __builtin_amdgcn_mfma_f32_32x32x2f32(u[t][x][e], v[nt][x][e], acc[t][nt][x], 0, 0, 0);
+  };
+  auto reload_u = [&](int c, int x) {
+#pragma unroll
+    for (int t = 0; t < CT; ++t) u[t][x] = load_u(c, x, t);
+  };
+  // LDS-DMA of a stage is visible to the other waves after the issuing wave's vmcnt
+  // wait and a barrier; the barrier is bare (a __syncthreads() would drain vmcnt to 0
+  // and wait for the chunk in flight too)
+  auto bar = [&]() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+  auto fence = [&]() { __builtin_amdgcn_sched_barrier(0); };
+
+  // Chunk c (U(c) in u, its B operands in v), MORE: it has a successor (a constant at
+  // both call sites, folded after inlining).
+  //   points 0-2, each followed by the load of its U for chunk c + 1 (into the registers
+  //   it just used: three points later it is needed); the wait for raw(c + 1) (issued a
+  //   chunk ago; the 4 CT younger U loads stay in flight); the barrier (raw(c + 1)
+  //   visible, every read of stage (c + 2) % 3 long done); raw(c + 2) -> that stage;
+  //   per N tile: chunk c + 1's window reads, point 3 (covers them), the transform of
+  //   chunk c + 1 into v; point 3's U load.  VMEM order per chunk: U pts 0-2, raw(c + 2),
+  //   U pt 3 -- the same counts every chunk (the prologue matches it), so the compiler's
+  //   own waits for u are 3 CT + P deep and this wait is 4 CT; a chunk past the end is
+  //   never loaded: raw(nch) re-reads the last chunk into the free stage.
+  auto chunk = [&](int c, int s, const bool more) {
+#pragma unroll
+    for (int x = 0; x < 3; ++x) {
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) mfma_point(x, nt);
+      if (more) reload_u(c + 1, x);
+      fence();
+    }
+    if (more) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * CT) : "memory");
+      bar();
+      issue_raw(c + 2 < nch ? c + 2 : nch - 1, s == 0 ? 2 : s - 1);
+    }
+    const int s1 = s == 2 ? 0 : s + 1;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      if (more) read_raw(s1, nt);
+      fence();
+      mfma_point(3, nt);
+      fence();
+      if (more) transform(nt);
+    }
+    if (more) reload_u(c + 1, 3);
+  };
+
+  // prologue in the steady state's VMEM order: raw(0), U(0) pts 0-2, raw(1), U(0) pt 3;
+  // wait for raw(0); chunk 0's B operands
+  issue_raw(0, 0);
+#pragma unroll
+  for (int x = 0; x < 3; ++x) reload_u(0, x);
+  issue_raw(nch > 1 ? 1 : 0, 1);
+  reload_u(0, 3);
+  if constexpr (P == 2) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * CT + 2) : "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * CT + 3) : "memory");
+  }
+  bar();
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    read_raw(0, nt);
+    transform(nt);
+  }
+  {
+    int s = 0;
+    for (int c = 0; c + 1 < nch; ++c) {
+      chunk(c, s, true);
+      s = s == 2 ? 0 : s + 1;
+    }
+    chunk(nch - 1, s, false);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMA past the end has landed
+  __syncthreads();  // every read of the stages done before the exchange reuses the LDS
+
+  // ---- output transform (kinds 1-4's order): Q[c] = sum_x M[x] A[x][c] of this wave's
+  // B^T row, Y[0][c] = (Q0 + Q1) + Q2, Y[1][c] = (Q1 - Q2) - Q3 over the four waves,
+  // exchanged through LDS one co tile at a time; wave yw then finishes output row
+  // r = yw & 1, column cc = yw >> 1 of its patches
+  cfloatx4* X = reinterpret_cast<cfloatx4*>(smem4);
+  const int r = yw & 1, cc = yw >> 1;
+  uint4* dst = a.dst_hi + (int64_t)img * a.dst_img;
+  auto store4 = [&](int64_t rec, const float* vv) {
+    dst[rec] = make_uint4(__float_as_uint(vv[0]), __float_as_uint(vv[1]), __float_as_uint(vv[2]), __float_as_uint(vv[3]));
+  };
+#pragma unroll
+  for (int t = 0; t < CT; ++t) {
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        cfloatx4 g;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int vi = 4 * k + e, c2 = vi >> 4, i = vi & 15;
+          const float m0 = acc[t][nt][0][i], m1 = acc[t][nt][1][i], m2 = acc[t][nt][2][i], m3 = acc[t][nt][3][i];
+          g[e] = c2 == 0 ? (m0 + m1) + m2 : (m1 - m2) - m3;
+        }
+        X[((nt * 4 + yw) * 8 + k) * 64 + lane] = g;
+      }
+    __syncthreads();
+    float yv[NT][16];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int k4 = 0; k4 < 4; ++k4) {
+        const int k = 4 * cc + k4;
+        const cfloatx4 q0 = X[((nt * 4 + 0) * 8 + k) * 64 + lane];
+        const cfloatx4 q1 = X[((nt * 4 + 1) * 8 + k) * 64 + lane];
+        const cfloatx4 q2 = X[((nt * 4 + 2) * 8 + k) * 64 + lane];
+        const cfloatx4 q3 = X[((nt * 4 + 3) * 8 + k) * 64 + lane];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) yv[nt][4 * k4 + e] = r == 0 ? (q0[e] + q1[e]) + q2[e] : (q1[e] - q2[e]) - q3[e];
+      }
+    __syncthreads();  // X is rewritten by the next co tile / the pool exchange
+    const int cobe = CT * cob + t;  // 32-channel block of this co tile
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int pr = 2 * nt + (j >> 4);
+      const int y = y0 + 2 * pr + r, x = x0 + 2 * jx + cc;
+      if constexpr (EPI == RRIN_EPI_SUBPIXEL) {
+        const int HH = 2 * a.h, WW = 2 * a.w, creal = a.cout >> 2;
+        if (cobe * 32 < a.cout && y < a.h && x < a.w) {
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq) {
+            const int Y = 2 * y + (qq >> 1), XX = 2 * x + (qq & 1);
+            const int64_t ri = ring_index(Y, XX, HH, WW);
+            if (ri >= 0) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e)
+                a.edge[((int64_t)img * creal + cobe * 8 + 4 * hh + e) * a.ring + ri] = yv[nt][4 * qq + e];
+            } else {
+              float vv[4];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) vv[e] = yv[nt][4 * qq + e] + a.bias[cobe * 32 + 8 * qq + 4 * hh + e];
+              store4((int64_t)(2 * cobe + hh) * a.dst_gp + (int64_t)(Y + 1) * a.dst_wp + XX + kH8PadLeft, vv);
+            }
+          }
+        }
+      } else {
+        float vv[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          float tv = yv[nt][i] + a.bias[cobe * 32 + 8 * (i >> 2) + 4 * hh + (i & 3)];
+          if constexpr (EPI != RRIN_EPI_LINEAR) tv = leaky(tv, a.slope);
+          vv[i] = tv;
+        }
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          if (cobe * 32 + 8 * qq < a.cout && y < a.h && x < a.w) {
+            const int64_t rec = (int64_t)(cobe * 8 + 2 * qq + hh) * a.dst_gp + (int64_t)(y + 1) * a.dst_wp + x + kH8PadLeft;
+            store4(rec, &vv[4 * qq]);
+            if constexpr (EPI == RRIN_EPI_LEAKY_REP) {  // edge replicate into the padding ring
+              const int dy0 = y == 0 ? -1 : 0, dy1 = y == a.h - 1 ? 1 : 0;
+              const int dx0 = x == 0 ? -1 : 0, dx1 = x == a.w - 1 ? 1 : 0;
+              for (int dy = dy0; dy <= dy1; ++dy)
+                for (int dx = dx0; dx <= dx1; ++dx)
+                  if (dy | dx) store4(rec + (int64_t)dy * a.dst_wp + dx, &vv[4 * qq]);
+            }
+          }
+        }
+        if constexpr (EPI == RRIN_EPI_LEAKY_POOL) {
+          // the patch's four outputs (yw = (r, c)) meet in LDS; wave 0 writes
+          // avg = 0.25 ((Y00 + Y10) + (Y01 + Y11)), kinds 1-4's order
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            cfloatx4 g;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) g[e] = vv[4 * k + e];
+            X[(yw * 4 + k) * 64 + lane] = g;
+          }
+          __syncthreads();
+          if (yw == 0) {
+            const int xp = x0 + 2 * jx, yp = y0 + 2 * pr;
+            uint4* pdst = a.pool_hi + (int64_t)img * a.pool_img;
+#pragma unroll
+            for (int qq = 0; qq < 4; ++qq) {
+              const cfloatx4 y00 = X[(0 * 4 + qq) * 64 + lane];
+              const cfloatx4 y10 = X[(1 * 4 + qq) * 64 + lane];
+              const cfloatx4 y01 = X[(2 * 4 + qq) * 64 + lane];
+              const cfloatx4 y11 = X[(3 * 4 + qq) * 64 + lane];
+              if (cobe * 32 + 8 * qq < a.cout && yp < a.h && xp < a.w) {
+                float s4[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) s4[e] = 0.25f * ((y00[e] + y10[e]) + (y01[e] + y11[e]));
+                const int64_t rec = (int64_t)(cobe * 8 + 2 * qq + hh) * a.pool_gp + (int64_t)(yp / 2 + 1) * a.pool_wp +
+                                    xp / 2 + kH8PadLeft;
+                pdst[rec] = make_uint4(__float_as_uint(s4[0]), __float_as_uint(s4[1]), __float_as_uint(s4[2]),
+                                       __float_as_uint(s4[3]));
+              }
+            }
+          }
+          __syncthreads();
+        }
+      }
+    }
+  }
+}
+
+template <int EPI, int CT, int NT>
+static int launch_winoc_k(const ConvH8Args& a, hipStream_t st) {
+  auto k = conv3x3_winoc_kernel<EPI, CT, NT>;
+  static LdsAttr attr;
+  constexpr size_t lds = WinoC<NT>::LDS;
+  if (int e = attr.ensure((const void*)k, (int)lds, st)) return e;
+  const int64_t grid = (int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n;
+  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256), lds, st, a);
+  return hip_code(hipGetLastError());
+}
+
+template <int CT, int NT>
+static int launch_winoc_e(const ConvH8Args& a, int epi, hipStream_t st) {
+  switch (epi) {
+    case RRIN_EPI_LINEAR: return launch_winoc_k<RRIN_EPI_LINEAR, CT, NT>(a, st);
+    case RRIN_EPI_LEAKY: return launch_winoc_k<RRIN_EPI_LEAKY, CT, NT>(a, st);
+    case RRIN_EPI_LEAKY_POOL: return launch_winoc_k<RRIN_EPI_LEAKY_POOL, CT, NT>(a, st);
+    case RRIN_EPI_LEAKY_REP: return launch_winoc_k<RRIN_EPI_LEAKY_REP, CT, NT>(a, st);
+    case RRIN_EPI_SUBPIXEL: return launch_winoc_k<RRIN_EPI_SUBPIXEL, CT, NT>(a, st);
+  }
+  return RRIN_E_ARG;
+}
+
+int launch_winoc(const ConvH8Args& a, int epi, int ct, hipStream_t st) {
+  return ct == 2 ? launch_winoc_e<2, 1>(a, epi, st) : launch_winoc_e<1, 2>(a, epi, st);
+}
+
+}  // namespace rrin

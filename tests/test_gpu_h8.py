@@ -52,17 +52,20 @@ NO_POOL_CFGS = (4, 16)
 
 
 def wino_cfgs():
-    """Ids of the Winograd exact-fp32 configs (R32 only): F(2x2,3x3) kinds 1-4, F(4x4,3x3) kind 5."""
+    """Ids of the Winograd exact-fp32 configs (R32 only): F(2x2,3x3) kinds 1-4 and the
+    register-U kinds 6-7, F(4x4,3x3) kind 5."""
     lib = _lib.lib()
     return tuple(c for c in range(lib.rrin_conv_h8_cfg_count()) if lib.rrin_conv_h8_cfg_wino(c))
 
 
 def cfgs(prec, cout, cin):
     lib = _lib.lib()
-    # the Winograd config stages whole records only: cin % 4 != 0 needs tail_finite (test_h8_conv_dma_finite_tail)
+    # the Winograd config stages whole records only: cin % 4 != 0 needs tail_finite (test_h8_conv_dma_finite_tail);
+    # the register-U kinds 6-7 stage both record groups of every 8-channel chunk: cin % 8 != 0 needs it too
     return [c for c in range(lib.rrin_conv_h8_cfg_count())
             if lib.rrin_conv_h8_cfg_fits(c, prec, cin) and lib.rrin_conv_h8_cfg_bm(c) <= max(32, 2 * cout)
-            and not (lib.rrin_conv_h8_cfg_wino(c) and cin % 4)]
+            and not (lib.rrin_conv_h8_cfg_wino(c) and cin % 4)
+            and not (lib.rrin_conv_h8_cfg_wino(c) in (6, 7) and cin % 8)]
 
 
 def pack_h8(w, b, cfg, prec, dev, perm=None):
