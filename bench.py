@@ -114,7 +114,7 @@ def parse():
                          "Winograd F(2x2,3x3)")
     ap.add_argument("--wino-kind", type=int, default=None,
                     help="A/B: Winograd tile kind of the exact-fp32 body convs (rrin_conv_h8_cfg_wino; "
-                         "default engine.WINO_KIND)")
+                         "0 = the register-U kinds 6/7 by output channels; default engine.WINO_KIND)")
     ap.add_argument("--wino-split", default=None,
                     help="A/B: split-K slices per grid level for every Winograd conv, e.g. '2:2,3:4,4:8' "
                          "(engine.WINO_SPLIT_LEVELS); 'none' disables the tuned splits")

@@ -111,11 +111,14 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winoc_kernel(ConvH8Args a) {
     const int col = pos < 17 ? 2 * pos : 2 * (pos - 17) + 1;
     voff[it] = (uint32_t)((idx < G::RAW ? (int64_t)g * a.src_gp : 0) + (int64_t)r * a.src_wp + col) * 16u;
   }
-  auto issue_raw = [&](int c, int s) {
-    const auto rs = buf_rsrc(tbase + (int64_t)(2 * c) * a.src_gp);
+  const int64_t chunk_stride = 2 * a.src_gp;  // records between the group pairs of consecutive chunks
+  auto issue_raw_at = [&](const uint4* base, int s) {
+    const auto rs = buf_rsrc(base);
 #pragma unroll
     for (int it = 0; it < P; ++it) buf_dma16(rs, smem4 + s * STAGE + 256 * it + 64 * yw, voff[it]);
   };
+  // the group pair of chunk min(c + 2, nch - 1), advanced by one chunk per steady chunk
+  const uint4* raw_next = tbase + (nch > 2 ? 2 : nch - 1) * chunk_stride;
 
   // ---- U (A operands) straight into registers: packing [cob][chunk][xi][hh][BM co][4 ch]
   // (rrin_pack_conv3x3_wino_bm, bm = BM); wave yw reads points 4 yw .. + 3, both halves
@@ -211,7 +214,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winoc_kernel(ConvH8Args a) {
     if (more) {
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * CT) : "memory");
       bar();
-      issue_raw(c + 2 < nch ? c + 2 : nch - 1, s == 0 ? 2 : s - 1);
+      issue_raw_at(raw_next, s == 0 ? 2 : s - 1);
+      if (c + 3 < nch) raw_next += chunk_stride;
     }
     const int s1 = s == 2 ? 0 : s + 1;
 #pragma unroll
@@ -227,10 +231,10 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winoc_kernel(ConvH8Args a) {
 
   // prologue in the steady state's VMEM order: raw(0), U(0) pts 0-2, raw(1), U(0) pt 3;
   // wait for raw(0); chunk 0's B operands
-  issue_raw(0, 0);
+  issue_raw_at(tbase, 0);
 #pragma unroll
   for (int x = 0; x < 3; ++x) reload_u(0, x);
-  issue_raw(nch > 1 ? 1 : 0, 1);
+  issue_raw_at(nch > 1 ? tbase + chunk_stride : tbase, 1);
   reload_u(0, 3);
   if constexpr (P == 2) {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * CT + 2) : "memory");

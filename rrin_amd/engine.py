@@ -176,6 +176,13 @@ WINO_DIRECT = {(6, 32, 0): 13}
 # (4 waves of 8 accumulators) on every conv shape of the Net, bitwise equal
 # (profiles/r03/cfgab_18_20.txt)
 WINO_KIND = 3
+# 0 = "auto": the register-U tiles (conv_winoc.hip, bitwise equal to kind 3) -- kind 6
+# (BM 64 x TH 4, each transformed input feeds 2 co tiles) where the conv's output rows
+# fill 64-channel blocks, else kind 7 (BM 32 x TH 8, each U record feeds 2 patch tiles)
+def wino_kind_for(cout: int) -> int:
+    if WINO_KIND != 0:
+        return WINO_KIND
+    return 6 if cout % 64 == 0 else 7
 # ... and kind 4 (the same arithmetic on TH 4 tiles of 4 waves: twice the
 # workgroups) on the few-tile deep convs where that wins, (cin, cout rows, grid
 # level) per size class as in WINO_DIRECT (a sub-pixel up conv: 4 x cout, the
@@ -242,7 +249,7 @@ def choose_cfg_h8(cin: int, cout: int, prec: int, level: int = 0, size: str = "l
         c = WINO_DIRECT.get((cin, cout, level))
         if c is not None and _lib.lib().rrin_conv_h8_cfg_fits(c, prec, cin):
             return c
-        return wino_cfg(4 if (cin, cout, level) in WINO_TH4.get(size, ()) else None)
+        return wino_cfg(4 if (cin, cout, level) in WINO_TH4.get(size, ()) else wino_kind_for(cout))
     table = H8_TUNED_BY_SIZE.get(size, {}).get(prec) or H8_TUNED.get(prec, {})
     cfg = table.get((cin, cout, level))
     if cfg is not None and _lib.lib().rrin_conv_h8_cfg_fits(cfg, prec, cin):
