@@ -515,6 +515,12 @@ int rrin_tpool2_bwd(const float* gy, float* gx, int32_t nc, int32_t h, int32_t w
 int rrin_tup2_fwd(const float* x, float* y, int32_t nc, int32_t h, int32_t w, void* stream);
 int rrin_tup2_bwd(const float* gy, float* gx, int32_t nc, int32_t h, int32_t w, void* stream);
 int64_t rrin_twarp_bwd_work_bytes(int32_t n, int32_t c, int32_t h, int32_t w);
+/* ABI 12: the Winograd packing of rrin_pack_conv3x3_wino_bm computed on the device (the
+ * training path repacks every step), bitwise the host packing.  mode 0: the conv of OIHW
+ * w [cout][cin][3][3] (rows cout, channels cin); mode 1: its data-gradient conv, w
+ * transposed and flipped (rows cin, channels cout).  wpack: rrin_pack_conv3x3_wino_bm_floats
+ * (rows, channels, bm) floats. */
+int rrin_tpack_wino(const float* w, int32_t cout, int32_t cin, int32_t bm, int32_t mode, float* wpack, void* stream);
 int rrin_twarp_bwd(const float* img, const float* flow, const float* gout, float* gimg, float* gflow,
                    void* work, int64_t work_bytes, int32_t n, int32_t c, int32_t h, int32_t w, void* stream);
 

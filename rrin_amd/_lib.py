@@ -143,6 +143,7 @@ SIGNATURES = {
     "rrin_net_conv_count": (C.c_int, []),
     "rrin_net_workspace_bytes": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32, C.c_int32]),
     "rrin_net_scratch_bytes": (C.c_int64, [C.POINTER(NetDesc)]),
+    "rrin_tpack_wino": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]),
     "rrin_unet_scratch_bytes": (C.c_int64, [C.POINTER(UNetDesc)]),
     "rrin_make_geom_h8": (C.c_int, [C.c_int32, C.c_int32, C.POINTER(Geom)]),
     "rrin_conv_h8_cfg_count": (C.c_int, []),

@@ -44,6 +44,68 @@ def _f32(t: torch.Tensor) -> torch.Tensor:
     return t.contiguous()
 
 
+# Forward and data-gradient convs on the inference path's exact-fp32 Winograd kernels
+# (conv_wino*.hip, record layout) instead of csrc/train.hip's general implicit GEMM:
+# the weights are packed on the device every call (rrin_tpack_wino: the host packing's
+# bits; the dgrad conv is the forward conv of the flipped, transposed weights), the NCHW
+# tensors of the autograd graph go through the record layout (rrin_nchw_to_h8 /
+# rrin_h8_to_nchw) in per-shape buffers reused in stream order.  False: train.hip for all
+# three (A/B).
+TRAIN_WINO = True
+_R32_BUFS: dict = {}
+
+
+def _r32_buf(n, c, h, w, device, role):
+    """A zero-padded fp32-record buffer of c channels (a multiple of 8) per shape and role;
+    every kernel touching it runs on the device's current stream, so reuse is ordered."""
+    from .pp import H8Tensor
+    key = (device, n, c, h, w, role)
+    t = _R32_BUFS.get(key)
+    if t is None:
+        t = H8Tensor(n, c, h, w, device, _lib.PREC_F32R)
+        _R32_BUFS[key] = t
+    return t
+
+
+def _wino_conv(x, wpack, bias, rows, cfg, leaky, st, role):
+    """y[n, rows] = conv3x3(x) + bias [, leaky] with packed Winograd weights (cfg's BM)."""
+    L = _lib.lib()
+    n, cin, h, w = x.shape
+    c8, r8 = (cin + 7) // 8 * 8, (rows + 7) // 8 * 8
+    xb = _r32_buf(n, c8, h, w, x.device, role + "x")
+    v = xb.view(0, c8)
+    _lib.check(L.rrin_nchw_to_h8(C.c_void_p(x.data_ptr()), n, cin, 0, C.byref(v), _lib.PREC_F32R, st),
+               "rrin_nchw_to_h8")
+    yb = _r32_buf(n, r8, h, w, x.device, role + "y")
+    d = _lib.ConvH8Desc()
+    d.n, d.cin, d.cout, d.cfg, d.prec = n, cin, r8, cfg, _lib.PREC_F32R
+    d.epi_mode = _lib.EPI_LEAKY if leaky else _lib.EPI_LINEAR
+    d.slope, d.inv_wscale, d.tail_finite = LEAKY_SLOPE, 1.0, 1  # channels [cin, c8) stay zero
+    d.src, d.dst = xb.view(0, c8), yb.view(0, r8)
+    d.whi, d.wlo, d.bias = wpack.data_ptr(), wpack.data_ptr(), bias.data_ptr()
+    _lib.check(L.rrin_conv3x3_h8_fwd(C.byref(d), st), "rrin_conv3x3_h8_fwd (training)")
+    y = torch.empty((n, rows, h, w), dtype=torch.float32, device=x.device)
+    vy = yb.view(0, r8)
+    _lib.check(L.rrin_h8_to_nchw(C.byref(vy), n, rows, 0, C.c_void_p(y.data_ptr()), _lib.PREC_F32R, st),
+               "rrin_h8_to_nchw")
+    return y
+
+
+def _wino_pack(weight, rows, cols, mode, st):
+    """(packed weights, cfg) of the forward (mode 0) or data-gradient (mode 1) conv."""
+    from . import engine
+    L = _lib.lib()
+    kind = 6 if rows % 64 == 0 else 7
+    cfg = engine.wino_cfg(kind)
+    bm = L.rrin_conv_h8_cfg_bm(cfg)
+    wp = torch.empty(int(L.rrin_pack_conv3x3_wino_bm_floats(rows, cols, bm)), dtype=torch.float32,
+                     device=weight.device)
+    cout, cin = weight.shape[:2]
+    _lib.check(L.rrin_tpack_wino(C.c_void_p(weight.data_ptr()), cout, cin, bm, mode, C.c_void_p(wp.data_ptr()), st),
+               "rrin_tpack_wino")
+    return wp, cfg, bm
+
+
 class _Conv3x3(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, leaky: bool):
@@ -53,11 +115,19 @@ class _Conv3x3(torch.autograd.Function):
         cout = weight.shape[0]
         if weight.shape != (cout, cin, 3, 3):
             raise ValueError(f"weight {tuple(weight.shape)} for input {tuple(x.shape)}")
-        y = torch.empty((n, cout, h, w), dtype=torch.float32, device=x.device)
-        d = _lib.TConvDesc(n=n, cin=cin, cout=cout, h=h, w=w, mode=_lib.TCONV_FWD, leaky=int(leaky),
-                           slope=LEAKY_SLOPE, x=x.data_ptr(), y=None, wt=weight.data_ptr(),
-                           bias=bias.data_ptr() if bias is not None else None, out=y.data_ptr())
-        _lib.check(_lib.lib().rrin_tconv3x3(C.byref(d), _stream(x.device)), "rrin_tconv3x3 (forward)")
+        st = _stream(x.device)
+        if TRAIN_WINO:
+            wp, cfg, bm = _wino_pack(weight, cout, cin, 0, st)
+            bp = torch.zeros(((cout + bm - 1) // bm) * bm, dtype=torch.float32, device=x.device)
+            if bias is not None:
+                bp[:cout] = bias
+            y = _wino_conv(x, wp, bp, cout, cfg, leaky, st, "f")
+        else:
+            y = torch.empty((n, cout, h, w), dtype=torch.float32, device=x.device)
+            d = _lib.TConvDesc(n=n, cin=cin, cout=cout, h=h, w=w, mode=_lib.TCONV_FWD, leaky=int(leaky),
+                               slope=LEAKY_SLOPE, x=x.data_ptr(), y=None, wt=weight.data_ptr(),
+                               bias=bias.data_ptr() if bias is not None else None, out=y.data_ptr())
+            _lib.check(_lib.lib().rrin_tconv3x3(C.byref(d), st), "rrin_tconv3x3 (forward)")
         ctx.leaky = bool(leaky)
         ctx.has_bias = bias is not None
         ctx.save_for_backward(x, weight, y if leaky else None)
@@ -72,7 +142,13 @@ class _Conv3x3(torch.autograd.Function):
         L = _lib.lib()
         st = _stream(x.device)
         gx = gw = gb = None
-        if ctx.needs_input_grad[0]:
+        if ctx.needs_input_grad[0] and TRAIN_WINO:
+            # g' = g * leaky'(pre), the sign of y being the pre-activation's (slope > 0)
+            gp = torch.where(y > 0, gy, gy * LEAKY_SLOPE) if ctx.leaky else gy
+            wp, cfg, bm = _wino_pack(weight, cin, cout, 1, st)
+            zb = torch.zeros(((cin + bm - 1) // bm) * bm, dtype=torch.float32, device=x.device)
+            gx = _wino_conv(gp, wp, zb, cin, cfg, False, st, "d")
+        elif ctx.needs_input_grad[0]:
             gx = torch.empty_like(x)
             d = _lib.TConvDesc(n=n, cin=cin, cout=cout, h=h, w=w, mode=_lib.TCONV_DGRAD, leaky=int(ctx.leaky),
                                slope=LEAKY_SLOPE, x=gy.data_ptr(), y=y.data_ptr() if ctx.leaky else None,

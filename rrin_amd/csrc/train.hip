@@ -462,3 +462,53 @@ extern "C" int rrin_twarp_bwd(const float* img, const float* flow, const float* 
                      (const unsigned*)mx, gimg, total, (int64_t)h * w);
   return hip_code(hipGetLastError());
 }
+
+// ---- Winograd weight pack on the device (training: the weights change every optimizer
+// step).  The layout and arithmetic of rrin_pack_conv3x3_wino_bm (conv_wino.hip): per
+// output row o, input channel i and point xi, u = sum_ky sum_kx G[xi/4][ky] G[xi%4][kx] g,
+// in double, that order, no contraction, rounded once -- the host packing's bits.
+// mode 0: g = W[o][i] (the forward conv); mode 1: g = W[i][o] flipped in y and x (the
+// data-gradient conv: out rows = cin, in channels = cout).
+#pragma clang fp contract(off)
+__global__ void tpack_wino_kernel(const float* __restrict__ w, int cout, int cin, int rows, int cols, int bm,
+                                  int mode, float* __restrict__ wpack, int64_t total) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  // i = (((cob * nch + c) * 16 + xi) * 2 + hh) * bm * 4 + col * 4 + e
+  const int e = (int)(i & 3);
+  int64_t t = i >> 2;
+  const int col = (int)(t % bm);
+  t /= bm;
+  const int hh = (int)(t & 1);
+  t >>= 1;
+  const int xi = (int)(t & 15);
+  t >>= 4;
+  const int nch = (cols + 7) / 8;
+  const int c = (int)(t % nch);
+  const int cob = (int)(t / nch);
+  const int o = cob * bm + col, ch = c * 8 + hh * 4 + e;
+  double u = 0.0;
+  if (o < rows && ch < cols) {
+    const double G[4][3] = {{1.0, 0.0, 0.0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0.0, 0.0, 1.0}};
+    const float* g = mode ? w + ((int64_t)ch * cin + o) * 9 : w + ((int64_t)o * cin + ch) * 9;
+    for (int ky = 0; ky < 3; ++ky)
+      for (int kx = 0; kx < 3; ++kx) {
+        const double gv = (double)(mode ? g[(2 - ky) * 3 + (2 - kx)] : g[ky * 3 + kx]);
+        const double p = G[xi >> 2][ky] * G[xi & 3][kx];
+        u = u + p * gv;
+      }
+  }
+  wpack[i] = (float)u;
+}
+#pragma clang fp contract(on)
+
+extern "C" int rrin_tpack_wino(const float* w, int32_t cout, int32_t cin, int32_t bm, int32_t mode, float* wpack,
+                               void* stream) {
+  if (!w || !wpack || cout < 1 || cin < 1 || (bm != 32 && bm != 64) || (mode != 0 && mode != 1)) return RRIN_E_ARG;
+  const int rows = mode ? cin : cout, cols = mode ? cout : cin;
+  const int64_t total = rrin_pack_conv3x3_wino_bm_floats(rows, cols, bm);
+  if (total < 0) return (int)total;
+  hipLaunchKernelGGL(tpack_wino_kernel, dim3(grid_of(total)), dim3(256), 0, (hipStream_t)stream, w, cout, cin, rows,
+                     cols, bm, mode, wpack, total);
+  return hip_code(hipGetLastError());
+}
