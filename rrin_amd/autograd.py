@@ -142,9 +142,13 @@ class _Conv3x3(torch.autograd.Function):
         L = _lib.lib()
         st = _stream(x.device)
         gx = gw = gb = None
+        gp = None
+        if TRAIN_WINO and ctx.leaky:
+            # g' = g * leaky'(pre), the sign of y being the pre-activation's (slope > 0): once,
+            # for both gradient convs
+            gp = torch.where(y > 0, gy, gy * LEAKY_SLOPE)
         if ctx.needs_input_grad[0] and TRAIN_WINO:
-            # g' = g * leaky'(pre), the sign of y being the pre-activation's (slope > 0)
-            gp = torch.where(y > 0, gy, gy * LEAKY_SLOPE) if ctx.leaky else gy
+            gp = gy if gp is None else gp
             wp, cfg, bm = _wino_pack(weight, cin, cout, 1, st)
             zb = torch.zeros(((cin + bm - 1) // bm) * bm, dtype=torch.float32, device=x.device)
             gx = _wino_conv(gp, wp, zb, cin, cfg, False, st, "d")
@@ -161,9 +165,14 @@ class _Conv3x3(torch.autograd.Function):
             if nw < 0:
                 _lib.check(nw, "rrin_tconv3x3_wgrad_work_floats")
             work = torch.empty((nw,), dtype=torch.float32, device=x.device)
-            d = _lib.TWgradDesc(n=n, cin=cin, cout=cout, h=h, w=w, leaky=int(ctx.leaky), slope=LEAKY_SLOPE,
-                                x=x.data_ptr(), g=gy.data_ptr(), y=y.data_ptr() if ctx.leaky else None,
-                                gw=gw.data_ptr(), gb=gb.data_ptr(), work=work.data_ptr())
+            if gp is not None:  # already masked
+                d = _lib.TWgradDesc(n=n, cin=cin, cout=cout, h=h, w=w, leaky=0, slope=LEAKY_SLOPE,
+                                    x=x.data_ptr(), g=gp.data_ptr(), y=None,
+                                    gw=gw.data_ptr(), gb=gb.data_ptr(), work=work.data_ptr())
+            else:
+                d = _lib.TWgradDesc(n=n, cin=cin, cout=cout, h=h, w=w, leaky=int(ctx.leaky), slope=LEAKY_SLOPE,
+                                    x=x.data_ptr(), g=gy.data_ptr(), y=y.data_ptr() if ctx.leaky else None,
+                                    gw=gw.data_ptr(), gb=gb.data_ptr(), work=work.data_ptr())
             _lib.check(L.rrin_tconv3x3_wgrad(C.byref(d), st), "rrin_tconv3x3_wgrad")
         return gx, gw, (gb if ctx.has_bias else None), None
 

@@ -374,39 +374,202 @@ extern "C" int rrin_tconv3x3(const rrin_tconv_desc* d, void* stream) {
   return hip_code(hipGetLastError());
 }
 
-// K slice of the weight gradient: whole 16-steps, ~32 slices at most, at least 4096 pixels each
-static int64_t twgrad_kslice(int64_t K) {
-  int64_t ks = (K + 31) / 32;
-  if (ks < 4096) ks = 4096;
-  return (ks + TBK - 1) / TBK * TBK;
+// ---- weight gradient, row-tiled (round 4): C[co][ci * 9 + tap] = sum over the pixels of a
+// slice of whole image rows of g'[co][p] x[ci][p + tap] on v_mfma_f32_32x32x2_f32.  A K chunk
+// is a 64-pixel segment of one row: g' for the block's co tiles and the 3 x 66-pixel input
+// rows (halo, zero padding) of 32 ci are staged in LDS, the pixels split by parity (pixel
+// 2 s + kh is K step s of MFMA lane half kh), the input rows also one-shifted, so every
+// operand of 4 K steps is one aligned ds_read_b128 and the 9 taps reuse the staged rows.
+// Wave (co tile ct, tap group tg) owns taps 3 tg .. 3 tg + 2: 3 accumulators.  Slices are
+// fixed per shape and summed in slice order (twgrad_reduce_kernel): deterministic.
+struct TWArgs {
+  int n, cin, cout, h, w, leaky;
+  float slope;
+  const float* x;
+  const float* g;
+  const float* y;
+  float* part;   // [slices][cout][cin * 9 + 1]
+  int rows_per_slice;
+};
+constexpr int kWgPx = 64, kWgSj = 36;  // pixels per K chunk; parity-row stride (33 + pad, 16-B aligned)
+
+template <int CT>
+constexpr size_t twgrad_lds() {
+  return (size_t)(CT * 32 * 2 * 32 + 2 * 32 * 3 * 2 * kWgSj) * 4;
+}
+
+template <int CT>
+__global__ __launch_bounds__(192 * CT, 2) void twgrad_tile_kernel(TWArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float tw_smem[];
+  float* sA = tw_smem;                      // [CT * 32 co][2 kh][32 s]
+  float* sB = tw_smem + CT * 32 * 2 * 32;   // [2 copies][32 ci][3 ky][2 p][kWgSj]
+  constexpr int NT = 192 * CT;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ct = wv % CT, tg = wv / CT;
+  const int ci0 = blockIdx.x * 32, co0 = blockIdx.y * (32 * CT), slice = blockIdx.z;
+  const int64_t hw = (int64_t)a.h * a.w;
+  const int rows = a.n * a.h;
+  const int r0 = slice * a.rows_per_slice, r1 = min(rows, r0 + a.rows_per_slice);
+  tfloatx16 acc[3];
+#pragma unroll
+  for (int t = 0; t < 3; ++t) acc[t] = tfloatx16{};
+  const int j = lane & 31, kh = lane >> 5;
+  // per tap: the LDS float offset of this lane's B operand run (copy, ky, parity) at s = 0
+  int boff[3];
+#pragma unroll
+  for (int t = 0; t < 3; ++t) {
+    const int tap = 3 * tg + t, ky = tap / 3, kx = tap % 3, c = kh + kx;
+    boff[t] = ((((c >> 1) * 32 + j) * 3 + ky) * 2 + (c & 1)) * kWgSj;
+  }
+  const int aoff = ((ct * 32 + j) * 2 + kh) * 32;
+  for (int R = r0; R < r1; ++R) {
+    const int img = R / a.h, yrow = R - img * a.h;
+    for (int x0 = 0; x0 < a.w; x0 += kWgPx) {
+      __syncthreads();  // every read of the previous chunk done
+      // A: g'[co][x0 .. x0 + 63], 4 pixels per item (one float4 load when w % 4 == 0),
+      // zero past w / cout
+      for (int i = tid; i < CT * 32 * 16; i += NT) {
+        const int col = i >> 4, q = i & 15, co = co0 + col, px = x0 + 4 * q;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (co < a.cout && px < a.w) {
+          const int64_t o = ((int64_t)img * a.cout + co) * hw + (int64_t)yrow * a.w + px;
+          float4 yv = make_float4(1.f, 1.f, 1.f, 1.f);
+          if ((a.w & 3) == 0) {
+            v = *reinterpret_cast<const float4*>(a.g + o);
+            if (a.leaky) yv = *reinterpret_cast<const float4*>(a.y + o);
+          } else {
+            float gv[4] = {0.f, 0.f, 0.f, 0.f}, yy4[4] = {1.f, 1.f, 1.f, 1.f};
+            for (int e = 0; e < 4 && px + e < a.w; ++e) {
+              gv[e] = a.g[o + e];
+              if (a.leaky) yy4[e] = a.y[o + e];
+            }
+            v = make_float4(gv[0], gv[1], gv[2], gv[3]);
+            yv = make_float4(yy4[0], yy4[1], yy4[2], yy4[3]);
+          }
+          if (a.leaky) {
+            v.x *= yv.x > 0.f ? 1.f : a.slope;
+            v.y *= yv.y > 0.f ? 1.f : a.slope;
+            v.z *= yv.z > 0.f ? 1.f : a.slope;
+            v.w *= yv.w > 0.f ? 1.f : a.slope;
+          }
+        }
+        *reinterpret_cast<float2*>(sA + (col * 2 + 0) * 32 + 2 * q) = make_float2(v.x, v.z);
+        *reinterpret_cast<float2*>(sA + (col * 2 + 1) * 32 + 2 * q) = make_float2(v.y, v.w);
+      }
+      // B: x[ci][yrow - 1 .. yrow + 1][x0 - 1 .. x0 + 64], zero outside; k = 2 jj + p
+      for (int i = tid; i < 32 * 3 * 66; i += NT) {
+        const int cl = i / 198, rem = i - cl * 198, ky = rem / 66, k = rem - ky * 66;
+        const int ci = ci0 + cl, yy = yrow + ky - 1, px = x0 - 1 + k;
+        float v = 0.f;
+        if (ci < a.cin && yy >= 0 && yy < a.h && px >= 0 && px < a.w)
+          v = a.x[((int64_t)img * a.cin + ci) * hw + (int64_t)yy * a.w + px];
+        const int p = k & 1, jj = k >> 1;
+        sB[((0 * 32 + cl) * 3 + ky) * 2 * kWgSj + p * kWgSj + jj] = v;
+        if (jj >= 1) sB[((1 * 32 + cl) * 3 + ky) * 2 * kWgSj + p * kWgSj + jj - 1] = v;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int s4 = 0; s4 < 8; ++s4) {
+        const float4 av = *reinterpret_cast<const float4*>(sA + aoff + 4 * s4);
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+          const float4 bv = *reinterpret_cast<const float4*>(sB + boff[t] + 4 * s4);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, bv.x, acc[t], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, bv.y, acc[t], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, bv.z, acc[t], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, bv.w, acc[t], 0, 0, 0);
+        }
+      }
+    }
+  }
+  // C[co][ci] of register r: co = 8 (r / 4) + 4 (lane / 32) + r % 4, ci = lane % 32
+  const int N = a.cin * 9 + 1, ci = ci0 + j;
+  if (ci >= a.cin) return;
+#pragma unroll
+  for (int t = 0; t < 3; ++t) {
+    const int tap = 3 * tg + t;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int co = co0 + ct * 32 + 8 * (r >> 2) + 4 * kh + (r & 3);
+      if (co < a.cout) a.part[((int64_t)slice * a.cout + co) * N + ci * 9 + tap] = acc[t][r];
+    }
+  }
+}
+
+// the bias column of a slice's partials: sum of g' over its rows, fixed order (per thread a
+// strided run, then a fixed tree): deterministic
+__global__ __launch_bounds__(256) void twgrad_bias_kernel(TWArgs a) {
+  __shared__ float red[256];
+  const int co = blockIdx.x, slice = blockIdx.y, tid = threadIdx.x;
+  const int64_t hw = (int64_t)a.h * a.w;
+  const int rows = a.n * a.h;
+  const int r0 = slice * a.rows_per_slice, r1 = min(rows, r0 + a.rows_per_slice);
+  float s = 0.f;
+  for (int R = r0; R < r1; ++R) {
+    const int img = R / a.h, yrow = R - img * a.h;
+    const int64_t base = ((int64_t)img * a.cout + co) * hw + (int64_t)yrow * a.w;
+    for (int px = tid; px < a.w; px += 256) {
+      float v = a.g[base + px];
+      if (a.leaky) v *= a.y[base + px] > 0.f ? 1.f : a.slope;
+      s += v;
+    }
+  }
+  red[tid] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) red[tid] += red[tid + o];
+    __syncthreads();
+  }
+  if (tid == 0) a.part[((int64_t)slice * a.cout + co) * (a.cin * 9 + 1) + a.cin * 9] = red[0];
+}
+
+// slices of whole rows: ~1024 tile workgroups per weight gradient
+static void twgrad_slices(int n, int cin, int cout, int h, int* rows_per_slice, int* slices) {
+  const int ct = cout % 64 == 0 ? 2 : 1;
+  const int64_t per = (int64_t)((cin + 31) / 32) * ((cout + 32 * ct - 1) / (32 * ct));
+  const int rows = n * h;
+  int64_t sl = (1024 + per - 1) / per;
+  if (sl > rows) sl = rows;
+  if (sl < 1) sl = 1;
+  *rows_per_slice = (int)((rows + sl - 1) / sl);
+  *slices = (rows + *rows_per_slice - 1) / *rows_per_slice;
 }
 
 extern "C" int64_t rrin_tconv3x3_wgrad_work_floats(int32_t n, int32_t cin, int32_t cout, int32_t h, int32_t w) {
   if (n < 1 || cin < 1 || cout < 1 || h < 1 || w < 1) return RRIN_E_ARG;
-  const int64_t K = (int64_t)n * h * w, ks = twgrad_kslice(K);
-  const int64_t slices = (K + ks - 1) / ks;
-  return slices * cout * ((int64_t)cin * 9 + 1);
+  int rps, sl;
+  twgrad_slices(n, cin, cout, h, &rps, &sl);
+  return (int64_t)sl * cout * ((int64_t)cin * 9 + 1);
+}
+
+template <int CT>
+static int launch_twgrad(const TWArgs& a, int slices, hipStream_t st) {
+  auto k = twgrad_tile_kernel<CT>;
+  static LdsAttr attr;
+  if (int e = attr.ensure((const void*)k, (int)twgrad_lds<CT>(), st)) return e;
+  dim3 grid((unsigned)((a.cin + 31) / 32), (unsigned)((a.cout + 32 * CT - 1) / (32 * CT)), (unsigned)slices);
+  hipLaunchKernelGGL(k, grid, dim3(192 * CT), twgrad_lds<CT>(), st, a);
+  return hip_code(hipGetLastError());
 }
 
 extern "C" int rrin_tconv3x3_wgrad(const rrin_twgrad_desc* d, void* stream) {
   if (!d || !d->x || !d->g || !d->gw || !d->work || (d->leaky && !d->y)) return RRIN_E_ARG;
   if (d->n < 1 || d->cin < 1 || d->cout < 1 || d->h < 1 || d->w < 1) return RRIN_E_ARG;
   if (d->leaky && !(d->slope > 0.f && d->slope <= 1.f)) return RRIN_E_ARG;
-  TConvArgs a;
+  TWArgs a;
   memset(&a, 0, sizeof(a));
   a.n = d->n, a.cin = d->cin, a.cout = d->cout, a.h = d->h, a.w = d->w;
-  a.leaky = d->leaky, a.slope = d->slope, a.x = d->x, a.g = d->g, a.y = d->y;
-  a.M = d->cout;
-  a.N = d->cin * 9 + 1;
-  a.K = (int64_t)d->n * d->h * d->w;
-  a.kslice = twgrad_kslice(a.K);
-  a.out = d->work;
-  const int slices = (int)((a.K + a.kslice - 1) / a.kslice);
+  a.leaky = d->leaky, a.slope = d->slope, a.x = d->x, a.g = d->g, a.y = d->y, a.part = d->work;
+  int slices;
+  twgrad_slices(a.n, a.cin, a.cout, a.h, &a.rows_per_slice, &slices);
   const hipStream_t st = (hipStream_t)stream;
-  dim3 grid((a.N + TBN - 1) / TBN, (a.M + TBM - 1) / TBM, slices);
-  hipLaunchKernelGGL(tconv3x3_kernel<TC_WGRAD>, grid, dim3(256), 0, st, a);
-  hipLaunchKernelGGL(twgrad_reduce_kernel, dim3(grid_of((int64_t)a.M * a.N)), dim3(256), 0, st,
-                     (const float*)d->work, slices, a.M, a.N, d->gw, d->gb);
+  const int rc = a.cout % 64 == 0 ? launch_twgrad<2>(a, slices, st) : launch_twgrad<1>(a, slices, st);
+  if (rc) return rc;
+  hipLaunchKernelGGL(twgrad_bias_kernel, dim3((unsigned)a.cout, (unsigned)slices), dim3(256), 0, st, a);
+  const int M = a.cout, N = a.cin * 9 + 1;
+  hipLaunchKernelGGL(twgrad_reduce_kernel, dim3(grid_of((int64_t)M * N)), dim3(256), 0, st, (const float*)d->work,
+                     slices, M, N, d->gw, d->gb);
   return hip_code(hipGetLastError());
 }
 

@@ -4,7 +4,7 @@
 # suite, then bitwise + timing against config 20 on the Net's conv shapes at 720p x 2.
 set -u
 O=${O:-gpurun_out/r04c}; mkdir -p $O; export TMPDIR=/tmp
-STEPS=${STEPS:-probe,dbg,h8,ab}
+STEPS=${STEPS:-probe,dbg,h8,ab,train}
 run() {  # name limit cmd...
   local name=$1 lim=$2; shift 2
   echo "=== $name"
@@ -22,6 +22,12 @@ S32=64:32:0:1,32:32:0:1,32:32:0:2,16:32:0:1,64:32:0:4
 if [[ $STEPS == *ab* ]]; then
   run ab_20_23 300 python3 -u tools/conv_lab.py cfgab --cfgs 20,23 --batch 2 --shapes $S64
   run ab_20_24 300 python3 -u tools/conv_lab.py cfgab --cfgs 20,24 --batch 2 --shapes $S64,$S32
+fi
+if [[ $STEPS == *train* ]]; then
+  run train_tests 600 python3 -u -m pytest tests/test_gpu_train.py -x -q --timeout 300 --timeout-method thread
+  run bench_train 300 python3 bench.py --train --steps 5 --warmup 2
+  run prof_train 300 rocprofv3 --kernel-trace --stats -d $O/prof_train -o run --output-format csv -- python3 bench.py --train --steps 3 --warmup 1
+  python3 tools/kernel_family_stats.py $(ls $O/prof_train/*/*kernel_stats.csv $O/prof_train/*kernel_stats.csv 2>/dev/null | head -1) > $O/kernel_family_train.txt 2>&1; head -20 $O/kernel_family_train.txt
 fi
 cat $O/probe2.log 2>/dev/null | tail -50
 exit 0
