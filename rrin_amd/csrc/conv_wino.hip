@@ -761,6 +761,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wino64_kernel(ConvH8Args a) {
 #ifndef RRIN_WINOQ_ORDER
 #define RRIN_WINOQ_ORDER 0  // A/B builds only: tile order of the workgroup index
 #endif
+#ifndef RRIN_WINOQ_AGPR
+#define RRIN_WINOQ_AGPR 0
+#endif
 #ifndef RRIN_WINOQ_PRIO
 #define RRIN_WINOQ_PRIO 0  // A/B builds only: 1 s_setprio around each MFMA cluster, 2 static for waves 4-7
 #endif
@@ -1167,6 +1170,9 @@ __global__ __launch_bounds__(256 * PT, 2) void conv3x3_winoq_kernel(ConvH8Args a
   }
   }
   __syncthreads();  // every read done before the exchange reuses the LDS
+#if RRIN_WINOQ_AGPR
+  asm volatile("" ::"a"(acc[0][0]));  // A/B: MFMA accumulators in AGPRs
+#endif
 
   // ---- output transform (cfg 19 scheme, one co tile): the four yw waves of a
   // patch-row pair exchange their Q[c] = sum_x M[x] A[x][c] through LDS, one

@@ -32,6 +32,10 @@
 // of the chunk; MFMA product e contracts channels e and 4 + e).
 #include "common.hpp"
 
+#ifndef RRIN_WINOC_AGPR
+#define RRIN_WINOC_AGPR 0
+#endif
+
 namespace rrin {
 
 typedef float cfloatx16 __attribute__((ext_vector_type(16)));
@@ -256,6 +260,10 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winoc_kernel(ConvH8Args a) {
     chunk(nch - 1, s, false);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMA past the end has landed
+#if RRIN_WINOC_AGPR
+  // A/B: an inline-asm AGPR operand makes the compiler keep MFMA accumulators in AGPRs
+  asm volatile("" ::"a"(acc[0][0][0][0]));
+#endif
   __syncthreads();  // every read of the stages done before the exchange reuses the LDS
 
   // ---- output transform (kinds 1-4's order): Q[c] = sum_x M[x] A[x][c] of this wave's

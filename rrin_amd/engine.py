@@ -176,13 +176,13 @@ WINO_DIRECT = {(6, 32, 0): 13}
 # (4 waves of 8 accumulators) on every conv shape of the Net, bitwise equal
 # (profiles/r03/cfgab_18_20.txt)
 WINO_KIND = 3
-# 0 = "auto": the register-U tiles (conv_winoc.hip, bitwise equal to kind 3) -- kind 6
-# (BM 64 x TH 4, each transformed input feeds 2 co tiles) where the conv's output rows
-# fill 64-channel blocks, else kind 7 (BM 32 x TH 8, each U record feeds 2 patch tiles)
+# 0 = "auto": the register-U tile kind 6 (conv_winoc.hip, BM 64 x TH 4, each transformed
+# input feeds 2 co tiles; bitwise equal to kind 3) where the conv's output rows fill
+# 64-channel blocks, else kind 3
 def wino_kind_for(cout: int) -> int:
     if WINO_KIND != 0:
         return WINO_KIND
-    return 6 if cout % 64 == 0 else 7
+    return 6 if cout % 64 == 0 else 3
 # ... and kind 4 (the same arithmetic on TH 4 tiles of 4 waves: twice the
 # workgroups) on the few-tile deep convs where that wins, (cin, cout rows, grid
 # level) per size class as in WINO_DIRECT (a sub-pixel up conv: 4 x cout, the
@@ -585,6 +585,13 @@ class RRINEngine:
         self._scratch[sk] = sc
         return sc
 
+    def _net_scratch(self, n: int, h: int, w: int, slot: int):
+        """The scratch of Net forward part (n, h, w, slot) for its conv table (cached)."""
+        d = _lib.NetDesc()
+        d.n, d.h, d.w, d.prec = n, h, w, self.prec
+        d.convs = self.conv_table_for(n, h, w)
+        return self.scratch((n, h, w, slot), d, self.lib.rrin_net_scratch_bytes)
+
     side_priority = 0  # torch.cuda.Stream priority of the side streams (-1: high)
 
     def _side_streams(self, k: int):
@@ -644,8 +651,11 @@ class RRINEngine:
             tapbuf = torch.full((13 * n * h * w,), float("nan"), dtype=torch.float32, device=self.device)
         with torch.cuda.device(self.device):
             main = torch.cuda.current_stream(self.device)
-            # workspaces first: a new one is zero-filled on the main stream, before the fork
+            # workspaces and split scratch first: a new one is zero-filled on the main stream,
+            # before the fork (a side stream only waits for what main enqueued before it)
             wss = [self.workspace(hi - lo, h, w, j) for j, (lo, hi) in enumerate(bounds)]
+            for j, (lo, hi) in enumerate(bounds):
+                self._net_scratch(hi - lo, h, w, j)
             sides = self._side_streams(k - 1)
             for s in sides:
                 s.wait_stream(main)
@@ -713,7 +723,7 @@ class RRINEngine:
         d.prec = self.prec
         d.prof = prof
         d.taps = tapbuf.data_ptr() if tapbuf is not None else None
-        sc = self.scratch(key, d, self.lib.rrin_net_scratch_bytes)
+        sc = self._net_scratch(n, h, w, slot)  # allocated (and zero-filled) before the fork
         if sc is not None:
             d.scratch, d.scratch_bytes = sc.data_ptr(), sc.numel()
         st = self._status_of(slot) if self.prec in (_lib.PREC_F16X3, _lib.PREC_F16) else None
