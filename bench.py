@@ -67,9 +67,26 @@ KERNEL = {"fp32": "conv3x3_h8_kernel on fp32 records (77 body convs, v_mfma_f32_
           "fp32_planar": "conv3x3_mfma_kernel, planar fp32 (77 body convs, v_mfma_f32_32x32x2_f32)",
           "fp32_split16": "conv3x3_h8_kernel (77 body convs, v_mfma_f32_32x32x16_f16 x3)",
           "fp16": "conv3x3_h8_kernel (77 body convs, v_mfma_f32_32x32x16_f16)"}
-KERNEL_WINO = ("conv3x3_winoq_kernel: Winograd F(2x2,3x3) on fp32 records (76 of the 77 body convs; fp32 "
-               "input/output transforms, v_mfma_f32_32x32x2_f32 contraction per transform point; 8 waves of 4 "
-               "accumulators per 32 co x 32 px x 8 row tile, 4 waves per SIMD)")
+# Winograd F(2x2,3x3) tiles by kind (rrin_conv_h8_cfg_wino; engine.wino_kind_for)
+WINO_KERNELS = {1: "conv3x3_wino_kernel (BM 32 x TH 8, 4 waves of 8 accumulators)",
+                3: "conv3x3_winoq_kernel (BM 32 x TH 8, 8 waves of 4 accumulators)",
+                4: "conv3x3_winoq_kernel (BM 32 x TH 4, 4 waves)",
+                6: "conv3x3_winoc_kernel (register-U, BM 64 x TH 4, 4 waves of 2 co tiles)",
+                7: "conv3x3_winoc_kernel (register-U, BM 32 x TH 8, 4 waves of 2 patch tiles)"}
+
+
+def kernel_wino(eng, n, h, w):
+    """The body convs' kernels of a forward part of n pairs at h x w, with counts."""
+    lib = _lib.lib()
+    t = eng.conv_table_for(n, h, w)
+    kinds = [lib.rrin_conv_h8_cfg_wino(t[i].cfg) for i in range(eng.expected_convs)]
+    parts = [f"{WINO_KERNELS.get(k, f'kind {k}')} x {kinds.count(k)}" for k in sorted(set(kinds)) if k]
+    if kinds.count(0):
+        parts.append(f"conv3x3_h8_kernel direct form x {kinds.count(0)}")
+    return ("Winograd F(2x2,3x3) on fp32 records, fp32 input/output transforms, v_mfma_f32_32x32x2_f32 "
+            "contraction per transform point: " + "; ".join(parts))
+
+
 DTYPE = {"fp32": "f32", "fp32_planar": "f32",
          "fp32_split16": "f16x3 (fp32-emulated: fp16 hi+lo split, 3 f16 MFMA products, f32 accumulate)",
          "fp16": "f16"}
@@ -114,7 +131,7 @@ def parse():
                          "Winograd F(2x2,3x3)")
     ap.add_argument("--wino-kind", type=int, default=None,
                     help="A/B: Winograd tile kind of the exact-fp32 body convs (rrin_conv_h8_cfg_wino; "
-                         "0 = the register-U kinds 6/7 by output channels; default engine.WINO_KIND)")
+                         "0 = auto: kind 6 where cout %% 64 == 0, else 3; default engine.WINO_KIND)")
     ap.add_argument("--wino-split", default=None,
                     help="A/B: split-K slices per grid level for every Winograd conv, e.g. '2:2,3:4,4:8' "
                          "(engine.WINO_SPLIT_LEVELS); 'none' disables the tuned splits")
@@ -466,7 +483,8 @@ def main():
         roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1),
                     "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None,
                     "mfma_issued_tflops": round(achieved * MFMA_PRODUCTS[args.precision], 1),
-                    "kernel": (KERNEL_WINO if algo in ("winograd", "mixed") and args.precision == "fp32"
+                    "kernel": (kernel_wino(eng, B // max(1, args.streams), H, W)
+                               if algo in ("winograd", "mixed") and args.precision == "fp32"
                                else KERNEL[args.precision]),
                     "conv_algorithm": algo,
                     "flops_basis": ("FLOPs of the algorithm the convs run: Winograd F(2x2,3x3) = 16 multiply-adds "
@@ -520,6 +538,7 @@ def main():
                           for u in ("Flow", "refine_flow", "Mask", "final"))
                 roofline["algorithmic_bytes_per_step_gb"] = round(B * alg / 1e9, 2)
                 roofline["traffic_source"] = f"profiles/pmc_traffic.json[{key}], build {build}"
+                roofline["traffic_kernels"] = ent.get("kernel_family")
 
     eng.check_range()  # fp16-stored precisions: no activation left the fp16 range (raises otherwise)
     gather_check = None

@@ -233,8 +233,11 @@ int launch_wino(const ConvH8Args& a, int epi, hipStream_t st);
 // zero channels [c0, c1) of a record-layout view (conv_f16.hip)
 int clear_channels_h8(const rrin_h8* v, int32_t n, int32_t c0, int32_t c1, int32_t prec, hipStream_t st);
 // 64-channel tile (8 waves, one block per CU): two stages of raw tile + 64-co U slab
+// (kind 2: built only into the lab library)
 constexpr size_t kWino64Lds = (size_t)2 * (704 + 16 * 2 * 64) * 16;
+#ifdef RRIN_LAB
 int launch_wino64(const ConvH8Args& a, int epi, hipStream_t st);
+#endif
 // cfg 18's tile on 8 waves of 4 accumulators (<= 128 VGPRs: 4 waves per SIMD),
 // two stages of [raw 680 | U 1024] records (three in A/B builds: two blocks per
 // CU would fill 163,584 B)
@@ -242,9 +245,10 @@ constexpr size_t kWinoQLds = (size_t)3 * (680 + 1024) * 16;
 // th = 8 (cfg 20: 8 waves) or 4 (cfg 21: 4 waves, the same arithmetic on half-height tiles)
 int launch_winoq(const ConvH8Args& a, int epi, int th, hipStream_t st);
 // Winograd F(4x4,3x3) (conv_wino4.hip): BM 32 x TH 16, 6 waves, 4-channel K chunks
+// (kind 5: built only into the lab library)
 constexpr size_t kWino4Lds = (size_t)2 * (612 + 1152) * 16;
-int launch_wino4(const ConvH8Args& a, int epi, hipStream_t st);
 #ifdef RRIN_LAB
+int launch_wino4(const ConvH8Args& a, int epi, hipStream_t st);
 int launch_wino4_lab(const ConvH8Args& a, int abl, hipStream_t st);
 #endif
 // register-U Winograd tiles (conv_winoc.hip): 4 waves, two blocks per CU, the U operands

@@ -1786,6 +1786,14 @@ static constexpr int kWino4Cfg = kNumCfgH8 - 3;
 static constexpr int kWinoC2Cfg = kNumCfgH8 - 2;
 static constexpr int kWinoC1Cfg = kNumCfgH8 - 1;
 static inline bool is_winoc(int cfg) { return cfg == kWinoC2Cfg || cfg == kWinoC1Cfg; }
+// tiles whose kernels only the lab library builds (kind 2 wino64, kind 5 F(4x4)):
+// the product library reports them as not usable (rrin_conv_h8_cfg_ok 0)
+static inline bool lab_only(int cfg) { return cfg == kWino64Cfg || cfg == kWino4Cfg; }
+#ifdef RRIN_LAB
+static constexpr bool kLabBuild = true;
+#else
+static constexpr bool kLabBuild = false;
+#endif
 static inline bool is_wino(int cfg) {
   return cfg == kWinoCfg || cfg == kWino64Cfg || cfg == kWinoQCfg || cfg == kWinoQ4Cfg || cfg == kWino4Cfg ||
          is_winoc(cfg);
@@ -1906,7 +1914,7 @@ static int h8_prepare(const rrin_conv_h8_desc* d, ConvH8Args& a, bool need_scrat
   if (!d || !d->whi || !d->bias) return RRIN_E_ARG;
   if (!rec_prec(d->prec)) return RRIN_E_ARG;
   if (d->prec == RRIN_PREC_F16X3 && !d->wlo) return RRIN_E_ARG;
-  if (d->cfg < 0 || d->cfg >= kNumCfgH8 ||
+  if (d->cfg < 0 || d->cfg >= kNumCfgH8 || (lab_only(d->cfg) && !kLabBuild) ||
       (planes_of(d->prec) == 2 ? kCfgH8[d->cfg].lds2 : kCfgH8[d->cfg].lds1) > kMaxLds)
     return RRIN_E_CONFIG;
   if (d->n < 1 || d->cin < 1 || d->cout < 8 || (d->cout & 7)) return RRIN_E_ARG;
@@ -2057,7 +2065,7 @@ extern "C" int rrin_conv_h8_cfg_wino(int32_t cfg) {
 }
 extern "C" int rrin_conv_h8_cfg_ok(int32_t cfg, int32_t prec) {
   if (cfg < 0 || cfg >= kNumCfgH8) return 0;
-  if (!rec_prec(prec)) return 0;
+  if (!rec_prec(prec) || (lab_only(cfg) && !kLabBuild)) return 0;
   if (is_wino(cfg) && prec != RRIN_PREC_F32R) return 0;
   return (planes_of(prec) == 2 ? kCfgH8[cfg].lds2 : kCfgH8[cfg].lds1) <= kMaxLds ? 1 : 0;
 }
@@ -2078,10 +2086,12 @@ extern "C" int rrin_conv3x3_h8_fwd(const rrin_conv_h8_desc* d, void* stream) {
   if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;
   if (d->cfg == kWinoCfg) return launch_wino(a, d->epi_mode, st);
-  if (d->cfg == kWino64Cfg) return launch_wino64(a, d->epi_mode, st);
   if (d->cfg == kWinoQCfg) return launch_winoq(a, d->epi_mode, 8, st);
   if (d->cfg == kWinoQ4Cfg) return launch_winoq(a, d->epi_mode, 4, st);
+#ifdef RRIN_LAB
+  if (d->cfg == kWino64Cfg) return launch_wino64(a, d->epi_mode, st);
   if (d->cfg == kWino4Cfg) return launch_wino4(a, d->epi_mode, st);
+#endif
   if (d->cfg == kWinoC2Cfg) return launch_winoc(a, d->epi_mode, 2, st);
   if (d->cfg == kWinoC1Cfg) return launch_winoc(a, d->epi_mode, 1, st);
   switch (d->cfg) {

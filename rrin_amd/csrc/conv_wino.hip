@@ -455,6 +455,7 @@ int launch_wino(const ConvH8Args& a, int epi, hipStream_t st) {
 }
 
 
+#ifdef RRIN_LAB  // kind 2 (BM 64, 8 waves, one block per CU): lost to kinds 3 and 6, lab library only
 // ============================================================================
 // 64-channel tile (config kWino64Cfg): 8 waves = 2 per SIMD, one block per CU.
 // Tile = 64 output channels (two MFMA co tiles) x 32 px x 8 rows (64 patches).
@@ -744,6 +745,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wino64_kernel(ConvH8Args a) {
     }
   }
 }
+#endif  // RRIN_LAB (wino64)
 
 
 // ============================================================================
@@ -1423,6 +1425,7 @@ int launch_winoq(const ConvH8Args& a, int epi, int th, hipStream_t st) {
   return RRIN_E_ARG;
 }
 
+#ifdef RRIN_LAB
 template <int EPI>
 static int launch_wino64_k(const ConvH8Args& a, hipStream_t st) {
   auto k = conv3x3_wino64_kernel<EPI>;
@@ -1444,7 +1447,6 @@ int launch_wino64(const ConvH8Args& a, int epi, hipStream_t st) {
   return RRIN_E_ARG;
 }
 
-#ifdef RRIN_LAB
 // kernel lab (librrin_lab.so only): the LEAKY conv with ablation bits
 int launch_wino_lab(const ConvH8Args& a, int abl, hipStream_t st) {
   switch (abl) {  // 1024 + bits: the 4-waves-per-SIMD tile (cfg 20)

@@ -38,6 +38,10 @@
 
 namespace rrin {
 
+// The F(4x4) tile (kind 5) lost to F(2x2) on every Net shape: its
+// kernel is built only into the lab library (`make lab`, RRIN_LAB); the product
+// library keeps the host packing below and reports config kind 5 as not built.
+#ifdef RRIN_LAB
 typedef float w4x16 __attribute__((ext_vector_type(16)));
 typedef float w4x4 __attribute__((ext_vector_type(4)));
 typedef float w4x2 __attribute__((ext_vector_type(2)));
@@ -376,7 +380,6 @@ int launch_wino4(const ConvH8Args& a, int epi, hipStream_t st) {
   return RRIN_E_ARG;
 }
 
-#ifdef RRIN_LAB
 int launch_wino4_lab(const ConvH8Args& a, int abl, hipStream_t st) {
   switch (abl) {
     case 0: return launch_wino4_k<RRIN_EPI_LEAKY, 0>(a, st);
@@ -391,7 +394,7 @@ int launch_wino4_lab(const ConvH8Args& a, int abl, hipStream_t st) {
   }
   return RRIN_E_CONFIG;
 }
-#endif
+#endif  // RRIN_LAB
 
 }  // namespace rrin
 

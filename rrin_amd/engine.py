@@ -171,14 +171,18 @@ WINO_SIZES = ("small", "medium", "large", "xlarge", "xxlarge")
 WINO_DIRECT = {(6, 32, 0): 13}
 
 
-# Winograd tile kind (rrin_conv_h8_cfg_wino): 3 = BM 32 x TH 8 on 8 waves of 4
-# accumulators (4 waves per SIMD) -- 1-9 % faster than kind 1
-# (4 waves of 8 accumulators) on every conv shape of the Net, bitwise equal
-# (profiles/r03/cfgab_18_20.txt)
-WINO_KIND = 3
-# 0 = "auto": the register-U tile kind 6 (conv_winoc.hip, BM 64 x TH 4, each transformed
-# input feeds 2 co tiles; bitwise equal to kind 3) where the conv's output rows fill
-# 64-channel blocks, else kind 3
+# Winograd tile kind (rrin_conv_h8_cfg_wino).  0 = "auto" (the default since round 4):
+# the register-U tile kind 6 (conv_winoc.hip, BM 64 x TH 4, U operands loaded straight
+# into registers, each transformed input feeding 2 co tiles; bitwise equal to kind 3)
+# where the conv's output rows fill 64-channel blocks -- 0.5-16 % faster per conv
+# (profiles/r04/ab_kind3_vs_kind6.log), whole 1280x720 x 4 forward 132.1 -> 142.2-142.8
+# pairs/s (profiles/r04/bench_kind_ab.txt) -- else kind 3 = BM 32 x TH 8 on 8 waves of
+# 4 accumulators (1-9 % faster than kind 1, profiles/r03/cfgab_18_20.txt); the 32-row
+# kind 7 loses to kind 3 on the level-0 32-channel convs (ab_kind3_vs_kind7.log).
+# A nonzero value forces that kind everywhere (A/B, bench.py --wino-kind).
+WINO_KIND = 0
+
+
 def wino_kind_for(cout: int) -> int:
     if WINO_KIND != 0:
         return WINO_KIND

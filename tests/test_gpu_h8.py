@@ -52,10 +52,12 @@ NO_POOL_CFGS = (4, 16)
 
 
 def wino_cfgs():
-    """Ids of the Winograd exact-fp32 configs (R32 only): F(2x2,3x3) kinds 1-4 and the
-    register-U kinds 6-7, F(4x4,3x3) kind 5."""
+    """Ids of the Winograd exact-fp32 configs the library builds (R32 only): F(2x2,3x3)
+    kinds 1, 3, 4 and the register-U kinds 6-7 (kind 2 and the F(4x4,3x3) kind 5 only
+    in the lab library)."""
     lib = _lib.lib()
-    return tuple(c for c in range(lib.rrin_conv_h8_cfg_count()) if lib.rrin_conv_h8_cfg_wino(c))
+    return tuple(c for c in range(lib.rrin_conv_h8_cfg_count())
+                 if lib.rrin_conv_h8_cfg_wino(c) and lib.rrin_conv_h8_cfg_ok(c, R32))  # kinds 2, 5: lab only
 
 
 def cfgs(prec, cout, cin):

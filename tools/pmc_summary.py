@@ -54,7 +54,7 @@ def main():
     ap.add_argument("--precision", default="fp32_split16")
     ap.add_argument("--config", default="1280x720x4", help="WxHxB of the profiled bench run")
     ap.add_argument("--family", default=None,
-                    help="conv kernel family (default by precision; exact fp32 runs conv3x3_wino_kernel)")
+                    help="conv kernel family, comma-separated kernels summed (default by precision)")
     ap.add_argument("--key", default=None, help="table key prefix (default: --precision)")
     a = ap.parse_args()
     fetch = load(a.fetch, "FETCH_SIZE")
@@ -78,13 +78,23 @@ def main():
         json.dump({"correction": "hbm = (2*FETCH_SIZE + WRITE_SIZE) KiB (gfx950 FETCH_SIZE = 1/2 of wide reads)",
                    "steps": a.steps, "kernels": res}, open(a.out, "w"), indent=1)
     if a.table:
-        fam_name = a.family or {"fp32_planar": "conv3x3_mfma_kernel", "fp32": "conv3x3_wino_kernel"}.get(
+        # the conv family = every body-conv kernel (bench.py's roofline covers all 77 body
+        # convs of a forward part): exact fp32 runs the Winograd tiles (kinds 3/4:
+        # conv3x3_winoq_kernel, 6/7: conv3x3_winoc_kernel) and the direct-form first conv
+        fam_name = a.family or {"fp32_planar": "conv3x3_mfma_kernel",
+                                "fp32": "conv3x3_winoq_kernel,conv3x3_winoc_kernel,conv3x3_h8_kernel"}.get(
             a.precision, "conv3x3_h8_kernel")
+        names = [n for n in fam_name.split(",") if n in res]
+        if not names:
+            sys.exit(f"no kernel of family {fam_name} in the counter files")
+        hbm_step = sum(res[n]["hbm_bytes_per_step"] for n in names)
+        launches = sum(res[n]["dispatches_per_step"] for n in names)
         tab = json.load(open(a.table)) if os.path.exists(a.table) else {}
-        r = res[fam_name]
         tab[f"{a.key or a.precision}@{a.config}"] = {
-            "kernel_family": fam_name, "hbm_bytes_per_launch": r["hbm_bytes_per_dispatch"],
-            "hbm_bytes_per_step": r["hbm_bytes_per_step"], "launches_per_step": r["dispatches_per_step"],
+            "kernel_family": ",".join(names), "hbm_bytes_per_launch": hbm_step / max(launches, 1e-9),
+            "hbm_bytes_per_step": hbm_step, "launches_per_step": launches,
+            "per_kernel": {n: {"hbm_bytes_per_step": res[n]["hbm_bytes_per_step"],
+                               "launches_per_step": res[n]["dispatches_per_step"]} for n in names},
             "correction": "hbm = (2*FETCH_SIZE + WRITE_SIZE) KiB, separate --pmc passes",
             "source": os.path.basename(os.path.normpath(a.fetch)) + " + " + os.path.basename(os.path.normpath(a.write)),
             # the library the profiled runs loaded (bench.py reports this entry only for that build)
