@@ -548,15 +548,21 @@ def abconv(args):
 
 
 def cfgab(args):
-    """Two tile configs of the product library on the same conv (each with its own
-    packing): outputs compared bitwise, interleaved timing (--cfgs A,B; shapes as
-    abconv without the cfg field: cin:cout:level:epi)."""
+    """Tile configs of the product library on the same conv (each with its own
+    packing), interleaved timing, medians relative to the first.  --cfgs A,B[,C...];
+    a variant "21s4" runs config 21 with a split-K of 4 slices (kinds 3, 4).
+    Variants without a split are compared bitwise with the first unsplit one; split
+    variants report their max-abs difference (a split rounds differently).  Shapes
+    as abconv without the cfg field: cin:cout:level:epi."""
     from rrin_amd.pp import H8Tensor
-    from tests.test_gpu_h8 import pack_h8
+    from tests.test_gpu_h8 import pack_h8, set_split
     dev = torch.device("cuda:0")
     L_ = _lib.lib()
     prec = _lib.PRECISIONS[args.precision]
-    ca, cb = (int(c) for c in args.cfgs.split(","))
+    variants = []
+    for v in args.cfgs.split(","):
+        c, _, k = v.partition("s")
+        variants.append((int(c), int(k) if k else 0))
     st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
     bad = 0
     for spec in args.shapes.split(","):
@@ -568,8 +574,13 @@ def cfgab(args):
         x = H8Tensor.from_nchw(torch.rand(n, cin, h, w, device=dev) * 2 - 1, prec)
         wt = torch.randn(cout, cin, 3, 3) / (3 * cin ** 0.5)
         bias = torch.randn(cout) * 0.1
-        outs, descs, keep = [], [], []
-        for cfg in (ca, cb):
+        outs, descs, keep, ok = [], [], [], []
+        for cfg, ks in variants:
+            if not L_.rrin_conv_h8_cfg_fits(cfg, prec, cin):
+                ok.append(False)
+                outs.append(None)
+                descs.append(None)
+                continue
             whi, wlo, bp, inv = pack_h8(wt, bias, cfg, prec, dev)
             dst = H8Tensor(n, cout // 4, 2 * h, 2 * w, dev, prec) if epi == 4 else H8Tensor(n, cout, h, w, dev, prec)
             pool = H8Tensor(n, cout, h // 2, w // 2, dev, prec) if epi == 2 else None
@@ -584,33 +595,47 @@ def cfgab(args):
                 ring = torch.zeros(n * (cout // 4) * (2 * (2 * w) + 2 * (2 * h - 2)), device=dev)
                 d.edge = ring.data_ptr()
             d.whi, d.wlo, d.bias = whi.data_ptr(), wlo.data_ptr(), bp.data_ptr()
+            set_split(d, ks, dev, keep)
             keep.append((whi, wlo, bp, ring))
             outs.append((dst, pool, ring))
             descs.append(d)
-        for d in descs:
-            _lib.check(L_.rrin_conv3x3_h8_fwd(C.byref(d), st))
+            ok.append(_lib.lib().rrin_conv3x3_h8_fwd(C.byref(d), st) == 0)
         torch.cuda.synchronize()
-        same = torch.equal(outs[0][0].to_nchw(), outs[1][0].to_nchw())
-        if epi == 2:
-            same = same and torch.equal(outs[0][1].to_nchw(), outs[1][1].to_nchw())
-        if epi == 4:
-            same = same and torch.equal(outs[0][2], outs[1][2])
-        times = [[], []]
+        ref = next(i for i, (c, k) in enumerate(variants) if ok[i] and not k)
+        notes = []
+        for i, (c, k) in enumerate(variants):
+            if not ok[i] or i == ref:
+                continue
+            a, b = outs[ref][0].to_nchw(), outs[i][0].to_nchw()
+            if k:
+                notes.append(f"{c}s{k} maxdiff {float((a - b).abs().max()):.1e}")
+            else:
+                same = torch.equal(a, b)
+                if epi == 2:
+                    same = same and torch.equal(outs[ref][1].to_nchw(), outs[i][1].to_nchw())
+                if epi == 4:
+                    same = same and torch.equal(outs[ref][2], outs[i][2])
+                bad += 0 if same else 1
+                notes.append(f"{c} {'bitwise' if same else 'DIFFERENT'}")
+        times = [[] for _ in variants]
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         for _ in range(args.rounds):
             for i, d in enumerate(descs):
+                if not ok[i]:
+                    continue
                 e0.record()
                 for _ in range(args.reps):
                     L_.rrin_conv3x3_h8_fwd(C.byref(d), st)
                 e1.record()
                 e1.synchronize()
                 times[i].append(e0.elapsed_time(e1) / args.reps)
-        med = [sorted(t)[len(t) // 2] for t in times]
+        med = [sorted(t)[len(t) // 2] if t else float("nan") for t in times]
         wf = 2 * 4 * cin * cout * h * w * n
-        print(f"{cin:4d}->{cout:4d} L{L} epi{epi} n{n}: cfg{ca} {med[0]:.4f} ms ({wf / (med[0] * 1e-3) / 1e12:.1f} TF)  "
-              f"cfg{cb} {med[1]:.4f} ms ({wf / (med[1] * 1e-3) / 1e12:.1f} TF)  B/A {med[1] / med[0]:.3f}  "
-              f"{'bitwise equal' if same else 'DIFFERENT'}", flush=True)
-        bad += 0 if same else 1
+        cols = "  ".join(f"{c}{'s%d' % k if k else ''} {med[i]:.4f} ({med[i] / med[0]:.3f})"
+                         for i, (c, k) in enumerate(variants))
+        best = min(m for m in med if m == m)
+        print(f"{cin:4d}->{cout:4d} L{L} epi{epi} n{n}: {cols}  best {wf / (best * 1e-3) / 1e12:.1f} TF(wino)  "
+              + "; ".join(notes), flush=True)
     if bad and args.check:
         sys.exit(3)
 
@@ -618,7 +643,7 @@ def cfgab(args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("mode", choices=["breakdown", "tune", "single", "ablate", "ablate32", "abconv", "cfgab"])
-    ap.add_argument("--cfgs", default="18,19", help="cfgab: the two tile configs")
+    ap.add_argument("--cfgs", default="20,23", help="cfgab: tile configs, e.g. 20,21,23,21s4 (s: split-K slices)")
     ap.add_argument("--lib", default=None, help="abconv: library A (default: the in-tree product library)")
     ap.add_argument("--lib-b", default=None, help="abconv: libraries B, C, ... (comma-separated)")
     ap.add_argument("--shapes", default="256:256:3:1:18,64:32:0:1:18,32:32:0:1:18,128:64:1:1:18",

@@ -42,10 +42,12 @@ if [[ $STEPS == *sq* ]]; then
   B2="python3 bench.py --steps 2 --warmup 1 --cpu-baseline off --no-prof --no-alt"
   run pmc_sq1 240 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS GRBM_GUI_ACTIVE --output-format csv -d $O/pmc_sq1 -o run -- $B2
   run pmc_sq2 240 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAIT_INST_LDS SQ_LDS_IDX_ACTIVE SQ_WAVE_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_MFMA --output-format csv -d $O/pmc_sq2 -o run -- $B2
-  for f in conv3x3_winoc_kernel conv3x3_winoq_kernel; do
-    python3 tools/pmc_counters.py $O/pmc_sq1 $O/pmc_sq2 --family $f --mfma-cycles 64 > $O/sum_sq_$f.txt 2>&1
+  for f in conv3x3_winoc_kernel conv3x3_winoq_kernel; do  # one summary per pass (the passes' dispatches differ)
+    for d in pmc_sq1 pmc_sq2; do
+      python3 tools/pmc_counters.py $O/$d --family $f --mfma-cycles 64 > $O/sum_${d}_$f.txt 2>&1
+    done
   done
-  cat $O/sum_sq_*.txt | cut -c1-200
+  cat $O/sum_pmc_sq*.txt | cut -c1-200
 fi
 [[ $STEPS == *train* ]] && run bench_train 300 python bench.py --train --steps 5 --warmup 2
 exit 0
