@@ -7,12 +7,12 @@
 // avg_pool2d output (unet.py:46), the cat by channel offset (unet.py:93) and the
 // sub-pixel form of Upsample + up conv (unet.py:77-78).
 //
-// Why this shape (tools/coissue_probe*.py): on gfx950 a wave's
-// v_mfma_f32_32x32x2_f32 stream does not overlap the other waves' VALU, LDS-read or
-// LDS-DMA instructions on the same SIMD -- their issue cycles add to the MFMA cycles.
-// The kernel time is therefore the MFMA cycles plus every other instruction's
-// price, whatever the occupancy, and what pays is fewer non-MFMA instructions per
-// MFMA:
+// Why this shape (tools/coissue_probe2.py): on gfx950 a
+// v_mfma_f32_32x32x2_f32 stream with its accumulators in VGPRs (the compiler's form
+// here) pays 6-8 pipe cycles for each VALU op and ~55 for each ds_write of the other
+// waves on its SIMD, and vector-memory instructions (global loads, LDS-DMA) do not
+// overlap it in either accumulator form; LDS reads and SALU do.  What pays is fewer
+// non-MFMA instructions per MFMA:
 //   * the A operands (transformed weights U) go straight from L2 into registers
 //     (buffer_load_dwordx4: one per 4 MFMAs of a co tile, each record holding 4
 //     K steps), loaded a chunk ahead: no LDS-DMA pieces and no LDS reads for U;
@@ -35,8 +35,20 @@
 #ifndef RRIN_WINOC_AGPR
 #define RRIN_WINOC_AGPR 0
 #endif
+// Diagnostic build only (tools/clock_probe.py, never the product library): each
+// workgroup stamps s_memtime / s_memrealtime at its start, after its main loop and at
+// its end into g_winoc_clk[bid % kClkSlots] (the in-kernel clock: MI355X_MICROARCH.md
+// 'DVFS give-back' item 6)
+#ifndef RRIN_WINOC_CLOCK
+#define RRIN_WINOC_CLOCK 0
+#endif
 
 namespace rrin {
+
+#if RRIN_WINOC_CLOCK
+constexpr int kClkSlots = 1 << 16;
+__device__ unsigned long long g_winoc_clk[kClkSlots * 4];
+#endif
 
 typedef float cfloatx16 __attribute__((ext_vector_type(16)));
 typedef float cfloatx4 __attribute__((ext_vector_type(4)));
@@ -89,6 +101,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winoc_kernel(ConvH8Args a) {
   }
   const int ntiles = a.co_blocks * a.tiles_x * a.tiles_y * a.n;
   if (bid >= ntiles) return;
+#if RRIN_WINOC_CLOCK
+  const unsigned long long clk_t0 = __builtin_amdgcn_s_memtime(), clk_r0 = __builtin_amdgcn_s_memrealtime();
+#endif
   const int nch = a.nchunks;
   int cob, x0, y0, img;
   {  // the co blocks of a tile position on consecutive workgroups (they share its raw tile)
@@ -260,6 +275,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winoc_kernel(ConvH8Args a) {
     chunk(nch - 1, s, false);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMA past the end has landed
+#if RRIN_WINOC_CLOCK
+  const unsigned long long clk_t1 = __builtin_amdgcn_s_memtime();
+#endif
 #if RRIN_WINOC_AGPR
   // A/B: an inline-asm AGPR operand makes the compiler keep MFMA accumulators in AGPRs
   asm volatile("" ::"a"(acc[0][0][0][0]));
@@ -388,6 +406,16 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winoc_kernel(ConvH8Args a) {
       }
     }
   }
+#if RRIN_WINOC_CLOCK
+  const unsigned long long clk_t2 = __builtin_amdgcn_s_memtime(), clk_r2 = __builtin_amdgcn_s_memrealtime();
+  if (tid == 0) {
+    unsigned long long* g = g_winoc_clk + (size_t)(bid % kClkSlots) * 4;
+    g[0] = clk_t2 - clk_t0;  // core clocks, whole workgroup
+    g[1] = clk_r2 - clk_r0;  // 100 MHz ticks
+    g[2] = clk_t1 - clk_t0;  // core clocks to the end of the main loop
+    g[3] = clk_r0;           // start (100 MHz ticks)
+  }
+#endif
 }
 
 template <int EPI, int CT, int NT>
@@ -418,3 +446,12 @@ int launch_winoc(const ConvH8Args& a, int epi, int ct, hipStream_t st) {
 }
 
 }  // namespace rrin
+
+#if RRIN_WINOC_CLOCK
+// diagnostic builds only: copy n workgroup stamps (4 x u64 each) to host memory
+extern "C" int rrin_winoc_clock_read(unsigned long long* host, int n) {
+  if (!host || n < 1 || n > rrin::kClkSlots) return RRIN_E_ARG;
+  return rrin::hip_code(hipMemcpyFromSymbol(host, HIP_SYMBOL(rrin::g_winoc_clk), (size_t)n * 4 * 8, 0,
+                                            hipMemcpyDeviceToHost));
+}
+#endif

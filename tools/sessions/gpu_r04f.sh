@@ -13,6 +13,8 @@ run() {  # name limit cmd...
   if [ $rc -ge 124 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then echo "fatal rc $rc in $name; stopping"; exit $rc; fi
   return 0
 }
+run clock 300 python3 -u tools/clock_probe.py --shapes 256:256:3:1,128:64:1:1,512:512:4:1,128:128:2:2,512:256:3:0,256:128:2:1,64:64:1:3,32:64:1:1 --batch 2
+run clock_c2 200 python3 -u tools/clock_probe.py --shapes 256:256:3:1,128:64:1:1,64:64:1:3,256:128:2:1 --batch 1 --height 368 --width 640 --seconds 2
 SH=32:64:1:1,64:64:1:2,128:64:1:1,64:64:1:3,64:128:1:4,64:128:2:1,128:128:2:2,256:128:2:1,128:128:2:3,128:256:2:4
 SH=$SH,128:256:3:1,256:256:3:1,256:256:3:2,512:256:3:0,256:256:3:3,256:512:3:4,256:512:4:1,512:512:4:1,512:1024:4:4
 run c2_kinds 400 python3 -u tools/conv_lab.py cfgab --cfgs 20,21,23,20s2,21s2,21s4 --height 368 --width 640 --batch 1 --shapes $SH --rounds 7 --reps 10
@@ -26,4 +28,5 @@ done
 for f in $O/c2_default_* $O/c2_k3_*; do python3 -c "
 import json,sys; l=[x for x in open('$f') if x.startswith('{')][-1]; d=json.loads(l); r=d['roofline']
 print('$(basename $f)', d['value'], d['ms_per_step'], r['frac'], r['conv_busy_ms_per_step'], d['unprofiled']['value'])"; done
+run bench_default 300 python bench.py --steps 20 --warmup 5
 exit 0
