@@ -134,7 +134,7 @@ def parse():
                          "0 = auto: kind 6 where cout %% 64 == 0, else 3; default engine.WINO_KIND)")
     ap.add_argument("--wino-split", default=None,
                     help="A/B: split-K slices per grid level for every Winograd conv, e.g. '2:2,3:4,4:8' "
-                         "(engine.WINO_SPLIT_LEVELS); 'none' disables the tuned splits")
+                         "(engine.WINO_SPLIT_LEVELS, replaces the geometry rule); 'none' disables split-K (engine.GEOM_SPLIT)")
     ap.add_argument("--no-ring-fold", action="store_true",
                     help="A/B: run the sub-pixel ring fix-up as its own launch (engine.RING_FOLD = False)")
     ap.add_argument("--no-wino-th4", action="store_true",
@@ -360,7 +360,7 @@ def main():
     if args.wino_kind is not None:
         engine_mod.WINO_KIND = args.wino_kind
     if args.wino_split == "none":
-        engine_mod.WINO_SPLIT = {}
+        engine_mod.GEOM_SPLIT = False
     elif args.wino_split:
         engine_mod.WINO_SPLIT_LEVELS.update({int(k): int(v) for k, v in
                                              (kv.split(":") for kv in args.wino_split.split(","))})

@@ -42,6 +42,12 @@
 #ifndef RRIN_WINOC_CLOCK
 #define RRIN_WINOC_CLOCK 0
 #endif
+// Ablation builds only (tools/build_wino_variant.sh, outputs wrong by design): 1 no U
+// loads after the prologue, 2 no raw DMA after the prologue, 4 no transform VALU,
+// 8 no epilogue stores, 16 no window reads after the prologue
+#ifndef RRIN_WINOC_ABL
+#define RRIN_WINOC_ABL 0
+#endif
 
 namespace rrin {
 
@@ -184,6 +190,10 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winoc_kernel(ConvH8Args a) {
     }
   };
   auto transform = [&](int nt) {
+    if constexpr ((RRIN_WINOC_ABL & 4) != 0) {
+      v[nt][0] = d[0], v[nt][1] = d[2], v[nt][2] = d[4], v[nt][3] = d[6];
+      return;
+    }
     cfloatx4 tr[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k)
@@ -227,25 +237,25 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winoc_kernel(ConvH8Args a) {
     for (int x = 0; x < 3; ++x) {
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) mfma_point(x, nt);
-      if (more) reload_u(c + 1, x);
+      if (more && !(RRIN_WINOC_ABL & 1)) reload_u(c + 1, x);
       fence();
     }
     if (more) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * CT) : "memory");
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((RRIN_WINOC_ABL & 1) ? 0 : 4 * CT) : "memory");
       bar();
-      issue_raw_at(raw_next, s == 0 ? 2 : s - 1);
+      if (!(RRIN_WINOC_ABL & 2)) issue_raw_at(raw_next, s == 0 ? 2 : s - 1);
       if (c + 3 < nch) raw_next += chunk_stride;
     }
     const int s1 = s == 2 ? 0 : s + 1;
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
-      if (more) read_raw(s1, nt);
+      if (more && !(RRIN_WINOC_ABL & 16)) read_raw(s1, nt);
       fence();
       mfma_point(3, nt);
       fence();
       if (more) transform(nt);
     }
-    if (more) reload_u(c + 1, 3);
+    if (more && !(RRIN_WINOC_ABL & 1)) reload_u(c + 1, 3);
   };
 
   // prologue in the steady state's VMEM order: raw(0), U(0) pts 0-2, raw(1), U(0) pt 3;
@@ -292,6 +302,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winoc_kernel(ConvH8Args a) {
   const int r = yw & 1, cc = yw >> 1;
   uint4* dst = a.dst_hi + (int64_t)img * a.dst_img;
   auto store4 = [&](int64_t rec, const float* vv) {
+    if constexpr ((RRIN_WINOC_ABL & 8) != 0) return;
     dst[rec] = make_uint4(__float_as_uint(vv[0]), __float_as_uint(vv[1]), __float_as_uint(vv[2]), __float_as_uint(vv[3]));
   };
 #pragma unroll

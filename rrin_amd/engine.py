@@ -201,20 +201,37 @@ WINO_TH4 = {"small": {(256, 512, 4), (512, 512, 4), (256, 512, 3)},
             "medium": {(256, 512, 4), (512, 512, 4), (512, 1024, 4)}}
 
 
-# Split-K of the Winograd convs (rrin_conv_h8_desc.ksplit; kinds 3, 4) per size
-# class, grid level -> slices: the few-tile deep convs of small forward parts, where a
-# tile per workgroup leaves most CUs idle.  A split conv sums its K slices in slice
-# order, a different rounding from the unsplit conv.  640x368 x 1
-# (profiles/r03/split_ab.txt): none 272.7 pairs/s, L4 / 4 277.6, L3 / 2 + L4 / 4 279.1,
-# L2 / 2 + L3 / 4 + L4 / 8 274.6 -- within the box-to-box spread; 1280x720 x 1 loses.
-# Off by default since round 4: the size class follows n*h*w, so a split class would
-# make a pair's bits depend on its batch size, stream split or shard (DESIGN §6/§7
-# promise batch == per-sample and sharded == unsharded bitwise at every n).  Every
-# class now rounds identically (tests/test_gpu_net.py::test_batch_size_bitwise_640x368);
-# the machinery stays for A/B (WINO_SPLIT_LEVELS, bench.py --wino-split).
-WINO_SPLIT = {}
-# A/B override: grid level -> slices for every Winograd conv at that level, all classes
+# Split-K of the Winograd convs (rrin_conv_h8_desc.ksplit; kinds 3, 4): the few-tile
+# deep convs of small images, where a tile per workgroup leaves most CUs idle.  A split
+# conv sums its K slices in slice order, a different rounding from the unsplit conv, so
+# the split is chosen from the per-image geometry only (the conv's grid h_l x w_l, its
+# input channels and output rows), never from the batch: a pair's bits do not depend on
+# its batch size, stream split or shard (tests/test_gpu_net.py::
+# test_batch_size_bitwise_640x368).  Rule (geom_split): K >= 256 channels,
+# slices of >= 8 chunks, and the kind-4 tiles of one image x slices <= GEOM_SPLIT_WGS.
+# 640x368 x 1 per conv (profiles/r04/c2_kinds.log, kind 4 + split vs the kind-6 tile):
+# 512->512 L4 0.0423 vs 0.0711 ms, 512->1024 sub-pixel 0.0356 vs 0.0719, 256->512 L4
+# 0.0263 vs 0.0391, 512->256 L3 0.0687 vs 0.0717; 720p and larger images never split
+# (their kind-4 tiles per image exceed the bound).  Round 3's split by size class
+# (n*h*w) made bits depend on the batch and is gone.
+GEOM_SPLIT = True
+GEOM_SPLIT_WGS = 800
+# A/B override: grid level -> slices for every Winograd conv at that level (bench.py
+# --wino-split); replaces the geometry rule
 WINO_SPLIT_LEVELS = {}
+
+
+def geom_split(cin: int, rows: int, hl: int, wl: int) -> int:
+    """Split-K slices (1 = none) of an exact-fp32 Winograd conv of cin input channels and
+    `rows` output rows (4 x cout for a sub-pixel up conv) on an hl x wl grid, one image."""
+    nch = (cin + 7) // 8
+    if not GEOM_SPLIT or nch < 32:
+        return 1
+    t4 = -(-hl // 4) * -(-wl // 32) * -(-rows // 32)  # kind-4 tiles (BM 32 x 32 px x TH 4)
+    for s in (4, 2):
+        if t4 * s <= GEOM_SPLIT_WGS and nch // s >= 8:
+            return s
+    return 1
 
 
 # Sub-pixel ring fold (rrin_conv_weights.subpixel = 2): the ring fix-up of an
@@ -227,13 +244,14 @@ WINO_SPLIT_LEVELS = {}
 RING_FOLD = False
 
 
-def choose_split(cin: int, cout: int, level: int, size: str, cfg: int) -> int:
-    """Slices of the split-K for this conv (0: none)."""
+def choose_split(level: int, cfg: int, geom: int) -> int:
+    """Slices of the split-K for a conv of tile config cfg at grid level `level` whose
+    geometry rule gave `geom` (0: none)."""
     if _lib.lib().rrin_conv_h8_cfg_wino(cfg) not in (3, 4):
         return 0
-    if level in WINO_SPLIT_LEVELS:
-        return WINO_SPLIT_LEVELS[level]
-    return WINO_SPLIT.get(size, {}).get(level, 0)
+    if WINO_SPLIT_LEVELS:
+        return WINO_SPLIT_LEVELS.get(level, 0)
+    return geom if geom > 1 else 0
 
 
 def wino_cfg(kind: int = None) -> int:
@@ -242,17 +260,19 @@ def wino_cfg(kind: int = None) -> int:
     return next(c for c in range(lib.rrin_conv_h8_cfg_count()) if lib.rrin_conv_h8_cfg_wino(c) == kind)
 
 
-def choose_cfg_h8(cin: int, cout: int, prec: int, level: int = 0, size: str = "large") -> int:
+def choose_cfg_h8(cin: int, cout: int, prec: int, level: int = 0, size: str = "large", split: int = 1) -> int:
     """Tile config of the record-layout conv (conv_f16.hip table) for a conv
     running on the grid of U-Net level ``level`` (a sub-pixel up conv runs on the
     low-res grid with 4x the output rows) in a forward part of size class
-    ``size``: exact fp32 takes the Winograd config (WINO_SIZES); otherwise the
-    swept choice (H8_TUNED_BY_SIZE, H8_TUNED), else a level rule from the same
-    sweep."""
+    ``size``: exact fp32 takes the Winograd config (WINO_SIZES; kind 4 where the
+    geometry splits K, ``split`` > 1); otherwise the swept choice (H8_TUNED_BY_SIZE,
+    H8_TUNED), else a level rule from the same sweep."""
     if prec == _lib.PREC_F32R and WINO and size in WINO_SIZES:
         c = WINO_DIRECT.get((cin, cout, level))
         if c is not None and _lib.lib().rrin_conv_h8_cfg_fits(c, prec, cin):
             return c
+        if split > 1:
+            return wino_cfg(4)
         return wino_cfg(4 if (cin, cout, level) in WINO_TH4.get(size, ()) else wino_kind_for(cout))
     table = H8_TUNED_BY_SIZE.get(size, {}).get(prec) or H8_TUNED.get(prec, {})
     cfg = table.get((cin, cout, level))
@@ -410,7 +430,7 @@ class RRINEngine:
             self.head_table[i].bias = b.data_ptr()
         self._packs = {}          # size class -> packing
         self._packs_by_cfgs = {}  # tuple of per-conv configs -> packing (shared between classes)
-        _, _, self.conv_table, self.cfgs = self._pack_h8("large")
+        _, _, self.conv_table, self.cfgs = self._pack_h8("large", None, None)
         self._scratch = {}
         self._ws = OrderedDict()
         self._flow_valid = {}
@@ -418,19 +438,31 @@ class RRINEngine:
         self._status = {}           # slot -> device int32 range flag (fp16-stored precisions)
         self._pending_status = []   # (event, pinned host copy) of flags not checked yet
 
-    def _pack_h8(self, size: str):
-        """(halves blob, bias blob, ConvWeights table, cfgs) of size class ``size``, cached;
-        classes whose tile configs agree share one packing."""
-        p = self._packs.get(size)
+    def _geom_splits(self, h, w):
+        """Per body conv: the geometry rule's split-K slices at image size h x w (exact fp32
+        Winograd; a tuple of 1s elsewhere or without a size)."""
+        if h is None or self.prec != _lib.PREC_F32R or not WINO:
+            return (1,) * len(self._h8_convs)
+        return tuple(geom_split(cin, cout, h >> level, w >> level)
+                     for (_, _, cin, cout, level, _, _) in self._h8_convs)
+
+    def _pack_h8(self, size: str, h: int = None, w: int = None):
+        """(halves blob, bias blob, ConvWeights table, cfgs) of size class ``size`` at image
+        size h x w (the split-K geometry; None: no split), cached; classes / geometries
+        whose tile configs agree share one packing."""
+        geo = self._geom_splits(h, w)
+        key = (size, geo)
+        p = self._packs.get(key)
         if p is not None:
             return p
         L = self.lib
-        cfgs = [choose_cfg_h8(cin, cout, self.prec, level, size) for (_, _, cin, cout, level, _, _) in self._h8_convs]
-        key = tuple(cfgs)
-        p = self._packs_by_cfgs.get(key)
+        cfgs = [choose_cfg_h8(cin, cout, self.prec, level, size, g)
+                for (_, _, cin, cout, level, _, _), g in zip(self._h8_convs, geo)]
+        ckey = tuple(cfgs)
+        p = self._packs_by_cfgs.get(ckey)
         if p is not None:
-            self._packs[size] = self._with_splits(p, size)
-            return self._packs[size]
+            self._packs[key] = self._with_splits(p, geo)
+            return self._packs[key]
         halves, biases, meta = [], [], []
         hoff = boff = 0
         f32 = self.prec == _lib.PREC_F32R
@@ -493,18 +525,18 @@ class RRINEngine:
                 e.wedge = edge[0].data_ptr()
                 e.bias_raw = edge[1].data_ptr()
         p = (blob, bias_blob, table, cfgs)
-        self._packs_by_cfgs[key] = p
-        self._packs[size] = self._with_splits(p, size)
-        return self._packs[size]
+        self._packs_by_cfgs[ckey] = p
+        self._packs[key] = self._with_splits(p, geo)
+        return self._packs[key]
 
-    def _with_splits(self, p, size: str):
-        """The packing p of class ``size`` with that class's split-K slices set in a copy
-        of its ConvWeights table (the weight blobs stay shared)."""
+    def _with_splits(self, p, geo):
+        """The packing p with the split-K slices of geometry ``geo`` (per conv) set in a
+        copy of its ConvWeights table (the weight blobs stay shared)."""
         if self.prec != _lib.PREC_F32R:
             return p
         blob, bias_blob, table, cfgs = p
-        ks = [choose_split(cin, cout, level, size, cfg)
-              for (_, _, cin, cout, level, _, _), cfg in zip(self._h8_convs, cfgs)]
+        ks = [choose_split(level, cfg, g)
+              for (_, _, cin, cout, level, _, _), cfg, g in zip(self._h8_convs, cfgs, geo)]
         if not any(ks):
             self._set_fold(table, cfgs)
             return p
@@ -536,7 +568,7 @@ class RRINEngine:
     def conv_table_for(self, n: int, h: int, w: int):
         """ConvWeights table of a forward part of n pairs at h x w (its tile-table size class)."""
         if self.force_size_class is not None and self.prec != _lib.PREC_F32:
-            return self._pack_h8(self.force_size_class)[2]
+            return self._pack_h8(self.force_size_class, h, w)[2]
         if self.prec == _lib.PREC_F32:
             if size_class(n * h * w) != "small":
                 return self.conv_table
@@ -554,7 +586,7 @@ class RRINEngine:
                         t[i].cfg = 4
                 self._table32_small = t
             return self._table32_small
-        return self._pack_h8(size_class(n * h * w))[2]
+        return self._pack_h8(size_class(n * h * w), h, w)[2]
 
     def workspace(self, n: int, h: int, w: int, slot: int = 0) -> torch.Tensor:
         key = (n, h, w, slot)

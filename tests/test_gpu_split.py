@@ -73,28 +73,35 @@ def test_split_subpixel(gpu, n, cin, cout, sh, sw):
 
 
 def test_split_net(gpu):
-    """Levels 2-4 split in every class: Net output within fp32 rounding of the unsplit Net;
+    """Split-K in the Net: the geometry rule (engine.geom_split, the default: 128x192
+    images split their level-3/4 convs) and levels 2-4 split by the A/B override with
+    every conv on a split-capable tile; each within fp32 rounding of the unsplit Net,
     batch == per-sample bitwise with the split."""
     net = make_net(gpu, stress=True)
-    saved, saved_cls = dict(engine_mod.WINO_SPLIT_LEVELS), dict(engine_mod.WINO_SPLIT)
+    saved = dict(engine_mod.WINO_SPLIT_LEVELS)
+    saved_geo, saved_kind = engine_mod.GEOM_SPLIT, engine_mod.WINO_KIND
     try:
         i0, i1 = synthetic_batch(2, 128, 192)
         i0, i1 = i0.to(gpu), i1.to(gpu)
         engine_mod.WINO_SPLIT_LEVELS.clear()
-        engine_mod.WINO_SPLIT.clear()
+        engine_mod.GEOM_SPLIT = False
         with torch.no_grad():
             net._engine = None
             base = net.engine().forward(i0, i1, 0.5).cpu()
-        engine_mod.WINO_SPLIT_LEVELS.update({2: 2, 3: 4, 4: 8})
-        net._engine = None
-        eng = net.engine()
-        with torch.no_grad():
-            both = eng.forward(i0, i1, 0.5).cpu()
-            one = eng.forward(i0[1:], i1[1:], 0.5).cpu()
-        torch.testing.assert_close(both, base, rtol=0, atol=2e-5)
-        assert torch.equal(both[1:], one)
+        for geo, levels, kind in ((True, {}, saved_kind), (False, {2: 2, 3: 4, 4: 8}, 3)):
+            engine_mod.GEOM_SPLIT, engine_mod.WINO_KIND = geo, kind
+            engine_mod.WINO_SPLIT_LEVELS.clear()
+            engine_mod.WINO_SPLIT_LEVELS.update(levels)
+            net._engine = None
+            eng = net.engine()
+            assert any(t.ksplit > 1 for t in eng.conv_table_for(2, 128, 192))
+            with torch.no_grad():
+                both = eng.forward(i0, i1, 0.5).cpu()
+                one = eng.forward(i0[1:], i1[1:], 0.5).cpu()
+            torch.testing.assert_close(both, base, rtol=0, atol=2e-5)
+            assert torch.equal(both[1:], one)
     finally:
         engine_mod.WINO_SPLIT_LEVELS.clear()
         engine_mod.WINO_SPLIT_LEVELS.update(saved)
-        engine_mod.WINO_SPLIT.update(saved_cls)
+        engine_mod.GEOM_SPLIT, engine_mod.WINO_KIND = saved_geo, saved_kind
         net._engine = None
