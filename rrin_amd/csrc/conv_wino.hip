@@ -1171,6 +1171,11 @@ __global__ __launch_bounds__(256 * PT, 2) void conv3x3_winoq_kernel(ConvH8Args a
     }
   }
   }
+  // the epilogue's bias values, loaded now: their latency hides behind the exchange
+  // instead of stalling the stores (the bias blob is padded to whole 32-row blocks)
+  float bsv[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) bsv[i] = a.bias[cob * 32 + 8 * (i >> 2) + 4 * hh + (i & 3)];
   __syncthreads();  // every read done before the exchange reuses the LDS
 #if RRIN_WINOQ_AGPR
   asm volatile("" ::"a"(acc[0][0]));  // A/B: MFMA accumulators in AGPRs
@@ -1297,7 +1302,7 @@ __global__ __launch_bounds__(256 * PT, 2) void conv3x3_winoq_kernel(ConvH8Args a
         } else {
           float vv[4];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) vv[e] = yv[4 * qq + e] + a.bias[cob * 32 + 8 * qq + 4 * hh + e];
+          for (int e = 0; e < 4; ++e) vv[e] = yv[4 * qq + e] + bsv[4 * qq + e];
           store4((int64_t)(2 * cob + hh) * a.dst_gp + (int64_t)(Y + 1) * a.dst_wp + XX + kH8PadLeft, vv);
         }
       }
@@ -1325,7 +1330,7 @@ __global__ __launch_bounds__(256 * PT, 2) void conv3x3_winoq_kernel(ConvH8Args a
     float vv[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      float tv = yv[i] + a.bias[cob * 32 + 8 * (i >> 2) + 4 * hh + (i & 3)];
+      float tv = yv[i] + bsv[i];
       if constexpr (EPI != RRIN_EPI_LINEAR) tv = leaky(tv, a.slope);
       vv[i] = tv;
     }

@@ -288,6 +288,13 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winoc_kernel(ConvH8Args a) {
 #if RRIN_WINOC_CLOCK
   const unsigned long long clk_t1 = __builtin_amdgcn_s_memtime();
 #endif
+  // the epilogue's bias values, loaded now: their latency hides behind the exchange
+  // instead of stalling the stores (the bias blob is padded to whole BM-row blocks)
+  float bsv[CT][16];
+#pragma unroll
+  for (int t = 0; t < CT; ++t)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) bsv[t][i] = a.bias[(CT * cob + t) * 32 + 8 * (i >> 2) + 4 * hh + (i & 3)];
 #if RRIN_WINOC_AGPR
   // A/B: an inline-asm AGPR operand makes the compiler keep MFMA accumulators in AGPRs
   asm volatile("" ::"a"(acc[0][0][0][0]));
@@ -354,7 +361,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winoc_kernel(ConvH8Args a) {
             } else {
               float vv[4];
 #pragma unroll
-              for (int e = 0; e < 4; ++e) vv[e] = yv[nt][4 * qq + e] + a.bias[cobe * 32 + 8 * qq + 4 * hh + e];
+              for (int e = 0; e < 4; ++e) vv[e] = yv[nt][4 * qq + e] + bsv[t][4 * qq + e];
               store4((int64_t)(2 * cobe + hh) * a.dst_gp + (int64_t)(Y + 1) * a.dst_wp + XX + kH8PadLeft, vv);
             }
           }
@@ -363,7 +370,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winoc_kernel(ConvH8Args a) {
         float vv[16];
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          float tv = yv[nt][i] + a.bias[cobe * 32 + 8 * (i >> 2) + 4 * hh + (i & 3)];
+          float tv = yv[nt][i] + bsv[t][i];
           if constexpr (EPI != RRIN_EPI_LINEAR) tv = leaky(tv, a.slope);
           vv[i] = tv;
         }
