@@ -206,6 +206,10 @@ struct ConvH8Args {
   const float* bias_raw;  // [cout/4]
   float* corr;            // [n][co_blocks][nseg][512]
   int* rcnt;              // [n][co_blocks][nseg], zero between launches
+  // register-U Winograd tiles (conv_winoc.hip): workgroup order in groups of cob_group
+  // co blocks (0: one group of all co blocks), tile positions within a group, the
+  // group's co blocks fastest -- see launch_winoc
+  int cob_group;
 };
 
 // Ring index of pixel (y, x) of an H x W image (rrin_ring_pixels order: top

@@ -112,10 +112,15 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winoc_kernel(ConvH8Args a) {
 #endif
   const int nch = a.nchunks;
   int cob, x0, y0, img;
-  {  // the co blocks of a tile position on consecutive workgroups (they share its raw tile)
-    int t = bid;
-    cob = t % a.co_blocks;
-    t /= a.co_blocks;
+  {  // groups of cob_group co blocks, tile positions within a group, the group's co blocks
+     // of a tile position on consecutive workgroups (they share its raw tile)
+    const int cpg = a.cob_group > 0 ? a.cob_group : a.co_blocks;
+    const int gsz = cpg * (ntiles / a.co_blocks);  // workgroups of a full group
+    const int g = bid / gsz;
+    const int r = bid - g * gsz;
+    const int cg = min(cpg, a.co_blocks - g * cpg);  // co blocks of this group (the last may be short)
+    cob = g * cpg + r % cg;
+    int t = r / cg;
     x0 = (t % a.tiles_x) * 32;
     t /= a.tiles_x;
     y0 = (t % a.tiles_y) * TH;
@@ -459,8 +464,28 @@ static int launch_winoc_e(const ConvH8Args& a, int epi, hipStream_t st) {
   return RRIN_E_ARG;
 }
 
+// Workgroup order (XCD-aware remap: an XCD runs a contiguous range of workgroups): a
+// workgroup streams its co block's whole U (nchunks x 32 BM records); when the co blocks'
+// U does not fit an XCD's 4 MB L2, co blocks of one tile position that started at
+// different times each stream U from HBM (PMC: up to 11x the algorithmic bytes on the
+// deep convs).  Groups of co blocks whose U fits kWinoCUGroupBytes put each XCD on one
+// group (its U read once per XCD, L2-resident) at the price of reading each raw tile
+// once per group.  The order does not change any result.
+#ifndef RRIN_WINOC_UGROUP_KB
+#define RRIN_WINOC_UGROUP_KB 2048
+#endif
+static int winoc_cob_group(const ConvH8Args& a, int bm) {
+  const int64_t per_cob = (int64_t)a.nchunks * 32 * bm * 16;  // U bytes of one co block
+  if (RRIN_WINOC_UGROUP_KB <= 0 || (int64_t)a.co_blocks * per_cob <= (int64_t)RRIN_WINOC_UGROUP_KB * 1024) return 0;
+  int g = 1;  // the largest power of two of co blocks whose U fits (at least one)
+  while (2 * g < a.co_blocks && 2 * g * per_cob <= (int64_t)RRIN_WINOC_UGROUP_KB * 1024) g *= 2;
+  return g;
+}
+
 int launch_winoc(const ConvH8Args& a, int epi, int ct, hipStream_t st) {
-  return ct == 2 ? launch_winoc_e<2, 1>(a, epi, st) : launch_winoc_e<1, 2>(a, epi, st);
+  ConvH8Args b = a;
+  b.cob_group = winoc_cob_group(a, 32 * ct);
+  return ct == 2 ? launch_winoc_e<2, 1>(b, epi, st) : launch_winoc_e<1, 2>(b, epi, st);
 }
 
 }  // namespace rrin
