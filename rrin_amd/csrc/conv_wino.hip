@@ -757,6 +757,11 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wino64_kernel(ConvH8Args a) {
 // others wait on LDS, barriers or their transform, instead of a deeper
 // per-wave pipeline.  The output transform meets through LDS as in cfg 19.
 // ============================================================================
+// RRIN_WINOQ_RU (A/B): the U operands straight from L2 into registers (buffer loads a
+// chunk ahead, as conv_winoc.hip) instead of LDS-DMA + LDS reads (2-stage loop only)
+#ifndef RRIN_WINOQ_RU
+#define RRIN_WINOQ_RU 0
+#endif
 #ifndef RRIN_WINOQ_STAGES
 #define RRIN_WINOQ_STAGES 2
 #endif
@@ -967,6 +972,7 @@ __global__ __launch_bounds__(256 * PT, 2) void conv3x3_winoq_kernel(ConvH8Args a
   static_assert(RAW > NT && RAW <= 2 * NT && kWnU % NT == 0, "two raw pieces, whole U pieces");
   constexpr int NS = PT == 2 ? kWqStages : 2;  // the 3-stage A/B ring is built for the 8-wave tile
   constexpr int UP = kWnU / NT;  // U pieces per thread
+  constexpr bool RU = RRIN_WINOQ_RU != 0 && NS == 2;
   extern __shared__ __attribute__((aligned(16))) uint4 smem4[];
   // kWqStages stages of [raw RAW | U 1024] records
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -1050,10 +1056,20 @@ __global__ __launch_bounds__(256 * PT, 2) void conv3x3_winoq_kernel(ConvH8Args a
         dma16(tsrc + off, base + NT * it + (tid & ~63));
       }
     }
+    if constexpr (!RU) {
 #pragma unroll
-    for (int it = 0; it < UP; ++it)
-      if (!((ABL & 1) && c > 0)) dma16(wsrc + (int64_t)c * kWnU + NT * it, base + RAW + NT * it + (tid & ~63));
+      for (int it = 0; it < UP; ++it)
+        if (!((ABL & 1) && c > 0)) dma16(wsrc + (int64_t)c * kWnU + NT * it, base + RAW + NT * it + (tid & ~63));
+    }
   };
+  // RU: U record (xi = 4 yw + x, hh, co = j) of chunk c straight into registers
+  const auto urs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(a.w_hi + ((int64_t)cob * a.nchunks + c0) * kWnU),
+                                                     0, 0x7fffffff, 0x00020000);
+  auto load_u = [&](int c, int x) {
+    const unsigned voff = (unsigned)(((4 * yw + x) * 64 + hh * 32 + j) * 16);
+    return __builtin_bit_cast(wfloatx4, __builtin_amdgcn_raw_buffer_load_b128(urs, voff, c * kWnU * 16, 0));
+  };
+  wfloatx4 ur[4];  // RU: U of the chunk being computed (point x reloaded after its MFMAs)
   const int pr = 2 * pt + (j >> 4), jx = (j + 12 * (j >> 4)) & 15;
   const int ra = yw == 0 ? 0 : (yw == 2 ? 2 : 1);
   const int rb = yw == 0 ? 2 : (yw == 1 ? 2 : (yw == 2 ? 1 : 3));
@@ -1069,7 +1085,7 @@ __global__ __launch_bounds__(256 * PT, 2) void conv3x3_winoq_kernel(ConvH8Args a
   wfloatx4 dk[8], uk[4];  // ABL 16 / 32: chunk 0's reads kept
   // one chunk in buffer b: window reads -> B^T row -> 4 points, then per point
   // its U record and 4 MFMAs (point-major, the cfg 18 accumulation order)
-  auto chunk = [&](int b, bool first) {
+  auto chunk = [&](int b, bool first, int c) {
     const uint4* rw = smem4 + b * STAGE + rw0;
     wfloatx4 t[4];
 #pragma unroll
@@ -1108,7 +1124,9 @@ __global__ __launch_bounds__(256 * PT, 2) void conv3x3_winoq_kernel(ConvH8Args a
 #pragma unroll
     for (int x = 0; x < 4; ++x) {
       wfloatx4 u;
-      if (!(ABL & 32) || first) {
+      if constexpr (RU) {
+        u = ur[x];
+      } else if (!(ABL & 32) || first) {
         u = __builtin_bit_cast(wfloatx4, su[x * 64]);
         if constexpr ((ABL & 32) != 0) uk[x] = u;
       } else {
@@ -1119,9 +1137,12 @@ __global__ __launch_bounds__(256 * PT, 2) void conv3x3_winoq_kernel(ConvH8Args a
         if constexpr ((ABL & 4) != 0) {
           asm volatile("" ::"v"(u[e]), "v"(v[x][e]));
         } else {
-          const wfloatx16 c = (first && e == 0) ? wfloatx16{} : acc[x];
-          acc[x] = __builtin_amdgcn_mfma_f32_32x32x2f32(u[e], v[x][e], c, 0, 0, 0);
+          const wfloatx16 cin_acc = (first && e == 0) ? wfloatx16{} : acc[x];
+          acc[x] = __builtin_amdgcn_mfma_f32_32x32x2f32(u[e], v[x][e], cin_acc, 0, 0, 0);
         }
+      }
+      if constexpr (RU) {
+        if (c + 1 < nch) ur[x] = load_u(c + 1, x);
       }
     }
 #if RRIN_WINOQ_PRIO == 1
@@ -1155,6 +1176,10 @@ __global__ __launch_bounds__(256 * PT, 2) void conv3x3_winoq_kernel(ConvH8Args a
   }
   {
   issue(0, 0);
+  if constexpr (RU) {
+#pragma unroll
+    for (int x = 0; x < 4; ++x) ur[x] = load_u(0, x);
+  }
   if (NS == 3 && nch > 1) issue(1, 1);
   for (int c = 0; c < nch; ++c) {
     if constexpr (NS == 3) {
@@ -1162,12 +1187,12 @@ __global__ __launch_bounds__(256 * PT, 2) void conv3x3_winoq_kernel(ConvH8Args a
       // bare barrier: __syncthreads() would drain vmcnt to 0 and wait for chunk c + 1 too
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       if (c + 2 < nch) issue(c + 2, (c + 2) % 3);
-      chunk(c % 3, c == 0);
+      chunk(c % 3, c == 0, c);
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();  // chunk c landed everywhere; stage (c + 1) & 1 was last read in chunk c - 1
       if (c + 1 < nch) issue(c + 1, (c + 1) & 1);
-      chunk(c & 1, c == 0);
+      chunk(c & 1, c == 0, c);
     }
   }
   }

@@ -2,7 +2,8 @@
 # Round 4 session j: register-U workgroup order in co-block groups whose U fits L2
 # (launch_winoc: RRIN_WINOC_UGROUP_KB 2048 = product; ab/..._nogrp.so: one group;
 # ab/..._grp4m.so: 4 MB groups) -- Winograd sweeps, per-conv A/B, whole-forward A/B
-# (library swapped in place on the box), PMC traffic of the product order.
+# (library swapped in place on the box), PMC traffic of the product order; the kind-3
+# tile with register U (ab/librrin_hip_qru.so, RRIN_WINOQ_RU=1).
 set -u
 O=${O:-gpurun_out/r04j}; mkdir -p $O; export TMPDIR=/tmp
 run() {  # name limit cmd...
@@ -17,11 +18,14 @@ run() {  # name limit cmd...
 run tests 600 python3 -u -m pytest tests/test_gpu_h8.py tests/test_gpu_split.py -x -q --timeout 300 --timeout-method thread -k "wino or split"
 SH=256:512:2:4:23,512:512:4:1:23,256:512:4:1:23,512:256:3:0:23,256:256:3:1:23,128:256:3:1:23,256:128:2:1:23,128:128:2:2:23
 run ab_order 400 python3 -u tools/conv_lab.py abconv --lib-b ab/librrin_hip_nogrp.so,ab/librrin_hip_grp4m.so --batch 2 --shapes $SH
+S3=64:32:0:1:20,32:32:0:1:20,32:32:0:2:20,16:32:0:1:20,256:256:3:1:20,512:512:4:1:21
+run ab_qru 300 python3 -u tools/conv_lab.py abconv --lib-b ab/librrin_hip_qru.so --batch 2 --shapes $S3
 cp rrin_amd/librrin_hip.so $O/prod.so.bak
 B="python bench.py --steps 20 --warmup 5 --cpu-baseline off --no-alt"
 for r in a b; do
   cp $O/prod.so.bak rrin_amd/librrin_hip.so && run bench_grp_$r 200 $B
   cp ab/librrin_hip_nogrp.so rrin_amd/librrin_hip.so && run bench_nogrp_$r 200 $B
+  cp ab/librrin_hip_qru.so rrin_amd/librrin_hip.so && run bench_qru_$r 200 $B
 done
 cp $O/prod.so.bak rrin_amd/librrin_hip.so && rm -f $O/prod.so.bak
 for f in $O/bench_*; do python3 -c "
