@@ -1046,8 +1046,12 @@ __global__ __launch_bounds__(256 * PT, 2) void conv3x3_winoq_kernel(ConvH8Args a
     p_off[it] = (int64_t)g * a.src_gp + r * a.src_wp + col;
     p_zero[it] = col - y0 * a.src_wp;
   }
-  auto issue = [&](int c, int b) {
-    uint4* base = smem4 + b * STAGE;
+  // LDS: NS == 2: stages [raw | U] x 2; NS == 3 (A/B): a raw ring of 3 stages (chunk c + 2
+  // staged while c computes) and a U ring of 2 (U is L2-resident: one chunk ahead)
+  auto raw_stage = [&](int c) { return NS == 3 ? smem4 + (c % 3) * RAW : smem4 + (c & 1) * STAGE; };
+  auto u_stage = [&](int c) { return NS == 3 ? smem4 + 3 * RAW + (c & 1) * kWnU : smem4 + (c & 1) * STAGE + RAW; };
+  auto issue_raw = [&](int c) {
+    uint4* base = raw_stage(c);
 #pragma unroll
     for (int it = 0; it < 2; ++it) {
       if ((it == 0 || tid < RAW - NT) && !((ABL & 2) && c > 0)) {
@@ -1056,11 +1060,18 @@ __global__ __launch_bounds__(256 * PT, 2) void conv3x3_winoq_kernel(ConvH8Args a
         dma16(tsrc + off, base + NT * it + (tid & ~63));
       }
     }
+  };
+  auto issue_u = [&](int c) {
     if constexpr (!RU) {
+      uint4* base = u_stage(c);
 #pragma unroll
       for (int it = 0; it < UP; ++it)
-        if (!((ABL & 1) && c > 0)) dma16(wsrc + (int64_t)c * kWnU + NT * it, base + RAW + NT * it + (tid & ~63));
+        if (!((ABL & 1) && c > 0)) dma16(wsrc + (int64_t)c * kWnU + NT * it, base + NT * it + (tid & ~63));
     }
+  };
+  auto issue = [&](int c) {
+    issue_raw(c);
+    issue_u(c);
   };
   // RU: U record (xi = 4 yw + x, hh, co = j) of chunk c straight into registers
   const auto urs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(a.w_hi + ((int64_t)cob * a.nchunks + c0) * kWnU),
@@ -1085,8 +1096,8 @@ __global__ __launch_bounds__(256 * PT, 2) void conv3x3_winoq_kernel(ConvH8Args a
   wfloatx4 dk[8], uk[4];  // ABL 16 / 32: chunk 0's reads kept
   // one chunk in buffer b: window reads -> B^T row -> 4 points, then per point
   // its U record and 4 MFMAs (point-major, the cfg 18 accumulation order)
-  auto chunk = [&](int b, bool first, int c) {
-    const uint4* rw = smem4 + b * STAGE + rw0;
+  auto chunk = [&](bool first, int c) {
+    const uint4* rw = raw_stage(c) + rw0;
     wfloatx4 t[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -1117,7 +1128,7 @@ __global__ __launch_bounds__(256 * PT, 2) void conv3x3_winoq_kernel(ConvH8Args a
       v[2] = t[2] - t[1];
       v[3] = t[1] - t[3];
     }
-    const uint4* su = smem4 + b * STAGE + RAW + su0;
+    const uint4* su = u_stage(c) + su0;
 #if RRIN_WINOQ_PRIO == 1
     __builtin_amdgcn_s_setprio(1);  // A/B: priority around the MFMA cluster (guide T5)
 #endif
@@ -1153,21 +1164,21 @@ __global__ __launch_bounds__(256 * PT, 2) void conv3x3_winoq_kernel(ConvH8Args a
   // A/B: static priority for the younger half of the workgroup (guide T5, static form)
   if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
 #endif
-  // kWqStages = 3 (A/B builds; 1-10 % slower than 2 stages on every shape,
-  // profiles/r03/ab_winoq_stages.txt): the DMA of chunk c + 2 is issued at the
-  // top of chunk c, so a chunk has two chunk-times to land.  At the top of chunk c a wave waits for
-  // its own pieces of chunk c (leaving chunk c + 1's in flight: 4 pieces for
-  // waves 0-2, which also stage the raw tile's 168-record tail, 3 for the rest),
-  // then the barrier makes every wave's pieces visible and ends every read of
-  // chunk c - 1, whose stage takes chunk c + 2.
+  // kWqStages = 3 (A/B builds): the raw tile of chunk c + 2 and the U slab of chunk c + 1
+  // are issued at the top of chunk c, U first; at the top of chunk c a wave waits until
+  // only its raw pieces of chunk c + 1 are in flight (2 for waves 0-2, which also stage
+  // the raw tile's 168-record tail, 1 for the rest), then the bare barrier makes every
+  // wave's pieces visible and ends every read of chunk c - 1, whose raw stage takes
+  // chunk c + 2 and whose U stage takes chunk c + 1.  (Round 3's 3-stage ring kept U in
+  // the same 3 stages: 82 KB per block.)
   const bool tail_wave = __builtin_amdgcn_readfirstlane(wv) < 3;
   auto wait_chunk = [&](bool next_in_flight) {
     if (!next_in_flight) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else if (tail_wave) {
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     } else {
-      asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
     }
   };
   if constexpr ((ABL & 4) != 0) {
@@ -1175,24 +1186,30 @@ __global__ __launch_bounds__(256 * PT, 2) void conv3x3_winoq_kernel(ConvH8Args a
     for (int x = 0; x < 4; ++x) acc[x] = wfloatx16{};
   }
   {
-  issue(0, 0);
+  if constexpr (NS == 3) {
+    issue_u(0);
+    issue_raw(0);
+    if (nch > 1) issue_raw(1);
+  } else {
+    issue(0);
+  }
   if constexpr (RU) {
 #pragma unroll
     for (int x = 0; x < 4; ++x) ur[x] = load_u(0, x);
   }
-  if (NS == 3 && nch > 1) issue(1, 1);
   for (int c = 0; c < nch; ++c) {
     if constexpr (NS == 3) {
       wait_chunk(c + 1 < nch);
       // bare barrier: __syncthreads() would drain vmcnt to 0 and wait for chunk c + 1 too
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      if (c + 2 < nch) issue(c + 2, (c + 2) % 3);
-      chunk(c % 3, c == 0, c);
+      if (c + 1 < nch) issue_u(c + 1);
+      if (c + 2 < nch) issue_raw(c + 2);
+      chunk(c == 0, c);
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();  // chunk c landed everywhere; stage (c + 1) & 1 was last read in chunk c - 1
-      if (c + 1 < nch) issue(c + 1, (c + 1) & 1);
-      chunk(c & 1, c == 0, c);
+      if (c + 1 < nch) issue(c + 1);
+      chunk(c == 0, c);
     }
   }
   }
@@ -1410,7 +1427,8 @@ template <int EPI, int ABL = 0, int PT = 2, int SK = 0, int RF = 0>
 static int launch_winoq_k(const ConvH8Args& a, hipStream_t st) {
   auto k = conv3x3_winoq_kernel<EPI, ABL, PT, SK, RF>;
   static LdsAttr attr;
-  constexpr size_t lds = (size_t)(PT == 2 ? kWqStages : 2) * (2 * (4 * PT + 2) * kWnRawCols + kWnU) * 16;
+  constexpr size_t raw = (size_t)2 * (4 * PT + 2) * kWnRawCols;
+  constexpr size_t lds = (PT == 2 && kWqStages == 3) ? (3 * raw + 2 * kWnU) * 16 : 2 * (raw + kWnU) * 16;
   if (int e = attr.ensure((const void*)k, (int)lds, st)) return e;
   const int64_t grid = (int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n * (SK ? a.ksplit : 1) + (RF ? a.nring : 0);
   hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256 * PT), lds, st, a);
