@@ -171,3 +171,24 @@ def test_autograd_stream_follows_tensor_device(monkeypatch):
     monkeypatch.setattr(torch.cuda, "current_stream", fake_current_stream)
     st = ag._stream(torch.device("cuda", 1))
     assert st.value == 1234 and seen == [torch.device("cuda", 1)]
+
+
+def test_geom_split_depends_on_image_geometry_only():
+    """Split-K slices (engine.geom_split) come from one image's geometry: the deep convs
+    of 640x368 images split, 720p and larger never do, and nothing in the rule sees the
+    batch size (the rounding of a pair must not depend on its batch / stream split)."""
+    from rrin_amd import engine
+    g = engine.geom_split
+    assert g(512, 512, 368 >> 4, 640 >> 4) == 4        # 23x40 level-4 grid
+    assert g(256, 512, 368 >> 4, 640 >> 4) == 4
+    assert g(256, 256, 368 >> 3, 640 >> 3) == 2        # 46x80: 288 kind-4 tiles
+    assert g(128, 256, 368 >> 3, 640 >> 3) == 1        # K = 128: never split
+    for cin, rows, lvl in ((512, 512, 4), (256, 256, 3), (512, 1024, 3)):
+        assert g(cin, rows, 720 >> lvl, 1280 >> lvl) == 1
+        assert g(cin, rows, 736 >> lvl, 1280 >> lvl) == 1
+    saved = engine.GEOM_SPLIT
+    try:
+        engine.GEOM_SPLIT = False
+        assert g(512, 512, 23, 40) == 1
+    finally:
+        engine.GEOM_SPLIT = saved
