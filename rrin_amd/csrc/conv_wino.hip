@@ -762,6 +762,12 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wino64_kernel(ConvH8Args a) {
 #ifndef RRIN_WINOQ_RU
 #define RRIN_WINOQ_RU 0
 #endif
+// Diagnostic build only (tools/clock_probe.py --kernel winoq): per-workgroup s_memtime
+// stamps after chunk 0 landed, at the end of the main loop and at the end, and the
+// s_memrealtime span and start
+#ifndef RRIN_WINOQ_CLOCK
+#define RRIN_WINOQ_CLOCK 0
+#endif
 #ifndef RRIN_WINOQ_STAGES
 #define RRIN_WINOQ_STAGES 2
 #endif
@@ -775,6 +781,10 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wino64_kernel(ConvH8Args a) {
 #define RRIN_WINOQ_PRIO 0  // A/B builds only: 1 s_setprio around each MFMA cluster, 2 static for waves 4-7
 #endif
 constexpr int kWqStages = RRIN_WINOQ_STAGES;
+#if RRIN_WINOQ_CLOCK
+constexpr int kQClkSlots = 1 << 16;
+__device__ unsigned long long g_winoq_clk[kQClkSlots * 6];
+#endif
 constexpr int kWqStage = kWnRaw + kWnU;  // records per stage of the 8-wave tile (raw 680 + U 1024)
 static_assert(kWinoQLds >= (size_t)kWqStages * kWqStage * 16, "LDS size");
 static_assert(2 * kWinoQLds <= 160 * 1024, "two blocks per CU");
@@ -999,6 +1009,10 @@ __global__ __launch_bounds__(256 * PT, 2) void conv3x3_winoq_kernel(ConvH8Args a
   const int ksn = SK ? a.ksplit : 1;  // K slices per tile
   if (bid >= ntiles * ksn) return;
   const int tile = SK ? bid / ksn : bid, ks = SK ? bid - tile * ksn : 0;
+#if RRIN_WINOQ_CLOCK
+  const unsigned long long qc_t0 = __builtin_amdgcn_s_memtime(), qc_r0 = __builtin_amdgcn_s_memrealtime();
+  unsigned long long qc_t1 = 0;
+#endif
   // this slice's chunks [c0, c0 + nch) of the conv's a.nchunks; staging below counts chunks
   // from c0 (source and weight bases moved by c0 chunks, cin_loc channels from there)
   const int c0 = SK ? ks * a.kper : 0;
@@ -1208,11 +1222,17 @@ __global__ __launch_bounds__(256 * PT, 2) void conv3x3_winoq_kernel(ConvH8Args a
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();  // chunk c landed everywhere; stage (c + 1) & 1 was last read in chunk c - 1
+#if RRIN_WINOQ_CLOCK
+      if (c == 0) qc_t1 = __builtin_amdgcn_s_memtime();
+#endif
       if (c + 1 < nch) issue(c + 1);
       chunk(c == 0, c);
     }
   }
   }
+#if RRIN_WINOQ_CLOCK
+  const unsigned long long qc_t2 = __builtin_amdgcn_s_memtime();
+#endif
   // the epilogue's bias values, loaded now: their latency hides behind the exchange
   // instead of stalling the stores (the bias blob is padded to whole 32-row blocks)
   float bsv[16];
@@ -1421,6 +1441,19 @@ __global__ __launch_bounds__(256 * PT, 2) void conv3x3_winoq_kernel(ConvH8Args a
       }
     }
   }
+#if RRIN_WINOQ_CLOCK
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the stores done
+  const unsigned long long qc_t3 = __builtin_amdgcn_s_memtime(), qc_r3 = __builtin_amdgcn_s_memrealtime();
+  if (tid == 0) {
+    unsigned long long* g = g_winoq_clk + (size_t)(bid % kQClkSlots) * 6;
+    g[0] = qc_t1 - qc_t0;  // core clocks until chunk 0 landed
+    g[1] = qc_t2 - qc_t0;  // ... until the end of the main loop
+    g[2] = qc_t3 - qc_t0;  // ... until the stores completed
+    g[3] = qc_r3 - qc_r0;  // 100 MHz ticks, whole workgroup
+    g[4] = qc_r0;          // start (100 MHz ticks)
+    g[5] = qc_r3;          // end
+  }
+#endif
 }
 
 template <int EPI, int ABL = 0, int PT = 2, int SK = 0, int RF = 0>
@@ -1525,6 +1558,15 @@ int launch_wino_lab(const ConvH8Args& a, int abl, hipStream_t st) {
 }  // namespace rrin
 
 using namespace rrin;
+
+#if RRIN_WINOQ_CLOCK
+// diagnostic builds only: copy n workgroup stamps (6 x u64 each) to host memory
+extern "C" int rrin_winoq_clock_read(unsigned long long* host, int n) {
+  if (!host || n < 1 || n > rrin::kQClkSlots) return RRIN_E_ARG;
+  return rrin::hip_code(hipMemcpyFromSymbol(host, HIP_SYMBOL(rrin::g_winoq_clk), (size_t)n * 6 * 8, 0,
+                                            hipMemcpyDeviceToHost));
+}
+#endif
 
 extern "C" int64_t rrin_pack_conv3x3_wino_floats(int32_t cout, int32_t cin) {
   return rrin_pack_conv3x3_wino_bm_floats(cout, cin, 32);
