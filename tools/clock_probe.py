@@ -35,13 +35,20 @@ def main():
     ap.add_argument("--height", type=int, default=720)
     ap.add_argument("--width", type=int, default=1280)
     ap.add_argument("--seconds", type=float, default=2.5)
+    ap.add_argument("--kernel", default="winoc", choices=["winoc", "winoq"],
+                    help="winoq: the kind-3 tile's phase stamps (ab/librrin_hip_qclk.so, RRIN_WINOQ_CLOCK=1): "
+                         "chunk 0 landed / main loop done / stores done, and the start-time spread")
     a = ap.parse_args()
+    if a.kernel == "winoq" and a.lib.endswith("librrin_hip_clk.so"):
+        a.lib = os.path.join(REPO, "ab", "librrin_hip_qclk.so")
     from tests.test_gpu_h8 import pack_h8
     lib = C.CDLL(os.path.abspath(a.lib))
     lib.rrin_conv3x3_h8_fwd.argtypes = [C.POINTER(_lib.ConvH8Desc), C.c_void_p]
     lib.rrin_conv3x3_h8_fwd.restype = C.c_int
-    lib.rrin_winoc_clock_read.argtypes = [C.c_void_p, C.c_int]
-    lib.rrin_winoc_clock_read.restype = C.c_int
+    rd = lib.rrin_winoq_clock_read if a.kernel == "winoq" else lib.rrin_winoc_clock_read
+    rd.argtypes = [C.c_void_p, C.c_int]
+    rd.restype = C.c_int
+    nf = 6 if a.kernel == "winoq" else 4
     dev = torch.device("cuda:0")
     prec = _lib.PREC_F32R
     st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -86,13 +93,28 @@ def main():
         e1.synchronize()
         ms = e0.elapsed_time(e1) / 20
         k = min(wgs, 1 << 16)
-        buf = np.zeros((k, 4), np.uint64)
-        _lib.check(lib.rrin_winoc_clock_read(buf.ctypes.data, k), "rrin_winoc_clock_read")
+        buf = np.zeros((k, nf), np.uint64)
+        _lib.check(rd(buf.ctypes.data, k), "clock read")
+        tf = 2 * 4 * cin * cout * h * w * n / (ms * 1e-3) / 1e12
+        if a.kernel == "winoq":
+            f = buf.astype(np.float64)
+            ok = f[:, 3] > 0
+            cyc = f[ok, 2]
+            ghz = float(np.median(cyc / f[ok, 3])) * 0.1
+            eff = tf / (ghz * 65.536)
+            pro, loop, epi = np.median(f[ok, 0]), np.median(f[ok, 1] - f[ok, 0]), np.median(f[ok, 2] - f[ok, 1])
+            life_us = np.median(f[ok, 3]) / 100.0
+            t0 = f[ok, 4] - f[ok, 4].min()
+            span_us = (f[ok, 5].max() - f[ok, 4].min()) / 100.0
+            print(f"{cin:5d}->{cout:5d} L{L} epi{epi} n{n} {ms:7.4f} {tf:8.1f} {ghz:9.3f} {eff:9.3f} wgs {wgs} | "
+                  f"wg life {life_us:6.2f} us: chunk0 {pro / (ghz * 1e3):5.2f} loop {loop / (ghz * 1e3):5.2f} "
+                  f"epilogue+stores {epi / (ghz * 1e3):5.2f} us | launch span {span_us:7.1f} us, "
+                  f"start p50/p90 {np.median(t0) / 100:6.1f}/{np.percentile(t0, 90) / 100:6.1f} us", flush=True)
+            continue
         cyc, ticks, loop = buf[:, 0].astype(np.float64), buf[:, 1].astype(np.float64), buf[:, 2].astype(np.float64)
         ok = ticks > 0
         ghz = float(np.median(cyc[ok] / ticks[ok])) * 0.1
         share = float(np.median(loop[ok] / cyc[ok]))
-        tf = 2 * 4 * cin * cout * h * w * n / (ms * 1e-3) / 1e12
         eff = tf / (ghz * 65.536)
         print(f"{cin:5d}->{cout:5d} L{L} epi{epi} n{n} {ms:7.4f} {tf:8.1f} {ghz:9.3f} {eff:9.3f} {share:10.3f} {wgs}",
               flush=True)
