@@ -72,7 +72,8 @@ WINO_KERNELS = {1: "conv3x3_wino_kernel (BM 32 x TH 8, 4 waves of 8 accumulators
                 3: "conv3x3_winoq_kernel (BM 32 x TH 8, 8 waves of 4 accumulators)",
                 4: "conv3x3_winoq_kernel (BM 32 x TH 4, 4 waves)",
                 6: "conv3x3_winoc_kernel (register-U, BM 64 x TH 4, 4 waves of 2 co tiles)",
-                7: "conv3x3_winoc_kernel (register-U, BM 32 x TH 8, 4 waves of 2 patch tiles)"}
+                7: "conv3x3_winoc_kernel (register-U, BM 32 x TH 8, 4 waves of 2 patch tiles)",
+                8: "conv3x3_winop_kernel (persistent register-U, BM 32 x TH 8, 8 waves)"}
 
 
 def kernel_wino(eng, n, h, w):
@@ -137,6 +138,9 @@ def parse():
                          "(engine.WINO_SPLIT_LEVELS, replaces the geometry rule); 'none' disables split-K (engine.GEOM_SPLIT)")
     ap.add_argument("--no-ring-fold", action="store_true",
                     help="A/B: run the sub-pixel ring fix-up as its own launch (engine.RING_FOLD = False)")
+    ap.add_argument("--wino-kind32", type=int, default=None,
+                    help="A/B: Winograd kind of the 32-output-channel convs in the auto mode "
+                         "(engine.WINO_KIND32: 3, or 8 the persistent register-U tile)")
     ap.add_argument("--no-wino-th4", action="store_true",
                     help="A/B: no TH-4 Winograd tiles on the deep convs (engine.WINO_TH4)")
     ap.add_argument("--split", default=None,
@@ -368,6 +372,8 @@ def main():
         engine_mod.RING_FOLD = False
     if args.no_wino_th4:
         engine_mod.WINO_TH4 = {}
+    if args.wino_kind32 is not None:
+        engine_mod.WINO_KIND32 = args.wino_kind32
     net = Net()
     sd = keyed_state_dict(net.state_dict())
     net.load_state_dict(sd, strict=True)

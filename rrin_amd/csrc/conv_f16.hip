@@ -1776,15 +1776,18 @@ static const CfgH8 kCfgH8[] = {
     {64, 4, kWinoCLds1, (size_t)1 << 30, 0, true, 0, 0},
     // kWinoC1Cfg: register-U tile, BM 32 x TH 8, 4 waves of 2 patch tiles
     {32, 8, kWinoCLds2, (size_t)1 << 30, 0, true, 0, 0},
+    // kWinoPCfg: persistent register-U tile, BM 32 x TH 8, 8 waves (conv_winop.hip; cout <= 32)
+    {32, 8, kWinoPLds, (size_t)1 << 30, 0, true, 0, 0},
 };
 static constexpr int kNumCfgH8 = sizeof(kCfgH8) / sizeof(kCfgH8[0]);
-static constexpr int kWinoCfg = kNumCfgH8 - 7;
-static constexpr int kWino64Cfg = kNumCfgH8 - 6;
-static constexpr int kWinoQCfg = kNumCfgH8 - 5;
-static constexpr int kWinoQ4Cfg = kNumCfgH8 - 4;
-static constexpr int kWino4Cfg = kNumCfgH8 - 3;
-static constexpr int kWinoC2Cfg = kNumCfgH8 - 2;
-static constexpr int kWinoC1Cfg = kNumCfgH8 - 1;
+static constexpr int kWinoCfg = kNumCfgH8 - 8;
+static constexpr int kWino64Cfg = kNumCfgH8 - 7;
+static constexpr int kWinoQCfg = kNumCfgH8 - 6;
+static constexpr int kWinoQ4Cfg = kNumCfgH8 - 5;
+static constexpr int kWino4Cfg = kNumCfgH8 - 4;
+static constexpr int kWinoC2Cfg = kNumCfgH8 - 3;
+static constexpr int kWinoC1Cfg = kNumCfgH8 - 2;
+static constexpr int kWinoPCfg = kNumCfgH8 - 1;
 static inline bool is_winoc(int cfg) { return cfg == kWinoC2Cfg || cfg == kWinoC1Cfg; }
 // tiles whose kernels only the lab library builds (kind 2 wino64, kind 5 F(4x4)):
 // the product library reports them as not usable (rrin_conv_h8_cfg_ok 0)
@@ -1796,7 +1799,7 @@ static constexpr bool kLabBuild = false;
 #endif
 static inline bool is_wino(int cfg) {
   return cfg == kWinoCfg || cfg == kWino64Cfg || cfg == kWinoQCfg || cfg == kWinoQ4Cfg || cfg == kWino4Cfg ||
-         is_winoc(cfg);
+         is_winoc(cfg) || cfg == kWinoPCfg;
 }
 static constexpr size_t kMaxLds = 160 * 1024;
 static constexpr int kMaxKSplit = 16;
@@ -1980,6 +1983,10 @@ static int h8_prepare(const rrin_conv_h8_desc* d, ConvH8Args& a, bool need_scrat
     if ((d->cin & 3) && !d->tail_finite) return RRIN_E_CONFIG;  // stages whole records only
     // the register-U tiles stage both record groups of every chunk: they must exist
     if (is_winoc(d->cfg) && (d->cin & 7) && !d->tail_finite) return RRIN_E_CONFIG;
+    // kind 8: one co block, no sub-pixel / replicate epilogue, no split
+    if (d->cfg == kWinoPCfg && (d->cout > 32 || d->epi_mode == RRIN_EPI_SUBPIXEL || d->epi_mode == RRIN_EPI_LEAKY_REP ||
+                                d->ksplit > 1))
+      return RRIN_E_CONFIG;
     // two record groups per K chunk; F(4x4): one
     a.nchunks = d->cfg == kWino4Cfg ? (d->cin + 3) / 4 : (d->cin + 7) / 8;
   }
@@ -2061,6 +2068,7 @@ extern "C" int rrin_conv_h8_cfg_wino(int32_t cfg) {
          : cfg == kWino4Cfg  ? 5
          : cfg == kWinoC2Cfg ? 6
          : cfg == kWinoC1Cfg ? 7
+         : cfg == kWinoPCfg  ? 8
                              : 0;
 }
 extern "C" int rrin_conv_h8_cfg_ok(int32_t cfg, int32_t prec) {
@@ -2094,6 +2102,7 @@ extern "C" int rrin_conv3x3_h8_fwd(const rrin_conv_h8_desc* d, void* stream) {
 #endif
   if (d->cfg == kWinoC2Cfg) return launch_winoc(a, d->epi_mode, 2, st);
   if (d->cfg == kWinoC1Cfg) return launch_winoc(a, d->epi_mode, 1, st);
+  if (d->cfg == kWinoPCfg) return launch_winop(a, d->epi_mode, st);
   switch (d->cfg) {
 #define X(id, nw, wm, wn, sc, pe) \
   case id:                        \

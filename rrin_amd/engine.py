@@ -183,10 +183,17 @@ WINO_DIRECT = {(6, 32, 0): 13}
 WINO_KIND = 0
 
 
+# the kind of the auto mode's 32-output-channel convs (the level-0 convs): 3, or the
+# persistent register-U tile 8 (conv_winop.hip)
+WINO_KIND32 = 3
+
+
 def wino_kind_for(cout: int) -> int:
     if WINO_KIND != 0:
         return WINO_KIND
-    return 6 if cout % 64 == 0 else 3
+    if cout % 64 == 0:
+        return 6
+    return WINO_KIND32 if cout <= 32 else 3
 # ... and kind 4 (the same arithmetic on TH 4 tiles of 4 waves: twice the
 # workgroups) on the few-tile deep convs where that wins, (cin, cout rows, grid
 # level) per size class as in WINO_DIRECT (a sub-pixel up conv: 4 x cout, the

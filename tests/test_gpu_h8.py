@@ -51,13 +51,22 @@ def keyed_conv(cin, cout, key="h8"):
 NO_POOL_CFGS = (4, 16)
 
 
-def wino_cfgs():
+def wino_cfgs(cout=32, epi=None):
     """Ids of the Winograd exact-fp32 configs the library builds (R32 only): F(2x2,3x3)
-    kinds 1, 3, 4 and the register-U kinds 6-7 (kind 2 and the F(4x4,3x3) kind 5 only
-    in the lab library)."""
+    kinds 1, 3, 4, the register-U kinds 6-7 and the persistent register-U kind 8 (cout
+    <= 32, epilogues LINEAR / LEAKY / LEAKY_POOL); kind 2 and the F(4x4,3x3) kind 5
+    only in the lab library."""
     lib = _lib.lib()
     return tuple(c for c in range(lib.rrin_conv_h8_cfg_count())
-                 if lib.rrin_conv_h8_cfg_wino(c) and lib.rrin_conv_h8_cfg_ok(c, R32))  # kinds 2, 5: lab only
+                 if lib.rrin_conv_h8_cfg_wino(c) and lib.rrin_conv_h8_cfg_ok(c, R32)  # kinds 2, 5: lab only
+                 and kind8_ok(c, cout, epi))
+
+
+def kind8_ok(cfg, cout, epi=None):
+    """Kind 8 (conv_winop.hip) takes one co block and no sub-pixel / replicate epilogue."""
+    if _lib.lib().rrin_conv_h8_cfg_wino(cfg) != 8:
+        return True
+    return cout <= 32 and epi not in (_lib.EPI_LEAKY_REP, _lib.EPI_SUBPIXEL)
 
 
 def cfgs(prec, cout, cin):
@@ -67,7 +76,8 @@ def cfgs(prec, cout, cin):
     return [c for c in range(lib.rrin_conv_h8_cfg_count())
             if lib.rrin_conv_h8_cfg_fits(c, prec, cin) and lib.rrin_conv_h8_cfg_bm(c) <= max(32, 2 * cout)
             and not (lib.rrin_conv_h8_cfg_wino(c) and cin % 4)
-            and not (lib.rrin_conv_h8_cfg_wino(c) in (6, 7) and cin % 8)]
+            and not (lib.rrin_conv_h8_cfg_wino(c) in (6, 7) and cin % 8)
+            and kind8_ok(c, cout)]
 
 
 def pack_h8(w, b, cfg, prec, dev, perm=None):
@@ -278,7 +288,7 @@ def test_h8_leaky_rep_writes_replicated_ring(gpu, prec):
     x = torch.rand(2, 32, 13, 45, device=gpu) * 2 - 1
     wt, b = keyed_conv(32, 64, "rep")
     ref = ref_conv(x, wt, b, 0.1)
-    for cfg in (0, 6) + (wino_cfgs() if prec == R32 else ()):
+    for cfg in (0, 6) + (wino_cfgs(64, _lib.EPI_LEAKY_REP) if prec == R32 else ()):
         dst, _ = conv_h8(H8Tensor.from_nchw(x, prec), wt, b, cfg, prec, epi=_lib.EPI_LEAKY_REP)
         np.testing.assert_allclose(dst.to_nchw().cpu().double().numpy(), ref.numpy(), **tol(prec, cfg))
         # the ring must equal the replicated border; everything else in the padding stays zero

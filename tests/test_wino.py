@@ -89,10 +89,11 @@ def test_wino_config_entry():
     ids = [c for c in range(lib.rrin_conv_h8_cfg_count()) if lib.rrin_conv_h8_cfg_wino(c)]
     # kinds 1 (BM 32, 4 waves), 2 (BM 64, 8 waves), 3 (BM 32, 8 waves of 4 accumulators), TH 8;
     # 4 (kind 3's arithmetic on TH 4 tiles, 4 waves); 5 F(4x4,3x3) on TH 16 tiles; the register-U
-    # tiles 6 (BM 64 x TH 4) and 7 (BM 32 x TH 8), 4 waves
-    assert sorted(lib.rrin_conv_h8_cfg_wino(c) for c in ids) == [1, 2, 3, 4, 5, 6, 7]
+    # tiles 6 (BM 64 x TH 4) and 7 (BM 32 x TH 8), 4 waves; 8 the persistent register-U tile
+    # for cout <= 32 (BM 32 x TH 8, 8 waves)
+    assert sorted(lib.rrin_conv_h8_cfg_wino(c) for c in ids) == [1, 2, 3, 4, 5, 6, 7, 8]
     assert {lib.rrin_conv_h8_cfg_wino(c): lib.rrin_conv_h8_cfg_bm(c) for c in ids} == {1: 32, 2: 64, 3: 32, 4: 32,
-                                                                                        5: 32, 6: 64, 7: 32}
+                                                                                        5: 32, 6: 64, 7: 32, 8: 32}
     for c in ids:
         kind = lib.rrin_conv_h8_cfg_wino(c)
         assert lib.rrin_conv_h8_cfg_th(c) == {4: 4, 5: 16, 6: 4}.get(kind, 8)
