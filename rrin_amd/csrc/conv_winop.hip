@@ -50,7 +50,7 @@ template <int EPI>
 __global__ __launch_bounds__(512, 4) void conv3x3_winop_kernel(ConvH8Args a) {
   extern __shared__ __attribute__((aligned(16))) uint4 smem4[];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int yw = wv & 3, pt = wv >> 2, j = lane & 31, hh = lane >> 5;
+  const int yw = wv & 3, pt = wv >> 2;
   const int G = gridDim.x;
   int bid;
   {  // XCD-aware bijective remap: an XCD's workgroups take consecutive first tiles
@@ -64,21 +64,14 @@ __global__ __launch_bounds__(512, 4) void conv3x3_winop_kernel(ConvH8Args a) {
   float* sbias = reinterpret_cast<float*>(smem4 + kPBias);
   if (tid < 32) sbias[tid] = a.bias[tid];  // visible after chunk 0's barrier
 
-  // raw staging (tile-independent lane offsets; kind 3's layout): pieces of 512 records,
-  // byte offsets from the tile's origin (an image is < 2^32 bytes)
-  unsigned p_off[2];
-  int p_g[2], p_col[2];
-#pragma unroll
-  for (int it = 0; it < 2; ++it) {
-    const int idx = tid + 512 * it;
-    const int g = idx >= kPRG ? 1 : 0;
-    const int rem = idx - g * kPRG;
-    const int r = rem / kPCols, pos = rem - r * kPCols;
-    const int col = pos < 17 ? 2 * pos : 2 * (pos - 17) + 1;
-    p_g[it] = g;
-    p_col[it] = col;
-    p_off[it] = (unsigned)(((int64_t)g * a.src_gp + (int64_t)r * a.src_wp + col) * 16);
-  }
+  // the lane id through an opaque move: values derived from it inside the loops are
+  // recomputed where used instead of being hoisted into registers held across the
+  // whole kernel (the 4-waves-per-SIMD budget is 128 VGPRs)
+  auto lane_id = [&]() {
+    int v;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(v) : "v"(tid));
+    return v;
+  };
   const bool tail_lane = tid < kPRaw - 512;  // second piece (waves 0-2)
   // a tile's origin: record (row y0 - 1, col x0 - 1) of group 0 of its image
   auto tile_src = [&](int t, int& y0) {
@@ -93,43 +86,51 @@ __global__ __launch_bounds__(512, 4) void conv3x3_winop_kernel(ConvH8Args a) {
                                                       0x00020000);
     // rs starts at the tile column's top padding row: channel groups past cin read it (zeros)
     const unsigned rowoff = (unsigned)((int64_t)y0 * a.src_wp * 16);
+    const int tl = lane_id();
 #pragma unroll
     for (int it = 0; it < 2; ++it) {
       if (it == 0 || tail_lane) {
-        const int gg = 2 * c + p_g[it];
-        const unsigned off = gg * 4 < a.cin ? rowoff + (unsigned)((int64_t)(2 * c) * a.src_gp * 16) + p_off[it]
-                                            : (unsigned)p_col[it] * 16u;
+        // raw staging (kind 3's layout): record idx of the stage's 680, byte offsets from
+        // the tile's origin (an image is < 2^32 bytes)
+        const int idx = tl + 512 * it;
+        const int g = idx >= kPRG ? 1 : 0;
+        const int rem = idx - g * kPRG;
+        const int r = rem / kPCols, pos = rem - r * kPCols;
+        const int col = pos < 17 ? 2 * pos : 2 * (pos - 17) + 1;
+        const int gg = 2 * c + g;
+        const unsigned off = gg * 4 < a.cin
+                                 ? rowoff + (unsigned)((((int64_t)(2 * c) + g) * a.src_gp + (int64_t)r * a.src_wp + col) * 16)
+                                 : (unsigned)col * 16u;
         wp_dma16(rs, smem4 + stage * kPRaw + 512 * it + (tid & ~63), off);
       }
     }
   };
   // U record (xi = 4 yw + x, hh, co = j) of chunk c, straight into registers
   const auto urs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(a.w_hi), 0, 0x7fffffff, 0x00020000);
-  const unsigned uvoff = (unsigned)(((4 * yw) * 64 + hh * 32 + j) * 16);
   auto load_u = [&](int c, int x) {
+    const int tl = lane_id() & 63;  // (hh, j) = (tl >> 5, tl & 31)
+    const unsigned uvoff = (unsigned)(((4 * yw) * 64 + tl) * 16);
     return __builtin_bit_cast(pfloatx4, __builtin_amdgcn_raw_buffer_load_b128(urs, uvoff + x * 1024, c * kPU * 16, 0));
   };
 
-  const int pr = 2 * pt + (j >> 4), jx = (j + 12 * (j >> 4)) & 15;
   const int ra = yw == 0 ? 0 : (yw == 2 ? 2 : 1);
   const int rb = yw == 0 ? 2 : (yw == 1 ? 2 : (yw == 2 ? 1 : 3));
   const float sg = yw == 1 ? 1.f : -1.f;
-  const int rw0 = hh * kPRG + (2 * pr) * kPCols;
   const int oa = ra * kPCols, ob = rb * kPCols;
-  int pc[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) pc[k] = wp_col(2 * jx + k);
 
   pfloatx16 acc[4];
   pfloatx4 ur[4];  // U of the chunk being computed (point x reloaded after its MFMAs)
   // a chunk in raw stage s; U of chunk next_c loaded after each point when `more`
   auto chunk = [&](int s, bool more, int next_c) {
-    const uint4* rw = smem4 + s * kPRaw + rw0;
+    const int tl = lane_id();
+    const int lj = tl & 31, lhh = (tl >> 5) & 1, lpr = 2 * pt + (lj >> 4), ljx = (lj + 12 * (lj >> 4)) & 15;
+    const uint4* rw = smem4 + s * kPRaw + lhh * kPRG + (2 * lpr) * kPCols;
     pfloatx4 t[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const pfloatx4 d0 = __builtin_bit_cast(pfloatx4, rw[oa + pc[k]]);
-      const pfloatx4 d1 = __builtin_bit_cast(pfloatx4, rw[ob + pc[k]]);
+      const int pck = wp_col(2 * ljx + k);
+      const pfloatx4 d0 = __builtin_bit_cast(pfloatx4, rw[oa + pck]);
+      const pfloatx4 d1 = __builtin_bit_cast(pfloatx4, rw[ob + pck]);
 #pragma unroll
       for (int e = 0; e < 4; ++e) t[k][e] = fmaf(sg, d1[e], d0[e]);
     }
@@ -209,6 +210,8 @@ __global__ __launch_bounds__(512, 4) void conv3x3_winop_kernel(ConvH8Args a) {
       yt0 = (tt % a.tiles_y) * 8;
       img = tt / a.tiles_y;
     }
+    const int el = lane_id() & 63, ej = el & 31;
+    const int pr = 2 * pt + (ej >> 4), jx = (ej + 12 * (ej >> 4)) & 15;
     const int y = yt0 + 2 * pr + r, x = x0 + 2 * jx + cc;
     float yv[16];
 #pragma unroll
@@ -247,20 +250,23 @@ __global__ __launch_bounds__(512, 4) void conv3x3_winop_kernel(ConvH8Args a) {
     __builtin_amdgcn_sched_barrier(0);  // keep those loads ahead of the stores below
     const auto drs = __builtin_amdgcn_make_buffer_rsrc(a.dst_hi + (int64_t)img * a.dst_img, 0, 0x7fffffff, 0x00020000);
     const bool in = y < a.h && x < a.w;
+    // 32-bit byte offsets within the image (an image is < 2^32 bytes)
+    const unsigned ehh = (unsigned)(el >> 5);
+    const unsigned pix = (unsigned)(((y + 1) * a.dst_wp + x + kH8PadLeft) * 16);
+    const unsigned gs = (unsigned)(a.dst_gp * 16);
     float vv[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      float tv = yv[i] + sbias[8 * (i >> 2) + 4 * hh + (i & 3)];
+      float tv = yv[i] + sbias[8 * (i >> 2) + 4 * (int)ehh + (i & 3)];
       if constexpr (EPI != RRIN_EPI_LINEAR) tv = leaky(tv, a.slope);
       vv[i] = tv;
     }
 #pragma unroll
     for (int qq = 0; qq < 4; ++qq) {
       const bool ok = in && 8 * qq < a.cout;
-      const int64_t rec = (int64_t)(2 * qq + hh) * a.dst_gp + (int64_t)(y + 1) * a.dst_wp + x + kH8PadLeft;
       const pu32x4 v4 = {__float_as_uint(vv[4 * qq]), __float_as_uint(vv[4 * qq + 1]), __float_as_uint(vv[4 * qq + 2]),
                          __float_as_uint(vv[4 * qq + 3])};
-      __builtin_amdgcn_raw_buffer_store_b128(v4, drs, ok ? (unsigned)(rec * 16) : 0x80000000u, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(v4, drs, ok ? (2 * qq + ehh) * gs + pix : 0x80000000u, 0, 0);
     }
     if constexpr (kPool) {
       // the patch's four outputs (yw = (r, c)) meet in the exchange area; wave yw 0 writes
@@ -287,11 +293,11 @@ __global__ __launch_bounds__(512, 4) void conv3x3_winop_kernel(ConvH8Args a) {
           float s4[4];
 #pragma unroll
           for (int e = 0; e < 4; ++e) s4[e] = 0.25f * ((y00[e] + y10[e]) + (y01[e] + y11[e]));
-          const int64_t rec =
-              (int64_t)(2 * qq + hh) * a.pool_gp + (int64_t)(yp / 2 + 1) * a.pool_wp + xp / 2 + kH8PadLeft;
+          const unsigned poff = (2 * qq + ehh) * (unsigned)(a.pool_gp * 16) +
+                                (unsigned)(((yp / 2 + 1) * a.pool_wp + xp / 2 + kH8PadLeft) * 16);
           const pu32x4 v4 = {__float_as_uint(s4[0]), __float_as_uint(s4[1]), __float_as_uint(s4[2]),
                              __float_as_uint(s4[3])};
-          __builtin_amdgcn_raw_buffer_store_b128(v4, prs, ok ? (unsigned)(rec * 16) : 0x80000000u, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(v4, prs, ok ? poff : 0x80000000u, 0, 0);
         }
       }
       bar();  // the exchange area is rewritten by the next tile's epilogue
