@@ -264,7 +264,9 @@ int launch_winoc(const ConvH8Args& a, int epi, int ct, hipStream_t st);
 // persistent register-U tile for cout <= 32 (conv_winop.hip, kind 8): 8 waves, two raw
 // stages + a separate exchange area + 32 bias floats
 constexpr size_t kWinoPLds = (size_t)(2 * 680 + 2048) * 16 + 128;
+#ifdef RRIN_LAB
 int launch_winop(const ConvH8Args& a, int epi, hipStream_t st);
+#endif
 #ifdef RRIN_LAB
 int launch_wino_lab(const ConvH8Args& a, int abl, hipStream_t st);  // ablation bits (conv_wino.hip)
 #endif

@@ -1789,9 +1789,10 @@ static constexpr int kWinoC2Cfg = kNumCfgH8 - 3;
 static constexpr int kWinoC1Cfg = kNumCfgH8 - 2;
 static constexpr int kWinoPCfg = kNumCfgH8 - 1;
 static inline bool is_winoc(int cfg) { return cfg == kWinoC2Cfg || cfg == kWinoC1Cfg; }
-// tiles whose kernels only the lab library builds (kind 2 wino64, kind 5 F(4x4)):
+// tiles whose kernels only the lab library builds (kind 2 wino64, kind 5 F(4x4), kind 8
+// the persistent register-U tile):
 // the product library reports them as not usable (rrin_conv_h8_cfg_ok 0)
-static inline bool lab_only(int cfg) { return cfg == kWino64Cfg || cfg == kWino4Cfg; }
+static inline bool lab_only(int cfg) { return cfg == kWino64Cfg || cfg == kWino4Cfg || cfg == kWinoPCfg; }
 #ifdef RRIN_LAB
 static constexpr bool kLabBuild = true;
 #else
@@ -2102,7 +2103,9 @@ extern "C" int rrin_conv3x3_h8_fwd(const rrin_conv_h8_desc* d, void* stream) {
 #endif
   if (d->cfg == kWinoC2Cfg) return launch_winoc(a, d->epi_mode, 2, st);
   if (d->cfg == kWinoC1Cfg) return launch_winoc(a, d->epi_mode, 1, st);
+#ifdef RRIN_LAB
   if (d->cfg == kWinoPCfg) return launch_winop(a, d->epi_mode, st);
+#endif
   switch (d->cfg) {
 #define X(id, nw, wm, wn, sc, pe) \
   case id:                        \

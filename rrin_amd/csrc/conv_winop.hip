@@ -22,8 +22,11 @@
 //     stores with a fixed count per wave (an out-of-range offset drops a store),
 //     so the next tile's chunk-0 wait is a counted vmcnt that skips them.
 // cout <= 32 (one co block); epilogues LINEAR, LEAKY, LEAKY_POOL.
+// Measured 20-33 % slower than kind 3 on every level-0 conv: built only
+// into the lab library (`make lab`, RRIN_LAB).
 #include "common.hpp"
 
+#ifdef RRIN_LAB
 #ifndef RRIN_WINOP_TILES
 #define RRIN_WINOP_TILES 4  // tiles per workgroup (the grid is ntiles / this, rounded up)
 #endif
@@ -331,3 +334,4 @@ int launch_winop(const ConvH8Args& a, int epi, hipStream_t st) {
 }
 
 }  // namespace rrin
+#endif  // RRIN_LAB

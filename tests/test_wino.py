@@ -97,9 +97,9 @@ def test_wino_config_entry():
     for c in ids:
         kind = lib.rrin_conv_h8_cfg_wino(c)
         assert lib.rrin_conv_h8_cfg_th(c) == {4: 4, 5: 16, 6: 4}.get(kind, 8)
-        # kinds 2 and 5 lost on every Net shape: their kernels are built only into the lab
+        # kinds 2, 5 and 8 lost on every Net shape: their kernels are built only into the lab
         # library (make lab), so the product library reports them as not usable
-        assert lib.rrin_conv_h8_cfg_ok(c, _lib.PREC_F32R) == (0 if kind in (2, 5) else 1)
+        assert lib.rrin_conv_h8_cfg_ok(c, _lib.PREC_F32R) == (0 if kind in (2, 5, 8) else 1)
         assert lib.rrin_conv_h8_cfg_ok(c, _lib.PREC_F16X3) == 0 and lib.rrin_conv_h8_cfg_ok(c, _lib.PREC_F16) == 0
     assert lib.rrin_pack_conv3x3_wino_floats(33, 5) == 2 * 1 * 16 * 2 * 32 * 4
     assert lib.rrin_pack_conv3x3_wino_floats(0, 5) < 0
