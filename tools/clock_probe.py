@@ -102,13 +102,13 @@ def main():
             cyc = f[ok, 2]
             ghz = float(np.median(cyc / f[ok, 3])) * 0.1
             eff = tf / (ghz * 65.536)
-            pro, loop, epi = np.median(f[ok, 0]), np.median(f[ok, 1] - f[ok, 0]), np.median(f[ok, 2] - f[ok, 1])
+            pro, loop, epl = np.median(f[ok, 0]), np.median(f[ok, 1] - f[ok, 0]), np.median(f[ok, 2] - f[ok, 1])
             life_us = np.median(f[ok, 3]) / 100.0
             t0 = f[ok, 4] - f[ok, 4].min()
             span_us = (f[ok, 5].max() - f[ok, 4].min()) / 100.0
             print(f"{cin:5d}->{cout:5d} L{L} epi{epi} n{n} {ms:7.4f} {tf:8.1f} {ghz:9.3f} {eff:9.3f} wgs {wgs} | "
                   f"wg life {life_us:6.2f} us: chunk0 {pro / (ghz * 1e3):5.2f} loop {loop / (ghz * 1e3):5.2f} "
-                  f"epilogue+stores {epi / (ghz * 1e3):5.2f} us | launch span {span_us:7.1f} us, "
+                  f"epilogue+stores {epl / (ghz * 1e3):5.2f} us | launch span {span_us:7.1f} us, "
                   f"start p50/p90 {np.median(t0) / 100:6.1f}/{np.percentile(t0, 90) / 100:6.1f} us", flush=True)
             continue
         cyc, ticks, loop = buf[:, 0].astype(np.float64), buf[:, 1].astype(np.float64), buf[:, 2].astype(np.float64)
