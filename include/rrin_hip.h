@@ -245,8 +245,9 @@ int64_t rrin_conv_h8_ring_floats(const rrin_conv_h8_desc* d, int64_t* cnt_ints);
  * rrin_pack_conv3x3_wino4 (a different rounding: 36 transform points).  Kinds
  * 3 and 4 take a split-K (rrin_conv_h8_desc.ksplit).  6 = BM 64 x TH 4 and 7 =
  * BM 32 x TH 8 on 4 waves with the U operands loaded straight into registers
- * (ABI 12; bitwise equal to kinds 1-4; cin % 8 == 0 or tail_finite).  Kinds 2 and
- * 5 are built only into the lab library: the product library reports them with
+ * (ABI 12; bitwise equal to kinds 1-4; cin % 8 == 0 or tail_finite).  8 = a
+ * persistent register-U tile for cout <= 32 (BM 32 x TH 8, 8 waves).  Kinds 2, 5
+ * and 8 are built only into the lab library: the product library reports them with
  * rrin_conv_h8_cfg_ok == 0 and rrin_conv3x3_h8_fwd returns RRIN_E_CONFIG.
  * 0: direct form. */
 int rrin_conv_h8_cfg_wino(int32_t cfg);
