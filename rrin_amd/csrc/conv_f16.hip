@@ -140,6 +140,18 @@ __device__ inline uint4 mask_halves(uint4 v, int nvalid) {
 // reads but drops the MFMAs, NO_EPI drops the epilogue; MFMA16 issues every
 // 32x32x16 product as two v_mfma_f32_16x16x32_f16 of the same FLOPs on the
 // same operands (a clock/throughput probe of the other MFMA shape).
+// Epilogue bias of the record kernel: 0 = each epilogue piece loads its 4 bias floats
+// just before its stores (then waits out every earlier store of the tile: vmcnt counts
+// stores too); 1 = every piece's bias loaded at the start of the epilogue (one wait);
+// 2 = loaded at the start of the tile, landed during the chunk loop (no wait, but 16 WM
+// more VGPRs live across it).  -1 (default): per tile shape, as measured at C3 fp16
+// (profiles/r04/h8_bias/): 2 where the accumulators are small (WM WN <= 2: the level-0
+// and level-4 tiles, 6-14 % faster per conv), 1 on the other unspread tiles (cfg 0 -8 %,
+// cfg 5 -3 %), 0 on the SPREAD tiles (cfg 10 / 11, which lose 1-7 % with either).
+#ifndef RRIN_H8_BIAS
+#define RRIN_H8_BIAS -1
+#endif
+
 enum : int {
   SCHED_NO_WDMA = 1, SCHED_NO_IDMA = 2, SCHED_NO_MFMA = 4, SCHED_NO_EPI = 8,
   SCHED_SPREAD = 16, SCHED_WRES = 32, SCHED_STAGGER = 64, SCHED_MFMA16 = 128
@@ -174,6 +186,7 @@ __global__ void RRIN_PK_CONV_ATTR __launch_bounds__(64 * NW) conv3x3_h8_kernel(C
   constexpr bool kStagger = DMA && !kSpread && (SCHED & SCHED_STAGGER) != 0 && NW >= 2;
   constexpr bool kWRes = DMA && (SCHED & SCHED_WRES) != 0;
   constexpr bool kMfma16 = (SCHED & SCHED_MFMA16) != 0;
+  constexpr int kBias = RRIN_H8_BIAS >= 0 ? RRIN_H8_BIAS : (WM * WN <= 2 ? 2 : (SCHED & SCHED_SPREAD) ? 0 : 1);
   // DMA pieces (one 16-B record per thread and plane) of one chunk: input tile, then weight slab
   constexpr int NPIECE = T::IN_IT + (kWRes ? 0 : T::W_IT);
 
@@ -420,7 +433,7 @@ __global__ void RRIN_PK_CONV_ATTR __launch_bounds__(64 * NW) conv3x3_h8_kernel(C
       if constexpr (PLANES == 2) reinterpret_cast<uint2*>(d[1] + rec)[hh] = lv;
     }
   };
-  auto epi_piece = [&](const TileId& tl, const auto& V, int mt, int q) {
+  auto epi_piece = [&](const TileId& tl, const auto& V, int mt, int q, const float* bs) {
     const int cob = tl.cob, x0 = tl.x0, img = tl.img;
     const int yb = tl.y0 + wn * WN;
     const int x = x0 + j;
@@ -432,10 +445,6 @@ __global__ void RRIN_PK_CONV_ATTR __launch_bounds__(64 * NW) conv3x3_h8_kernel(C
       const int grp = (cob * BM + mt * 32) >> 5;
       if (grp * 32 >= a.cout) return;
       const int py = q >> 1, px = q & 1;
-      const int co0 = cob * BM + mt * 32 + 8 * q;
-      float bs[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) bs[e] = a.bias[co0 + 4 * hh + e];
 #pragma unroll
       for (int nt = 0; nt < WN; ++nt) {
         const int y = yb + nt;
@@ -465,9 +474,6 @@ __global__ void RRIN_PK_CONV_ATTR __launch_bounds__(64 * NW) conv3x3_h8_kernel(C
       }
       const int co0 = cob * BM + mt * 32 + 8 * q;  // first channel of the 8-channel block
       const int grp = F32 ? (co0 >> 2) + hh : co0 >> 3;  // record group this lane writes
-      float bs[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) bs[e] = a.bias[co0 + 4 * hh + e];
       float v[WN][4];
 #pragma unroll
       for (int nt = 0; nt < WN; ++nt) {
@@ -521,6 +527,18 @@ __global__ void RRIN_PK_CONV_ATTR __launch_bounds__(64 * NW) conv3x3_h8_kernel(C
           V[mt][nt][i] = PLANES == 2 ? fmaf(accx[mt][nt][i], kLoUnscale, acc[mt][nt][i]) : acc[mt][nt][i];
   };
   constexpr int NPIECE_EPI = WM * 4;
+  // bias of epilogue piece (mt, q): channels co0 + 4hh .. co0 + 4hh + 3 of lane half hh,
+  // co0 = cob BM + 32 mt + 8 q (pieces past cout store nothing: their bias stays 0)
+  auto load_bias_piece = [&](int cob, int mt, int q, float* bq) {
+    const int co0 = cob * BM + mt * 32 + 8 * q;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bq[e] = co0 < a.cout ? a.bias[co0 + 4 * hh + e] : 0.f;
+  };
+  float bsv[kBias ? WM : 1][4][4];
+  auto load_bias = [&](int cob) {
+#pragma unroll
+    for (int p = 0; p < NPIECE_EPI; ++p) load_bias_piece(cob, p / 4, p % 4, bsv[kBias ? p / 4 : 0][p % 4]);
+  };
 
   int tile = bid;
   if (tile >= ntiles) return;
@@ -555,6 +573,7 @@ __global__ void RRIN_PK_CONV_ATTR __launch_bounds__(64 * NW) conv3x3_h8_kernel(C
           accx[mt][nt][i] = 0.f;
           if constexpr (kMfma16) p16[mt][nt][i >> 3][(i >> 2) & (PLANES - 1)][i & 3] = 0.f;
         }
+    if constexpr (kBias == 2) load_bias(cur.cob);
     for (int c = 0; c < a.nchunks; ++c) {
       // staged during this chunk: chunk c+1 of this tile, or chunk 0 of the next tile
       const bool last = c + 1 == a.nchunks;
@@ -630,8 +649,21 @@ __global__ void RRIN_PK_CONV_ATTR __launch_bounds__(64 * NW) conv3x3_h8_kernel(C
     } else {
       floatx16 V[WM][WN];
       combine(V);
+      if constexpr (kBias == 1) load_bias(cur.cob);
+      // the bias has landed (mode 2: long ago, the chunk loop drained vmcnt): a wait the
+      // compiler sees, so that it does not wait out each piece's stores before the next
+      // piece's bias (vmcnt(0), as s_waitcnt's 16-bit immediate)
+      if constexpr (kBias != 0) __builtin_amdgcn_s_waitcnt(0x0F70);
 #pragma unroll
-      for (int p = 0; p < NPIECE_EPI; ++p) epi_piece(cur, V, p / 4, p % 4);
+      for (int p = 0; p < NPIECE_EPI; ++p) {
+        if constexpr (kBias == 0) {
+          float bq[4];
+          load_bias_piece(cur.cob, p / 4, p % 4, bq);
+          epi_piece(cur, V, p / 4, p % 4, bq);
+        } else {
+          epi_piece(cur, V, p / 4, p % 4, bsv[p / 4][p % 4]);
+        }
+      }
     }
     if (!more) break;
     tile = ntile;
