@@ -757,6 +757,11 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wino64_kernel(ConvH8Args a) {
 // others wait on LDS, barriers or their transform, instead of a deeper
 // per-wave pipeline.  The output transform meets through LDS as in cfg 19.
 // ============================================================================
+// RRIN_WINOQ_EPIWAIT 1: a compiler-visible vmcnt(0) after the main loop, before the
+// epilogue's bias loads (0: the A/B build without it; profiles/r04/winoq_epiwait/)
+#ifndef RRIN_WINOQ_EPIWAIT
+#define RRIN_WINOQ_EPIWAIT 1
+#endif
 // RRIN_WINOQ_RU (A/B): the U operands straight from L2 into registers (buffer loads a
 // chunk ahead, as conv_winoc.hip) instead of LDS-DMA + LDS reads (2-stage loop only)
 #ifndef RRIN_WINOQ_RU
@@ -1232,6 +1237,12 @@ __global__ __launch_bounds__(256 * PT, 2) void conv3x3_winoq_kernel(ConvH8Args a
   }
 #if RRIN_WINOQ_CLOCK
   const unsigned long long qc_t2 = __builtin_amdgcn_s_memtime();
+#endif
+  // every stage DMA has landed (the last chunk waited for it): said with a wait the
+  // compiler sees, so that it does not drain vmcnt at the exchange barrier below for the
+  // LDS-DMA it cannot see completed -- which would wait out the bias loads too
+#if RRIN_WINOQ_EPIWAIT
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
 #endif
   // the epilogue's bias values, loaded now: their latency hides behind the exchange
   // instead of stalling the stores (the bias blob is padded to whole 32-row blocks)
