@@ -1,48 +1,74 @@
-"""Derive the H8 tile-config table (engine.H8_TUNED keys: (cin, cout rows, grid
-level)) from a `conv_lab.py tune` sweep: per key the config with the least
-summed time over the schedule's convs of that key (only configs valid for every
-epilogue mode of the key).
+#!/usr/bin/env python3
+"""Turn a `conv_lab.py tune` JSON into a tile table for engine.H8_TUNED and compare it
+with the table in use: per conv shape (cin, rows, level; the epilogue variants of one
+shape summed, weighted by how often the Net runs them) the fastest config, and the
+schedule time of the current vs the new choice.
 
-  python tools/tune_table.py gpurun_out/tune_split.json [fp32_split16]"""
+  python3 tools/tune_table.py gpurun_out/r04t/tune_fp16_1280x736x2.json --precision fp16
+"""
+import argparse
 import collections
 import json
 import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from rrin_amd import _lib  # noqa: E402
-from rrin_amd.engine import H8_TUNED  # noqa: E402
-from tools.conv_lab import schedule  # noqa: E402
 
 
-def main(path, precision="fp32_split16"):
-    r = json.load(open(path))
-    cnt = collections.Counter((e[2], e[3], e[4], e[6]) for e in schedule(720, 1280, True) if e[5] >= 0)
-    by = collections.defaultdict(lambda: collections.defaultdict(float))
-    variants = collections.defaultdict(set)
-    have = collections.defaultdict(lambda: collections.defaultdict(set))
-    ncfg = _lib.lib().rrin_conv_h8_cfg_count()
-    for e in r:
-        if e["cfg"] >= ncfg:  # a config of an older build, not in this library
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("json")
+    ap.add_argument("--precision", default="fp16")
+    ap.add_argument("--height", type=int, default=736)
+    ap.add_argument("--width", type=int, default=1280)
+    a = ap.parse_args()
+    from rrin_amd import _lib, engine
+    from tools.conv_lab import schedule
+    prec = _lib.PRECISIONS[a.precision]
+    cur = engine.H8_TUNED[prec]
+    rows = json.load(open(a.json))
+    t = {}
+    for r in rows:
+        kout = 4 * r["cout"] if r["epi"] == 4 else r["cout"]
+        lvl = r["level"] + 1 if r["epi"] == 4 else r["level"]  # sub-pixel: the low-res grid
+        t[(r["cin"], kout, lvl, r["epi"], r["cfg"])] = r["ms"]
+    # how often each (shape, epi) runs per forward
+    count = collections.Counter()
+    for e in schedule(a.height, a.width, True):
+        if e[5] < 0:
             continue
-        k = (e["cin"], 4 * e["cout"], e["level"] + 1) if e["epi"] == 4 else (e["cin"], e["cout"], e["level"])
-        by[k][e["cfg"]] += e["ms"] * cnt[(e["cin"], e["cout"], e["level"], e["epi"])]
-        variants[k].add(e["epi"])
-        have[k][e["cfg"]].add(e["epi"])
-    cur = H8_TUNED[_lib.PRECISIONS[precision]]
-    new, tc, tn = {}, 0.0, 0.0
-    for k, v in sorted(by.items()):
-        ok = {c: t for c, t in v.items() if have[k][c] == variants[k]}
-        b = min(ok, key=ok.get)
-        c = cur.get(k)
-        print(k, "cur", c, f"{ok.get(c, float('nan')):.3f}", "best", b, f"{ok[b]:.3f}")
-        tc += ok.get(c, 0.0)
-        tn += ok[b]
-        new[k] = b
-    print(f"sum over the schedule: current {tc:.3f} ms, best {tn:.3f} ms")
-    print(json.dumps({str(k).replace(" ", ""): v for k, v in new.items() if cur.get(k) != v}))
-    print("full table:", {k: new[k] for k in sorted(new)})
+        cin, cout, L, src, epi = e[2], e[3], e[4], e[5], e[6]
+        kout = 4 * cout if epi == 4 else cout
+        lvl = L + 1 if epi == 4 else L
+        count[(cin, kout, lvl, epi)] += 1
+    shapes = collections.defaultdict(list)
+    for (cin, kout, lvl, epi), c in count.items():
+        shapes[(cin, kout, lvl)].append((epi, c))
+    new, tot_cur, tot_new = {}, 0.0, 0.0
+    for key in sorted(shapes):
+        cfgs = {k[4] for k in t if k[:3] == key}
+        def cost(cfg):
+            s = 0.0
+            for epi, c in shapes[key]:
+                ms = t.get(key + (epi, cfg))
+                if ms is None:
+                    return None
+                s += c * ms
+            return s
+        costs = {c: cost(c) for c in cfgs if cost(c) is not None}
+        if not costs:
+            continue
+        best = min(costs, key=costs.get)
+        c0 = cur.get(key)
+        cc = costs.get(c0)
+        new[key] = best
+        tot_new += costs[best]
+        tot_cur += cc if cc is not None else costs[best]
+        flag = "" if best == c0 else f"  <- was cfg {c0} ({cc:.3f} ms)" if cc is not None else f"  <- was cfg {c0}"
+        print(f"{key}: cfg {best} {costs[best]:.3f} ms{flag}")
+    print(f"schedule sum: current {tot_cur:.3f} ms, new {tot_new:.3f} ms")
+    print("table:", "{" + ", ".join(f"{k}: {v}" for k, v in sorted(new.items())) + "}")
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:])
+    main()
