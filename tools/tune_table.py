@@ -5,6 +5,9 @@ shape summed, weighted by how often the Net runs them) the fastest config, and t
 schedule time of the current vs the new choice.
 
   python3 tools/tune_table.py gpurun_out/r04t/tune_fp16_1280x736x2.json --precision fp16
+
+(Round 4 rewrite of the round-1 tool: same per-key choice -- the config with the least
+schedule-weighted time over the key's epilogue variants -- plus the comparison.)
 """
 import argparse
 import collections
@@ -18,10 +21,13 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("json")
+    ap.add_argument("precision_pos", nargs="?", default=None, help="the precision, positionally (older usage)")
     ap.add_argument("--precision", default="fp16")
     ap.add_argument("--height", type=int, default=736)
     ap.add_argument("--width", type=int, default=1280)
     a = ap.parse_args()
+    if a.precision_pos:
+        a.precision = a.precision_pos
     from rrin_amd import _lib, engine
     from tools.conv_lab import schedule
     prec = _lib.PRECISIONS[a.precision]
