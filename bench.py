@@ -81,6 +81,12 @@ def kernel_wino(eng, n, h, w):
     lib = _lib.lib()
     t = eng.conv_table_for(n, h, w)
     kinds = [lib.rrin_conv_h8_cfg_wino(t[i].cfg) for i in range(eng.expected_convs)]
+    if eng.precision == "fp16":
+        parts = [f"conv3x3_winoh_kernel (register-U, BM 64 x TH 4, 4 waves of 2 co tiles) x {kinds.count(6)}"]
+        if kinds.count(0):
+            parts.append(f"conv3x3_h8_kernel direct form x {kinds.count(0)}")
+        return ("Winograd F(2x2,3x3) on fp16 records, packed-fp16 input transform, v_mfma_f32_32x32x16_f16 "
+                "contraction per transform point, fp32 output transform: " + "; ".join(parts))
     parts = [f"{WINO_KERNELS.get(k, f'kind {k}')} x {kinds.count(k)}" for k in sorted(set(kinds)) if k]
     if kinds.count(0):
         parts.append(f"conv3x3_h8_kernel direct form x {kinds.count(0)}")
@@ -128,8 +134,10 @@ def parse():
     ap.add_argument("--size-class", default=None, choices=["small", "medium", "large", "xlarge", "xxlarge"],
                     help="A/B: force the tile table of this size class for every forward part")
     ap.add_argument("--no-wino", action="store_true",
-                    help="A/B: exact fp32 on the direct-form conv (v_mfma_f32_32x32x2_f32 per tap) instead of "
-                         "Winograd F(2x2,3x3)")
+                    help="A/B: the direct-form conv (one MFMA product per tap) instead of Winograd F(2x2,3x3), "
+                         "exact fp32 and fp16")
+    ap.add_argument("--wino-f16-levels", default=None,
+                    help="A/B: grid levels of the fp16 Winograd convs, e.g. '2,3,4' (engine.WINO_F16_LEVELS)")
     ap.add_argument("--wino-kind", type=int, default=None,
                     help="A/B: Winograd tile kind of the exact-fp32 body convs (rrin_conv_h8_cfg_wino; "
                          "0 = auto: kind 6 where cout %% 64 == 0, else 3; default engine.WINO_KIND)")
@@ -361,6 +369,9 @@ def main():
 
     if args.no_wino:
         engine_mod.WINO = False
+        engine_mod.WINO_F16 = False
+    if args.wino_f16_levels is not None:
+        engine_mod.WINO_F16_LEVELS = tuple(int(v) for v in args.wino_f16_levels.split(",") if v)
     if args.wino_kind is not None:
         engine_mod.WINO_KIND = args.wino_kind
     if args.wino_split == "none":
@@ -490,13 +501,15 @@ def main():
                     "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None,
                     "mfma_issued_tflops": round(achieved * MFMA_PRODUCTS[args.precision], 1),
                     "kernel": (kernel_wino(eng, B // max(1, args.streams), H, W)
-                               if algo in ("winograd", "mixed") and args.precision == "fp32"
+                               if algo in ("winograd", "mixed") and args.precision in ("fp32", "fp16")
                                else KERNEL[args.precision]),
                     "conv_algorithm": algo,
                     "flops_basis": ("FLOPs of the algorithm the convs run: Winograd F(2x2,3x3) = 16 multiply-adds "
                                     "per 2x2 output patch and channel pair (4/9 of the direct form's)"
-                                    + ("; the 6-channel first conv runs the direct form (engine.WINO_DIRECT) and counts "
-                                       "its direct-form FLOPs" if algo == "mixed" else "")
+                                    + (("; the 6-channel first conv runs the direct form (engine.WINO_DIRECT) and counts "
+                                        "its direct-form FLOPs" if args.precision == "fp32" else
+                                        "; the direct-form convs (engine.wino_f16_ok false: level 0, cout 32, cin % 16) "
+                                        "count their direct-form FLOPs") if algo == "mixed" else "")
                                     if algo in ("winograd", "mixed") else "direct-form conv FLOPs (2*9*Cin*Cout*H*W)"),
                     "direct_equivalent_tflops": round(direct_fl / (conv_busy * 1e-3) / 1e12, 2),
                     "flops_per_launch_avg": conv_fl / max(conv_launches, 1),

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define RRIN_ABI_VERSION 12
+#define RRIN_ABI_VERSION 13
 
 #define RRIN_OK 0
 #define RRIN_E_SHAPE (-1)     /* H or W not a multiple of 16, or N < 1          */
@@ -246,7 +246,10 @@ int64_t rrin_conv_h8_ring_floats(const rrin_conv_h8_desc* d, int64_t* cnt_ints);
  * 3 and 4 take a split-K (rrin_conv_h8_desc.ksplit).  6 = BM 64 x TH 4 and 7 =
  * BM 32 x TH 8 on 4 waves with the U operands loaded straight into registers
  * (ABI 12; bitwise equal to kinds 1-4; cin % 8 == 0 or tail_finite).  8 = a
- * persistent register-U tile for cout <= 32 (BM 32 x TH 8, 8 waves).  Kinds 2, 5
+ * persistent register-U tile for cout <= 32 (BM 32 x TH 8, 8 waves).  Kind 6 also
+ * runs at RRIN_PREC_F16, and 9 = BM 64 x TH 8 (4 waves, one block per CU) at
+ * RRIN_PREC_F16 only (ABI 13: fp16 Winograd, packed by rrin_pack_conv3x3_wino_h8;
+ * cin % 16 == 0 or tail_finite; no split-K, no ring fold).  Kinds 2, 5
  * and 8 are built only into the lab library: the product library reports them with
  * rrin_conv_h8_cfg_ok == 0 and rrin_conv3x3_h8_fwd returns RRIN_E_CONFIG.
  * 0: direct form. */
@@ -280,6 +283,16 @@ int rrin_pack_conv3x3_wino(const float* w, const float* b, int32_t cout, int32_t
 int64_t rrin_pack_conv3x3_wino4_floats(int32_t cout, int32_t cin);
 int rrin_pack_conv3x3_wino4(const float* w, const float* b, int32_t cout, int32_t cin, const int32_t* perm,
                             float* wpack, float* bpack);
+
+/* fp16 Winograd packing (ABI 13; kind 6 at RRIN_PREC_F16): U = G g G^T per (co, ci)
+ * in double, times a power of two that puts max|U| in [2^12, 2^13), rounded once to
+ * fp16, laid out [co_block of 64][chunk of 16 ci][xi 16][half 2][co 64][8 ci] (half hh
+ * holds input channels chunk*16 + 8*hh .. +7); *inv_wscale receives the exact inverse
+ * scale (pass it in rrin_conv_h8_desc.inv_wscale).  bm must be 64.  bpack:
+ * rrin_pack_bias_floats(cout, 64) floats. */
+int64_t rrin_pack_conv3x3_wino_h8_halves(int32_t cout, int32_t cin, int32_t bm);
+int rrin_pack_conv3x3_wino_h8(const float* w, const float* b, int32_t cout, int32_t cin, int32_t bm,
+                              const int32_t* perm, uint16_t* whi, float* bpack, float* inv_wscale);
 
 /* Host packing: [co_block][chunk of 16 ci][tap][half][bm][8] halves, weights
  * pre-scaled by a power of two so max|w| lands in [2^12, 2^13) (keeps lo

@@ -9,7 +9,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-ABI_VERSION = 12
+ABI_VERSION = 13
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "librrin_hip.so")
 
 # enums (rrin_hip.h)
@@ -165,6 +165,9 @@ SIGNATURES = {
                                             C.c_void_p, C.c_void_p]),
     "rrin_pack_conv3x3_wino": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p,
                                          C.c_void_p]),
+    "rrin_pack_conv3x3_wino_h8_halves": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32]),
+    "rrin_pack_conv3x3_wino_h8": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p,
+                                            C.c_void_p, C.c_void_p, C.POINTER(C.c_float)]),
     "rrin_pack_conv3x3_h8_halves": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32]),
     "rrin_pack_conv3x3_h8": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p,
                                        C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(C.c_float)]),

@@ -1810,16 +1810,21 @@ static const CfgH8 kCfgH8[] = {
     {32, 8, kWinoCLds2, (size_t)1 << 30, 0, true, 0, 0},
     // kWinoPCfg: persistent register-U tile, BM 32 x TH 8, 8 waves (conv_winop.hip; cout <= 32)
     {32, 8, kWinoPLds, (size_t)1 << 30, 0, true, 0, 0},
+    // kWinoH2Cfg: fp16 only, the register-U tile on 2 patch tiles, BM 64 x TH 8, 4 waves, one
+    // block per CU (conv_winoh.hip)
+    {64, 8, kWinoCLds2, (size_t)1 << 30, 0, true, 0, 0},
 };
 static constexpr int kNumCfgH8 = sizeof(kCfgH8) / sizeof(kCfgH8[0]);
-static constexpr int kWinoCfg = kNumCfgH8 - 8;
-static constexpr int kWino64Cfg = kNumCfgH8 - 7;
-static constexpr int kWinoQCfg = kNumCfgH8 - 6;
-static constexpr int kWinoQ4Cfg = kNumCfgH8 - 5;
-static constexpr int kWino4Cfg = kNumCfgH8 - 4;
-static constexpr int kWinoC2Cfg = kNumCfgH8 - 3;
-static constexpr int kWinoC1Cfg = kNumCfgH8 - 2;
-static constexpr int kWinoPCfg = kNumCfgH8 - 1;
+static constexpr int kWinoCfg = kNumCfgH8 - 9;
+static constexpr int kWino64Cfg = kNumCfgH8 - 8;
+static constexpr int kWinoQCfg = kNumCfgH8 - 7;
+static constexpr int kWinoQ4Cfg = kNumCfgH8 - 6;
+static constexpr int kWino4Cfg = kNumCfgH8 - 5;
+static constexpr int kWinoC2Cfg = kNumCfgH8 - 4;
+static constexpr int kWinoC1Cfg = kNumCfgH8 - 3;
+static constexpr int kWinoPCfg = kNumCfgH8 - 2;
+static constexpr int kWinoH2Cfg = kNumCfgH8 - 1;
+static_assert(kWinoCfg == 18, "the direct-form configs keep ids 0-17 (engine tile tables)");
 static inline bool is_winoc(int cfg) { return cfg == kWinoC2Cfg || cfg == kWinoC1Cfg; }
 // tiles whose kernels only the lab library builds (kind 2 wino64, kind 5 F(4x4), kind 8
 // the persistent register-U tile):
@@ -1832,8 +1837,10 @@ static constexpr bool kLabBuild = false;
 #endif
 static inline bool is_wino(int cfg) {
   return cfg == kWinoCfg || cfg == kWino64Cfg || cfg == kWinoQCfg || cfg == kWinoQ4Cfg || cfg == kWino4Cfg ||
-         is_winoc(cfg) || cfg == kWinoPCfg;
+         is_winoc(cfg) || cfg == kWinoPCfg || cfg == kWinoH2Cfg;
 }
+// the fp16 Winograd tiles (conv_winoh.hip): kind 6 and the fp16-only kind 9
+static inline bool is_winoh(int cfg) { return cfg == kWinoC2Cfg || cfg == kWinoH2Cfg; }
 static constexpr size_t kMaxLds = 160 * 1024;
 static constexpr int kMaxKSplit = 16;
 
@@ -2011,8 +2018,12 @@ static int h8_prepare(const rrin_conv_h8_desc* d, ConvH8Args& a, bool need_scrat
   a.co_blocks = (d->cout + ci.bm - 1) / ci.bm;
   a.tiles_x = (w + 31) / 32;
   a.tiles_y = (h + ci.th - 1) / ci.th;
-  if (is_wino(d->cfg)) {
-    if (d->prec != RRIN_PREC_F32R) return RRIN_E_CONFIG;
+  if (is_wino(d->cfg) && d->prec == RRIN_PREC_F16) {
+    // fp16 Winograd (kind 6 only): 16-channel chunks of both record groups, no split / fold
+    if (!is_winoh(d->cfg) || d->ksplit > 1 || d->ring_w) return RRIN_E_CONFIG;
+    if ((d->cin & 15) && !d->tail_finite) return RRIN_E_CONFIG;
+  } else if (is_wino(d->cfg)) {
+    if (d->prec != RRIN_PREC_F32R || d->cfg == kWinoH2Cfg) return RRIN_E_CONFIG;
     if ((d->cin & 3) && !d->tail_finite) return RRIN_E_CONFIG;  // stages whole records only
     // the register-U tiles stage both record groups of every chunk: they must exist
     if (is_winoc(d->cfg) && (d->cin & 7) && !d->tail_finite) return RRIN_E_CONFIG;
@@ -2102,12 +2113,16 @@ extern "C" int rrin_conv_h8_cfg_wino(int32_t cfg) {
          : cfg == kWinoC2Cfg ? 6
          : cfg == kWinoC1Cfg ? 7
          : cfg == kWinoPCfg  ? 8
+         : cfg == kWinoH2Cfg ? 9
                              : 0;
 }
 extern "C" int rrin_conv_h8_cfg_ok(int32_t cfg, int32_t prec) {
   if (cfg < 0 || cfg >= kNumCfgH8) return 0;
   if (!rec_prec(prec) || (lab_only(cfg) && !kLabBuild)) return 0;
-  if (is_wino(cfg) && prec != RRIN_PREC_F32R) return 0;
+  // Winograd tiles: exact fp32 records (kinds 1-8); the register-U kind 6 also at fp16 and
+  // kind 9 at fp16 only (conv_winoh.hip)
+  if (is_wino(cfg) && (prec == RRIN_PREC_F16 ? !is_winoh(cfg) : prec != RRIN_PREC_F32R || cfg == kWinoH2Cfg))
+    return 0;
   return (planes_of(prec) == 2 ? kCfgH8[cfg].lds2 : kCfgH8[cfg].lds1) <= kMaxLds ? 1 : 0;
 }
 
@@ -2133,6 +2148,7 @@ extern "C" int rrin_conv3x3_h8_fwd(const rrin_conv_h8_desc* d, void* stream) {
   if (d->cfg == kWino64Cfg) return launch_wino64(a, d->epi_mode, st);
   if (d->cfg == kWino4Cfg) return launch_wino4(a, d->epi_mode, st);
 #endif
+  if (is_winoh(d->cfg) && d->prec == RRIN_PREC_F16) return launch_winoh(a, d->epi_mode, d->cfg == kWinoH2Cfg ? 2 : 1, st);
   if (d->cfg == kWinoC2Cfg) return launch_winoc(a, d->epi_mode, 2, st);
   if (d->cfg == kWinoC1Cfg) return launch_winoc(a, d->epi_mode, 1, st);
 #ifdef RRIN_LAB

@@ -91,8 +91,11 @@ struct Plan {
   int64_t bytes;
 };
 
-// Caller-provided scratch (rrin_net_desc.scratch): [cnt_ints tickets | part floats]
-constexpr int64_t kScratchTickets = 4096;  // ints at the head of the scratch (16 KB)
+// Caller-provided scratch (rrin_net_desc.scratch): [tickets | part floats].  The ticket count is
+// a function of the schedule (n, h, w, the conv table): at least kScratchTickets, else the
+// schedule's largest split conv's tile count rounded up to 1024 (scratch_tickets); the size
+// query and the forward derive it the same way, so the part slab starts at the same byte.
+constexpr int64_t kScratchTickets = 4096;  // minimum ints at the head of the scratch (16 KB)
 // ring fix-up: cross-workgroup K split up to this many workgroups (one per CU;
 // RRIN_EDGE_CROSS_MAX: A/B builds)
 #ifndef RRIN_EDGE_CROSS_MAX
@@ -177,13 +180,18 @@ void make_plan(int n, int h, int w, int prec, char* base, Plan& p) {
   p.bytes = off;
 }
 
-// The caller's scratch into the plan (F32R only; null / too small: no splits).
-void attach_scratch(Plan& p, void* scratch, int64_t bytes) {
-  if (p.prec != RRIN_PREC_F32R || !scratch || bytes < kScratchTickets * 4) return;
+inline int64_t scratch_tickets(int64_t cnt_ints) {
+  return cnt_ints <= kScratchTickets ? kScratchTickets : (cnt_ints + 1023) / 1024 * 1024;
+}
+
+// The caller's scratch into the plan (F32R only; null / too small: no splits); `tickets` from
+// scratch_tickets of the schedule's need.
+void attach_scratch(Plan& p, void* scratch, int64_t bytes, int64_t tickets) {
+  if (p.prec != RRIN_PREC_F32R || !scratch || bytes < tickets * 4) return;
   p.CNT = reinterpret_cast<int32_t*>(scratch);
-  p.cnt_ints = kScratchTickets;
-  p.PART = reinterpret_cast<float*>(reinterpret_cast<char*>(scratch) + kScratchTickets * 4);
-  p.part_floats = (bytes - kScratchTickets * 4) / 4;
+  p.cnt_ints = tickets;
+  p.PART = reinterpret_cast<float*>(reinterpret_cast<char*>(scratch) + tickets * 4);
+  p.part_floats = (bytes - tickets * 4) / 4;
 }
 
 // H8 view of channels [ch_off, ch_off+channels) of a buffer, at geometry g
@@ -345,7 +353,7 @@ int conv_h8(const Plan& p, const rrin_conv_weights& cw, int cin, int cout, int e
   // multiply-adds per output and input channel in the direct form, 4 in Winograd F(2x2,3x3)
   // (16 per 2x2 patch)
   const int creal = epi == RRIN_EPI_SUBPIXEL ? cout / 4 : cout;
-  const int macs = p.prec == RRIN_PREC_F32R && rrin_conv_h8_cfg_wino(cw.cfg) ? 4 : 9;
+  const int macs = rrin_conv_h8_cfg_wino(cw.cfg) ? 4 : 9;  // Winograd: exact fp32 (F32R) or fp16 (kind 6)
   ProfScope ps(p.prof, st, RRIN_KIND_CONV, 2.0 * macs * cin * creal * (double)dst.g.h * dst.g.w * p.n);
   rrin_conv_h8_desc d;
   memset(&d, 0, sizeof(d));
@@ -537,13 +545,11 @@ extern "C" int64_t rrin_net_workspace_bytes(int32_t n, int32_t h, int32_t w, int
 // Scratch the schedule of d needs (F32R: the split convs' slabs and tickets, the ring
 // fix-up's cross-workgroup K split; other precisions 0): the schedule walked with every
 // launch skipped.
-static int64_t scratch_bytes_of(int n, int h, int w, int prec, const rrin_conv_weights* convs, const UNetSpec* us,
-                                int nu) {
-  if (prec != RRIN_PREC_F32R) return 0;
+static int scratch_need_of(int n, int h, int w, int prec, const rrin_conv_weights* convs, const UNetSpec* us, int nu,
+                           ScratchNeed& need) {
   Plan p;
   // a stand-in base so the views pass the descriptor checks; never dereferenced
   make_plan(n, h, w, prec, reinterpret_cast<char*>((uintptr_t)1 << 30), p);
-  ScratchNeed need;
   p.dry = &need;
   const rrin_head_weights hw{};
   int k = 0;
@@ -551,9 +557,25 @@ static int64_t scratch_bytes_of(int n, int h, int w, int prec, const rrin_conv_w
     RRIN_TRY(run_unet_h8(p, us[u], convs + k, hw, HeadIO{nullptr, nullptr, nullptr}, nullptr));
     k += convs_of(us[u].depth);
   }
+  return 0;
+}
+
+static int64_t scratch_bytes_of(int n, int h, int w, int prec, const rrin_conv_weights* convs, const UNetSpec* us,
+                                int nu) {
+  if (prec != RRIN_PREC_F32R) return 0;
+  ScratchNeed need;
+  RRIN_TRY(scratch_need_of(n, h, w, prec, convs, us, nu, need));
   if (need.part_floats == 0 && need.cnt_ints == 0) return 0;
-  if (need.cnt_ints > kScratchTickets) return RRIN_E_CONFIG;
-  return kScratchTickets * 4 + need.part_floats * 4;
+  return scratch_tickets(need.cnt_ints) * 4 + need.part_floats * 4;
+}
+
+// The ticket count of the caller's scratch for this schedule (the layout scratch_bytes_of sized)
+static int64_t scratch_tickets_of(int n, int h, int w, int prec, const rrin_conv_weights* convs, const UNetSpec* us,
+                                  int nu, const void* scratch) {
+  if (prec != RRIN_PREC_F32R || !scratch) return kScratchTickets;
+  ScratchNeed need;
+  if (scratch_need_of(n, h, w, prec, convs, us, nu, need)) return kScratchTickets;
+  return scratch_tickets(need.cnt_ints);
 }
 
 extern "C" int64_t rrin_net_scratch_bytes(const rrin_net_desc* d) {
@@ -571,7 +593,8 @@ extern "C" int rrin_net_fwd(const rrin_net_desc* d, void* stream) {
   Plan p;
   make_plan(d->n, d->h, d->w, d->prec, reinterpret_cast<char*>(d->workspace), p);
   if (d->workspace_bytes < p.bytes) return RRIN_E_WORKSPACE;
-  attach_scratch(p, d->scratch, d->scratch_bytes);
+  attach_scratch(p, d->scratch, d->scratch_bytes,
+                 scratch_tickets_of(d->n, d->h, d->w, d->prec, d->convs, kUNets, 4, d->scratch));
   p.prof = d->prof;  // per call: concurrent calls never share launch state
   if (p.prof) p.prof->chain = false;  // the call's first launch records its own start
   hipStream_t st = (hipStream_t)stream;
@@ -650,7 +673,11 @@ extern "C" int rrin_unet_fwd(const rrin_unet_desc* d, void* stream) {
   Plan p;
   make_plan(d->n, d->h, d->w, d->prec, reinterpret_cast<char*>(d->workspace), p);
   if (d->workspace_bytes < p.bytes) return RRIN_E_WORKSPACE;
-  attach_scratch(p, d->scratch, d->scratch_bytes);
+  {
+    const UNetSpec u{d->in_ch, d->out_ch, d->depth, RRIN_HEAD_PLAIN};
+    attach_scratch(p, d->scratch, d->scratch_bytes,
+                   scratch_tickets_of(d->n, d->h, d->w, d->prec, d->convs, &u, 1, d->scratch));
+  }
   p.prof = d->prof;
   if (p.prof) p.prof->chain = false;
   hipStream_t st = (hipStream_t)stream;

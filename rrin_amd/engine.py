@@ -267,6 +267,19 @@ def wino_cfg(kind: int = None) -> int:
     return next(c for c in range(lib.rrin_conv_h8_cfg_count()) if lib.rrin_conv_h8_cfg_wino(c) == kind)
 
 
+# fp16 (BASELINE C3-C5): Winograd F(2x2,3x3) with f16 MFMAs (conv_winoh.hip, the kind-6
+# register-U tile at fp16) on the convs whose output rows fill 64-channel blocks and whose
+# input channels fill 16-channel chunks, at the grid levels in WINO_F16_LEVELS; the rest
+# (the 32-channel level-0 convs, the 6-16-channel first convs) stay on the direct-form
+# tables.  False: the direct form everywhere (A/B, bench.py --no-wino).
+WINO_F16 = True
+WINO_F16_LEVELS = (1, 2, 3, 4)
+
+
+def wino_f16_ok(cin: int, cout: int, level: int) -> bool:
+    return WINO_F16 and level in WINO_F16_LEVELS and cout % 64 == 0 and cin % 16 == 0
+
+
 def choose_cfg_h8(cin: int, cout: int, prec: int, level: int = 0, size: str = "large", split: int = 1) -> int:
     """Tile config of the record-layout conv (conv_f16.hip table) for a conv
     running on the grid of U-Net level ``level`` (a sub-pixel up conv runs on the
@@ -281,6 +294,8 @@ def choose_cfg_h8(cin: int, cout: int, prec: int, level: int = 0, size: str = "l
         if split > 1:
             return wino_cfg(4)
         return wino_cfg(4 if (cin, cout, level) in WINO_TH4.get(size, ()) else wino_kind_for(cout))
+    if prec == _lib.PREC_F16 and wino_f16_ok(cin, cout, level):
+        return wino_cfg(6)
     table = H8_TUNED_BY_SIZE.get(size, {}).get(prec) or H8_TUNED.get(prec, {})
     cfg = table.get((cin, cout, level))
     if cfg is not None and _lib.lib().rrin_conv_h8_cfg_fits(cfg, prec, cin):
@@ -493,6 +508,21 @@ class RRINEngine:
                 meta.append((hoff, None, boff, cfg, 1.0, edge))
                 halves.append(wp)
                 hoff += wp.size
+                biases.append(bp)
+                boff += bp.size
+                continue
+            if L.rrin_conv_h8_cfg_wino(cfg):  # fp16 Winograd: U = G g G^T in fp16 (conv_winoh.hip)
+                nh = L.rrin_pack_conv3x3_wino_h8_halves(cout, cin, bm)
+                whi = np.empty(nh, np.uint16)
+                bp = np.empty(L.rrin_pack_bias_floats(cout, bm), np.float32)
+                inv = C.c_float()
+                _lib.check(L.rrin_pack_conv3x3_wino_h8(
+                    w.ctypes.data, b.ctypes.data, cout, cin, bm,
+                    perm_arr.ctypes.data if perm_arr is not None else None, whi.ctypes.data, bp.ctypes.data,
+                    C.byref(inv)), "rrin_pack_conv3x3_wino_h8")
+                meta.append((hoff, None, boff, cfg, inv.value, edge))
+                halves.append(whi)
+                hoff += nh
                 biases.append(bp)
                 boff += bp.size
                 continue

@@ -77,6 +77,7 @@ def cfgs(prec, cout, cin):
             if lib.rrin_conv_h8_cfg_fits(c, prec, cin) and lib.rrin_conv_h8_cfg_bm(c) <= max(32, 2 * cout)
             and not (lib.rrin_conv_h8_cfg_wino(c) and cin % 4)
             and not (lib.rrin_conv_h8_cfg_wino(c) in (6, 7) and cin % 8)
+            and not (prec == F16 and lib.rrin_conv_h8_cfg_wino(c) and cin % 16)  # fp16 kind 6: 16-ch chunks
             and kind8_ok(c, cout)]
 
 
@@ -111,6 +112,15 @@ def pack_h8(w, b, cfg, prec, dev, perm=None):
                                              bp.ctypes.data))
         wt = torch.from_numpy(wp).to(dev)
         return wt, wt, torch.from_numpy(bp).to(dev), 1.0
+    if prec == F16 and lib.rrin_conv_h8_cfg_wino(cfg):  # fp16 Winograd (kind 6): fp16 U, scaled
+        whi = np.zeros(lib.rrin_pack_conv3x3_wino_h8_halves(cout, cin, bm), np.uint16)
+        bp = np.zeros(lib.rrin_pack_bias_floats(cout, bm), np.float32)
+        inv = C.c_float()
+        _lib.check(lib.rrin_pack_conv3x3_wino_h8(w.ctypes.data, b.ctypes.data, cout, cin, bm,
+                                                 pa.ctypes.data if pa is not None else None, whi.ctypes.data,
+                                                 bp.ctypes.data, C.byref(inv)))
+        wt = torch.from_numpy(whi.view(np.int16)).to(dev)
+        return wt, wt, torch.from_numpy(bp).to(dev), inv.value
     nh = lib.rrin_pack_conv3x3_h8_halves(cout, cin, bm)
     whi = np.zeros(nh, np.uint16)
     wlo = np.zeros(nh, np.uint16)

@@ -7,6 +7,8 @@ contraction, output Y = A^T M A -- must reproduce the direct 3x3 conv (zero
 padding, reference unet.py:29) of the same weights.  The GPU tests
 (tests/test_gpu_h8.py, the Winograd config in every config sweep) check the
 kernel itself against float64."""
+import ctypes as C
+
 import numpy as np
 import pytest
 import torch
@@ -91,20 +93,55 @@ def test_wino_config_entry():
     # 4 (kind 3's arithmetic on TH 4 tiles, 4 waves); 5 F(4x4,3x3) on TH 16 tiles; the register-U
     # tiles 6 (BM 64 x TH 4) and 7 (BM 32 x TH 8), 4 waves; 8 the persistent register-U tile
     # for cout <= 32 (BM 32 x TH 8, 8 waves)
-    assert sorted(lib.rrin_conv_h8_cfg_wino(c) for c in ids) == [1, 2, 3, 4, 5, 6, 7, 8]
-    assert {lib.rrin_conv_h8_cfg_wino(c): lib.rrin_conv_h8_cfg_bm(c) for c in ids} == {1: 32, 2: 64, 3: 32, 4: 32,
-                                                                                        5: 32, 6: 64, 7: 32, 8: 32}
+    # 9: the fp16-only register-U tile on 2 patch tiles (BM 64 x TH 8, one block per CU)
+    assert sorted(lib.rrin_conv_h8_cfg_wino(c) for c in ids) == [1, 2, 3, 4, 5, 6, 7, 8, 9]
+    assert min(ids) == 18  # the direct-form configs keep ids 0-17 (engine tile tables)
+    assert {lib.rrin_conv_h8_cfg_wino(c): lib.rrin_conv_h8_cfg_bm(c) for c in ids} == {
+        1: 32, 2: 64, 3: 32, 4: 32, 5: 32, 6: 64, 7: 32, 8: 32, 9: 64}
     for c in ids:
         kind = lib.rrin_conv_h8_cfg_wino(c)
         assert lib.rrin_conv_h8_cfg_th(c) == {4: 4, 5: 16, 6: 4}.get(kind, 8)
         # kinds 2, 5 and 8 lost on every Net shape: their kernels are built only into the lab
         # library (make lab), so the product library reports them as not usable
-        assert lib.rrin_conv_h8_cfg_ok(c, _lib.PREC_F32R) == (0 if kind in (2, 5, 8) else 1)
-        assert lib.rrin_conv_h8_cfg_ok(c, _lib.PREC_F16X3) == 0 and lib.rrin_conv_h8_cfg_ok(c, _lib.PREC_F16) == 0
+        assert lib.rrin_conv_h8_cfg_ok(c, _lib.PREC_F32R) == (0 if kind in (2, 5, 8, 9) else 1)
+        # split16 never runs a Winograd tile; fp16 runs kinds 6 and 9 (conv_winoh.hip, ABI 13)
+        assert lib.rrin_conv_h8_cfg_ok(c, _lib.PREC_F16X3) == 0
+        assert lib.rrin_conv_h8_cfg_ok(c, _lib.PREC_F16) == (1 if kind in (6, 9) else 0)
     assert lib.rrin_pack_conv3x3_wino_floats(33, 5) == 2 * 1 * 16 * 2 * 32 * 4
     assert lib.rrin_pack_conv3x3_wino_floats(0, 5) < 0
     assert lib.rrin_pack_conv3x3_wino_bm_floats(65, 9, 64) == 2 * 2 * 16 * 2 * 64 * 4
     assert lib.rrin_pack_conv3x3_wino_bm_floats(8, 8, 48) < 0
+    assert lib.rrin_pack_conv3x3_wino_h8_halves(65, 17, 64) == 2 * 2 * 16 * 2 * 64 * 8
+    assert lib.rrin_pack_conv3x3_wino_h8_halves(64, 16, 32) < 0  # BM 64 only
+
+
+@pytest.mark.parametrize("cout,cin", [(64, 16), (72, 40), (128, 32)])
+def test_pack_wino_h8_layout(cout, cin):
+    """fp16 Winograd packing: [cob 64][16-ch chunk][xi][half][64 co][8 ci] of fp16(U * 2^s),
+    U = G g G^T in double, 2^s putting max|U| in [2^12, 2^13), *inv_wscale = 2^-s."""
+    lib = _lib.lib()
+    rng = np.random.default_rng(cout + cin)
+    w = (rng.standard_normal((cout, cin, 3, 3)) * 0.05).astype(np.float32)
+    b = rng.standard_normal(cout).astype(np.float32)
+    nh = lib.rrin_pack_conv3x3_wino_h8_halves(cout, cin, 64)
+    whi = np.zeros(nh, np.uint16)
+    bp = np.zeros(lib.rrin_pack_bias_floats(cout, 64), np.float32)
+    inv = C.c_float()
+    _lib.check(lib.rrin_pack_conv3x3_wino_h8(w.ctypes.data, b.ctypes.data, cout, cin, 64, None, whi.ctypes.data,
+                                             bp.ctypes.data, C.byref(inv)))
+    G = np.array([[1, 0, 0], [.5, .5, .5], [.5, -.5, .5], [0, 0, 1]], np.float64)
+    U = np.einsum("ak,oikl,bl->oiab", G, w.astype(np.float64), G).reshape(cout, cin, 16)
+    e = np.frexp(np.abs(U).max())[1]
+    assert inv.value == 2.0 ** -(13 - e)
+    cob, nch = -(-cout // 64), -(-cin // 16)
+    want = np.zeros((cob * 64, nch * 16, 16))
+    want[:cout, :cin] = U * 2.0 ** (13 - e)
+    # [cob][chunk][xi][hh][co][e] <- want[cob*64 + co][chunk*16 + hh*8 + e][xi]
+    want = want.reshape(cob, 64, nch, 2, 8, 16).transpose(0, 2, 5, 3, 1, 4).reshape(-1)
+    got = whi.view(np.float16).astype(np.float64)
+    np.testing.assert_array_equal(got, want.astype(np.float16).astype(np.float64))
+    np.testing.assert_array_equal(bp[:cout], b)
+    assert not bp[cout:].any()
 
 
 # F(4x4,3x3), interpolation points 0, 1, -1, 1/2, -2, inf; B^T scaled to integers
@@ -259,5 +296,11 @@ def test_net_scratch_bytes():
     split = need(1, 368, 640, ks={3: 2, 4: 4})
     assert split > base
     assert need(3, 368, 640, ks={3: 2, 4: 4}) > split  # the slabs scale with the batch
+    # large batches: the split convs' tickets (one per tile, tiles grow with the batch) outgrow
+    # the 4096-int minimum head (RRIN_E_CONFIG from about 11 pairs); the head grows
+    n16, n32 = need(16, 368, 640, ks={3: 2, 4: 4}), need(32, 368, 640, ks={3: 2, 4: 4})
+    assert n16 > 0 and n32 > n16
+    # head = max(4096, tickets rounded up to 1024) ints: the bytes grow by more than the slabs
+    assert n32 - n16 >= 16 * (split - base) - 1
     assert need(1, 368, 640, prec=_lib.PREC_F16) == 0
     assert need(1, 72, 80) < 0  # not /16
