@@ -302,22 +302,40 @@ def train_main(args):
         opt.step()
         return loss
 
+    from rrin_amd import autograd as ag
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
+    ag.PROF = []  # per-launch conv events (forward, dgrad, wgrad) on each launch's stream
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
-    units = ("Flow", "refine_flow", "Mask", "final")
-    fwd = B * sum(fl for u in units for _, fl, _, _ in conv_work(getattr(net, u), H, W))
-    # dgrad of every body conv except Flow's first (its input, cat(I0, I1), needs no
-    # gradient: autograd skips it); wgrad of every body conv (the heads, 1 % of the
-    # FLOPs, are left out of all three)
-    first_flow = B * conv_work(net.Flow, H, W)[0][1]
-    step_fl = 3 * fwd - first_flow
-    ach = step_fl / (el / args.steps) / 1e12
+    events, ag.PROF = ag.PROF, None
+    # conv busy time = the union of the conv launch spans, on one clock: every event's time
+    # from the first start event
+    ref = events[0][0]
+    spans = [(ref.elapsed_time(e0), ref.elapsed_time(e1)) for e0, e1, _, _ in events]
+    busy_ms = union_ms(spans)
+    conv_fl = sum(f for _, _, f, _ in events)
+    by_kind = {}
+    for (a, b), (_, _, f, k) in zip(spans, events):
+        kk = by_kind.setdefault(k, [0, 0.0, 0.0])
+        kk[0] += 1
+        kk[1] += b - a
+        kk[2] += f
+    ach = conv_fl / (busy_ms * 1e-3) / 1e12
+    step_ach = conv_fl / el / 1e12
+    wino = ag.TRAIN_WINO
+    kernel = ("forward and dgrad: the exact-fp32 Winograd F(2x2,3x3) register-U tiles (conv3x3_winoc_kernel, "
+              "kinds 6/7, v_mfma_f32_32x32x2_f32; weights packed on the device by rrin_tpack_wino, dgrad = the "
+              "forward conv of the flipped transposed weights); wgrad: csrc/train.hip row-tiled MFMA "
+              "(conv3x3 wgrad, v_mfma_f32_32x32x2_f32, direct form, deterministic split-K)" if wino else
+              "csrc/train.hip implicit GEMM for forward / dgrad / wgrad (v_mfma_f32_32x32x2_f32, direct form)")
+    basis = ("FLOPs of the algorithm each launch runs: Winograd F(2x2,3x3) = 2*4*Cin*Cout*H*W per image for the "
+             "forward and dgrad convs, direct form 2*9*Cin*Cout*H*W for wgrad" if wino else
+             "direct-form conv FLOPs 2*9*Cin*Cout*H*W per image for forward, dgrad and wgrad")
     res = {
         "metric": f"training steps at {W}x{H} fp32 (Net forward + backward + AdamW, frame pairs/s)",
         "value": round(B * args.steps / el, 3), "unit": "pairs/s", "n_gpus": 1, "steps": args.steps,
@@ -329,13 +347,15 @@ def train_main(args):
                    "global_batch": B, "height": H, "width": W, "parallelism": "single GPU"},
         "roofline": {"bound": "mfma", "achieved": round(ach, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(ach / FP32_PEAK_TFLOPS, 4), "traffic": None,
-                     "kernel": "rrin_amd.autograd over csrc/train.hip (conv forward / dgrad / wgrad on "
-                               "v_mfma_f32_32x32x2_f32, direct form)",
-                     "flops_basis": "direct-form conv FLOPs of forward + dgrad + wgrad of the 77 body convs "
-                                    "(Flow's first conv has no dgrad)",
-                     "conv_tflop_per_step": round(step_fl / 1e12, 4),
-                     "frac_basis": "conv FLOPs / whole step time (includes the glue, loss and optimizer: a "
-                                   "lower bound on the conv kernels' own rate)"},
+                     "kernel": kernel, "flops_basis": basis,
+                     "conv_tflop_per_step": round(conv_fl / args.steps / 1e12, 4),
+                     "conv_busy_ms_per_step": round(busy_ms / args.steps, 3),
+                     "launches_per_step": {k: v[0] // args.steps for k, v in by_kind.items()},
+                     "tflops_by_kind": {k: round(v[2] / (v[1] * 1e-3) / 1e12, 2) for k, v in by_kind.items()},
+                     "frac_basis": "algorithmic conv FLOPs of every conv launch (the 81 forward convs incl. the "
+                                   "heads, their dgrads but Flow's first, every wgrad) / conv busy time = union of "
+                                   "the launch spans (HIP events recorded on each launch's own stream)",
+                     "whole_step_tflops": round(step_ach, 2)},
         "loss": float(loss.item()),
         "cpu_baseline": None,
     }

@@ -52,19 +52,59 @@ def _f32(t: torch.Tensor) -> torch.Tensor:
 # rrin_h8_to_nchw) in per-shape buffers reused in stream order.  False: train.hip for all
 # three (A/B).
 TRAIN_WINO = True
-_R32_BUFS: dict = {}
+# Record-layout buffers by (device, stream, shape, role), least recently used first.  A buffer
+# is only touched by kernels on its own stream, so reusing it is ordered; an evicted buffer goes
+# back to the caching allocator's pool of that stream.  Bounded: training with varying crop
+# sizes does not keep every shape's buffers for the life of the process.
+_R32_BUFS: "OrderedDict" = None
+R32_BUFS_MAX = 96
 
 
 def _r32_buf(n, c, h, w, device, role):
-    """A zero-padded fp32-record buffer of c channels (a multiple of 8) per shape and role;
-    every kernel touching it runs on the device's current stream, so reuse is ordered."""
+    """A zero-padded fp32-record buffer of c channels (a multiple of 8) per stream, shape and
+    role (the padding and the channel tail are never written, so they stay zero)."""
+    from collections import OrderedDict
+
     from .pp import H8Tensor
-    key = (device, n, c, h, w, role)
+    global _R32_BUFS
+    if _R32_BUFS is None:
+        _R32_BUFS = OrderedDict()
+    key = (device, torch.cuda.current_stream(device).cuda_stream, n, c, h, w, role)
     t = _R32_BUFS.get(key)
     if t is None:
         t = H8Tensor(n, c, h, w, device, _lib.PREC_F32R)
         _R32_BUFS[key] = t
+        while len(_R32_BUFS) > R32_BUFS_MAX:
+            _R32_BUFS.popitem(last=False)
+    else:
+        _R32_BUFS.move_to_end(key)
     return t
+
+
+# Per-launch conv timing for bench.py --train: a list to collect (start event, end event,
+# algorithmic FLOPs, kind) of every conv kernel launch (forward, dgrad, wgrad) on the
+# launch's own stream; None (default): no events.
+PROF = None
+
+
+class _ProfScope:
+    def __init__(self, device, flops, kind):
+        self.on = PROF is not None
+        if self.on:
+            self.st = torch.cuda.current_stream(device)
+            self.e0, self.e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            self.flops, self.kind = flops, kind
+
+    def __enter__(self):
+        if self.on:
+            self.e0.record(self.st)
+        return self
+
+    def __exit__(self, *exc):
+        if self.on:
+            self.e1.record(self.st)
+            PROF.append((self.e0, self.e1, self.flops, self.kind))
+        return False
 
 
 def _wino_conv(x, wpack, bias, rows, cfg, leaky, st, role):
@@ -83,7 +123,9 @@ def _wino_conv(x, wpack, bias, rows, cfg, leaky, st, role):
     d.slope, d.inv_wscale, d.tail_finite = LEAKY_SLOPE, 1.0, 1  # channels [cin, c8) stay zero
     d.src, d.dst = xb.view(0, c8), yb.view(0, r8)
     d.whi, d.wlo, d.bias = wpack.data_ptr(), wpack.data_ptr(), bias.data_ptr()
-    _lib.check(L.rrin_conv3x3_h8_fwd(C.byref(d), st), "rrin_conv3x3_h8_fwd (training)")
+    # Winograd F(2x2,3x3): 4 multiply-adds per output, input channel and pixel
+    with _ProfScope(x.device, 2.0 * 4 * cin * rows * h * w * n, "fwd" if role == "f" else "dgrad"):
+        _lib.check(L.rrin_conv3x3_h8_fwd(C.byref(d), st), "rrin_conv3x3_h8_fwd (training)")
     y = torch.empty((n, rows, h, w), dtype=torch.float32, device=x.device)
     vy = yb.view(0, r8)
     _lib.check(L.rrin_h8_to_nchw(C.byref(vy), n, rows, 0, C.c_void_p(y.data_ptr()), _lib.PREC_F32R, st),
@@ -127,7 +169,8 @@ class _Conv3x3(torch.autograd.Function):
             d = _lib.TConvDesc(n=n, cin=cin, cout=cout, h=h, w=w, mode=_lib.TCONV_FWD, leaky=int(leaky),
                                slope=LEAKY_SLOPE, x=x.data_ptr(), y=None, wt=weight.data_ptr(),
                                bias=bias.data_ptr() if bias is not None else None, out=y.data_ptr())
-            _lib.check(_lib.lib().rrin_tconv3x3(C.byref(d), st), "rrin_tconv3x3 (forward)")
+            with _ProfScope(x.device, 2.0 * 9 * cin * cout * h * w * n, "fwd"):
+                _lib.check(_lib.lib().rrin_tconv3x3(C.byref(d), st), "rrin_tconv3x3 (forward)")
         ctx.leaky = bool(leaky)
         ctx.has_bias = bias is not None
         ctx.save_for_backward(x, weight, y if leaky else None)
@@ -157,7 +200,8 @@ class _Conv3x3(torch.autograd.Function):
             d = _lib.TConvDesc(n=n, cin=cin, cout=cout, h=h, w=w, mode=_lib.TCONV_DGRAD, leaky=int(ctx.leaky),
                                slope=LEAKY_SLOPE, x=gy.data_ptr(), y=y.data_ptr() if ctx.leaky else None,
                                wt=weight.data_ptr(), bias=None, out=gx.data_ptr())
-            _lib.check(L.rrin_tconv3x3(C.byref(d), st), "rrin_tconv3x3 (dgrad)")
+            with _ProfScope(x.device, 2.0 * 9 * cin * cout * h * w * n, "dgrad"):
+                _lib.check(L.rrin_tconv3x3(C.byref(d), st), "rrin_tconv3x3 (dgrad)")
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
             gw = torch.empty_like(weight)
             gb = torch.empty((cout,), dtype=torch.float32, device=x.device)
@@ -173,7 +217,9 @@ class _Conv3x3(torch.autograd.Function):
                 d = _lib.TWgradDesc(n=n, cin=cin, cout=cout, h=h, w=w, leaky=int(ctx.leaky), slope=LEAKY_SLOPE,
                                     x=x.data_ptr(), g=gy.data_ptr(), y=y.data_ptr() if ctx.leaky else None,
                                     gw=gw.data_ptr(), gb=gb.data_ptr(), work=work.data_ptr())
-            _lib.check(L.rrin_tconv3x3_wgrad(C.byref(d), st), "rrin_tconv3x3_wgrad")
+            # direct form: 9 multiply-adds per weight, image and pixel
+            with _ProfScope(x.device, 2.0 * 9 * cin * cout * h * w * n, "wgrad"):
+                _lib.check(L.rrin_tconv3x3_wgrad(C.byref(d), st), "rrin_tconv3x3_wgrad")
         return gx, gw, (gb if ctx.has_bias else None), None
 
 

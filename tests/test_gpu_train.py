@@ -170,3 +170,48 @@ def test_net_backward_is_deterministic(gpu):
         net(a0, i1.to(gpu), 0.3).square().mean().backward()
         grads.append([a0.grad.clone()] + [p.grad.clone() for p in net.parameters()])
     assert all(torch.equal(a, b) for a, b in zip(*grads))
+
+
+@pytest.mark.parametrize("cout,cin", [(64, 32), (40, 24), (3, 13), (128, 64)])
+@pytest.mark.parametrize("bm", [32, 64])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_tpack_wino_matches_host_packing(gpu, cout, cin, bm, mode):
+    """rrin_tpack_wino (device) is bitwise the host packing rrin_pack_conv3x3_wino_bm: mode 0 of
+    W, mode 1 (the dgrad conv) of W transposed (ci <-> co) and flipped (ky, kx -> 2 - ky, 2 - kx);
+    channel counts that are not multiples of 8 pad with zeros the same way."""
+    import ctypes as C
+
+    import numpy as np
+
+    from rrin_amd import _lib
+    lib = _lib.lib()
+    torch.manual_seed(cout * 7 + cin + bm + mode)
+    w = torch.randn(cout, cin, 3, 3)
+    ref_w = w if mode == 0 else w.transpose(0, 1).flip(2, 3)
+    rows, cols = ref_w.shape[:2]
+    wn = ref_w.contiguous().numpy()
+    nf = lib.rrin_pack_conv3x3_wino_bm_floats(rows, cols, bm)
+    host = np.zeros(nf, np.float32)
+    bp = np.zeros(lib.rrin_pack_bias_floats(rows, bm), np.float32)
+    b = np.zeros(rows, np.float32)
+    _lib.check(lib.rrin_pack_conv3x3_wino_bm(wn.ctypes.data, b.ctypes.data, rows, cols, bm, None, host.ctypes.data,
+                                             bp.ctypes.data))
+    wd = w.to(gpu).contiguous()
+    dev = torch.full((nf,), float("nan"), device=gpu)
+    _lib.check(lib.rrin_tpack_wino(C.c_void_p(wd.data_ptr()), cout, cin, bm, mode, C.c_void_p(dev.data_ptr()),
+                                   C.c_void_p(torch.cuda.current_stream(gpu).cuda_stream)))
+    torch.cuda.synchronize(gpu)
+    assert torch.equal(dev.cpu(), torch.from_numpy(host))
+
+
+def test_r32_buffers_per_stream_and_bounded(gpu):
+    """The training convs' record buffers are cached per (stream, shape, role) and the cache is
+    bounded: two streams get distinct buffers, and many shapes do not grow it."""
+    a = ag._r32_buf(1, 8, 16, 32, gpu, "tx")
+    s = torch.cuda.Stream(gpu)
+    with torch.cuda.stream(s):
+        b = ag._r32_buf(1, 8, 16, 32, gpu, "tx")
+    assert a is not b and ag._r32_buf(1, 8, 16, 32, gpu, "tx") is a
+    for h in range(16, 16 + 16 * (ag.R32_BUFS_MAX + 8), 16):
+        ag._r32_buf(1, 8, h, 32, gpu, "ty")
+    assert len(ag._R32_BUFS) <= ag.R32_BUFS_MAX

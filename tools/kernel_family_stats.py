@@ -3,17 +3,26 @@
 instantiations of one kernel summed), to compare the conv family's average
 launch duration with the one bench.py measures with HIP events.
 
-  python tools/kernel_family_stats.py profiles/r01_v9/kernel_stats_split16.csv [kernel_trace.csv FORWARDS [FAMILY]]
+  python tools/kernel_family_stats.py kernel_stats.csv [kernel_trace.csv STEPS [FAMILY ...]]
+        [--parts P] [--ms-per-step MS]
 
-With a kernel_trace.csv and the number of forward steps it holds (warm-up
-included), also the conv family's busy time per step = the union of its
-dispatch spans (the quantity bench.py's roofline divides by when the batch is
-split over several streams).
+With a kernel_trace.csv, also each FAMILY's busy time per step = the union of its
+dispatch spans (the quantity bench.py's roofline divides by when the batch is split
+over several streams).  STEPS is the number of bench steps the trace holds, or
+"auto": the dispatches of the once-per-forward-part kernel (pack_g16_*: one per
+stream part) / P (= bench --streams, default 2).  A profiled `bench.py --steps K
+--warmup W` runs W + K steps plus bench's unprofiled re-run of the K steps: "auto"
+counts them all.  With --ms-per-step (the bench line's own ms_per_step), a family
+whose union per step exceeds it is an error (exit 2): a union longer than the step
+means the step count is wrong.
 """
+import argparse
 import csv
 import re
 import sys
 from collections import defaultdict
+
+MARKER = re.compile(r"^pack_g16_(r32|h8)_kernel$")
 
 
 def family(name):
@@ -21,7 +30,7 @@ def family(name):
     return m.group(1) if m else name[:48]
 
 
-def main(path):
+def stats(path):
     fam = defaultdict(lambda: [0, 0.0])
     for row in csv.DictReader(open(path)):
         f = fam[family(row["Name"])]
@@ -33,21 +42,64 @@ def main(path):
         print(f"{k:32s} {n:6d} {ns / 1e6:10.3f} {ns / 1e6 / n:9.4f} {100 * ns / total:5.1f}%")
 
 
-def busy(trace, forwards, fam_name="conv3x3_h8_kernel"):
-    spans = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]))
-                   for r in csv.DictReader(open(trace)) if family(r["Kernel_Name"]) == fam_name)
+def union_ns(spans):
     tot, end = 0, None
-    for a, b in spans:
+    for a, b in sorted(spans):
         if end is None or a > end:
             tot, end = tot + b - a, b
         elif b > end:
             tot, end = tot + b - end, b
-    dur = sum(b - a for a, b in spans)
-    print(f"{fam_name}: {len(spans)} dispatches, busy (union) {tot / 1e6 / forwards:.3f} ms per step, "
-          f"sum of durations {dur / 1e6 / forwards:.3f} ms per step, overlap {dur / max(tot, 1):.3f}")
+    return tot
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("stats")
+    ap.add_argument("trace", nargs="?")
+    ap.add_argument("steps", nargs="?", default="auto")
+    ap.add_argument("families", nargs="*")
+    ap.add_argument("--parts", type=int, default=2, help="forward parts per step (bench --streams)")
+    ap.add_argument("--ms-per-step", type=float, default=None,
+                    help="the bench line's ms_per_step: a family union above it is an error")
+    a = ap.parse_args()
+    stats(a.stats)
+    if not a.trace:
+        return 0
+    rows = [(family(r["Kernel_Name"]), int(r["Start_Timestamp"]), int(r["End_Timestamp"]))
+            for r in csv.DictReader(open(a.trace))]
+    markers = sum(1 for f, _, _ in rows if MARKER.match(f))
+    if a.steps == "auto":
+        if markers == 0 or markers % a.parts:
+            print(f"cannot derive the step count: {markers} pack_g16 dispatches for {a.parts} parts per step")
+            return 2
+        steps = markers // a.parts
+        how = f"{markers} pack_g16 dispatches / {a.parts} parts"
+    else:
+        steps = int(a.steps)
+        how = "given"
+        if markers and markers != steps * a.parts:
+            print(f"warning: {steps} steps x {a.parts} parts != {markers} pack_g16 dispatches in the trace")
+    print(f"steps in the trace: {steps} ({how})")
+    fams = a.families or ["conv3x3_winoc_kernel"]
+    bad = 0
+    for fam_name in fams:
+        spans = [(s, e) for f, s, e in rows if f == fam_name]
+        if not spans:
+            print(f"{fam_name}: no dispatches")
+            continue
+        tot = union_ns(spans)
+        dur = sum(e - s for s, e in spans)
+        per = tot / 1e6 / steps
+        print(f"{fam_name}: {len(spans)} dispatches ({len(spans) / steps:.1f} per step), busy (union) "
+              f"{per:.3f} ms per step, sum of durations {dur / 1e6 / steps:.3f} ms per step, "
+              f"overlap {dur / max(tot, 1):.3f}")
+        if a.ms_per_step is not None and per > a.ms_per_step:
+            print(f"ERROR: {fam_name} union {per:.3f} ms per step > the bench's {a.ms_per_step:.3f} ms per step")
+            bad += 1
+    allspans = [(s, e) for _, s, e in rows]
+    print(f"all kernels: busy (union) {union_ns(allspans) / 1e6 / steps:.3f} ms per step")
+    return 2 if bad else 0
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
-    if len(sys.argv) > 3:
-        busy(sys.argv[2], int(sys.argv[3]), *sys.argv[4:5])
+    sys.exit(main())

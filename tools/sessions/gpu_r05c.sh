@@ -15,3 +15,5 @@ run() {  # name limit cmd...
 run h8tests 400 python -u -m pytest tests/test_gpu_h8.py -x -q --timeout 120 --timeout-method thread
 SH=32:64:1:1,64:64:1:2,64:64:1:3,128:64:1:1,64:128:2:1,128:128:2:2,128:128:2:3,256:128:2:1,128:256:3:1,256:256:3:1,256:256:3:3,512:256:3:0,256:512:4:1,512:512:4:1,64:128:0:4,128:256:1:4,256:512:2:4
 run cfgab 300 python -u tools/conv_lab.py cfgab --precision fp16 --height 736 --width 1280 --batch 2 --cfgs 10,11,23,26 --shapes $SH --rounds 5 --reps 5
+run traintests 400 python -u -m pytest tests/test_gpu_train.py -x -q --timeout 200 --timeout-method thread
+run bench_train 300 python bench.py --train --steps 5 --warmup 2
