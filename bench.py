@@ -546,6 +546,13 @@ def main():
         # SURVEY §8d per-layer bound: sum_l max(FLOP_l / peak, bytes_l / 8 TB/s) over the body convs
         bpv = 2 if args.precision == "fp16" else 4
         fscale = 4.0 / 9.0 if algo in ("winograd", "mixed") else 1.0
+        if args.precision == "fp16" and algo == "mixed":
+            # per conv: Winograd where engine.wino_f16_ok puts it (an up conv runs on the
+            # low-res grid with 4 x cout rows), else the direct form
+            def fscale(tag, cin, cout, lvl):
+                up = tag.endswith(".up") and lvl <= eng.subpixel_max_level
+                ok = engine_mod.wino_f16_ok(cin, 4 * cout if up else cout, lvl + 1 if up else lvl)
+                return 4.0 / 9.0 if ok else 1.0
         tlb = B * sum(roofline_bound_s(getattr(net, u), H, W, bpv, peak * 1e12, HBM_PEAK_GBS * 1e9, fscale)
                       for u in ("Flow", "refine_flow", "Mask", "final"))
         roofline["t_lb_conv_ms_per_step"] = round(1e3 * tlb, 3)

@@ -249,7 +249,8 @@ int64_t rrin_conv_h8_ring_floats(const rrin_conv_h8_desc* d, int64_t* cnt_ints);
  * persistent register-U tile for cout <= 32 (BM 32 x TH 8, 8 waves).  Kind 6 also
  * runs at RRIN_PREC_F16, and 9 = BM 64 x TH 8 (4 waves, one block per CU) at
  * RRIN_PREC_F16 only (ABI 13: fp16 Winograd, packed by rrin_pack_conv3x3_wino_h8;
- * cin % 16 == 0 or tail_finite; no split-K, no ring fold).  Kinds 2, 5
+ * cin % 16 == 0 or tail_finite; no split-K, no ring fold); 10 and 11 = kinds 6 and 9 on
+ * a persistent grid (workgroups walk tiles; bitwise equal; fp16 only).  Kinds 2, 5
  * and 8 are built only into the lab library: the product library reports them with
  * rrin_conv_h8_cfg_ok == 0 and rrin_conv3x3_h8_fwd returns RRIN_E_CONFIG.
  * 0: direct form. */

@@ -263,8 +263,11 @@ constexpr size_t kWinoCLds2 = (size_t)4096 * 16;  // TH 8: 3 x 768 < 4096
 int launch_winoc(const ConvH8Args& a, int epi, int ct, hipStream_t st);
 // the kind-6 tile at fp16 (conv_winoh.hip): H8 records, v_mfma_f32_32x32x16_f16, packed-f16
 // input transform; same LDS as kWinoCLds1
-// nt = 1 (kind 6: BM 64 x TH 4, two blocks per CU) or 2 (kind 9: BM 64 x TH 8, one block per CU)
-int launch_winoh(const ConvH8Args& a, int epi, int nt, hipStream_t st);
+// nt = 1 (kind 6: BM 64 x TH 4, two blocks per CU) or 2 (kind 9: BM 64 x TH 8, one block per CU);
+// persistent: the tile-walking form (kinds 10 / 11), same bits
+int launch_winoh(const ConvH8Args& a, int epi, int nt, bool persistent, hipStream_t st);
+constexpr size_t kWinoHP1Lds = (size_t)(3 * 512 + 2048 + 128) * 16;  // persistent TH 4: stages + exchange + bias
+constexpr size_t kWinoHP2Lds = (size_t)(3 * 768 + 4096 + 128) * 16;  // persistent TH 8
 // persistent register-U tile for cout <= 32 (conv_winop.hip, kind 8): 8 waves, two raw
 // stages + a separate exchange area + 32 bias floats
 constexpr size_t kWinoPLds = (size_t)(2 * 680 + 2048) * 16 + 128;

@@ -1813,17 +1813,22 @@ static const CfgH8 kCfgH8[] = {
     // kWinoH2Cfg: fp16 only, the register-U tile on 2 patch tiles, BM 64 x TH 8, 4 waves, one
     // block per CU (conv_winoh.hip)
     {64, 8, kWinoCLds2, (size_t)1 << 30, 0, true, 0, 0},
+    // kWinoHP1Cfg / kWinoHP2Cfg: fp16 only, kinds 6 / 9 on a persistent grid (tile-walking workgroups)
+    {64, 4, kWinoHP1Lds, (size_t)1 << 30, 0, true, 0, 0},
+    {64, 8, kWinoHP2Lds, (size_t)1 << 30, 0, true, 0, 0},
 };
 static constexpr int kNumCfgH8 = sizeof(kCfgH8) / sizeof(kCfgH8[0]);
-static constexpr int kWinoCfg = kNumCfgH8 - 9;
-static constexpr int kWino64Cfg = kNumCfgH8 - 8;
-static constexpr int kWinoQCfg = kNumCfgH8 - 7;
-static constexpr int kWinoQ4Cfg = kNumCfgH8 - 6;
-static constexpr int kWino4Cfg = kNumCfgH8 - 5;
-static constexpr int kWinoC2Cfg = kNumCfgH8 - 4;
-static constexpr int kWinoC1Cfg = kNumCfgH8 - 3;
-static constexpr int kWinoPCfg = kNumCfgH8 - 2;
-static constexpr int kWinoH2Cfg = kNumCfgH8 - 1;
+static constexpr int kWinoCfg = kNumCfgH8 - 11;
+static constexpr int kWino64Cfg = kNumCfgH8 - 10;
+static constexpr int kWinoQCfg = kNumCfgH8 - 9;
+static constexpr int kWinoQ4Cfg = kNumCfgH8 - 8;
+static constexpr int kWino4Cfg = kNumCfgH8 - 7;
+static constexpr int kWinoC2Cfg = kNumCfgH8 - 6;
+static constexpr int kWinoC1Cfg = kNumCfgH8 - 5;
+static constexpr int kWinoPCfg = kNumCfgH8 - 4;
+static constexpr int kWinoH2Cfg = kNumCfgH8 - 3;
+static constexpr int kWinoHP1Cfg = kNumCfgH8 - 2;
+static constexpr int kWinoHP2Cfg = kNumCfgH8 - 1;
 static_assert(kWinoCfg == 18, "the direct-form configs keep ids 0-17 (engine tile tables)");
 static inline bool is_winoc(int cfg) { return cfg == kWinoC2Cfg || cfg == kWinoC1Cfg; }
 // tiles whose kernels only the lab library builds (kind 2 wino64, kind 5 F(4x4), kind 8
@@ -1837,10 +1842,12 @@ static constexpr bool kLabBuild = false;
 #endif
 static inline bool is_wino(int cfg) {
   return cfg == kWinoCfg || cfg == kWino64Cfg || cfg == kWinoQCfg || cfg == kWinoQ4Cfg || cfg == kWino4Cfg ||
-         is_winoc(cfg) || cfg == kWinoPCfg || cfg == kWinoH2Cfg;
+         is_winoc(cfg) || cfg == kWinoPCfg || cfg == kWinoH2Cfg || cfg == kWinoHP1Cfg || cfg == kWinoHP2Cfg;
 }
-// the fp16 Winograd tiles (conv_winoh.hip): kind 6 and the fp16-only kind 9
-static inline bool is_winoh(int cfg) { return cfg == kWinoC2Cfg || cfg == kWinoH2Cfg; }
+// fp16-only Winograd tiles: kind 9 and the persistent kinds 10, 11
+static inline bool f16_only(int cfg) { return cfg == kWinoH2Cfg || cfg == kWinoHP1Cfg || cfg == kWinoHP2Cfg; }
+// the fp16 Winograd tiles (conv_winoh.hip): kind 6 and the fp16-only kinds
+static inline bool is_winoh(int cfg) { return cfg == kWinoC2Cfg || f16_only(cfg); }
 static constexpr size_t kMaxLds = 160 * 1024;
 static constexpr int kMaxKSplit = 16;
 
@@ -2023,7 +2030,7 @@ static int h8_prepare(const rrin_conv_h8_desc* d, ConvH8Args& a, bool need_scrat
     if (!is_winoh(d->cfg) || d->ksplit > 1 || d->ring_w) return RRIN_E_CONFIG;
     if ((d->cin & 15) && !d->tail_finite) return RRIN_E_CONFIG;
   } else if (is_wino(d->cfg)) {
-    if (d->prec != RRIN_PREC_F32R || d->cfg == kWinoH2Cfg) return RRIN_E_CONFIG;
+    if (d->prec != RRIN_PREC_F32R || f16_only(d->cfg)) return RRIN_E_CONFIG;
     if ((d->cin & 3) && !d->tail_finite) return RRIN_E_CONFIG;  // stages whole records only
     // the register-U tiles stage both record groups of every chunk: they must exist
     if (is_winoc(d->cfg) && (d->cin & 7) && !d->tail_finite) return RRIN_E_CONFIG;
@@ -2114,6 +2121,8 @@ extern "C" int rrin_conv_h8_cfg_wino(int32_t cfg) {
          : cfg == kWinoC1Cfg ? 7
          : cfg == kWinoPCfg  ? 8
          : cfg == kWinoH2Cfg ? 9
+         : cfg == kWinoHP1Cfg ? 10
+         : cfg == kWinoHP2Cfg ? 11
                              : 0;
 }
 extern "C" int rrin_conv_h8_cfg_ok(int32_t cfg, int32_t prec) {
@@ -2121,7 +2130,7 @@ extern "C" int rrin_conv_h8_cfg_ok(int32_t cfg, int32_t prec) {
   if (!rec_prec(prec) || (lab_only(cfg) && !kLabBuild)) return 0;
   // Winograd tiles: exact fp32 records (kinds 1-8); the register-U kind 6 also at fp16 and
   // kind 9 at fp16 only (conv_winoh.hip)
-  if (is_wino(cfg) && (prec == RRIN_PREC_F16 ? !is_winoh(cfg) : prec != RRIN_PREC_F32R || cfg == kWinoH2Cfg))
+  if (is_wino(cfg) && (prec == RRIN_PREC_F16 ? !is_winoh(cfg) : prec != RRIN_PREC_F32R || f16_only(cfg)))
     return 0;
   return (planes_of(prec) == 2 ? kCfgH8[cfg].lds2 : kCfgH8[cfg].lds1) <= kMaxLds ? 1 : 0;
 }
@@ -2148,7 +2157,9 @@ extern "C" int rrin_conv3x3_h8_fwd(const rrin_conv_h8_desc* d, void* stream) {
   if (d->cfg == kWino64Cfg) return launch_wino64(a, d->epi_mode, st);
   if (d->cfg == kWino4Cfg) return launch_wino4(a, d->epi_mode, st);
 #endif
-  if (is_winoh(d->cfg) && d->prec == RRIN_PREC_F16) return launch_winoh(a, d->epi_mode, d->cfg == kWinoH2Cfg ? 2 : 1, st);
+  if (is_winoh(d->cfg) && d->prec == RRIN_PREC_F16)
+    return launch_winoh(a, d->epi_mode, d->cfg == kWinoH2Cfg || d->cfg == kWinoHP2Cfg ? 2 : 1,
+                        d->cfg == kWinoHP1Cfg || d->cfg == kWinoHP2Cfg, st);
   if (d->cfg == kWinoC2Cfg) return launch_winoc(a, d->epi_mode, 2, st);
   if (d->cfg == kWinoC1Cfg) return launch_winoc(a, d->epi_mode, 1, st);
 #ifdef RRIN_LAB

@@ -184,6 +184,14 @@ def roofline_bound_s(unet: UNet, h: int, w: int, bytes_per_value: int, peak_flop
                      flop_scale: float = 1.0) -> float:
     """Per-layer roofline bound T_LB = sum over body convs of max(FLOP/peak, bytes/BW)
     (SURVEY §8d), in seconds for one image.  ``flop_scale``: FLOPs of the algorithm
-    the convs run per direct-form FLOP (Winograd F(2x2,3x3): 4/9)."""
-    return sum(max(flop_scale * fl / peak_flops, (r + wb) / bw)
-               for _, fl, r, wb in conv_work(unet, h, w, bytes_per_value))
+    the convs run per direct-form FLOP (Winograd F(2x2,3x3): 4/9) -- a number for every
+    conv, or a function of (tag, cin, cout, level) when the form differs by conv."""
+    convs = dict(unet.conv_list())
+
+    def scale(tag):
+        if not callable(flop_scale):
+            return flop_scale
+        c = convs[tag]
+        return flop_scale(tag, c.in_channels, c.out_channels, _level_of(unet, tag))
+    return sum(max(scale(tag) * fl / peak_flops, (r + wb) / bw)
+               for tag, fl, r, wb in conv_work(unet, h, w, bytes_per_value))

@@ -1,0 +1,120 @@
+"""GPU: the fp16 Winograd F(2x2,3x3) tiles (rrin_amd/csrc/conv_winoh.hip) through the C ABI.
+
+Kinds 6 (BM 64 x TH 4, two blocks per CU) and 9 (BM 64 x TH 8, one block per CU) run one tile
+per workgroup; kinds 10 and 11 are the same tiles on a persistent grid: each workgroup walks
+several tiles, its chunk pipeline loads the next tile's first chunks during the current tile's
+last ones, and every epilogue store is an unconditional buffer store (out-of-image positions
+dropped).  The persistent kinds must give the bits of their one-tile forms on grids with many
+more tiles than workgroups (so that the tile walk, the cross-tile prefetch and the counted
+waits all run), for every epilogue; all of them sit within the fp16 gate of float64.
+
+The sizes here have more tiles than a persistent grid has workgroups (2 x 256 for kind 10,
+256 for kind 11 on 256 CUs)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from rrin_amd import _lib
+from rrin_amd.pp import H8Tensor
+from tests.test_gpu_h8 import (conv_h8, keyed_conv, ref_conv, replicate_ring, subpixel_upconv)
+
+pytestmark = pytest.mark.gpu
+F16 = _lib.PREC_F16
+TOLF = dict(rtol=2e-2, atol=2e-2)
+
+
+def kinds():
+    lib = _lib.lib()
+    return {lib.rrin_conv_h8_cfg_wino(c): c for c in range(lib.rrin_conv_h8_cfg_count())
+            if lib.rrin_conv_h8_cfg_ok(c, F16) and lib.rrin_conv_h8_cfg_wino(c)}
+
+
+PAIRS = [(6, 10), (9, 11)]  # one-tile kind -> its persistent kind
+
+
+def test_fp16_winograd_kinds_present():
+    k = kinds()
+    assert set(k) == {6, 9, 10, 11}, k
+    lib = _lib.lib()
+    for a, b in PAIRS:
+        assert lib.rrin_conv_h8_cfg_bm(k[a]) == lib.rrin_conv_h8_cfg_bm(k[b]) == 64
+        assert lib.rrin_conv_h8_cfg_th(k[a]) == lib.rrin_conv_h8_cfg_th(k[b])
+
+
+@pytest.mark.parametrize("epi", [_lib.EPI_LINEAR, _lib.EPI_LEAKY, _lib.EPI_LEAKY_REP, _lib.EPI_LEAKY_POOL])
+@pytest.mark.parametrize("n,cin,cout,h,w", [(2, 64, 128, 96, 256), (1, 256, 256, 46, 80), (3, 32, 64, 36, 300)])
+def test_persistent_bitwise_and_parity(gpu, epi, n, cin, cout, h, w):
+    if epi == _lib.EPI_LEAKY_POOL and (h % 2 or w % 2):
+        pytest.skip("pool needs even sizes")
+    torch.manual_seed(n * cin + cout + h + epi)
+    x = torch.rand(n, cin, h, w, device=gpu) * 2 - 1
+    wt, b = keyed_conv(cin, cout, "winoh")
+    slope = None if epi == _lib.EPI_LINEAR else 0.1
+    ref = ref_conv(x, wt, b, slope)
+    k = kinds()
+    for a, p in PAIRS:
+        outs = []
+        for cfg in (k[a], k[p]):
+            kw = {}
+            if epi == _lib.EPI_LEAKY_POOL:  # the bridge half of a CAT buffer, as the Net writes it
+                kw = dict(dst_off=cout, dst=H8Tensor(n, 2 * cout, h, w, gpu, F16))
+            dst, pool = conv_h8(H8Tensor.from_nchw(x, F16), wt, b, cfg, F16, epi=epi, **kw)
+            outs.append((dst, pool))
+            got = dst.to_nchw(cout, cout) if epi == _lib.EPI_LEAKY_POOL else dst.to_nchw()
+            np.testing.assert_allclose(got.cpu().double().numpy(), ref.numpy(), **TOLF, err_msg=f"cfg {cfg}")
+            if epi == _lib.EPI_LEAKY_POOL:
+                np.testing.assert_allclose(pool.to_nchw().cpu().double().numpy(), F.avg_pool2d(ref, 2).numpy(),
+                                           **TOLF, err_msg=f"cfg {cfg} pool")
+                assert not dst.to_nchw(0, cout).any()
+        (d0, p0), (d1, p1) = outs
+        assert torch.equal(d0.hi, d1.hi), f"kind {p} differs from kind {a}"  # padding / replicated ring too
+        if epi == _lib.EPI_LEAKY_POOL:
+            assert torch.equal(p0.hi, p1.hi)
+        if epi == _lib.EPI_LEAKY_REP:
+            ring = d1.hi[:, :, 0, 8:8 + w]  # the replicated top row equals the first image row
+            assert torch.equal(ring, d1.hi[:, :, 1, 8:8 + w])
+
+
+@pytest.mark.parametrize("n,cin,cout,sh,sw", [(2, 128, 64, 48, 128), (1, 256, 128, 23, 40)])
+def test_persistent_subpixel(gpu, n, cin, cout, sh, sw):
+    """The sub-pixel up conv (unet.py:77-78) on the persistent kinds: ring scratch + interior
+    stores, bitwise the one-tile kinds, within the fp16 gate of upsample-then-conv."""
+    torch.manual_seed(cin + sh)
+    x = torch.rand(n, cin, sh, sw, device=gpu) * 2 - 1
+    wt, b = keyed_conv(cin, cout, "winoh_sub")
+    up = F.interpolate(x.double().cpu(), scale_factor=2, mode="bilinear", align_corners=False)
+    ref = F.conv2d(up, wt.double().cpu(), b.double().cpu(), padding=1)
+    src = H8Tensor.from_nchw(x, F16)
+    replicate_ring(src)
+    k = kinds()
+    for a, p in PAIRS:
+        d0 = subpixel_upconv(src, wt, b, k[a], F16, dst=H8Tensor(n, 2 * cout, 2 * sh, 2 * sw, gpu, F16))
+        d1 = subpixel_upconv(src, wt, b, k[p], F16, dst=H8Tensor(n, 2 * cout, 2 * sh, 2 * sw, gpu, F16))
+        np.testing.assert_allclose(d1.to_nchw(0, cout).cpu().double().numpy(), ref.numpy(), **TOLF)
+        assert torch.equal(d0.hi, d1.hi), f"kind {p} differs from kind {a}"
+        assert not d1.to_nchw(cout, cout).any()
+
+
+def test_persistent_range_guard(gpu):
+    """A value past the fp16 range sets the status flag in the persistent kinds as well."""
+    import ctypes as C
+
+    from tests import hip_helpers as H
+    from tests.test_gpu_h8 import pack_h8
+    n, cin, cout, h, w = 1, 64, 128, 64, 256
+    x = torch.full((n, cin, h, w), 60000.0, device=gpu)
+    wt = torch.full((cout, cin, 3, 3), 1.0)
+    b = torch.zeros(cout)
+    src = H8Tensor.from_nchw(x, F16)
+    for cfg in kinds().values():
+        dst = H8Tensor(n, cout, h, w, gpu, F16)
+        whi, _, bp, inv = pack_h8(wt, b, cfg, F16, gpu)
+        status = torch.zeros(1, dtype=torch.int32, device=gpu)
+        d = _lib.ConvH8Desc()
+        d.n, d.cin, d.cout, d.cfg, d.prec, d.epi_mode, d.slope, d.inv_wscale = n, cin, cout, cfg, F16, 1, 0.1, inv
+        d.src, d.dst = src.view(0, cin), dst.view(0, cout)
+        d.whi, d.bias, d.status = whi.data_ptr(), bp.data_ptr(), status.data_ptr()
+        _lib.check(_lib.lib().rrin_conv3x3_h8_fwd(C.byref(d), H.stream(gpu)))
+        torch.cuda.synchronize(gpu)
+        assert int(status.item()) == 1, f"cfg {cfg}"
