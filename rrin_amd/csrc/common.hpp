@@ -260,7 +260,9 @@ int launch_wino4_lab(const ConvH8Args& a, int abl, hipStream_t st);
 // LDS: max(3 raw stages, the output-transform exchange)
 constexpr size_t kWinoCLds1 = (size_t)2048 * 16;  // TH 4: 3 x 512 stage records < 2048 exchange
 constexpr size_t kWinoCLds2 = (size_t)4096 * 16;  // TH 8: 3 x 768 < 4096
-int launch_winoc(const ConvH8Args& a, int epi, int ct, hipStream_t st);
+// persistent: kind 12 (kind 6 on a persistent grid, conv3x3_winocp_kernel; same bits)
+int launch_winoc(const ConvH8Args& a, int epi, int ct, bool persistent, hipStream_t st);
+constexpr size_t kWinoCPLds = (size_t)(3 * 512 + 2048 + 128) * 16;  // stages + exchange + bias
 // the kind-6 tile at fp16 (conv_winoh.hip): H8 records, v_mfma_f32_32x32x16_f16, packed-f16
 // input transform; same LDS as kWinoCLds1
 // nt = 1 (kind 6: BM 64 x TH 4, two blocks per CU) or 2 (kind 9: BM 64 x TH 8, one block per CU);

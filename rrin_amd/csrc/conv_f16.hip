@@ -1816,21 +1816,24 @@ static const CfgH8 kCfgH8[] = {
     // kWinoHP1Cfg / kWinoHP2Cfg: fp16 only, kinds 6 / 9 on a persistent grid (tile-walking workgroups)
     {64, 4, kWinoHP1Lds, (size_t)1 << 30, 0, true, 0, 0},
     {64, 8, kWinoHP2Lds, (size_t)1 << 30, 0, true, 0, 0},
+    // kWinoCPCfg: exact fp32, kind 6 on a persistent grid (conv3x3_winocp_kernel)
+    {64, 4, kWinoCPLds, (size_t)1 << 30, 0, true, 0, 0},
 };
 static constexpr int kNumCfgH8 = sizeof(kCfgH8) / sizeof(kCfgH8[0]);
-static constexpr int kWinoCfg = kNumCfgH8 - 11;
-static constexpr int kWino64Cfg = kNumCfgH8 - 10;
-static constexpr int kWinoQCfg = kNumCfgH8 - 9;
-static constexpr int kWinoQ4Cfg = kNumCfgH8 - 8;
-static constexpr int kWino4Cfg = kNumCfgH8 - 7;
-static constexpr int kWinoC2Cfg = kNumCfgH8 - 6;
-static constexpr int kWinoC1Cfg = kNumCfgH8 - 5;
-static constexpr int kWinoPCfg = kNumCfgH8 - 4;
-static constexpr int kWinoH2Cfg = kNumCfgH8 - 3;
-static constexpr int kWinoHP1Cfg = kNumCfgH8 - 2;
-static constexpr int kWinoHP2Cfg = kNumCfgH8 - 1;
+static constexpr int kWinoCfg = kNumCfgH8 - 12;
+static constexpr int kWino64Cfg = kNumCfgH8 - 11;
+static constexpr int kWinoQCfg = kNumCfgH8 - 10;
+static constexpr int kWinoQ4Cfg = kNumCfgH8 - 9;
+static constexpr int kWino4Cfg = kNumCfgH8 - 8;
+static constexpr int kWinoC2Cfg = kNumCfgH8 - 7;
+static constexpr int kWinoC1Cfg = kNumCfgH8 - 6;
+static constexpr int kWinoPCfg = kNumCfgH8 - 5;
+static constexpr int kWinoH2Cfg = kNumCfgH8 - 4;
+static constexpr int kWinoHP1Cfg = kNumCfgH8 - 3;
+static constexpr int kWinoHP2Cfg = kNumCfgH8 - 2;
+static constexpr int kWinoCPCfg = kNumCfgH8 - 1;
 static_assert(kWinoCfg == 18, "the direct-form configs keep ids 0-17 (engine tile tables)");
-static inline bool is_winoc(int cfg) { return cfg == kWinoC2Cfg || cfg == kWinoC1Cfg; }
+static inline bool is_winoc(int cfg) { return cfg == kWinoC2Cfg || cfg == kWinoC1Cfg || cfg == kWinoCPCfg; }
 // tiles whose kernels only the lab library builds (kind 2 wino64, kind 5 F(4x4), kind 8
 // the persistent register-U tile):
 // the product library reports them as not usable (rrin_conv_h8_cfg_ok 0)
@@ -2123,6 +2126,7 @@ extern "C" int rrin_conv_h8_cfg_wino(int32_t cfg) {
          : cfg == kWinoH2Cfg ? 9
          : cfg == kWinoHP1Cfg ? 10
          : cfg == kWinoHP2Cfg ? 11
+         : cfg == kWinoCPCfg ? 12
                              : 0;
 }
 extern "C" int rrin_conv_h8_cfg_ok(int32_t cfg, int32_t prec) {
@@ -2160,8 +2164,9 @@ extern "C" int rrin_conv3x3_h8_fwd(const rrin_conv_h8_desc* d, void* stream) {
   if (is_winoh(d->cfg) && d->prec == RRIN_PREC_F16)
     return launch_winoh(a, d->epi_mode, d->cfg == kWinoH2Cfg || d->cfg == kWinoHP2Cfg ? 2 : 1,
                         d->cfg == kWinoHP1Cfg || d->cfg == kWinoHP2Cfg, st);
-  if (d->cfg == kWinoC2Cfg) return launch_winoc(a, d->epi_mode, 2, st);
-  if (d->cfg == kWinoC1Cfg) return launch_winoc(a, d->epi_mode, 1, st);
+  if (d->cfg == kWinoC2Cfg) return launch_winoc(a, d->epi_mode, 2, false, st);
+  if (d->cfg == kWinoCPCfg) return launch_winoc(a, d->epi_mode, 2, true, st);
+  if (d->cfg == kWinoC1Cfg) return launch_winoc(a, d->epi_mode, 1, false, st);
 #ifdef RRIN_LAB
   if (d->cfg == kWinoPCfg) return launch_winop(a, d->epi_mode, st);
 #endif

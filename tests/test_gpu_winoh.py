@@ -1,4 +1,5 @@
-"""GPU: the fp16 Winograd F(2x2,3x3) tiles (rrin_amd/csrc/conv_winoh.hip) through the C ABI.
+"""GPU: the fp16 Winograd F(2x2,3x3) tiles (rrin_amd/csrc/conv_winoh.hip) and the persistent
+exact-fp32 tile (kind 12, conv_winoc.hip) through the C ABI.
 
 Kinds 6 (BM 64 x TH 4, two blocks per CU) and 9 (BM 64 x TH 8, one block per CU) run one tile
 per workgroup; kinds 10 and 11 are the same tiles on a persistent grid: each workgroup walks
@@ -118,3 +119,52 @@ def test_persistent_range_guard(gpu):
         _lib.check(_lib.lib().rrin_conv3x3_h8_fwd(C.byref(d), H.stream(gpu)))
         torch.cuda.synchronize(gpu)
         assert int(status.item()) == 1, f"cfg {cfg}"
+
+
+R32 = _lib.PREC_F32R
+
+
+def kind_cfg(kind, prec):
+    lib = _lib.lib()
+    return next(c for c in range(lib.rrin_conv_h8_cfg_count())
+                if lib.rrin_conv_h8_cfg_wino(c) == kind and lib.rrin_conv_h8_cfg_ok(c, prec))
+
+
+@pytest.mark.parametrize("epi", [_lib.EPI_LINEAR, _lib.EPI_LEAKY, _lib.EPI_LEAKY_REP, _lib.EPI_LEAKY_POOL])
+@pytest.mark.parametrize("n,cin,cout,h,w", [(2, 64, 128, 96, 256), (1, 256, 256, 46, 80), (3, 32, 64, 36, 300)])
+def test_fp32_persistent_bitwise(gpu, epi, n, cin, cout, h, w):
+    """Exact fp32: kind 12 (kind 6 on a persistent grid) gives kind 6's bits on grids of many
+    tiles per workgroup, for every epilogue, within 1e-5 of float64."""
+    if epi == _lib.EPI_LEAKY_POOL and (h % 2 or w % 2):
+        pytest.skip("pool needs even sizes")
+    torch.manual_seed(n * cin + cout + h + epi)
+    x = torch.rand(n, cin, h, w, device=gpu) * 2 - 1
+    wt, b = keyed_conv(cin, cout, "winocp")
+    ref = ref_conv(x, wt, b, None if epi == _lib.EPI_LINEAR else 0.1)
+    outs = []
+    for cfg in (kind_cfg(6, R32), kind_cfg(12, R32)):
+        kw = {}
+        if epi == _lib.EPI_LEAKY_POOL:
+            kw = dict(dst_off=cout, dst=H8Tensor(n, 2 * cout, h, w, gpu, R32))
+        dst, pool = conv_h8(H8Tensor.from_nchw(x, R32), wt, b, cfg, R32, epi=epi, **kw)
+        got = dst.to_nchw(cout, cout) if epi == _lib.EPI_LEAKY_POOL else dst.to_nchw()
+        np.testing.assert_allclose(got.cpu().double().numpy(), ref.numpy(), rtol=1e-5, atol=1e-5)
+        outs.append((dst, pool))
+    assert torch.equal(outs[0][0].hi, outs[1][0].hi)
+    if epi == _lib.EPI_LEAKY_POOL:
+        assert torch.equal(outs[0][1].hi, outs[1][1].hi)
+
+
+@pytest.mark.parametrize("n,cin,cout,sh,sw", [(2, 128, 64, 48, 128), (1, 64, 32, 90, 160)])
+def test_fp32_persistent_subpixel(gpu, n, cin, cout, sh, sw):
+    torch.manual_seed(cin + sh)
+    x = torch.rand(n, cin, sh, sw, device=gpu) * 2 - 1
+    wt, b = keyed_conv(cin, cout, "winocp_sub")
+    up = F.interpolate(x.double().cpu(), scale_factor=2, mode="bilinear", align_corners=False)
+    ref = F.conv2d(up, wt.double().cpu(), b.double().cpu(), padding=1)
+    src = H8Tensor.from_nchw(x, R32)
+    replicate_ring(src)
+    d0 = subpixel_upconv(src, wt, b, kind_cfg(6, R32), R32, dst=H8Tensor(n, 2 * cout, 2 * sh, 2 * sw, gpu, R32))
+    d1 = subpixel_upconv(src, wt, b, kind_cfg(12, R32), R32, dst=H8Tensor(n, 2 * cout, 2 * sh, 2 * sw, gpu, R32))
+    np.testing.assert_allclose(d1.to_nchw(0, cout).cpu().double().numpy(), ref.numpy(), rtol=1e-5, atol=1e-5)
+    assert torch.equal(d0.hi, d1.hi)

@@ -19,3 +19,5 @@ SH=32:64:1:1,64:64:1:2,64:64:1:3,128:64:1:1,64:128:2:1,128:128:2:2,128:128:2:3,2
 run cfgab 400 python -u tools/conv_lab.py cfgab --precision fp16 --height 736 --width 1280 --batch 2 --cfgs 10,11,23,26,27,28 --shapes $SH --rounds 5 --reps 5
 run traintests 400 python -u -m pytest tests/test_gpu_train.py -x -q --timeout 200 --timeout-method thread
 run bench_train 300 python bench.py --train --steps 5 --warmup 2
+SH32=32:64:1:1,64:64:1:2,64:64:1:3,128:64:1:1,64:128:2:1,128:128:2:2,256:128:2:1,128:256:3:1,256:256:3:1,512:512:4:1,64:128:0:4,128:256:1:4,256:512:2:4
+run cfgab32 400 python -u tools/conv_lab.py cfgab --precision fp32 --height 720 --width 1280 --batch 2 --cfgs 23,29 --shapes $SH32 --rounds 5 --reps 3
