@@ -73,7 +73,13 @@ WINO_KERNELS = {1: "conv3x3_wino_kernel (BM 32 x TH 8, 4 waves of 8 accumulators
                 4: "conv3x3_winoq_kernel (BM 32 x TH 4, 4 waves)",
                 6: "conv3x3_winoc_kernel (register-U, BM 64 x TH 4, 4 waves of 2 co tiles)",
                 7: "conv3x3_winoc_kernel (register-U, BM 32 x TH 8, 4 waves of 2 patch tiles)",
-                8: "conv3x3_winop_kernel (persistent register-U, BM 32 x TH 8, 8 waves)"}
+                8: "conv3x3_winop_kernel (persistent register-U, BM 32 x TH 8, 8 waves)",
+                12: "conv3x3_winocp_kernel (register-U, BM 64 x TH 4, persistent grid)"}
+# fp16 Winograd tiles (conv_winoh.hip)
+WINO_KERNELS_F16 = {6: "conv3x3_winoh_kernel (register-U, BM 64 x TH 4)",
+                    9: "conv3x3_winoh_kernel (register-U, BM 64 x TH 8, U on 2 patch tiles)",
+                    10: "conv3x3_winohp_kernel (register-U, BM 64 x TH 4, persistent grid)",
+                    11: "conv3x3_winohp_kernel (register-U, BM 64 x TH 8, persistent grid)"}
 
 
 def kernel_wino(eng, n, h, w):
@@ -82,7 +88,7 @@ def kernel_wino(eng, n, h, w):
     t = eng.conv_table_for(n, h, w)
     kinds = [lib.rrin_conv_h8_cfg_wino(t[i].cfg) for i in range(eng.expected_convs)]
     if eng.precision == "fp16":
-        parts = [f"conv3x3_winoh_kernel (register-U, BM 64 x TH 4, 4 waves of 2 co tiles) x {kinds.count(6)}"]
+        parts = [f"{WINO_KERNELS_F16.get(k, f'kind {k}')} x {kinds.count(k)}" for k in sorted(set(kinds)) if k]
         if kinds.count(0):
             parts.append(f"conv3x3_h8_kernel direct form x {kinds.count(0)}")
         return ("Winograd F(2x2,3x3) on fp16 records, packed-fp16 input transform, v_mfma_f32_32x32x16_f16 "
@@ -136,6 +142,10 @@ def parse():
     ap.add_argument("--no-wino", action="store_true",
                     help="A/B: the direct-form conv (one MFMA product per tap) instead of Winograd F(2x2,3x3), "
                          "exact fp32 and fp16")
+    ap.add_argument("--no-wino-persistent", action="store_true",
+                    help="A/B: exact fp32 kind 6 instead of its persistent form kind 12 (engine.WINO_PERSISTENT)")
+    ap.add_argument("--wino-f16-kind", type=int, default=None,
+                    help="A/B: fp16 Winograd tile kind (6, 9, 10, 11; engine.WINO_F16_KIND)")
     ap.add_argument("--wino-f16-levels", default=None,
                     help="A/B: grid levels of the fp16 Winograd convs, e.g. '2,3,4' (engine.WINO_F16_LEVELS)")
     ap.add_argument("--wino-kind", type=int, default=None,
@@ -390,6 +400,10 @@ def main():
     if args.no_wino:
         engine_mod.WINO = False
         engine_mod.WINO_F16 = False
+    if args.no_wino_persistent:
+        engine_mod.WINO_PERSISTENT = False
+    if args.wino_f16_kind is not None:
+        engine_mod.WINO_F16_KIND = args.wino_f16_kind
     if args.wino_f16_levels is not None:
         engine_mod.WINO_F16_LEVELS = tuple(int(v) for v in args.wino_f16_levels.split(",") if v)
     if args.wino_kind is not None:

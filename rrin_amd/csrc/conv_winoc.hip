@@ -790,12 +790,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winocp_kernel(ConvH8Args a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <int EPI>
-static int launch_winocp_k(const ConvH8Args& a, hipStream_t st) {
-  auto k = conv3x3_winocp_kernel<EPI>;
-  static LdsAttr attr;
-  constexpr size_t lds = WinoCP<EPI>::LDS;
-  if (int e = attr.ensure((const void*)k, (int)lds, st)) return e;
+// CUs of the stream's device (cached per device)
+static int winoc_cus(hipStream_t st) {
   static std::atomic<int> cus[kMaxDevices];
   const int dev = stream_device(st);
   int ncu = cus[dev].load(std::memory_order_relaxed);
@@ -803,6 +799,15 @@ static int launch_winocp_k(const ConvH8Args& a, hipStream_t st) {
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
     cus[dev].store(ncu, std::memory_order_relaxed);
   }
+  return ncu;
+}
+
+template <int EPI>
+static int launch_winocp_k(const ConvH8Args& a, int ncu, hipStream_t st) {
+  auto k = conv3x3_winocp_kernel<EPI>;
+  static LdsAttr attr;
+  constexpr size_t lds = WinoCP<EPI>::LDS;
+  if (int e = attr.ensure((const void*)k, (int)lds, st)) return e;
   const int64_t tiles = (int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n;
   const int64_t grid = tiles < 2 * (int64_t)ncu ? tiles : 2 * (int64_t)ncu;
   hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256), lds, st, a);
@@ -850,22 +855,31 @@ static int winoc_cob_group(const ConvH8Args& a, int bm) {
   return g;
 }
 
+#ifndef RRIN_WINOCP_MIN_WALK
+#define RRIN_WINOCP_MIN_WALK 2
+#endif
 int launch_winoc(const ConvH8Args& a, int epi, int ct, bool persistent, hipStream_t st) {
   ConvH8Args b = a;
   b.cob_group = winoc_cob_group(a, 32 * ct);
   // the persistent form (kind 12: ct 2) needs 2+ chunks, 32-bit byte offsets within an image of
-  // every output view, and 2+ pixels each way for the replicate epilogue; else kind 6 (same bits)
+  // every output view, and 2+ pixels each way for the replicate epilogue; and it pays only where
+  // workgroups walk tiles: from RRIN_WINOCP_MIN_WALK tiles per workgroup slot (two per CU) on
+  // average (a grid of 1.1 tiles per slot -- the 720p level-4 convs -- ran 26 % slower, its few
+  // two-tile workgroups serialising the tail).  Otherwise kind 6: the same bits.
   const int64_t lim = (int64_t)1 << 31;
+  const int ncu = winoc_cus(st);
+  const int64_t tiles = (int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n;
   const bool fits = a.nchunks >= 2 && a.dst_img * 16 < lim && (!a.pool_hi || a.pool_img * 16 < lim) &&
                     (epi != RRIN_EPI_SUBPIXEL || (int64_t)(a.cout >> 2) * a.ring * 4 < lim) &&
-                    (epi != RRIN_EPI_LEAKY_REP || (a.h >= 2 && a.w >= 2));
+                    (epi != RRIN_EPI_LEAKY_REP || (a.h >= 2 && a.w >= 2)) &&
+                    tiles >= (int64_t)RRIN_WINOCP_MIN_WALK * 2 * ncu;
   if (ct == 2 && persistent && fits) {
     switch (epi) {
-      case RRIN_EPI_LINEAR: return launch_winocp_k<RRIN_EPI_LINEAR>(b, st);
-      case RRIN_EPI_LEAKY: return launch_winocp_k<RRIN_EPI_LEAKY>(b, st);
-      case RRIN_EPI_LEAKY_POOL: return launch_winocp_k<RRIN_EPI_LEAKY_POOL>(b, st);
-      case RRIN_EPI_LEAKY_REP: return launch_winocp_k<RRIN_EPI_LEAKY_REP>(b, st);
-      case RRIN_EPI_SUBPIXEL: return launch_winocp_k<RRIN_EPI_SUBPIXEL>(b, st);
+      case RRIN_EPI_LINEAR: return launch_winocp_k<RRIN_EPI_LINEAR>(b, ncu, st);
+      case RRIN_EPI_LEAKY: return launch_winocp_k<RRIN_EPI_LEAKY>(b, ncu, st);
+      case RRIN_EPI_LEAKY_POOL: return launch_winocp_k<RRIN_EPI_LEAKY_POOL>(b, ncu, st);
+      case RRIN_EPI_LEAKY_REP: return launch_winocp_k<RRIN_EPI_LEAKY_REP>(b, ncu, st);
+      case RRIN_EPI_SUBPIXEL: return launch_winocp_k<RRIN_EPI_SUBPIXEL>(b, ncu, st);
     }
     return RRIN_E_ARG;
   }

@@ -836,12 +836,7 @@ static int winoh_cob_group(const ConvH8Args& a) {
   return g;
 }
 
-template <int EPI, int NT>
-static int launch_winohp_k(const ConvH8Args& a, hipStream_t st) {
-  auto k = conv3x3_winohp_kernel<EPI, NT>;
-  static LdsAttr attr;
-  constexpr size_t lds = WinoHP<EPI, NT>::LDS;
-  if (int e = attr.ensure((const void*)k, (int)lds, st)) return e;
+static int winoh_cus(hipStream_t st) {
   static std::atomic<int> cus[kMaxDevices];
   const int dev = stream_device(st);
   int ncu = cus[dev].load(std::memory_order_relaxed);
@@ -849,6 +844,16 @@ static int launch_winohp_k(const ConvH8Args& a, hipStream_t st) {
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
     cus[dev].store(ncu, std::memory_order_relaxed);
   }
+  return ncu;
+}
+
+template <int EPI, int NT>
+static int launch_winohp_k(const ConvH8Args& a, hipStream_t st) {
+  auto k = conv3x3_winohp_kernel<EPI, NT>;
+  static LdsAttr attr;
+  constexpr size_t lds = WinoHP<EPI, NT>::LDS;
+  if (int e = attr.ensure((const void*)k, (int)lds, st)) return e;
+  const int ncu = winoh_cus(st);
   const int64_t tiles = (int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n;
   const int64_t grid = std::min<int64_t>(tiles, (int64_t)ncu * (NT == 1 ? 2 : 1));
   hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256), lds, st, a);
@@ -887,9 +892,13 @@ int launch_winoh(const ConvH8Args& a, int epi, int nt, bool persistent, hipStrea
   // grid of 2+ pixels each way for the replicate epilogue (one row side, one column side per
   // edge pixel); otherwise the one-tile-per-workgroup form of the same tile (same bits)
   const int64_t lim = (int64_t)1 << 31;
+  // ... and it pays only where workgroups walk tiles (as conv_winoc.hip's kind 12): from 2 tiles
+  // per workgroup slot on average
+  const int64_t tiles = (int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n;
   const bool fits = a.nchunks >= 2 && a.dst_img * 16 < lim && (!a.pool_hi || a.pool_img * 16 < lim) &&
                     (epi != RRIN_EPI_SUBPIXEL || (int64_t)(a.cout >> 2) * a.ring * 4 < lim) &&
-                    (epi != RRIN_EPI_LEAKY_REP || (a.h >= 2 && a.w >= 2));
+                    (epi != RRIN_EPI_LEAKY_REP || (a.h >= 2 && a.w >= 2)) &&
+                    tiles >= (int64_t)2 * winoh_cus(st) * (nt == 1 ? 2 : 1);
   if (persistent && fits) return nt == 2 ? launch_winohp_e<2>(b, epi, st) : launch_winohp_e<1>(b, epi, st);
   return nt == 2 ? launch_winoh_e<2>(b, epi, st) : launch_winoh_e<1>(b, epi, st);
 }

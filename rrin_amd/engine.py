@@ -188,11 +188,19 @@ WINO_KIND = 0
 WINO_KIND32 = 3
 
 
+# Kind 12 (round 5): kind 6 on a persistent grid (conv3x3_winocp_kernel: workgroups walk tiles,
+# the next tile's first chunks load during the current tile's last ones; bitwise kind 6).  Per
+# conv at 1280x720 x 2 (profiles/r05/cfgab32_persistent.log): 0.86-0.96 of kind 6's time on the
+# cin 32-128 convs, 0.99-1.00 on the deep ones; the library runs kind 6 itself where a grid has
+# fewer than 2 tiles per workgroup slot (the 720p level-4 convs: 1.26x there).  False: kind 6.
+WINO_PERSISTENT = False  # measured slower in the two-stream forward
+
+
 def wino_kind_for(cout: int) -> int:
     if WINO_KIND != 0:
         return WINO_KIND
     if cout % 64 == 0:
-        return 6
+        return 12 if WINO_PERSISTENT else 6
     return WINO_KIND32 if cout <= 32 else 3
 # ... and kind 4 (the same arithmetic on TH 4 tiles of 4 waves: twice the
 # workgroups) on the few-tile deep convs where that wins, (cin, cout rows, grid
@@ -273,7 +281,12 @@ def wino_cfg(kind: int = None) -> int:
 # (the 32-channel level-0 convs, the 6-16-channel first convs) stay on the direct-form
 # tables.  False: the direct form everywhere (A/B, bench.py --no-wino).
 WINO_F16 = True
-WINO_F16_LEVELS = (1, 2, 3, 4)
+# Per conv at the C3 part size (1280x736 x 2, profiles/r05/cfgab_fp16_winograd.log) the fp16
+# Winograd tile (kind 6) runs 0.77-0.81 of the best direct tile's time at level 4 and 0.92-0.98 at
+# level 3; at levels 1-2 1.0-1.5 (the direct form keeps more operand reuse per VMEM instruction
+# than Winograd's U stream)
+WINO_F16_LEVELS = (4,)
+WINO_F16_KIND = 6
 
 
 def wino_f16_ok(cin: int, cout: int, level: int) -> bool:
@@ -295,7 +308,7 @@ def choose_cfg_h8(cin: int, cout: int, prec: int, level: int = 0, size: str = "l
             return wino_cfg(4)
         return wino_cfg(4 if (cin, cout, level) in WINO_TH4.get(size, ()) else wino_kind_for(cout))
     if prec == _lib.PREC_F16 and wino_f16_ok(cin, cout, level):
-        return wino_cfg(6)
+        return wino_cfg(WINO_F16_KIND)
     table = H8_TUNED_BY_SIZE.get(size, {}).get(prec) or H8_TUNED.get(prec, {})
     cfg = table.get((cin, cout, level))
     if cfg is not None and _lib.lib().rrin_conv_h8_cfg_fits(cfg, prec, cin):

@@ -9,8 +9,9 @@ dropped).  The persistent kinds must give the bits of their one-tile forms on gr
 more tiles than workgroups (so that the tile walk, the cross-tile prefetch and the counted
 waits all run), for every epilogue; all of them sit within the fp16 gate of float64.
 
-The sizes here have more tiles than a persistent grid has workgroups (2 x 256 for kind 10,
-256 for kind 11 on 256 CUs)."""
+The persistent kinds fall back to their one-tile forms below 2 tiles per workgroup slot (two
+slots per CU for kinds 10 and 12, one for kind 11): every size here is above that (checked),
+so the tile walk runs."""
 import numpy as np
 import pytest
 import torch
@@ -34,6 +35,14 @@ def kinds():
 PAIRS = [(6, 10), (9, 11)]  # one-tile kind -> its persistent kind
 
 
+def assert_walks(n, cout_rows, h, w, th, slots_per_cu):
+    """The grid of this conv has >= 2 tiles per persistent workgroup slot (else the library runs
+    the one-tile form and the comparison would test nothing)."""
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    tiles = -(-cout_rows // 64) * -(-w // 32) * -(-h // th) * n
+    assert tiles >= 2 * slots_per_cu * cus, (tiles, cus)
+
+
 def test_fp16_winograd_kinds_present():
     k = kinds()
     assert set(k) == {6, 9, 10, 11}, k
@@ -44,10 +53,12 @@ def test_fp16_winograd_kinds_present():
 
 
 @pytest.mark.parametrize("epi", [_lib.EPI_LINEAR, _lib.EPI_LEAKY, _lib.EPI_LEAKY_REP, _lib.EPI_LEAKY_POOL])
-@pytest.mark.parametrize("n,cin,cout,h,w", [(2, 64, 128, 96, 256), (1, 256, 256, 46, 80), (3, 32, 64, 36, 300)])
+@pytest.mark.parametrize("n,cin,cout,h,w", [(2, 64, 128, 192, 256), (2, 256, 256, 184, 160), (8, 32, 64, 72, 300)])
 def test_persistent_bitwise_and_parity(gpu, epi, n, cin, cout, h, w):
     if epi == _lib.EPI_LEAKY_POOL and (h % 2 or w % 2):
         pytest.skip("pool needs even sizes")
+    assert_walks(n, cout, h, w, 4, 2)
+    assert_walks(n, cout, h, w, 8, 1)
     torch.manual_seed(n * cin + cout + h + epi)
     x = torch.rand(n, cin, h, w, device=gpu) * 2 - 1
     wt, b = keyed_conv(cin, cout, "winoh")
@@ -77,10 +88,12 @@ def test_persistent_bitwise_and_parity(gpu, epi, n, cin, cout, h, w):
             assert torch.equal(ring, d1.hi[:, :, 1, 8:8 + w])
 
 
-@pytest.mark.parametrize("n,cin,cout,sh,sw", [(2, 128, 64, 48, 128), (1, 256, 128, 23, 40)])
+@pytest.mark.parametrize("n,cin,cout,sh,sw", [(2, 128, 64, 96, 256), (2, 256, 128, 92, 160)])
 def test_persistent_subpixel(gpu, n, cin, cout, sh, sw):
     """The sub-pixel up conv (unet.py:77-78) on the persistent kinds: ring scratch + interior
     stores, bitwise the one-tile kinds, within the fp16 gate of upsample-then-conv."""
+    assert_walks(n, 4 * cout, sh, sw, 4, 2)
+    assert_walks(n, 4 * cout, sh, sw, 8, 1)
     torch.manual_seed(cin + sh)
     x = torch.rand(n, cin, sh, sw, device=gpu) * 2 - 1
     wt, b = keyed_conv(cin, cout, "winoh_sub")
@@ -131,12 +144,13 @@ def kind_cfg(kind, prec):
 
 
 @pytest.mark.parametrize("epi", [_lib.EPI_LINEAR, _lib.EPI_LEAKY, _lib.EPI_LEAKY_REP, _lib.EPI_LEAKY_POOL])
-@pytest.mark.parametrize("n,cin,cout,h,w", [(2, 64, 128, 96, 256), (1, 256, 256, 46, 80), (3, 32, 64, 36, 300)])
+@pytest.mark.parametrize("n,cin,cout,h,w", [(2, 64, 128, 192, 256), (2, 256, 256, 184, 160), (8, 32, 64, 72, 300)])
 def test_fp32_persistent_bitwise(gpu, epi, n, cin, cout, h, w):
     """Exact fp32: kind 12 (kind 6 on a persistent grid) gives kind 6's bits on grids of many
     tiles per workgroup, for every epilogue, within 1e-5 of float64."""
     if epi == _lib.EPI_LEAKY_POOL and (h % 2 or w % 2):
         pytest.skip("pool needs even sizes")
+    assert_walks(n, cout, h, w, 4, 2)
     torch.manual_seed(n * cin + cout + h + epi)
     x = torch.rand(n, cin, h, w, device=gpu) * 2 - 1
     wt, b = keyed_conv(cin, cout, "winocp")
@@ -155,8 +169,9 @@ def test_fp32_persistent_bitwise(gpu, epi, n, cin, cout, h, w):
         assert torch.equal(outs[0][1].hi, outs[1][1].hi)
 
 
-@pytest.mark.parametrize("n,cin,cout,sh,sw", [(2, 128, 64, 48, 128), (1, 64, 32, 90, 160)])
+@pytest.mark.parametrize("n,cin,cout,sh,sw", [(2, 128, 64, 96, 256), (5, 64, 32, 90, 160)])
 def test_fp32_persistent_subpixel(gpu, n, cin, cout, sh, sw):
+    assert_walks(n, 4 * cout, sh, sw, 4, 2)
     torch.manual_seed(cin + sh)
     x = torch.rand(n, cin, sh, sw, device=gpu) * 2 - 1
     wt, b = keyed_conv(cin, cout, "winocp_sub")
