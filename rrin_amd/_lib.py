@@ -11,6 +11,9 @@ import os
 
 ABI_VERSION = 13
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "librrin_hip.so")
+# A/B sessions only (tools/sessions/): another build of the same library, e.g. ab/librrin_hip_X.so
+if os.environ.get("RRIN_LIB_AB"):
+    LIB_PATH = os.path.abspath(os.environ["RRIN_LIB_AB"])
 
 # enums (rrin_hip.h)
 SRC_DIRECT, SRC_UPSAMPLE2X = 0, 1

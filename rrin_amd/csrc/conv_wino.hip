@@ -1039,9 +1039,18 @@ __global__ __launch_bounds__(256 * PT, 2) void conv3x3_winoq_kernel(ConvH8Args a
     cob = t % a.co_blocks;
     t /= a.co_blocks;
     t = t * a.tiles_y + ty_;
-#else  // the co blocks of a tile position on consecutive workgroups (they share its raw tile)
-    cob = t % a.co_blocks;
-    t /= a.co_blocks;
+#else  // groups of a.cob_group co blocks (0: one group of all), tile positions within a group,
+       // the group's co blocks of a tile position on consecutive workgroups (they share its raw
+       // tile); an XCD runs consecutive workgroups, so with groups it streams one group's U
+    {
+      const int cpg = a.cob_group > 0 ? a.cob_group : a.co_blocks;
+      const int gsz = cpg * (ntiles / a.co_blocks);
+      const int g = t / gsz;
+      const int r = t - g * gsz;
+      const int cg = min(cpg, a.co_blocks - g * cpg);
+      cob = g * cpg + r % cg;
+      t = r / cg;
+    }
     x0 = (t % a.tiles_x) * 32;
     t /= a.tiles_x;
 #endif
@@ -1491,7 +1500,26 @@ static int launch_winoq_sk(const ConvH8Args& a, int epi, hipStream_t st) {
   return RRIN_E_ARG;
 }
 
-int launch_winoq(const ConvH8Args& a, int epi, int th, hipStream_t st) {
+// Workgroup order of kinds 3 / 4 (as kind 6's, conv_winoc.hip::winoc_cob_group): when the co
+// blocks' U (nchunks x 16 KB each) exceeds RRIN_WINOQ_UGROUP_KB, groups of co blocks whose U fits
+// it, each group's workgroups consecutive -- an XCD then streams one group's U instead of every
+// co block's (the deep split-K convs of small images read each U once per XCD otherwise).  The
+// order changes no result.  Ring-folding launches keep their own index space.
+#ifndef RRIN_WINOQ_UGROUP_KB
+#define RRIN_WINOQ_UGROUP_KB 2048
+#endif
+static int winoq_cob_group(const ConvH8Args& a) {
+  const int64_t per_cob = (int64_t)a.nchunks * kWnU * 16;
+  const int64_t cap = (int64_t)RRIN_WINOQ_UGROUP_KB * 1024;
+  if (RRIN_WINOQ_UGROUP_KB <= 0 || a.nring > 0 || (int64_t)a.co_blocks * per_cob <= cap) return 0;
+  int g = 1;
+  while (2 * g < a.co_blocks && 2 * g * per_cob <= cap) g *= 2;
+  return g;
+}
+
+int launch_winoq(const ConvH8Args& a0, int epi, int th, hipStream_t st) {
+  ConvH8Args a = a0;
+  a.cob_group = winoq_cob_group(a0);
   if (a.ksplit > 1) return th == 4 ? launch_winoq_sk<1>(a, epi, st) : launch_winoq_sk<2>(a, epi, st);
   if (a.nring > 0) {
     if (th != 8 || epi != RRIN_EPI_SUBPIXEL) return RRIN_E_CONFIG;

@@ -82,7 +82,9 @@ def main():
         # convs of a forward part): exact fp32 runs the Winograd tiles (kinds 3/4:
         # conv3x3_winoq_kernel, 6/7: conv3x3_winoc_kernel) and the direct-form first conv
         fam_name = a.family or {"fp32_planar": "conv3x3_mfma_kernel",
-                                "fp32": "conv3x3_winoq_kernel,conv3x3_winoc_kernel,conv3x3_winop_kernel,conv3x3_h8_kernel"}.get(
+                                "fp32": "conv3x3_winoq_kernel,conv3x3_winoc_kernel,conv3x3_winocp_kernel,"
+                                        "conv3x3_winop_kernel,conv3x3_h8_kernel",
+                                "fp16": "conv3x3_h8_kernel,conv3x3_winoh_kernel,conv3x3_winohp_kernel"}.get(
             a.precision, "conv3x3_h8_kernel")
         names = [n for n in fam_name.split(",") if n in res]
         if not names:
