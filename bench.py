@@ -142,8 +142,9 @@ def parse():
     ap.add_argument("--no-wino", action="store_true",
                     help="A/B: the direct-form conv (one MFMA product per tap) instead of Winograd F(2x2,3x3), "
                          "exact fp32 and fp16")
-    ap.add_argument("--no-wino-persistent", action="store_true",
-                    help="A/B: exact fp32 kind 6 instead of its persistent form kind 12 (engine.WINO_PERSISTENT)")
+    ap.add_argument("--wino-persistent", type=int, default=None, choices=[0, 1],
+                    help="A/B: exact fp32 kind 12 (kind 6 on a persistent grid) for the cout %% 64 convs (1) or "
+                         "kind 6 (0); default engine.WINO_PERSISTENT")
     ap.add_argument("--wino-f16-kind", type=int, default=None,
                     help="A/B: fp16 Winograd tile kind (6, 9, 10, 11; engine.WINO_F16_KIND)")
     ap.add_argument("--wino-f16-levels", default=None,
@@ -400,8 +401,8 @@ def main():
     if args.no_wino:
         engine_mod.WINO = False
         engine_mod.WINO_F16 = False
-    if args.no_wino_persistent:
-        engine_mod.WINO_PERSISTENT = False
+    if args.wino_persistent is not None:
+        engine_mod.WINO_PERSISTENT = bool(args.wino_persistent)
     if args.wino_f16_kind is not None:
         engine_mod.WINO_F16_KIND = args.wino_f16_kind
     if args.wino_f16_levels is not None:

@@ -1837,7 +1837,14 @@ static inline bool is_winoc(int cfg) { return cfg == kWinoC2Cfg || cfg == kWinoC
 // tiles whose kernels only the lab library builds (kind 2 wino64, kind 5 F(4x4), kind 8
 // the persistent register-U tile):
 // the product library reports them as not usable (rrin_conv_h8_cfg_ok 0)
-static inline bool lab_only(int cfg) { return cfg == kWino64Cfg || cfg == kWino4Cfg || cfg == kWinoPCfg; }
+// Round 5: the fp16 kinds 9 (one wave per SIMD: 1.2-2.3x kind 6's time per conv) and 10 / 11 (kinds
+// 6 / 9 on a persistent grid: slower in the two-stream forward, and an A/B build with one
+// workgroup per CU ran the C3 forward non-deterministically -- a race not found)
+// are lab-only too.
+static inline bool lab_only(int cfg) {
+  return cfg == kWino64Cfg || cfg == kWino4Cfg || cfg == kWinoPCfg || cfg == kWinoH2Cfg || cfg == kWinoHP1Cfg ||
+         cfg == kWinoHP2Cfg;
+}
 #ifdef RRIN_LAB
 static constexpr bool kLabBuild = true;
 #else

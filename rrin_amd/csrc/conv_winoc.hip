@@ -446,8 +446,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winoc_kernel(ConvH8Args a) {
 // next tile's chunk 0 (raw tile, U) and chunk 1 (raw tile) load during the current tile's last
 // chunks; the exchange area is separate from the raw stages; the epilogue's barriers are bare;
 // every epilogue store is an unconditional buffer store (an out-of-image position gets an offset
-// past the buffer: dropped), so a wave's VMEM count per epilogue is the constant S and the first
-// chunk after it waits for exactly its raw tile; the tile's bias is staged into LDS by LDS-DMA.
+// past the buffer: dropped); the first chunk after an epilogue waits for its raw tile by counting
+// the younger loads only (stores complete out of order with loads); the tile's bias is staged
+// into LDS by LDS-DMA.
 // The cin 32-64 convs (4-8 chunks per tile) spend ~40 % of a one-tile workgroup's life outside
 // its main loop; here that part overlaps the next tile's loads.  Same arithmetic
 // in the same order as kinds 1-7: bitwise equal outputs.
@@ -593,7 +594,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winocp_kernel(ConvH8Args a) {
   const uint4* tbn = tile_base(nxt);
 
   // chunk c (see conv_winoh.hip's persistent chunk): FIRST = chunk 0 of a tile (an epilogue's
-  // S stores and one bias DMA before its loads), LAST = a tile's last chunk (loads the next
+  // stores and one bias DMA before its loads), LAST = a tile's last chunk (loads the next
   // tile's chunk 0 U and chunk 1 raw tile, does not transform)
   auto chunk = [&](int c, int s, const bool first, const bool last) {
     const auto un = last ? urn : ur;
@@ -606,7 +607,11 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winocp_kernel(ConvH8Args a) {
       fence();
     }
     if (first) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * CT + PP::S + 1 < 63 ? 4 * CT + PP::S + 1 : 63) : "memory");
+      // loads complete in order among themselves, stores not in order with them: the younger
+      // LOADS of raw(c + 1) are U(c) pt 3, the bias DMA and U(c + 1) pts 0-2 (the epilogue's
+      // stores in between are not counted -- a count that included them could pass with the
+      // raw tile still in flight once the stores had completed)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * CT + 1) : "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * CT) : "memory");
     }
@@ -636,11 +641,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winocp_kernel(ConvH8Args a) {
   for (int t = 0; t < CT; ++t) u[t][3] = load_u(ur, 0, 3, t);
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * CT + P) : "memory");
   bar();
-  {  // S + 1 VMEM no-ops (distinct offsets past the buffer end: dropped, never merged)
-    const auto nrs = buf_rsrc(a.dst_hi);
-#pragma unroll
-    for (int i = 0; i < PP::S + 1; ++i) __builtin_amdgcn_raw_buffer_store_b32(0u, nrs, kOOB + 256u * i, 0, 0);
-  }
+  issue_bias(cur, tp);  // again, in the after-epilogue position: chunk 0 waits as after an epilogue
   read_raw(0);
   transform();
 
@@ -802,6 +803,11 @@ static int winoc_cus(hipStream_t st) {
   return ncu;
 }
 
+// persistent workgroups per CU (A/B builds: 1 leaves the other slot of every CU to the other
+// stream's kernels)
+#ifndef RRIN_WINOCP_BPC
+#define RRIN_WINOCP_BPC 2
+#endif
 template <int EPI>
 static int launch_winocp_k(const ConvH8Args& a, int ncu, hipStream_t st) {
   auto k = conv3x3_winocp_kernel<EPI>;
@@ -809,7 +815,8 @@ static int launch_winocp_k(const ConvH8Args& a, int ncu, hipStream_t st) {
   constexpr size_t lds = WinoCP<EPI>::LDS;
   if (int e = attr.ensure((const void*)k, (int)lds, st)) return e;
   const int64_t tiles = (int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n;
-  const int64_t grid = tiles < 2 * (int64_t)ncu ? tiles : 2 * (int64_t)ncu;
+  const int64_t slots = (int64_t)RRIN_WINOCP_BPC * ncu;
+  const int64_t grid = tiles < slots ? tiles : slots;
   hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256), lds, st, a);
   return hip_code(hipGetLastError());
 }
@@ -872,7 +879,7 @@ int launch_winoc(const ConvH8Args& a, int epi, int ct, bool persistent, hipStrea
   const bool fits = a.nchunks >= 2 && a.dst_img * 16 < lim && (!a.pool_hi || a.pool_img * 16 < lim) &&
                     (epi != RRIN_EPI_SUBPIXEL || (int64_t)(a.cout >> 2) * a.ring * 4 < lim) &&
                     (epi != RRIN_EPI_LEAKY_REP || (a.h >= 2 && a.w >= 2)) &&
-                    tiles >= (int64_t)RRIN_WINOCP_MIN_WALK * 2 * ncu;
+                    tiles >= (int64_t)RRIN_WINOCP_MIN_WALK * RRIN_WINOCP_BPC * ncu;
   if (ct == 2 && persistent && fits) {
     switch (epi) {
       case RRIN_EPI_LINEAR: return launch_winocp_k<RRIN_EPI_LINEAR>(b, ncu, st);

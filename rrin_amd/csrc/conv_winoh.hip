@@ -411,6 +411,7 @@ __global__ __launch_bounds__(256, NT == 1 ? 2 : 1) void conv3x3_winoh_kernel(Con
   if (bad && a.status) *a.status = 1;
 }
 
+#ifdef RRIN_LAB  // kinds 9-11 (one block per CU, persistent grids): lab library only
 // ---- persistent form (kinds 10 / 11): a workgroup walks tiles bid, bid + grid, ... and its
 // chunk pipeline runs on across tile boundaries.  At fp16 a tile's MFMAs take a few us, about
 // what its prologue (raw tile and U from memory) and epilogue (output-transform exchange,
@@ -419,8 +420,10 @@ __global__ __launch_bounds__(256, NT == 1 ? 2 : 1) void conv3x3_winoh_kernel(Con
 // current tile's last chunks, and its B operands transformed, before the epilogue runs.  The
 // exchange area is separate from the raw stages; the epilogue's barriers are bare (no vmcnt
 // drain); every epilogue store is an unconditional buffer store (an out-of-image position gets
-// an offset past the buffer: the store is dropped), so a wave's VMEM count per epilogue is a
-// constant (WinoHP::S) and the first chunk after it waits for exactly its raw tile.  The bias
+// an offset past the buffer: the store is dropped).  The first chunk after an epilogue waits for
+// its raw tile by counting the younger loads only: loads complete in order among themselves, but
+// not in order with stores (LLVM's waitcnt pass treats mixed pending reads and writes the same
+// way), so a count that included the epilogue's stores could pass early.  The bias
 // of a tile is staged into LDS by LDS-DMA at the tile's start.  Same arithmetic, in the same
 // order, as conv3x3_winoh_kernel: the outputs are bitwise those of kinds 6 / 9.
 template <int EPI, int NT>
@@ -574,8 +577,8 @@ __global__ __launch_bounds__(256, NT == 1 ? 2 : 1) void conv3x3_winohp_kernel(Co
   // the next tile; raw(c + 2) is this tile's chunk c + 2 or the next tile's chunk c + 2 - nch.
   // Without a next tile the loads re-read this tile's (a dummy raw tile into the free stage, U
   // of chunk 0 into registers no MFMA reads again), so every chunk issues the same VMEM.
-  // FIRST (chunk 0 of a tile): the epilogue's PP::S stores and one bias DMA sit between
-  // raw(c + 1) and this chunk's loads (the first tile's prologue pads to the same count).
+  // FIRST (chunk 0 of a tile): the epilogue's stores and one bias DMA sit between raw(c + 1) and
+  // this chunk's loads (the first tile's prologue issues the same bias DMA).
   // A tile's last chunk does not transform: the next tile's chunk 0 is read and transformed
   // after the epilogue, so its B operands are not live across it.
   auto chunk = [&](int c, int s, const bool first, const bool last) {
@@ -590,8 +593,11 @@ __global__ __launch_bounds__(256, NT == 1 ? 2 : 1) void conv3x3_winohp_kernel(Co
       fence();
     }
     if (first) {
-      // (vmcnt holds 6 bits: a larger count waits for some of the epilogue's stores too)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * CT + PP::S + 1 < 63 ? 4 * CT + PP::S + 1 : 63) : "memory");
+      // loads complete in order among themselves, stores not in order with them: the younger
+      // LOADS of raw(c + 1) are U(c) pt 3, the bias DMA and U(c + 1) pts 0-2 (the epilogue's
+      // stores in between are not counted -- a count that included them could pass with the
+      // raw tile still in flight once the stores had completed)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * CT + 1) : "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * CT) : "memory");
     }
@@ -616,9 +622,8 @@ __global__ __launch_bounds__(256, NT == 1 ? 2 : 1) void conv3x3_winohp_kernel(Co
     for (int t = 0; t < CT; ++t) u[t][3] = load_u(un, cn, 3, t);
   };
 
-  // prologue (first tile): bias, raw(0), U(0) pts 0-2, raw(1), U(0) pt 3; wait for raw(0); then
-  // PP::S + 1 VMEM no-ops (stores past the buffer end, dropped) so that chunk 0 waits as after
-  // an epilogue
+  // prologue (first tile): bias, raw(0), U(0) pts 0-2, raw(1), U(0) pt 3; wait for raw(0); the
+  // bias DMA again, so that chunk 0 waits as after an epilogue
   int tp = 0;
   issue_bias(cur, tp);
   issue_raw_at(tb, 0);
@@ -631,12 +636,7 @@ __global__ __launch_bounds__(256, NT == 1 ? 2 : 1) void conv3x3_winohp_kernel(Co
   for (int t = 0; t < CT; ++t) u[t][3] = load_u(ur, 0, 3, t);
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * CT + P) : "memory");
   bar();
-  {
-    const auto nrs = wh_rsrc(a.dst_hi);
-    // distinct, non-adjacent offsets: the compiler neither drops nor merges them
-#pragma unroll
-    for (int i = 0; i < PP::S + 1; ++i) __builtin_amdgcn_raw_buffer_store_b32(0u, nrs, kOOB + 256u * i, 0, 0);
-  }
+  issue_bias(cur, tp);  // again, in the after-epilogue position: chunk 0 waits as after an epilogue
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) {
     read_raw(0, nt);
@@ -765,8 +765,8 @@ __global__ __launch_bounds__(256, NT == 1 ? 2 : 1) void conv3x3_winohp_kernel(Co
               X[(yw * 4 + k) * 64 + lane] = g;
             }
             bar();
-            // every wave stores (wave 0's values; the other waves' stores are dropped), so the
-            // store count per wave is PP::S
+            // every wave stores (wave 0's values; the other waves' stores are dropped): no
+            // wave-dependent branch around stores
             const int xp = cur.x0 + 2 * jx, yp = cur.y0 + 2 * pr;
             const auto prs = wh_rsrc(a.pool_hi + (int64_t)cur.img * a.pool_img);
 #pragma unroll
@@ -812,6 +812,7 @@ __global__ __launch_bounds__(256, NT == 1 ? 2 : 1) void conv3x3_winohp_kernel(Co
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every LDS-DMA has landed before the workgroup ends
   if (bad && a.status) *a.status = 1;
 }
+#endif  // RRIN_LAB (conv3x3_winohp_kernel)
 
 template <int EPI, int NT>
 static int launch_winoh_k(const ConvH8Args& a, hipStream_t st) {
@@ -836,6 +837,7 @@ static int winoh_cob_group(const ConvH8Args& a) {
   return g;
 }
 
+#ifdef RRIN_LAB
 static int winoh_cus(hipStream_t st) {
   static std::atomic<int> cus[kMaxDevices];
   const int dev = stream_device(st);
@@ -847,6 +849,10 @@ static int winoh_cus(hipStream_t st) {
   return ncu;
 }
 
+// persistent workgroups per CU of kind 10 (A/B builds: 1 leaves a slot per CU to the other stream)
+#ifndef RRIN_WINOHP_BPC
+#define RRIN_WINOHP_BPC 2
+#endif
 template <int EPI, int NT>
 static int launch_winohp_k(const ConvH8Args& a, hipStream_t st) {
   auto k = conv3x3_winohp_kernel<EPI, NT>;
@@ -855,7 +861,7 @@ static int launch_winohp_k(const ConvH8Args& a, hipStream_t st) {
   if (int e = attr.ensure((const void*)k, (int)lds, st)) return e;
   const int ncu = winoh_cus(st);
   const int64_t tiles = (int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n;
-  const int64_t grid = std::min<int64_t>(tiles, (int64_t)ncu * (NT == 1 ? 2 : 1));
+  const int64_t grid = std::min<int64_t>(tiles, (int64_t)ncu * (NT == 1 ? RRIN_WINOHP_BPC : 1));
   hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256), lds, st, a);
   return hip_code(hipGetLastError());
 }
@@ -871,6 +877,7 @@ static int launch_winohp_e(const ConvH8Args& b, int epi, hipStream_t st) {
   }
   return RRIN_E_ARG;
 }
+#endif  // RRIN_LAB
 
 template <int NT>
 static int launch_winoh_e(const ConvH8Args& b, int epi, hipStream_t st) {
@@ -891,6 +898,7 @@ int launch_winoh(const ConvH8Args& a, int epi, int nt, bool persistent, hipStrea
   // byte offsets within an image of every output view (its stores are buffer stores), and a
   // grid of 2+ pixels each way for the replicate epilogue (one row side, one column side per
   // edge pixel); otherwise the one-tile-per-workgroup form of the same tile (same bits)
+#ifdef RRIN_LAB
   const int64_t lim = (int64_t)1 << 31;
   // ... and it pays only where workgroups walk tiles (as conv_winoc.hip's kind 12): from 2 tiles
   // per workgroup slot on average
@@ -898,9 +906,13 @@ int launch_winoh(const ConvH8Args& a, int epi, int nt, bool persistent, hipStrea
   const bool fits = a.nchunks >= 2 && a.dst_img * 16 < lim && (!a.pool_hi || a.pool_img * 16 < lim) &&
                     (epi != RRIN_EPI_SUBPIXEL || (int64_t)(a.cout >> 2) * a.ring * 4 < lim) &&
                     (epi != RRIN_EPI_LEAKY_REP || (a.h >= 2 && a.w >= 2)) &&
-                    tiles >= (int64_t)2 * winoh_cus(st) * (nt == 1 ? 2 : 1);
+                    tiles >= (int64_t)2 * winoh_cus(st) * (nt == 1 ? RRIN_WINOHP_BPC : 1);
   if (persistent && fits) return nt == 2 ? launch_winohp_e<2>(b, epi, st) : launch_winohp_e<1>(b, epi, st);
   return nt == 2 ? launch_winoh_e<2>(b, epi, st) : launch_winoh_e<1>(b, epi, st);
+#else
+  if (persistent || nt != 1) return RRIN_E_CONFIG;  // kinds 9-11: lab library only
+  return launch_winoh_e<1>(b, epi, st);
+#endif
 }
 
 }  // namespace rrin

@@ -11,7 +11,10 @@ waits all run), for every epilogue; all of them sit within the fp16 gate of floa
 
 The persistent kinds fall back to their one-tile forms below 2 tiles per workgroup slot (two
 slots per CU for kinds 10 and 12, one for kind 11): every size here is above that (checked),
-so the tile walk runs."""
+so the tile walk runs.
+
+Kinds 9-11 are built into the lab library only: their tests run against it
+(RRIN_LIB_AB=rrin_amd/librrin_lab.so after `make lab`) and skip on the product library."""
 import numpy as np
 import pytest
 import torch
@@ -35,6 +38,11 @@ def kinds():
 PAIRS = [(6, 10), (9, 11)]  # one-tile kind -> its persistent kind
 
 
+def need_lab_kinds():
+    if not {9, 10, 11} <= set(kinds()):
+        pytest.skip("fp16 kinds 9-11: lab library only")
+
+
 def assert_walks(n, cout_rows, h, w, th, slots_per_cu):
     """The grid of this conv has >= 2 tiles per persistent workgroup slot (else the library runs
     the one-tile form and the comparison would test nothing)."""
@@ -45,7 +53,8 @@ def assert_walks(n, cout_rows, h, w, th, slots_per_cu):
 
 def test_fp16_winograd_kinds_present():
     k = kinds()
-    assert set(k) == {6, 9, 10, 11}, k
+    assert set(k) in ({6}, {6, 9, 10, 11}), k
+    need_lab_kinds()
     lib = _lib.lib()
     for a, b in PAIRS:
         assert lib.rrin_conv_h8_cfg_bm(k[a]) == lib.rrin_conv_h8_cfg_bm(k[b]) == 64
@@ -55,6 +64,7 @@ def test_fp16_winograd_kinds_present():
 @pytest.mark.parametrize("epi", [_lib.EPI_LINEAR, _lib.EPI_LEAKY, _lib.EPI_LEAKY_REP, _lib.EPI_LEAKY_POOL])
 @pytest.mark.parametrize("n,cin,cout,h,w", [(2, 64, 128, 192, 256), (2, 256, 256, 184, 160), (8, 32, 64, 72, 300)])
 def test_persistent_bitwise_and_parity(gpu, epi, n, cin, cout, h, w):
+    need_lab_kinds()
     if epi == _lib.EPI_LEAKY_POOL and (h % 2 or w % 2):
         pytest.skip("pool needs even sizes")
     assert_walks(n, cout, h, w, 4, 2)
@@ -92,6 +102,7 @@ def test_persistent_bitwise_and_parity(gpu, epi, n, cin, cout, h, w):
 def test_persistent_subpixel(gpu, n, cin, cout, sh, sw):
     """The sub-pixel up conv (unet.py:77-78) on the persistent kinds: ring scratch + interior
     stores, bitwise the one-tile kinds, within the fp16 gate of upsample-then-conv."""
+    need_lab_kinds()
     assert_walks(n, 4 * cout, sh, sw, 4, 2)
     assert_walks(n, 4 * cout, sh, sw, 8, 1)
     torch.manual_seed(cin + sh)
@@ -112,6 +123,7 @@ def test_persistent_subpixel(gpu, n, cin, cout, sh, sw):
 
 def test_persistent_range_guard(gpu):
     """A value past the fp16 range sets the status flag in the persistent kinds as well."""
+    need_lab_kinds()
     import ctypes as C
 
     from tests import hip_helpers as H
@@ -183,3 +195,46 @@ def test_fp32_persistent_subpixel(gpu, n, cin, cout, sh, sw):
     d1 = subpixel_upconv(src, wt, b, kind_cfg(12, R32), R32, dst=H8Tensor(n, 2 * cout, 2 * sh, 2 * sw, gpu, R32))
     np.testing.assert_allclose(d1.to_nchw(0, cout).cpu().double().numpy(), ref.numpy(), rtol=1e-5, atol=1e-5)
     assert torch.equal(d0.hi, d1.hi)
+
+
+@pytest.mark.parametrize("prec,kind", [(F16, 6), (F16, 10), (R32, 6), (R32, 12)])
+def test_winograd_conv_bitwise_beside_side_stream_conv(gpu, prec, kind):
+    """A Winograd conv (cin 256, a 920-tile grid as at the C3 part size's level 3) is bitwise the
+    same whether or not an LDS-DMA + MFMA conv loops on another stream (the two share CUs):
+    the fp16 tiles' packed-f16 input transform and the persistent tiles' cross-tile pipeline
+    beside another kernel (DESIGN.md §9's hazard class)."""
+    import ctypes as C
+
+    from tests import hip_helpers as H
+    from tests.test_gpu_concurrency import side_conv
+    n, cin, cout, h, w = 2, 256, 256, 92, 160
+    x = H8Tensor.from_nchw(torch.rand(n, cin, h, w, device=gpu) * 2 - 1, prec)
+    wt, b = keyed_conv(cin, cout, "conc")
+    if kind not in kinds() and prec == F16:
+        pytest.skip(f"fp16 kind {kind}: lab library only")
+    cfg = kind_cfg(kind, prec)
+    ref, _ = conv_h8(x, wt, b, cfg, prec, epi=_lib.EPI_LEAKY)
+    lib, d, keep = side_conv(gpu, F16)
+    side = torch.cuda.Stream(gpu)
+    main = torch.cuda.current_stream(gpu)
+    from tests.test_gpu_h8 import pack_h8
+    whi, _, bp, inv = pack_h8(wt, b, cfg, prec, gpu)
+    outs = [H8Tensor(n, cout, h, w, gpu, prec) for _ in range(8)]
+    dd = []
+    for o in outs:
+        e = _lib.ConvH8Desc()
+        e.n, e.cin, e.cout, e.cfg, e.prec, e.epi_mode, e.slope, e.inv_wscale = n, cin, cout, cfg, prec, 1, 0.1, inv
+        e.src, e.dst = x.view(0, cin), o.view(0, cout)
+        e.whi, e.wlo, e.bias = whi.data_ptr(), whi.data_ptr(), bp.data_ptr()
+        dd.append(e)
+    bad = 0
+    for _ in range(4):
+        side.wait_stream(main)
+        st = C.c_void_p(side.cuda_stream)
+        for _ in range(200):
+            _lib.check(lib.rrin_conv3x3_h8_fwd(C.byref(d), st))
+        for e in dd:
+            _lib.check(_lib.lib().rrin_conv3x3_h8_fwd(C.byref(e), H.stream(gpu)))
+        torch.cuda.synchronize(gpu)
+        bad += sum(int(not torch.equal(o.hi, ref.hi)) for o in outs)
+    assert bad == 0, f"{bad}/32 convs differ from the serial result"

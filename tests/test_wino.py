@@ -94,7 +94,7 @@ def test_wino_config_entry():
     # tiles 6 (BM 64 x TH 4) and 7 (BM 32 x TH 8), 4 waves; 8 the persistent register-U tile
     # for cout <= 32 (BM 32 x TH 8, 8 waves)
     # 9: the fp16-only register-U tile on 2 patch tiles (BM 64 x TH 8, one block per CU); 10, 11:
-    # kinds 6 and 9 on a persistent grid (fp16 only)
+    # kinds 6 and 9 on a persistent grid (fp16 only; 9-11 are built into the lab library only)
     # 12: kind 6 on a persistent grid (exact fp32)
     assert sorted(lib.rrin_conv_h8_cfg_wino(c) for c in ids) == [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12]
     assert min(ids) == 18  # the direct-form configs keep ids 0-17 (engine tile tables)
@@ -106,9 +106,10 @@ def test_wino_config_entry():
         # kinds 2, 5 and 8 lost on every Net shape: their kernels are built only into the lab
         # library (make lab), so the product library reports them as not usable
         assert lib.rrin_conv_h8_cfg_ok(c, _lib.PREC_F32R) == (0 if kind in (2, 5, 8, 9, 10, 11) else 1)
-        # split16 never runs a Winograd tile; fp16 runs kinds 6, 9, 10, 11 (conv_winoh.hip, ABI 13)
+        # split16 never runs a Winograd tile; fp16 runs kind 6 (conv_winoh.hip, ABI 13; the lab
+        # library also 9, 10, 11)
         assert lib.rrin_conv_h8_cfg_ok(c, _lib.PREC_F16X3) == 0
-        assert lib.rrin_conv_h8_cfg_ok(c, _lib.PREC_F16) == (1 if kind in (6, 9, 10, 11) else 0)
+        assert lib.rrin_conv_h8_cfg_ok(c, _lib.PREC_F16) == (1 if kind == 6 else 0)
     assert lib.rrin_pack_conv3x3_wino_floats(33, 5) == 2 * 1 * 16 * 2 * 32 * 4
     assert lib.rrin_pack_conv3x3_wino_floats(0, 5) < 0
     assert lib.rrin_pack_conv3x3_wino_bm_floats(65, 9, 64) == 2 * 2 * 16 * 2 * 64 * 4
