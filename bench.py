@@ -89,8 +89,12 @@ def kernel_wino(eng, n, h, w):
     kinds = [lib.rrin_conv_h8_cfg_wino(t[i].cfg) for i in range(eng.expected_convs)]
     if eng.precision == "fp16":
         parts = [f"{WINO_KERNELS_F16.get(k, f'kind {k}')} x {kinds.count(k)}" for k in sorted(set(kinds)) if k]
-        if kinds.count(0):
-            parts.append(f"conv3x3_h8_kernel direct form x {kinds.count(0)}")
+        fused = sum(int(t[i].fuse_next) for i in range(eng.expected_convs))
+        if fused:
+            parts.append(f"conv_block0_h8_kernel (fused level-0 UNetConvBlock, conv a's tile in LDS) x {fused} "
+                         f"(= {2 * fused} convs)")
+        if kinds.count(0) - 2 * fused:
+            parts.append(f"conv3x3_h8_kernel direct form x {kinds.count(0) - 2 * fused}")
         return ("Winograd F(2x2,3x3) on fp16 records, packed-fp16 input transform, v_mfma_f32_32x32x16_f16 "
                 "contraction per transform point, fp32 output transform: " + "; ".join(parts))
     parts = [f"{WINO_KERNELS.get(k, f'kind {k}')} x {kinds.count(k)}" for k in sorted(set(kinds)) if k]
@@ -142,6 +146,9 @@ def parse():
     ap.add_argument("--no-wino", action="store_true",
                     help="A/B: the direct-form conv (one MFMA product per tap) instead of Winograd F(2x2,3x3), "
                          "exact fp32 and fp16")
+    ap.add_argument("--fuse-l0", type=int, default=None, choices=[0, 1],
+                    help="fp16: each level-0 UNetConvBlock as one fused launch (1) or two (0); "
+                         "default engine.FUSE_L0")
     ap.add_argument("--wino-persistent", type=int, default=None, choices=[0, 1],
                     help="A/B: exact fp32 kind 12 (kind 6 on a persistent grid) for the cout %% 64 convs (1) or "
                          "kind 6 (0); default engine.WINO_PERSISTENT")
@@ -403,6 +410,8 @@ def main():
         engine_mod.WINO_F16 = False
     if args.wino_persistent is not None:
         engine_mod.WINO_PERSISTENT = bool(args.wino_persistent)
+    if args.fuse_l0 is not None:
+        engine_mod.FUSE_L0 = bool(args.fuse_l0)
     if args.wino_f16_kind is not None:
         engine_mod.WINO_F16_KIND = args.wino_f16_kind
     if args.wino_f16_levels is not None:

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define RRIN_ABI_VERSION 13
+#define RRIN_ABI_VERSION 14
 
 #define RRIN_OK 0
 #define RRIN_E_SHAPE (-1)     /* H or W not a multiple of 16, or N < 1          */
@@ -221,6 +221,28 @@ typedef struct rrin_conv_h8_desc {
                                   every call leaves it zero again */
 } rrin_conv_h8_desc;
 
+/* Fused level-0 UNetConvBlock at fp16 (unet.py:59-63, and :46 for down_path[0]): conv a
+ * (cin -> 32) + LeakyReLU, conv b (32 -> 32) + LeakyReLU, optionally the 2x2 average pool of the
+ * result, in one launch; conv a's output never reaches memory (an 8 x 62 output tile's conv-a
+ * values, 1-pixel halo recomputed, stay in LDS).  The weights are the two convs' own
+ * rrin_pack_conv3x3_h8 packs (fp16, the bm of cfg_a / cfg_b, direct-form configs); the outputs
+ * are bitwise those of the two rrin_conv3x3_h8_fwd calls (EPI_LEAKY into a 32-channel tensor,
+ * then EPI_LEAKY or EPI_LEAKY_POOL) at fp16.  dst must not overlap src.  ABI 14. */
+typedef struct rrin_block0_h8_desc {
+  int32_t n, cin;              /* conv a: cin -> 32 (cin % 8 == 0 or tail_finite); conv b: 32 -> 32 */
+  int32_t cfg_a, cfg_b;        /* rrin_conv_h8 configs the packs were made for (direct form) */
+  float slope;                 /* 0 <= slope <= 1 */
+  float inv_wscale_a, inv_wscale_b; /* from rrin_pack_conv3x3_h8 */
+  int32_t tail_finite;         /* as rrin_conv_h8_desc.tail_finite */
+  rrin_h8 src, dst, pool;      /* fp16 records; pool.hi NULL: no pool output */
+  const void* whi_a;
+  const float* bias_a;
+  const void* whi_b;
+  const float* bias_b;
+  int32_t* status;             /* optional fp16 range flag, as rrin_conv_h8_desc.status */
+} rrin_block0_h8_desc;
+int rrin_conv_block0_h8_fwd(const rrin_block0_h8_desc* d, void* stream);
+
 int rrin_conv_h8_cfg_count(void);
 int rrin_conv_h8_cfg_bm(int32_t cfg);
 int rrin_conv_h8_cfg_th(int32_t cfg);
@@ -392,6 +414,9 @@ typedef struct rrin_conv_weights {
                            the forward's workspace holds the split scratch */
   const float* wedge;   /* subpixel: original weights [cin][9][cout] fp32      */
   const float* bias_raw;/* subpixel: original bias [cout]                      */
+  int32_t fuse_next;    /* F16, level-0 conv a of a UNetConvBlock: 1 = run it and the next
+                           conv as one rrin_conv_block0_h8_fwd launch (ABI 14) */
+  int32_t pad_;
 } rrin_conv_weights;
 
 typedef struct rrin_head_weights {

@@ -9,7 +9,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-ABI_VERSION = 13
+ABI_VERSION = 14
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "librrin_hip.so")
 # A/B sessions only (tools/sessions/): another build of the same library, e.g. ab/librrin_hip_X.so
 if os.environ.get("RRIN_LIB_AB"):
@@ -58,7 +58,7 @@ class HeadDesc(C.Structure):
 class ConvWeights(C.Structure):
     _fields_ = [("wpack", C.c_void_p), ("bias", C.c_void_p), ("cfg", C.c_int32), ("inv_wscale", C.c_float),
                 ("whi", C.c_void_p), ("wlo", C.c_void_p), ("subpixel", C.c_int32), ("ksplit", C.c_int32),
-                ("wedge", C.c_void_p), ("bias_raw", C.c_void_p)]
+                ("wedge", C.c_void_p), ("bias_raw", C.c_void_p), ("fuse_next", C.c_int32), ("pad_", C.c_int32)]
 
 
 class H8(C.Structure):
@@ -73,6 +73,13 @@ class ConvH8Desc(C.Structure):
                 ("bias", C.c_void_p), ("edge", C.c_void_p), ("status", C.c_void_p), ("ksplit", C.c_int32),
                 ("pad2_", C.c_int32), ("part", C.c_void_p), ("cnt", C.c_void_p), ("ring_w", C.c_void_p),
                 ("ring_bias", C.c_void_p), ("ring_corr", C.c_void_p), ("ring_cnt", C.c_void_p)]
+
+
+class Block0Desc(C.Structure):
+    _fields_ = [("n", C.c_int32), ("cin", C.c_int32), ("cfg_a", C.c_int32), ("cfg_b", C.c_int32),
+                ("slope", C.c_float), ("inv_wscale_a", C.c_float), ("inv_wscale_b", C.c_float),
+                ("tail_finite", C.c_int32), ("src", H8), ("dst", H8), ("pool", H8), ("whi_a", C.c_void_p),
+                ("bias_a", C.c_void_p), ("whi_b", C.c_void_p), ("bias_b", C.c_void_p), ("status", C.c_void_p)]
 
 
 class EdgeFixDesc(C.Structure):
@@ -155,6 +162,7 @@ SIGNATURES = {
     "rrin_conv_h8_cfg_ok": (C.c_int, [C.c_int32, C.c_int32]),
     "rrin_conv_h8_cfg_fits": (C.c_int, [C.c_int32, C.c_int32, C.c_int32]),
     "rrin_conv3x3_h8_fwd": (C.c_int, [C.POINTER(ConvH8Desc), C.c_void_p]),
+    "rrin_conv_block0_h8_fwd": (C.c_int, [C.POINTER(Block0Desc), C.c_void_p]),
     "rrin_conv_h8_cfg_wino": (C.c_int, [C.c_int32]),
     "rrin_conv_h8_split_floats": (C.c_int64, [C.c_void_p, C.c_void_p]),
     "rrin_conv_h8_ring_floats": (C.c_int64, [C.c_void_p, C.c_void_p]),

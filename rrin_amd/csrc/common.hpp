@@ -270,6 +270,42 @@ constexpr size_t kWinoCPLds = (size_t)(3 * 512 + 2048 + 128) * 16;  // stages + 
 int launch_winoh(const ConvH8Args& a, int epi, int nt, bool persistent, hipStream_t st);
 constexpr size_t kWinoHP1Lds = (size_t)(3 * 512 + 2048 + 128) * 16;  // persistent TH 4: stages + exchange + bias
 constexpr size_t kWinoHP2Lds = (size_t)(3 * 768 + 4096 + 128) * 16;  // persistent TH 8
+// fused level-0 UNetConvBlock at fp16 (conv_block0.hip): conv a (cin -> 32) + leaky, conv b
+// (32 -> 32) + leaky (+ pool), conv a's output tile in LDS.  Tile kB0TH x kB0TW outputs; conv a
+// runs on (kB0TH + 2) x (kB0TW + 2) positions from a (kB0TH + 4) x (kB0TW + 4) input tile
+struct Block0Args {
+  const uint4* src;
+  int64_t src_img, src_gp;  // records per image / group plane
+  int src_wp, src_hp;       // records per row, rows per plane
+  int cin, ngroups, nch;    // input channels, their record groups, 16-channel chunks
+  const uint4* wa;          // conv a: rrin_pack_conv3x3_h8 halves (co block 0 of width bma)
+  int bma;
+  const float* ba;
+  float isa;
+  const uint4* wb;          // conv b
+  int bmb;
+  const float* bb;
+  float isb;
+  uint4* dst;
+  int64_t dst_img, dst_gp;
+  int dst_wp;
+  uint4* pool;              // nullptr: no pool output
+  int64_t pool_img, pool_gp;
+  int pool_wp;
+  float slope;
+  int h, w, n, tiles_x, tiles_y;
+  int* status;
+};
+constexpr int kB0TH = 8, kB0TW = 62;
+constexpr int kB0IR = kB0TH + 4, kB0IC = kB0TW + 4;  // input tile rows / columns
+constexpr int kB0MR = kB0TH + 2, kB0MC = kB0TW + 4;  // conv-a tile rows / columns (64 computed + 2 pad)
+constexpr int kB0In = 2 * kB0IR * kB0IC;             // input records per 16-channel chunk
+constexpr int kB0Pieces = (kB0In + 255) / 256;       // LDS-DMA pieces per thread and chunk
+constexpr int kB0Stage = kB0Pieces * 256;            // records per input stage (tail: dummy)
+constexpr int kB0Mid = 4 * kB0MR * kB0MC;            // conv-a tile records (aliases the stages)
+constexpr size_t kB0Lds = (size_t)(2 * kB0Stage > kB0Mid ? 2 * kB0Stage : kB0Mid) * 16;
+static_assert(2 * kB0Lds <= 160 * 1024, "two fused-block workgroups per CU");
+int launch_block0(const Block0Args& a, hipStream_t st);
 // persistent register-U tile for cout <= 32 (conv_winop.hip, kind 8): 8 waves, two raw
 // stages + a separate exchange area + 32 bias floats
 constexpr size_t kWinoPLds = (size_t)(2 * 680 + 2048) * 16 + 128;

@@ -1,0 +1,294 @@
+// Fused level-0 UNetConvBlock at fp16 (H8 records): conv a (cin -> 32) + LeakyReLU, conv b
+// (32 -> 32) + LeakyReLU (+ the down block's avg_pool2d output) in one launch, conv a's output
+// tile kept in LDS.  Replaces unet.py:59-63 (the block's two Conv2d + LeakyReLU) and :46 (the pool
+// of down_path[0]) at level 0, where the direct-form pair (conv3x3_h8_kernel twice) is bound by
+// HBM: a 32-channel full-resolution fp16 tensor is written by conv a and read back by conv b.
+//
+// Tile: 8 output rows x 62 output columns x 32 channels of one image.  Conv a runs on the
+// 10 x 64 positions conv b needs (the 1-pixel halo is recomputed by the neighbouring tiles:
+// 1.29x conv a's MACs), from a 12 x 66 input tile; positions outside the image are set to 0
+// (conv b's zero padding).  4 waves, two workgroups per CU:
+//   * input: 16-channel chunks (2 record groups) by LDS-DMA (buffer_load ... lds), two stages;
+//     conv a's weights straight from L2 into registers (9 records per lane and chunk), a chunk
+//     ahead;
+//   * conv a: wave wv owns the 5 MFMA tiles (32 co x 32 px) of rows wv/2, wv/2 + 2, ..., column
+//     half wv % 2; per chunk and tap one ds_read_b128 per tile (its B operand);
+//   * conv a's epilogue (scale, bias, leaky, zero outside the image, one fp16 rounding) writes
+//     the 32-channel tile into LDS over the dead input stages;
+//   * conv b: wave wv owns rows 4 (wv/2) .. + 3 of column half wv % 2 (a pool pair is in one
+//     wave), B operands from the LDS tile, weights from L2 into registers;
+//   * conv b's epilogue as conv3x3_h8_kernel's (store, range guard, 2x2 average pool).
+// The arithmetic is that of two conv3x3_h8_kernel launches at fp16 (same packed weights, chunk
+// then tap order of the fp32 accumulation, same epilogue expressions and roundings): the outputs
+// are bitwise those of the unfused pair (tests/test_gpu_block0.py).
+#include <algorithm>
+
+#include "common.hpp"
+
+namespace rrin {
+
+typedef _Float16 b0h8 __attribute__((ext_vector_type(8)));
+typedef _Float16 b0h2 __attribute__((ext_vector_type(2)));
+typedef float b0f2 __attribute__((ext_vector_type(2)));
+typedef float b0f16 __attribute__((ext_vector_type(16)));
+
+constexpr float kB0F16Max = 65504.0f;
+
+__device__ inline __amdgpu_buffer_rsrc_t b0_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
+}
+__device__ inline void b0_dma16(__amdgpu_buffer_rsrc_t rs, uint4* lds_wave_base, uint32_t voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)lds_wave_base, 16, voff, 0, 0,
+                                           0);
+}
+__device__ inline b0h8 b0_load16(__amdgpu_buffer_rsrc_t rs, uint32_t voff, int soff) {
+  return __builtin_bit_cast(b0h8, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0));
+}
+// 4 fp32 values -> 4 RNE fp16 values (one 8-B record half), as split4 of conv_f16.hip
+__device__ inline uint2 b0_pack4(const float* v) {
+  const b0h2 h0 = __builtin_convertvector((b0f2){v[0], v[1]}, b0h2);
+  const b0h2 h1 = __builtin_convertvector((b0f2){v[2], v[3]}, b0h2);
+  return make_uint2(__builtin_bit_cast(unsigned, h0), __builtin_bit_cast(unsigned, h1));
+}
+
+template <bool POOL>
+__global__ __launch_bounds__(256, 2) void conv_block0_h8_kernel(Block0Args a) {
+  constexpr int TH = kB0TH, TW = kB0TW, IR = kB0IR, IC = kB0IC, MR = kB0MR, MC = kB0MC;
+  constexpr int P = kB0Pieces, STAGE = kB0Stage;
+  extern __shared__ __attribute__((aligned(16))) uint4 smem4[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int j = lane & 31, hh = lane >> 5;
+  const int half = wv & 1;  // column half of this wave's MFMA tiles (wave-uniform)
+  int bid;
+  {  // XCD-aware bijective remap: an XCD's workgroups are consecutive tiles (shared halo rows in its L2)
+    const int nwg = gridDim.x, q = nwg >> 3, r = nwg & 7;
+    const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+  }
+  if (bid >= a.tiles_x * a.tiles_y * a.n) return;
+  const int tx = bid % a.tiles_x, ty = (bid / a.tiles_x) % a.tiles_y, img = bid / (a.tiles_x * a.tiles_y);
+  const int x0 = tx * TW, y0 = ty * TH;
+  const int nch = a.nch;
+
+  // ---- input tile: rows y0 - 2 .. y0 + 9, cols x0 - 2 .. x0 + 63 of a chunk's two record groups,
+  // clamped into the padded plane (a clamped row / column only feeds conv-a positions outside
+  // the image, which are zeroed); groups past the input's last read its zero top padding row
+  // (the direct kernel's convention); lanes past the tile re-read record 0 into the dummy tail
+  const auto rs_in = b0_rsrc(a.src + (int64_t)img * a.src_img);
+  uint32_t voff[P], zoff[P];
+  int gl[P];
+#pragma unroll
+  for (int it = 0; it < P; ++it) {
+    const int idx = tid + 256 * it;
+    const bool ok = idx < kB0In;
+    const int g = idx >= IR * IC ? 1 : 0;
+    const int rem = ok ? idx - g * IR * IC : 0;
+    const int r = rem / IC, col = rem - r * IC;
+    const int yb = min(max(y0 - 2 + r + 1, 0), a.src_hp - 1);
+    const int xr = min(max(x0 - 2 + col + kH8PadLeft, 0), a.src_wp - 1);
+    voff[it] = ok ? (uint32_t)(((int64_t)g * a.src_gp + (int64_t)yb * a.src_wp + xr) * 16) : 0u;
+    zoff[it] = ok ? (uint32_t)xr * 16u : 0u;
+    gl[it] = ok ? g : 0;
+  }
+  const uint32_t cstride = (uint32_t)(2 * a.src_gp * 16);  // bytes between consecutive chunks' group pairs
+  auto issue_chunk = [&](int c, int s) {
+#pragma unroll
+    for (int it = 0; it < P; ++it) {
+      const uint32_t o = 2 * c + gl[it] < a.ngroups ? voff[it] + (uint32_t)c * cstride : zoff[it];
+      b0_dma16(rs_in, smem4 + s * STAGE + 256 * it + 64 * wv, o);
+    }
+  };
+
+  // ---- conv a's weights (packing of rrin_pack_conv3x3_h8, co block 0): lane (j, hh) of tap t
+  // of chunk c is record ((c * 9 + t) * 2 + hh) * bm + j
+  const auto rs_wa = b0_rsrc(a.wa);
+  const uint32_t wa_voff = (uint32_t)(hh * a.bma + j) * 16u;
+  b0h8 wcur[9], wnxt[9];
+  auto load_wa = [&](int c, b0h8 (&wd)[9]) {
+#pragma unroll
+    for (int t = 0; t < 9; ++t) wd[t] = b0_load16(rs_wa, wa_voff, (c * 9 + t) * 2 * a.bma * 16);
+  };
+  auto bar = [&]() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+  auto fence = [&]() { __builtin_amdgcn_sched_barrier(0); };
+
+  // ---- conv a
+  b0f16 acc[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) acc[i] = b0f16{};
+  // B operand of tile i (row wv / 2 + 2 i, column half) at tap (ky, kx): input record
+  // (group hh, row m + ky, column 32 half + j + kx)
+  const int a_base = hh * IR * IC + (wv >> 1) * IC + 32 * half + j;
+  auto compute_a = [&](int s) {
+    const uint4* base = smem4 + s * STAGE + a_base;
+    b0h8 b[2][5];
+    auto ld = [&](int t, int slot) {
+      const int ky = t / 3, kx = t - 3 * (t / 3);
+#pragma unroll
+      for (int i = 0; i < 5; ++i) b[slot][i] = __builtin_bit_cast(b0h8, base[(2 * i + ky) * IC + kx]);
+    };
+    ld(0, 0);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      if (t + 1 < 9) ld(t + 1, (t + 1) & 1);
+#pragma unroll
+      for (int i = 0; i < 5; ++i)
+        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wcur[t], b[t & 1][i], acc[i], 0, 0, 0);
+    }
+  };
+
+  // prologue: chunk 0 (DMA), its weights, chunk 1 (DMA); wait for the first two
+  issue_chunk(0, 0);
+  load_wa(0, wcur);
+  if (nch > 1) {
+    issue_chunk(1, 1);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P) : "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  bar();
+  fence();
+  for (int c = 0; c < nch; ++c) {
+    const int s = c & 1;
+    const bool more = c + 1 < nch;
+    if (more) load_wa(c + 1, wnxt);
+    fence();
+    compute_a(s);
+    fence();
+    if (more) {
+      // chunk c + 1 (DMA) and its weights landed; every wave done with stage s
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      bar();
+      if (c + 2 < nch) issue_chunk(c + 2, s);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) wcur[t] = wnxt[t];
+    }
+    fence();
+  }
+
+  // ---- conv a's epilogue into the LDS tile [4 groups][MR rows][MC cols] over the input stages
+  const auto rs_wb = b0_rsrc(a.wb);
+  const uint32_t wb_voff = (uint32_t)(hh * a.bmb + j) * 16u;
+  auto load_wb = [&](int c, b0h8 (&wd)[9]) {
+#pragma unroll
+    for (int t = 0; t < 9; ++t) wd[t] = b0_load16(rs_wb, wb_voff, (c * 9 + t) * 2 * a.bmb * 16);
+  };
+  float bsa[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) bsa[i] = a.ba[8 * (i >> 2) + 4 * hh + (i & 3)];
+  load_wb(0, wcur);
+  bool bad = false;  // a stored value fp16 cannot hold (range guard)
+  bar();             // every wave done reading the stages
+  {
+    const int x = x0 - 1 + 32 * half + j;
+    const bool xin = x >= 0 && x < a.w;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      const int m = (wv >> 1) + 2 * i;
+      const int y = y0 - 1 + m;
+      const bool in = xin && y >= 0 && y < a.h;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float t = acc[i][4 * q + e];
+          t = t * a.isa + bsa[4 * q + e];
+          v[e] = in ? leaky(t, a.slope) : 0.f;
+        }
+        bad |= !(fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))) <= kB0F16Max);
+        reinterpret_cast<uint2*>(smem4 + (q * MR + m) * MC + 32 * half + j)[hh] = b0_pack4(v);
+      }
+    }
+  }
+  bar();
+  fence();
+
+  // ---- conv b: rows 4 (wv / 2) + i, column half; chunk cb = record groups 2 cb, 2 cb + 1
+  b0f16 acc2[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc2[i] = b0f16{};
+  const int b_base = hh * MR * MC + ((wv >> 1) * 4) * MC + 32 * half + j;
+#pragma unroll
+  for (int cb = 0; cb < 2; ++cb) {
+    if (cb == 0) load_wb(1, wnxt);
+    const uint4* base = smem4 + b_base + 2 * cb * MR * MC;
+    b0h8 b[2][4];
+    auto ld = [&](int t, int slot) {
+      const int ky = t / 3, kx = t - 3 * (t / 3);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) b[slot][i] = __builtin_bit_cast(b0h8, base[(i + ky) * MC + kx]);
+    };
+    ld(0, 0);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      if (t + 1 < 9) ld(t + 1, (t + 1) & 1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        acc2[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(cb ? wnxt[t] : wcur[t], b[t & 1][i], acc2[i], 0, 0, 0);
+    }
+  }
+
+  // ---- conv b's epilogue (conv3x3_h8_kernel's EPI_LEAKY / EPI_LEAKY_POOL expressions)
+  float bsb[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) bsb[i] = a.bb[8 * (i >> 2) + 4 * hh + (i & 3)];
+  const int xc = 32 * half + j;  // tile column
+  const int x = x0 + xc;
+  const bool xok = xc < TW && x < a.w;
+  uint4* dst = a.dst + (int64_t)img * a.dst_img;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    float v[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int y = y0 + (wv >> 1) * 4 + i;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float t = acc2[i][4 * q + e];
+        t = t * a.isb + bsb[4 * q + e];
+        v[i][e] = leaky(t, a.slope);
+      }
+      if (xok && y < a.h) {
+        bad |= !(fmaxf(fmaxf(fabsf(v[i][0]), fabsf(v[i][1])), fmaxf(fabsf(v[i][2]), fabsf(v[i][3]))) <= kB0F16Max);
+        const int64_t rec = (int64_t)q * a.dst_gp + (int64_t)(y + 1) * a.dst_wp + x + kH8PadLeft;
+        reinterpret_cast<uint2*>(dst + rec)[hh] = b0_pack4(v[i]);
+      }
+    }
+    if constexpr (POOL) {
+      uint4* pdst = a.pool + (int64_t)img * a.pool_img;
+#pragma unroll
+      for (int p2 = 0; p2 < 2; ++p2) {
+        float s4[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float s = v[2 * p2][e] + v[2 * p2 + 1][e];
+          s4[e] = 0.25f * (s + __shfl_xor(s, 1));
+        }
+        const int y = y0 + (wv >> 1) * 4 + 2 * p2;
+        if (!(j & 1) && xok && y < a.h) {
+          bad |= !(fmaxf(fmaxf(fabsf(s4[0]), fabsf(s4[1])), fmaxf(fabsf(s4[2]), fabsf(s4[3]))) <= kB0F16Max);
+          const int64_t rec = (int64_t)q * a.pool_gp + (int64_t)(y / 2 + 1) * a.pool_wp + x / 2 + kH8PadLeft;
+          reinterpret_cast<uint2*>(pdst + rec)[hh] = b0_pack4(s4);
+        }
+      }
+    }
+  }
+  if (bad && a.status) *a.status = 1;
+}
+
+template <bool POOL>
+static int launch_block0_k(const Block0Args& a, hipStream_t st) {
+  auto k = conv_block0_h8_kernel<POOL>;
+  static LdsAttr attr;
+  if (int e = attr.ensure((const void*)k, (int)kB0Lds, st)) return e;
+  const int64_t grid = (int64_t)a.tiles_x * a.tiles_y * a.n;
+  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256), kB0Lds, st, a);
+  return hip_code(hipGetLastError());
+}
+
+int launch_block0(const Block0Args& a, hipStream_t st) {
+  return a.pool ? launch_block0_k<true>(a, st) : launch_block0_k<false>(a, st);
+}
+
+}  // namespace rrin

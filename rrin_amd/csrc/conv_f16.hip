@@ -2136,6 +2136,62 @@ extern "C" int rrin_conv_h8_cfg_wino(int32_t cfg) {
          : cfg == kWinoCPCfg ? 12
                              : 0;
 }
+// Fused level-0 UNetConvBlock (conv_block0.hip): validate and launch.
+extern "C" int rrin_conv_block0_h8_fwd(const rrin_block0_h8_desc* d, void* stream) {
+  if (!d || !d->whi_a || !d->bias_a || !d->whi_b || !d->bias_b) return RRIN_E_ARG;
+  for (int cfg : {d->cfg_a, d->cfg_b})
+    if (cfg < 0 || cfg >= kNumCfgH8 || is_wino(cfg)) return RRIN_E_CONFIG;  // direct-form packs only
+  if (d->n < 1 || d->cin < 1 || ((d->cin & 7) && !d->tail_finite)) return RRIN_E_ARG;
+  if (!(d->slope >= 0.f && d->slope <= 1.f)) return RRIN_E_ARG;
+  const int prec = RRIN_PREC_F16;
+  if (!h8_ok(d->src, prec) || !h8_ok(d->dst, prec) || d->src.lo || d->dst.lo) return RRIN_E_SHAPE;
+  const int h = d->src.g.h, w = d->src.g.w;
+  if (d->dst.g.h != h || d->dst.g.w != w || d->dst.groups < 4 || d->cin > 8 * d->src.groups) return RRIN_E_SHAPE;
+  const bool pool = d->pool.hi != nullptr;
+  if (pool && (!h8_ok(d->pool, prec) || d->pool.lo || (h & 1) || (w & 1) || d->pool.g.h * 2 != h ||
+               d->pool.g.w * 2 != w || d->pool.groups < 4))
+    return RRIN_E_SHAPE;
+  // 32-bit byte offsets within an image (buffer loads of the input tile)
+  if (d->src.img_stride * 16 >= ((int64_t)1 << 31)) return RRIN_E_SHAPE;
+  Block0Args a;
+  memset(&a, 0, sizeof(a));
+  a.src = static_cast<const uint4*>(d->src.hi) + (int64_t)d->src.g_off * d->src.g.plane;
+  a.src_img = d->src.img_stride;
+  a.src_gp = d->src.g.plane;
+  a.src_wp = d->src.g.wp;
+  a.src_hp = d->src.g.hp;
+  a.cin = d->cin;
+  a.ngroups = (d->cin + 7) / 8;
+  a.nch = (d->cin + 15) / 16;
+  a.wa = static_cast<const uint4*>(d->whi_a);
+  a.bma = kCfgH8[d->cfg_a].bm;
+  a.ba = d->bias_a;
+  a.isa = d->inv_wscale_a;
+  a.wb = static_cast<const uint4*>(d->whi_b);
+  a.bmb = kCfgH8[d->cfg_b].bm;
+  a.bb = d->bias_b;
+  a.isb = d->inv_wscale_b;
+  a.dst = static_cast<uint4*>(d->dst.hi) + (int64_t)d->dst.g_off * d->dst.g.plane;
+  a.dst_img = d->dst.img_stride;
+  a.dst_gp = d->dst.g.plane;
+  a.dst_wp = d->dst.g.wp;
+  if (pool) {
+    a.pool = static_cast<uint4*>(d->pool.hi) + (int64_t)d->pool.g_off * d->pool.g.plane;
+    a.pool_img = d->pool.img_stride;
+    a.pool_gp = d->pool.g.plane;
+    a.pool_wp = d->pool.g.wp;
+  }
+  a.slope = d->slope;
+  a.h = h;
+  a.w = w;
+  a.n = d->n;
+  a.tiles_x = (w + kB0TW - 1) / kB0TW;
+  a.tiles_y = (h + kB0TH - 1) / kB0TH;
+  a.status = d->status;
+  if ((int64_t)a.tiles_x * a.tiles_y * a.n > 0x7fffffff) return RRIN_E_SHAPE;
+  return launch_block0(a, static_cast<hipStream_t>(stream));
+}
+
 extern "C" int rrin_conv_h8_cfg_ok(int32_t cfg, int32_t prec) {
   if (cfg < 0 || cfg >= kNumCfgH8) return 0;
   if (!rec_prec(prec) || (lab_only(cfg) && !kLabBuild)) return 0;

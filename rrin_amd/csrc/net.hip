@@ -401,6 +401,33 @@ int conv_h8(const Plan& p, const rrin_conv_weights& cw, int cin, int cout, int e
   return rrin_conv3x3_h8_fwd(&d, st);
 }
 
+// Fused level-0 UNetConvBlock (conv a = ca: cin -> 32, conv b = cb: 32 -> 32, + pool): one
+// rrin_conv_block0_h8_fwd launch, bitwise the two conv_h8 calls it replaces
+int block0_h8(const Plan& p, const rrin_conv_weights& ca, const rrin_conv_weights& cb, int cin, const rrin_h8& src,
+              const rrin_h8& dst, const rrin_h8* pool, hipStream_t st) {
+  ProfScope ps(p.prof, st, RRIN_KIND_CONV, 2.0 * 9 * (cin * 32 + 32 * 32) * (double)dst.g.h * dst.g.w * p.n);
+  rrin_block0_h8_desc d;
+  memset(&d, 0, sizeof(d));
+  d.n = p.n;
+  d.cin = cin;
+  d.cfg_a = ca.cfg;
+  d.cfg_b = cb.cfg;
+  d.slope = 0.1f;
+  d.inv_wscale_a = ca.inv_wscale;
+  d.inv_wscale_b = cb.inv_wscale;
+  d.tail_finite = 1;  // as conv_h8
+  d.src = src;
+  d.dst = dst;
+  if (pool) d.pool = *pool;
+  d.whi_a = ca.whi;
+  d.bias_a = ca.bias;
+  d.whi_b = cb.whi;
+  d.bias_b = cb.bias;
+  d.status = p.status;
+  if (p.dry) return 0;
+  return rrin_conv_block0_h8_fwd(&d, st);
+}
+
 // up.1 conv of the up block at level L on the sub-pixel path: low-res x (2C ch,
 // edge-replicated) -> CAT[L][0, C), then the ring fix-up.
 int upconv_subpixel(const Plan& p, const rrin_conv_weights& cw, int C, const rrin_h8& x, const rrin_h8& up,
@@ -447,6 +474,11 @@ int upconv_subpixel(const Plan& p, const rrin_conv_weights& cw, int C, const rri
   return rrin_subpixel_edge_fix_h8(&e, st);
 }
 
+// conv cw (a level-0 conv a) runs fused with the next conv: fp16, asked for by the table
+static bool fused_block0(const Plan& p, const rrin_conv_weights& cw) {
+  return p.prec == RRIN_PREC_F16 && cw.fuse_next == 1;
+}
+
 // One U-Net on the split-fp16 path: same dataflow as run_unet.  An up conv
 // either has sub-pixel weights (upsample folded into the conv; its producer then
 // writes the low-res tensor into LRB with edge-replicate padding) or runs after
@@ -461,6 +493,13 @@ int run_unet_h8(const Plan& p, const UNetSpec& u, const rrin_conv_weights* cw, c
     const int cin = L ? chans(L - 1) : u.in_ch;
     const rrin_h8 in = L ? hview(p.X[L], 0, cin) : hview(p.G, 0, cin);
     const rrin_h8 t = hview(p.T[L], 0, C);
+    if (L == 0 && D >= 2 && fused_block0(p, cw[k])) {  // down_path[0] in one launch
+      const rrin_h8 bridge = hview(p.CAT[0], C, C);
+      const rrin_h8 pooled = hview(p.X[1], 0, C);
+      RRIN_TRY(block0_h8(p, cw[k], cw[k + 1], cin, in, bridge, &pooled, st));
+      k += 2;
+      continue;
+    }
     RRIN_TRY(conv_h8(p, cw[k++], cin, C, RRIN_EPI_LEAKY, in, t, nullptr, st));
     if (L < D - 1) {
       const rrin_h8 bridge = hview(p.CAT[L], C, C);
@@ -492,6 +531,13 @@ int run_unet_h8(const Plan& p, const UNetSpec& u, const rrin_conv_weights* cw, c
     }
     const rrin_h8 cat = hview(p.CAT[L], 0, 2 * C);
     const rrin_h8 t = hview(p.T[L], 0, C);
+    if (L == 0 && fused_block0(p, cw[k])) {  // the last up block's conv_block in one launch: its
+      // output goes to T[0] (the launch reads all of CAT[0] while it writes)
+      RRIN_TRY(block0_h8(p, cw[k], cw[k + 1], 2 * C, cat, t, nullptr, st));
+      k += 2;
+      x = t;
+      continue;
+    }
     RRIN_TRY(conv_h8(p, cw[k++], 2 * C, C, RRIN_EPI_LEAKY, cat, t, nullptr, st));
     // conv b; cw[k + 1] is the next level's up conv
     const bool sub = L > 0 && cw[k + 1].subpixel;

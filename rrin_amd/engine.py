@@ -289,6 +289,28 @@ WINO_F16_LEVELS = (4,)
 WINO_F16_KIND = 6
 
 
+# fp16: each level-0 UNetConvBlock (conv a: in -> 32, conv b: 32 -> 32, unet.py:59-63) as one
+# launch with conv a's output tile in LDS (conv_block0.hip, rrin_conv_block0_h8_fwd; bitwise the
+# two direct-form launches).  False: two launches (A/B, bench.py --fuse-l0 0).
+FUSE_L0 = False
+
+
+def fused_pairs(convs) -> list:
+    """Indices i of the (cin, cout, level, edge) list whose conv and conv i + 1 form a level-0
+    UNetConvBlock: conv i (not an up conv) -> 32 channels at level 0, conv i + 1 32 -> 32 at
+    level 0."""
+    out, i = [], 0
+    while i + 1 < len(convs):
+        cin, cout, level, edge = convs[i]
+        c2, o2, l2, e2 = convs[i + 1]
+        if level == 0 and cout == 32 and edge is None and (c2, o2, l2) == (32, 32, 0) and e2 is None:
+            out.append(i)
+            i += 2
+        else:
+            i += 1
+    return out
+
+
 def wino_f16_ok(cin: int, cout: int, level: int) -> bool:
     return WINO_F16 and level in WINO_F16_LEVELS and cout % 64 == 0 and cin % 16 == 0
 
@@ -459,6 +481,7 @@ class RRINEngine:
                 self._h8_convs.append((w, b, cin, cout, level, perm_arr, edge))
         if len(self._h8_convs) != self.expected_convs:
             raise RuntimeError(f"packed {len(self._h8_convs)} convs, expected {self.expected_convs}")
+        self._block0 = fused_pairs([(cin, cout, level, edge) for (_, _, cin, cout, level, _, edge) in self._h8_convs])
         self.head_table = (_lib.HeadWeights * len(self.heads_t))()
         for i, (w, b) in enumerate(self.heads_t):
             self.head_table[i].w = w.data_ptr()
@@ -486,14 +509,14 @@ class RRINEngine:
         size h x w (the split-K geometry; None: no split), cached; classes / geometries
         whose tile configs agree share one packing."""
         geo = self._geom_splits(h, w)
-        key = (size, geo)
+        key = (size, geo, FUSE_L0)
         p = self._packs.get(key)
         if p is not None:
             return p
         L = self.lib
         cfgs = [choose_cfg_h8(cin, cout, self.prec, level, size, g)
                 for (_, _, cin, cout, level, _, _), g in zip(self._h8_convs, geo)]
-        ckey = tuple(cfgs)
+        ckey = (tuple(cfgs), FUSE_L0)
         p = self._packs_by_cfgs.get(ckey)
         if p is not None:
             self._packs[key] = self._with_splits(p, geo)
@@ -574,6 +597,10 @@ class RRINEngine:
                 e.subpixel = 1
                 e.wedge = edge[0].data_ptr()
                 e.bias_raw = edge[1].data_ptr()
+        if FUSE_L0 and self.prec == _lib.PREC_F16:
+            for i in self._block0:  # both convs on direct-form packs (the fused kernel's weights)
+                if not (L.rrin_conv_h8_cfg_wino(cfgs[i]) or L.rrin_conv_h8_cfg_wino(cfgs[i + 1])):
+                    table[i].fuse_next = 1
         p = (blob, bias_blob, table, cfgs)
         self._packs_by_cfgs[ckey] = p
         self._packs[key] = self._with_splits(p, geo)
