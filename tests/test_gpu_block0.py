@@ -169,16 +169,35 @@ def test_net_fused_blocks_bitwise(gpu, h, w, n):
     net.precision = "fp16"
     i0, i1 = synthetic_batch(n, h, w, first_index=3)
     i0, i1 = i0.to(gpu), i1.to(gpu)
+    lib = _lib.lib()
+
+    def conv_launches(eng):  # conv launches of one forward, from the schedule's launch profiler
+        prof = C.c_void_p()
+        _lib.check(lib.rrin_prof_create(4096, C.byref(prof)))
+        try:
+            eng.forward(i0, i1, 0.5, prof=prof, streams=1)
+            torch.cuda.synchronize(gpu)
+            cap = 4096
+            kinds, ms, fl, cnt = (C.c_int32 * cap)(), (C.c_float * cap)(), (C.c_double * cap)(), C.c_int32()
+            _lib.check(lib.rrin_prof_read(prof, kinds, ms, fl, cap, C.byref(cnt)))
+            return sum(1 for i in range(cnt.value) if kinds[i] == 0), sum(fl[i] for i in range(cnt.value) if kinds[i] == 0)
+        finally:
+            lib.rrin_prof_destroy(prof)
+
     saved = engine_mod.FUSE_L0
     try:
         with torch.no_grad():
             engine_mod.FUSE_L0 = False
-            ref = net(i0, i1, 0.5)
-            engine_mod.FUSE_L0 = True
             eng = net.engine()
+            ref = eng.forward(i0, i1, 0.5, streams=1)
+            n0, f0 = conv_launches(eng)
+            engine_mod.FUSE_L0 = True
             t = eng.conv_table_for(n, h, w)
             assert sum(int(t[i].fuse_next) for i in range(eng.expected_convs)) == 8
-            out = net(i0, i1, 0.5)
+            out = eng.forward(i0, i1, 0.5, streams=1)
+            n1, f1 = conv_launches(eng)
     finally:
         engine_mod.FUSE_L0 = saved
+    assert n1 == n0 - 8, (n0, n1)  # the fused launches ran (one per two convs)
+    assert abs(f1 - f0) <= 1e-9 * f0  # same algorithmic FLOPs counted
     assert torch.equal(out, ref)
