@@ -273,9 +273,9 @@ constexpr size_t kWinoHP2Lds = (size_t)(3 * 768 + 4096 + 128) * 16;  // persiste
 // fused level-0 UNetConvBlock at fp16 (conv_block0.hip): conv a (cin -> 32) + leaky, conv b
 // (32 -> 32) + leaky (+ pool), conv a's output tile in LDS.  Tile kB0TH x kB0TW outputs; conv a
 // runs on (kB0TH + 2) x (kB0TW + 2) positions from a (kB0TH + 4) x (kB0TW + 4) input tile
-struct Block0Args {
+struct Block0Args {  // strides in records; every image of src / dst / pool spans < 2^31 bytes
   const uint4* src;
-  int64_t src_img, src_gp;  // records per image / group plane
+  int src_img, src_gp;      // records per image / group plane
   int src_wp, src_hp;       // records per row, rows per plane
   int cin, ngroups, nch;    // input channels, their record groups, 16-channel chunks
   const uint4* wa;          // conv a: rrin_pack_conv3x3_h8 halves (co block 0 of width bma)
@@ -287,10 +287,10 @@ struct Block0Args {
   const float* bb;
   float isb;
   uint4* dst;
-  int64_t dst_img, dst_gp;
+  int dst_img, dst_gp;
   int dst_wp;
   uint4* pool;              // nullptr: no pool output
-  int64_t pool_img, pool_gp;
+  int pool_img, pool_gp;
   int pool_wp;
   float slope;
   int h, w, n, tiles_x, tiles_y;
@@ -302,8 +302,10 @@ constexpr int kB0MR = kB0TH + 2, kB0MC = kB0TW + 4;  // conv-a tile rows / colum
 constexpr int kB0In = 2 * kB0IR * kB0IC;             // input records per 16-channel chunk
 constexpr int kB0Pieces = (kB0In + 255) / 256;       // LDS-DMA pieces per thread and chunk
 constexpr int kB0Stage = kB0Pieces * 256;            // records per input stage (tail: dummy)
-constexpr int kB0Mid = 4 * kB0MR * kB0MC;            // conv-a tile records (aliases the stages)
-constexpr size_t kB0Lds = (size_t)(2 * kB0Stage > kB0Mid ? 2 * kB0Stage : kB0Mid) * 16;
+constexpr int kB0Mid = 4 * kB0MR * kB0MC;            // conv-a tile records (aliases input stage Y)
+// LDS: conv-a tile | input stage X | 64 bias floats (stage Y inside the conv-a tile)
+constexpr size_t kB0Lds = (size_t)(kB0Mid + kB0Stage + 16) * 16;
+static_assert(kB0Stage <= kB0Mid, "stage Y inside the conv-a tile");
 static_assert(2 * kB0Lds <= 160 * 1024, "two fused-block workgroups per CU");
 int launch_block0(const Block0Args& a, hipStream_t st);
 // persistent register-U tile for cout <= 32 (conv_winop.hip, kind 8): 8 waves, two raw

@@ -22,6 +22,8 @@
 // then tap order of the fp32 accumulation, same epilogue expressions and roundings): the outputs
 // are bitwise those of the unfused pair (tests/test_gpu_block0.py).
 #include <algorithm>
+#include <atomic>
+#include <type_traits>
 
 #include "common.hpp"
 
@@ -66,66 +68,97 @@ __global__ __launch_bounds__(256, 2) void conv_block0_h8_kernel(Block0Args a) {
     const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
     bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
   }
-  if (bid >= a.tiles_x * a.tiles_y * a.n) return;
-  const int tx = bid % a.tiles_x, ty = (bid / a.tiles_x) % a.tiles_y, img = bid / (a.tiles_x * a.tiles_y);
-  const int x0 = tx * TW, y0 = ty * TH;
+  const int ntiles = a.tiles_x * a.tiles_y * a.n;
+  int tile = bid;
+  if (tile >= ntiles) return;
   const int nch = a.nch;
+  // LDS: [conv-a tile (kB0Mid) | stage X (chunks 0, 2, ..) | 64 bias floats]; stage Y (chunks 1,
+  // 3, ..) aliases the conv-a tile.  Stage X is free during conv b: the next tile's chunk 0 lands
+  // there while conv b and its epilogue run (the grid is persistent: a workgroup walks tiles
+  // bid, bid + grid, ...)
+  uint4* const stX = smem4 + kB0Mid;
+  uint4* const stY = smem4;
+  float* const sbias = reinterpret_cast<float*>(smem4 + kB0Mid + STAGE);
+  if (tid < 64) sbias[tid] = tid < 32 ? a.ba[tid] : a.bb[tid - 32];  // read after the prologue barrier
 
   // ---- input tile: rows y0 - 2 .. y0 + 9, cols x0 - 2 .. x0 + 63 of a chunk's two record groups,
   // clamped into the padded plane (a clamped row / column only feeds conv-a positions outside
   // the image, which are zeroed); groups past the input's last read its zero top padding row
   // (the direct kernel's convention); lanes past the tile re-read record 0 into the dummy tail
-  const auto rs_in = b0_rsrc(a.src + (int64_t)img * a.src_img);
-  uint32_t voff[P], zoff[P];
-  int gl[P];
-#pragma unroll
-  for (int it = 0; it < P; ++it) {
-    const int idx = tid + 256 * it;
-    const bool ok = idx < kB0In;
-    const int g = idx >= IR * IC ? 1 : 0;
-    const int rem = ok ? idx - g * IR * IC : 0;
-    const int r = rem / IC, col = rem - r * IC;
-    const int yb = min(max(y0 - 2 + r + 1, 0), a.src_hp - 1);
-    const int xr = min(max(x0 - 2 + col + kH8PadLeft, 0), a.src_wp - 1);
-    voff[it] = ok ? (uint32_t)(((int64_t)g * a.src_gp + (int64_t)yb * a.src_wp + xr) * 16) : 0u;
-    zoff[it] = ok ? (uint32_t)xr * 16u : 0u;
-    gl[it] = ok ? g : 0;
-  }
-  const uint32_t cstride = (uint32_t)(2 * a.src_gp * 16);  // bytes between consecutive chunks' group pairs
-  auto issue_chunk = [&](int c, int s) {
+  uint32_t voff[P];
+  auto set_offsets = [&](int x0, int y0) {
 #pragma unroll
     for (int it = 0; it < P; ++it) {
-      const uint32_t o = 2 * c + gl[it] < a.ngroups ? voff[it] + (uint32_t)c * cstride : zoff[it];
-      b0_dma16(rs_in, smem4 + s * STAGE + 256 * it + 64 * wv, o);
+      const int idx = tid + 256 * it;
+      const bool ok = idx < kB0In;
+      const int g = idx >= IR * IC ? 1 : 0;
+      const int rem = ok ? idx - g * IR * IC : 0;
+      const int r = rem / IC, col = rem - r * IC;
+      const int yb = min(max(y0 - 2 + r + 1, 0), a.src_hp - 1);
+      const int xr = min(max(x0 - 2 + col + kH8PadLeft, 0), a.src_wp - 1);
+      voff[it] = ok ? (uint32_t)(g * a.src_gp + yb * a.src_wp + xr) * 16u : 0u;
     }
   };
-
-  // ---- conv a's weights (packing of rrin_pack_conv3x3_h8, co block 0): lane (j, hh) of tap t
-  // of chunk c is record ((c * 9 + t) * 2 + hh) * bm + j
-  const auto rs_wa = b0_rsrc(a.wa);
-  const uint32_t wa_voff = (uint32_t)(hh * a.bma + j) * 16u;
-  b0h8 wcur[9], wnxt[9];
-  auto load_wa = [&](int c, b0h8 (&wd)[9]) {
+  const uint32_t cstride = (uint32_t)(2 * a.src_gp * 16);  // bytes between consecutive chunks' group pairs
+  // (a chunk's second group past the input's last -- cin % 16 in 1..8 -- is staged from the
+  // first group's position and zeroed in the B operands: compute_a<true>)
+  const uint32_t gstride = (uint32_t)(a.src_gp * 16);
+  auto issue_chunk = [&](const uint4* ibase, int c, uint4* st) {
+    const auto rs = b0_rsrc(ibase);
+    const bool past = 2 * c + 1 >= a.ngroups;
 #pragma unroll
-    for (int t = 0; t < 9; ++t) wd[t] = b0_load16(rs_wa, wa_voff, (c * 9 + t) * 2 * a.bma * 16);
+    for (int it = 0; it < P; ++it) {
+      const bool g1 = tid + 256 * it >= IR * IC && tid + 256 * it < kB0In;
+      b0_dma16(rs, st + 256 * it + 64 * wv, voff[it] + (uint32_t)c * cstride - (past && g1 ? gstride : 0u));
+    }
+  };
+  auto tile_pos = [&](int t, int& img, int& x0, int& y0) {
+    const int tx = t % a.tiles_x;
+    t /= a.tiles_x;
+    y0 = (t % a.tiles_y) * TH;
+    img = t / a.tiles_y;
+    x0 = tx * TW;
+  };
+
+  // ---- weights (packing of rrin_pack_conv3x3_h8, co block 0): lane (j, hh) of tap t of chunk c
+  // is record ((c * 9 + t) * 2 + hh) * bm + j; from L2 straight into registers.  One set of 9
+  // records: after tap t's MFMAs of a chunk, tap t of the next chunk (conv a's next, conv b's
+  // first, conv b's second, the next tile's conv-a first) replaces w[t]
+  const auto rs_wa = b0_rsrc(a.wa);
+  const auto rs_wb = b0_rsrc(a.wb);
+  const uint32_t wa_voff = (uint32_t)(hh * a.bma + j) * 16u;
+  const uint32_t wb_voff = (uint32_t)(hh * a.bmb + j) * 16u;
+  const int wa_tap = 2 * a.bma * 16, wb_tap = 2 * a.bmb * 16;  // bytes per tap
+  b0h8 w[9];
+  // source of the weights that replace w[] during a chunk: conv (0 a, 1 b), chunk; none if conv < 0
+  struct WNext {
+    int conv, c;
+  };
+  auto wload = [&](const WNext& nx, int t) {
+    if (nx.conv == 0) w[t] = b0_load16(rs_wa, wa_voff, (nx.c * 9 + t) * wa_tap);
+    if (nx.conv == 1) w[t] = b0_load16(rs_wb, wb_voff, (nx.c * 9 + t) * wb_tap);
   };
   auto bar = [&]() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
   auto fence = [&]() { __builtin_amdgcn_sched_barrier(0); };
 
-  // ---- conv a
-  b0f16 acc[5];
-#pragma unroll
-  for (int i = 0; i < 5; ++i) acc[i] = b0f16{};
-  // B operand of tile i (row wv / 2 + 2 i, column half) at tap (ky, kx): input record
+  // B operand of conv-a tile i (row wv / 2 + 2 i, column half) at tap (ky, kx): input record
   // (group hh, row m + ky, column 32 half + j + kx)
   const int a_base = hh * IR * IC + (wv >> 1) * IC + 32 * half + j;
-  auto compute_a = [&](int s) {
-    const uint4* base = smem4 + s * STAGE + a_base;
+  b0f16 acc[5];
+  auto compute_a = [&](const uint4* st, bool zero_g1, const WNext& nx) {
+    const uint4* base = st + a_base;
+    // channels 8..15 of a chunk past cin (cin % 16 in 1..8): zero operands, as the direct kernel's
+    // zero row (the stage holds the first group's records there)
+    const unsigned keep = zero_g1 && hh ? 0u : ~0u;
     b0h8 b[2][5];
     auto ld = [&](int t, int slot) {
       const int ky = t / 3, kx = t - 3 * (t / 3);
 #pragma unroll
-      for (int i = 0; i < 5; ++i) b[slot][i] = __builtin_bit_cast(b0h8, base[(2 * i + ky) * IC + kx]);
+      for (int i = 0; i < 5; ++i) {
+        uint4 r = base[(2 * i + ky) * IC + kx];
+        r.x &= keep, r.y &= keep, r.z &= keep, r.w &= keep;
+        b[slot][i] = __builtin_bit_cast(b0h8, r);
+      }
     };
     ld(0, 0);
 #pragma unroll
@@ -133,156 +166,213 @@ __global__ __launch_bounds__(256, 2) void conv_block0_h8_kernel(Block0Args a) {
       if (t + 1 < 9) ld(t + 1, (t + 1) & 1);
 #pragma unroll
       for (int i = 0; i < 5; ++i)
-        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wcur[t], b[t & 1][i], acc[i], 0, 0, 0);
+        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(w[t], b[t & 1][i], acc[i], 0, 0, 0);
+      wload(nx, t);
+      fence();  // one weight set live: tap t's replacement issues after tap t's MFMAs
     }
   };
 
-  // prologue: chunk 0 (DMA), its weights, chunk 1 (DMA); wait for the first two
-  issue_chunk(0, 0);
-  load_wa(0, wcur);
+  int img, x0, y0;
+  tile_pos(tile, img, x0, y0);
+  set_offsets(x0, y0);
+  const uint4* ibase = a.src + (size_t)img * a.src_img;
+  // prologue of the first tile: chunk 0 (DMA), its weights, chunk 1 (DMA); wait for the first two
+  issue_chunk(ibase, 0, stX);
+#pragma unroll
+  for (int t = 0; t < 9; ++t) wload(WNext{0, 0}, t);
   if (nch > 1) {
-    issue_chunk(1, 1);
+    issue_chunk(ibase, 1, stY);
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P) : "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   bar();
-  fence();
-  for (int c = 0; c < nch; ++c) {
-    const int s = c & 1;
-    const bool more = c + 1 < nch;
-    if (more) load_wa(c + 1, wnxt);
+  bool bad = false;  // a stored value fp16 cannot hold (range guard)
+  for (;;) {
     fence();
-    compute_a(s);
-    fence();
-    if (more) {
-      // chunk c + 1 (DMA) and its weights landed; every wave done with stage s
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      bar();
-      if (c + 2 < nch) issue_chunk(c + 2, s);
+    // ---- conv a: chunk c from stage X (c even) / Y (c odd)
 #pragma unroll
-      for (int t = 0; t < 9; ++t) wcur[t] = wnxt[t];
+    for (int i = 0; i < 5; ++i) acc[i] = b0f16{};
+    for (int c = 0; c < nch; ++c) {
+      const bool more = c + 1 < nch;
+      fence();
+      compute_a((c & 1) ? stY : stX, 2 * c + 1 >= a.ngroups, more ? WNext{0, c + 1} : WNext{1, 0});
+      fence();
+      if (more) {
+        // chunk c + 1 (DMA) landed; every wave done with this chunk's stage
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        bar();
+        if (c + 2 < nch) issue_chunk(ibase, c + 2, (c & 1) ? stY : stX);
+      }
+      fence();
+    }
+    bar();  // every wave done reading the stages: Y becomes the conv-a tile, X takes the next tile
+    const int ntile = tile + (int)gridDim.x;
+    const bool has_next = ntile < ntiles;
+    int nimg = img, nx0 = x0, ny0 = y0;
+    const uint4* nbase = ibase;
+    if (has_next) {
+      tile_pos(ntile, nimg, nx0, ny0);
+      set_offsets(nx0, ny0);
+      nbase = a.src + (size_t)nimg * a.src_img;
+      issue_chunk(nbase, 0, stX);
+    }
+
+    // ---- conv a's epilogue into the LDS tile [4 groups][MR rows][MC cols]
+    {
+      const float4* bq = reinterpret_cast<const float4*>(sbias) + hh;  // channels 8 q + 4 hh ..
+      const int x = x0 - 1 + 32 * half + j;
+      const bool xin = x >= 0 && x < a.w;
+#pragma unroll
+      for (int i = 0; i < 5; ++i) {
+        const int m = (wv >> 1) + 2 * i;
+        const int y = y0 - 1 + m;
+        const bool in = xin && y >= 0 && y < a.h;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 bs = bq[2 * q];
+          const float bsa[4] = {bs.x, bs.y, bs.z, bs.w};
+          float v[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float t = acc[i][4 * q + e];
+            t = t * a.isa + bsa[e];
+            v[e] = in ? leaky(t, a.slope) : 0.f;
+          }
+          bad |= !(fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))) <= kB0F16Max);
+          reinterpret_cast<uint2*>(smem4 + (q * MR + m) * MC + 32 * half + j)[hh] = b0_pack4(v);
+        }
+      }
+    }
+    bar();
+    fence();
+
+    // ---- conv b: rows 4 (wv / 2) + i, column half; chunk cb = record groups 2 cb, 2 cb + 1
+    b0f16 acc2[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc2[i] = b0f16{};
+    const int b_base = hh * MR * MC + ((wv >> 1) * 4) * MC + 32 * half + j;
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) {
+      const uint4* base = smem4 + b_base + 2 * cb * MR * MC;
+      const WNext nx = cb == 0 ? WNext{1, 1} : (has_next ? WNext{0, 0} : WNext{-1, 0});
+      b0h8 b[2][4];
+      auto ld = [&](int t, int slot) {
+        const int ky = t / 3, kx = t - 3 * (t / 3);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) b[slot][i] = __builtin_bit_cast(b0h8, base[(i + ky) * MC + kx]);
+      };
+      ld(0, 0);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        if (t + 1 < 9) ld(t + 1, (t + 1) & 1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          acc2[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(w[t], b[t & 1][i], acc2[i], 0, 0, 0);
+        wload(nx, t);
+        fence();
+      }
     }
     fence();
-  }
 
-  // ---- conv a's epilogue into the LDS tile [4 groups][MR rows][MC cols] over the input stages
-  const auto rs_wb = b0_rsrc(a.wb);
-  const uint32_t wb_voff = (uint32_t)(hh * a.bmb + j) * 16u;
-  auto load_wb = [&](int c, b0h8 (&wd)[9]) {
-#pragma unroll
-    for (int t = 0; t < 9; ++t) wd[t] = b0_load16(rs_wb, wb_voff, (c * 9 + t) * 2 * a.bmb * 16);
-  };
-  float bsa[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) bsa[i] = a.ba[8 * (i >> 2) + 4 * hh + (i & 3)];
-  load_wb(0, wcur);
-  bool bad = false;  // a stored value fp16 cannot hold (range guard)
-  bar();             // every wave done reading the stages
-  {
-    const int x = x0 - 1 + 32 * half + j;
-    const bool xin = x >= 0 && x < a.w;
-#pragma unroll
-    for (int i = 0; i < 5; ++i) {
-      const int m = (wv >> 1) + 2 * i;
-      const int y = y0 - 1 + m;
-      const bool in = xin && y >= 0 && y < a.h;
+    // ---- conv b's epilogue (conv3x3_h8_kernel's EPI_LEAKY / EPI_LEAKY_POOL expressions); buffer
+    // stores of 8-B record halves, an invalid position's offset past the buffer (dropped)
+    {
+      constexpr uint32_t kOOB = 0x80000000u;
+      const float4* bq = reinterpret_cast<const float4*>(sbias + 32) + hh;
+      const int xc = 32 * half + j;  // tile column
+      const int x = x0 + xc;
+      const bool xok = xc < TW && x < a.w;
+      const auto rs_d = b0_rsrc(a.dst + (size_t)img * a.dst_img);
+      const auto rs_p = b0_rsrc(POOL ? a.pool + (size_t)img * a.pool_img : a.dst);
+      const int yb = y0 + (wv >> 1) * 4;
+      const uint32_t d0 = (uint32_t)((yb + 1) * a.dst_wp + x + kH8PadLeft) * 16u + hh * 8u;
+      const uint32_t p0 = (uint32_t)((yb / 2 + 1) * a.pool_wp + x / 2 + kH8PadLeft) * 16u + hh * 8u;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        float v[4];
+        const float4 bs = bq[2 * q];
+        const float bsb[4] = {bs.x, bs.y, bs.z, bs.w};
+        float v[4][4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float t = acc[i][4 * q + e];
-          t = t * a.isa + bsa[4 * q + e];
-          v[e] = in ? leaky(t, a.slope) : 0.f;
+        for (int i = 0; i < 4; ++i) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float t = acc2[i][4 * q + e];
+            t = t * a.isb + bsb[e];
+            v[i][e] = leaky(t, a.slope);
+          }
+          const bool ok = xok && yb + i < a.h;
+          if (ok)
+            bad |= !(fmaxf(fmaxf(fabsf(v[i][0]), fabsf(v[i][1])), fmaxf(fabsf(v[i][2]), fabsf(v[i][3]))) <=
+                     kB0F16Max);
+          const uint2 pk = b0_pack4(v[i]);
+          __builtin_amdgcn_raw_buffer_store_b64((unsigned __attribute__((ext_vector_type(2)))){pk.x, pk.y}, rs_d,
+                                                ok ? d0 + (uint32_t)(q * a.dst_gp + i * a.dst_wp) * 16u : kOOB, 0, 0);
         }
-        bad |= !(fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))) <= kB0F16Max);
-        reinterpret_cast<uint2*>(smem4 + (q * MR + m) * MC + 32 * half + j)[hh] = b0_pack4(v);
-      }
-    }
-  }
-  bar();
-  fence();
-
-  // ---- conv b: rows 4 (wv / 2) + i, column half; chunk cb = record groups 2 cb, 2 cb + 1
-  b0f16 acc2[4];
+        if constexpr (POOL) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) acc2[i] = b0f16{};
-  const int b_base = hh * MR * MC + ((wv >> 1) * 4) * MC + 32 * half + j;
+          for (int p2 = 0; p2 < 2; ++p2) {
+            float s4[4];
 #pragma unroll
-  for (int cb = 0; cb < 2; ++cb) {
-    if (cb == 0) load_wb(1, wnxt);
-    const uint4* base = smem4 + b_base + 2 * cb * MR * MC;
-    b0h8 b[2][4];
-    auto ld = [&](int t, int slot) {
-      const int ky = t / 3, kx = t - 3 * (t / 3);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) b[slot][i] = __builtin_bit_cast(b0h8, base[(i + ky) * MC + kx]);
-    };
-    ld(0, 0);
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      if (t + 1 < 9) ld(t + 1, (t + 1) & 1);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        acc2[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(cb ? wnxt[t] : wcur[t], b[t & 1][i], acc2[i], 0, 0, 0);
-    }
-  }
-
-  // ---- conv b's epilogue (conv3x3_h8_kernel's EPI_LEAKY / EPI_LEAKY_POOL expressions)
-  float bsb[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) bsb[i] = a.bb[8 * (i >> 2) + 4 * hh + (i & 3)];
-  const int xc = 32 * half + j;  // tile column
-  const int x = x0 + xc;
-  const bool xok = xc < TW && x < a.w;
-  uint4* dst = a.dst + (int64_t)img * a.dst_img;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    float v[4][4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int y = y0 + (wv >> 1) * 4 + i;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float t = acc2[i][4 * q + e];
-        t = t * a.isb + bsb[4 * q + e];
-        v[i][e] = leaky(t, a.slope);
-      }
-      if (xok && y < a.h) {
-        bad |= !(fmaxf(fmaxf(fabsf(v[i][0]), fabsf(v[i][1])), fmaxf(fabsf(v[i][2]), fabsf(v[i][3]))) <= kB0F16Max);
-        const int64_t rec = (int64_t)q * a.dst_gp + (int64_t)(y + 1) * a.dst_wp + x + kH8PadLeft;
-        reinterpret_cast<uint2*>(dst + rec)[hh] = b0_pack4(v[i]);
-      }
-    }
-    if constexpr (POOL) {
-      uint4* pdst = a.pool + (int64_t)img * a.pool_img;
-#pragma unroll
-      for (int p2 = 0; p2 < 2; ++p2) {
-        float s4[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float s = v[2 * p2][e] + v[2 * p2 + 1][e];
-          s4[e] = 0.25f * (s + __shfl_xor(s, 1));
-        }
-        const int y = y0 + (wv >> 1) * 4 + 2 * p2;
-        if (!(j & 1) && xok && y < a.h) {
-          bad |= !(fmaxf(fmaxf(fabsf(s4[0]), fabsf(s4[1])), fmaxf(fabsf(s4[2]), fabsf(s4[3]))) <= kB0F16Max);
-          const int64_t rec = (int64_t)q * a.pool_gp + (int64_t)(y / 2 + 1) * a.pool_wp + x / 2 + kH8PadLeft;
-          reinterpret_cast<uint2*>(pdst + rec)[hh] = b0_pack4(s4);
+            for (int e = 0; e < 4; ++e) {
+              const float s = v[2 * p2][e] + v[2 * p2 + 1][e];
+              s4[e] = 0.25f * (s + __shfl_xor(s, 1));
+            }
+            const bool ok = !(j & 1) && xok && yb + 2 * p2 < a.h;
+            if (ok)
+              bad |= !(fmaxf(fmaxf(fabsf(s4[0]), fabsf(s4[1])), fmaxf(fabsf(s4[2]), fabsf(s4[3]))) <= kB0F16Max);
+            const uint2 pk = b0_pack4(s4);
+            __builtin_amdgcn_raw_buffer_store_b64((unsigned __attribute__((ext_vector_type(2)))){pk.x, pk.y}, rs_p,
+                                                  ok ? p0 + (uint32_t)(q * a.pool_gp + p2 * a.pool_wp) * 16u : kOOB,
+                                                  0, 0);
+          }
         }
       }
     }
+    if (!has_next) break;
+    // every wave done reading the conv-a tile: the next tile's chunk 1 goes into stage Y; wait for
+    // its chunk 0 and chunk-0 weights by counting the younger loads only (loads complete in
+    // order among themselves, not in order with the epilogue's stores)
+    bar();
+    if (nch > 1) {
+      issue_chunk(nbase, 1, stY);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    bar();
+    tile = ntile;
+    img = nimg;
+    x0 = nx0;
+    y0 = ny0;
+    ibase = nbase;
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (bad && a.status) *a.status = 1;
 }
 
+// CUs of the stream's device (cached per device)
+static int block0_cus(hipStream_t st) {
+  static std::atomic<int> cus[kMaxDevices];
+  const int dev = stream_device(st);
+  int ncu = cus[dev].load(std::memory_order_relaxed);
+  if (ncu <= 0) {
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
+    cus[dev].store(ncu, std::memory_order_relaxed);
+  }
+  return ncu;
+}
+
+#ifndef RRIN_BLOCK0_BPC
+#define RRIN_BLOCK0_BPC 2  // persistent workgroups per CU (the LDS holds two)
+#endif
 template <bool POOL>
 static int launch_block0_k(const Block0Args& a, hipStream_t st) {
   auto k = conv_block0_h8_kernel<POOL>;
   static LdsAttr attr;
   if (int e = attr.ensure((const void*)k, (int)kB0Lds, st)) return e;
-  const int64_t grid = (int64_t)a.tiles_x * a.tiles_y * a.n;
+  const int64_t tiles = (int64_t)a.tiles_x * a.tiles_y * a.n;
+  const int64_t grid = std::min<int64_t>(tiles, (int64_t)RRIN_BLOCK0_BPC * block0_cus(st));
   hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256), kB0Lds, st, a);
   return hip_code(hipGetLastError());
 }

@@ -2151,13 +2151,15 @@ extern "C" int rrin_conv_block0_h8_fwd(const rrin_block0_h8_desc* d, void* strea
   if (pool && (!h8_ok(d->pool, prec) || d->pool.lo || (h & 1) || (w & 1) || d->pool.g.h * 2 != h ||
                d->pool.g.w * 2 != w || d->pool.groups < 4))
     return RRIN_E_SHAPE;
-  // 32-bit byte offsets within an image (buffer loads of the input tile)
-  if (d->src.img_stride * 16 >= ((int64_t)1 << 31)) return RRIN_E_SHAPE;
+  // 32-bit byte offsets within an image (buffer loads and stores)
+  const int64_t lim = (int64_t)1 << 31;
+  if (d->src.img_stride * 16 >= lim || d->dst.img_stride * 16 >= lim || (pool && d->pool.img_stride * 16 >= lim))
+    return RRIN_E_SHAPE;
   Block0Args a;
   memset(&a, 0, sizeof(a));
   a.src = static_cast<const uint4*>(d->src.hi) + (int64_t)d->src.g_off * d->src.g.plane;
-  a.src_img = d->src.img_stride;
-  a.src_gp = d->src.g.plane;
+  a.src_img = (int)d->src.img_stride;
+  a.src_gp = (int)d->src.g.plane;
   a.src_wp = d->src.g.wp;
   a.src_hp = d->src.g.hp;
   a.cin = d->cin;
@@ -2172,13 +2174,13 @@ extern "C" int rrin_conv_block0_h8_fwd(const rrin_block0_h8_desc* d, void* strea
   a.bb = d->bias_b;
   a.isb = d->inv_wscale_b;
   a.dst = static_cast<uint4*>(d->dst.hi) + (int64_t)d->dst.g_off * d->dst.g.plane;
-  a.dst_img = d->dst.img_stride;
-  a.dst_gp = d->dst.g.plane;
+  a.dst_img = (int)d->dst.img_stride;
+  a.dst_gp = (int)d->dst.g.plane;
   a.dst_wp = d->dst.g.wp;
   if (pool) {
     a.pool = static_cast<uint4*>(d->pool.hi) + (int64_t)d->pool.g_off * d->pool.g.plane;
-    a.pool_img = d->pool.img_stride;
-    a.pool_gp = d->pool.g.plane;
+    a.pool_img = (int)d->pool.img_stride;
+    a.pool_gp = (int)d->pool.g.plane;
     a.pool_wp = d->pool.g.wp;
   }
   a.slope = d->slope;
