@@ -27,6 +27,14 @@
 
 #include "common.hpp"
 
+// Ablation builds only (tools/build_wino_variant.sh NAME -DRRIN_B0_ABL=bits conv_block0; outputs wrong
+// by design): 1 no conv-a MFMAs, 2 no conv-b MFMAs, 4 no B-operand LDS reads after a tile's first
+// tap, 8 no conv-b epilogue stores, 16 no input DMA after the first tile's, 32 no weight loads
+// after the prologue
+#ifndef RRIN_B0_ABL
+#define RRIN_B0_ABL 0
+#endif
+
 namespace rrin {
 
 typedef _Float16 b0h8 __attribute__((ext_vector_type(8)));
@@ -103,7 +111,10 @@ __global__ __launch_bounds__(256, 2) void conv_block0_h8_kernel(Block0Args a) {
   // (a chunk's second group past the input's last -- cin % 16 in 1..8 -- is staged from the
   // first group's position and zeroed in the B operands: compute_a<true>)
   const uint32_t gstride = (uint32_t)(a.src_gp * 16);
+  bool first_tile = true;
   auto issue_chunk = [&](const uint4* ibase, int c, uint4* st) {
+    if constexpr ((RRIN_B0_ABL & 16) != 0)
+      if (!first_tile) return;
     const auto rs = b0_rsrc(ibase);
     const bool past = 2 * c + 1 >= a.ngroups;
 #pragma unroll
@@ -135,6 +146,7 @@ __global__ __launch_bounds__(256, 2) void conv_block0_h8_kernel(Block0Args a) {
     int conv, c;
   };
   auto wload = [&](const WNext& nx, int t) {
+    if constexpr ((RRIN_B0_ABL & 32) != 0) return;
     if (nx.conv == 0) w[t] = b0_load16(rs_wa, wa_voff, (nx.c * 9 + t) * wa_tap);
     if (nx.conv == 1) w[t] = b0_load16(rs_wb, wb_voff, (nx.c * 9 + t) * wb_tap);
   };
@@ -155,6 +167,8 @@ __global__ __launch_bounds__(256, 2) void conv_block0_h8_kernel(Block0Args a) {
       const int ky = t / 3, kx = t - 3 * (t / 3);
 #pragma unroll
       for (int i = 0; i < 5; ++i) {
+        if constexpr ((RRIN_B0_ABL & 4) != 0)
+          if (t > 0) continue;
         uint4 r = base[(2 * i + ky) * IC + kx];
         r.x &= keep, r.y &= keep, r.z &= keep, r.w &= keep;
         b[slot][i] = __builtin_bit_cast(b0h8, r);
@@ -166,7 +180,10 @@ __global__ __launch_bounds__(256, 2) void conv_block0_h8_kernel(Block0Args a) {
       if (t + 1 < 9) ld(t + 1, (t + 1) & 1);
 #pragma unroll
       for (int i = 0; i < 5; ++i)
-        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(w[t], b[t & 1][i], acc[i], 0, 0, 0);
+        if constexpr ((RRIN_B0_ABL & 1) != 0)
+          asm volatile("" ::"v"(w[t]), "v"(b[t & 1][i]));
+        else
+          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(w[t], b[t & 1][i], acc[i], 0, 0, 0);
       wload(nx, t);
       fence();  // one weight set live: tap t's replacement issues after tap t's MFMAs
     }
@@ -179,7 +196,7 @@ __global__ __launch_bounds__(256, 2) void conv_block0_h8_kernel(Block0Args a) {
   // prologue of the first tile: chunk 0 (DMA), its weights, chunk 1 (DMA); wait for the first two
   issue_chunk(ibase, 0, stX);
 #pragma unroll
-  for (int t = 0; t < 9; ++t) wload(WNext{0, 0}, t);
+  for (int t = 0; t < 9; ++t) w[t] = b0_load16(rs_wa, wa_voff, t * wa_tap);
   if (nch > 1) {
     issue_chunk(ibase, 1, stY);
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P) : "memory");
@@ -260,7 +277,11 @@ __global__ __launch_bounds__(256, 2) void conv_block0_h8_kernel(Block0Args a) {
       auto ld = [&](int t, int slot) {
         const int ky = t / 3, kx = t - 3 * (t / 3);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) b[slot][i] = __builtin_bit_cast(b0h8, base[(i + ky) * MC + kx]);
+        for (int i = 0; i < 4; ++i) {
+          if constexpr ((RRIN_B0_ABL & 4) != 0)
+            if (t > 0) continue;
+          b[slot][i] = __builtin_bit_cast(b0h8, base[(i + ky) * MC + kx]);
+        }
       };
       ld(0, 0);
 #pragma unroll
@@ -268,7 +289,10 @@ __global__ __launch_bounds__(256, 2) void conv_block0_h8_kernel(Block0Args a) {
         if (t + 1 < 9) ld(t + 1, (t + 1) & 1);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-          acc2[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(w[t], b[t & 1][i], acc2[i], 0, 0, 0);
+          if constexpr ((RRIN_B0_ABL & 2) != 0)
+            asm volatile("" ::"v"(w[t]), "v"(b[t & 1][i]));
+          else
+            acc2[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(w[t], b[t & 1][i], acc2[i], 0, 0, 0);
         wload(nx, t);
         fence();
       }
@@ -306,7 +330,8 @@ __global__ __launch_bounds__(256, 2) void conv_block0_h8_kernel(Block0Args a) {
             bad |= !(fmaxf(fmaxf(fabsf(v[i][0]), fabsf(v[i][1])), fmaxf(fabsf(v[i][2]), fabsf(v[i][3]))) <=
                      kB0F16Max);
           const uint2 pk = b0_pack4(v[i]);
-          __builtin_amdgcn_raw_buffer_store_b64((unsigned __attribute__((ext_vector_type(2)))){pk.x, pk.y}, rs_d,
+          if constexpr ((RRIN_B0_ABL & 8) == 0)
+            __builtin_amdgcn_raw_buffer_store_b64((unsigned __attribute__((ext_vector_type(2)))){pk.x, pk.y}, rs_d,
                                                 ok ? d0 + (uint32_t)(q * a.dst_gp + i * a.dst_wp) * 16u : kOOB, 0, 0);
         }
         if constexpr (POOL) {
@@ -322,7 +347,8 @@ __global__ __launch_bounds__(256, 2) void conv_block0_h8_kernel(Block0Args a) {
             if (ok)
               bad |= !(fmaxf(fmaxf(fabsf(s4[0]), fabsf(s4[1])), fmaxf(fabsf(s4[2]), fabsf(s4[3]))) <= kB0F16Max);
             const uint2 pk = b0_pack4(s4);
-            __builtin_amdgcn_raw_buffer_store_b64((unsigned __attribute__((ext_vector_type(2)))){pk.x, pk.y}, rs_p,
+            if constexpr ((RRIN_B0_ABL & 8) == 0)
+              __builtin_amdgcn_raw_buffer_store_b64((unsigned __attribute__((ext_vector_type(2)))){pk.x, pk.y}, rs_p,
                                                   ok ? p0 + (uint32_t)(q * a.pool_gp + p2 * a.pool_wp) * 16u : kOOB,
                                                   0, 0);
           }
@@ -341,6 +367,7 @@ __global__ __launch_bounds__(256, 2) void conv_block0_h8_kernel(Block0Args a) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     bar();
+    first_tile = false;
     tile = ntile;
     img = nimg;
     x0 = nx0;
@@ -364,7 +391,7 @@ static int block0_cus(hipStream_t st) {
 }
 
 #ifndef RRIN_BLOCK0_BPC
-#define RRIN_BLOCK0_BPC 2  // persistent workgroups per CU (the LDS holds two)
+#define RRIN_BLOCK0_BPC 2  // persistent workgroups per CU (the LDS holds two); 0: one tile per workgroup
 #endif
 template <bool POOL>
 static int launch_block0_k(const Block0Args& a, hipStream_t st) {
@@ -372,7 +399,8 @@ static int launch_block0_k(const Block0Args& a, hipStream_t st) {
   static LdsAttr attr;
   if (int e = attr.ensure((const void*)k, (int)kB0Lds, st)) return e;
   const int64_t tiles = (int64_t)a.tiles_x * a.tiles_y * a.n;
-  const int64_t grid = std::min<int64_t>(tiles, (int64_t)RRIN_BLOCK0_BPC * block0_cus(st));
+  const int64_t grid =
+      RRIN_BLOCK0_BPC > 0 ? std::min<int64_t>(tiles, (int64_t)RRIN_BLOCK0_BPC * block0_cus(st)) : tiles;
   hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256), kB0Lds, st, a);
   return hip_code(hipGetLastError());
 }
