@@ -14,7 +14,7 @@
 //   * conv a: wave wv owns the 5 MFMA tiles (32 co x 32 px) of rows wv/2, wv/2 + 2, ..., column
 //     half wv % 2; per chunk and tap one ds_read_b128 per tile (its B operand);
 //   * conv a's epilogue (scale, bias, leaky, zero outside the image, one fp16 rounding) writes
-//     the 32-channel tile into LDS over the dead input stages;
+//     the 32-channel tile into LDS over the dead input stage Y;
 //   * conv b: wave wv owns rows 4 (wv/2) .. + 3 of column half wv % 2 (a pool pair is in one
 //     wave), B operands from the LDS tile, weights from L2 into registers;
 //   * conv b's epilogue as conv3x3_h8_kernel's (store, range guard, 2x2 average pool).
@@ -123,6 +123,17 @@ __global__ __launch_bounds__(256, 2) void conv_block0_h8_kernel(Block0Args a) {
       b0_dma16(rs, st + 256 * it + 64 * wv, voff[it] + (uint32_t)c * cstride - (past && g1 ? gstride : 0u));
     }
   };
+  // a chunk's second group past the input's last (cin % 16 in 1..8) was staged from the first
+  // group's position: once its DMA has landed (after the wait that covers it, before the barrier
+  // that publishes it) its records become zeros, the direct kernel's zero-row operands
+  auto zero_past = [&](int c, uint4* st) {
+    if (2 * c + 1 < a.ngroups) return;
+#pragma unroll
+    for (int it = 0; it < P; ++it) {
+      const int idx = tid + 256 * it;
+      if (idx >= IR * IC && idx < kB0In) st[idx] = make_uint4(0u, 0u, 0u, 0u);
+    }
+  };
   auto tile_pos = [&](int t, int& img, int& x0, int& y0) {
     const int tx = t % a.tiles_x;
     t /= a.tiles_x;
@@ -157,11 +168,8 @@ __global__ __launch_bounds__(256, 2) void conv_block0_h8_kernel(Block0Args a) {
   // (group hh, row m + ky, column 32 half + j + kx)
   const int a_base = hh * IR * IC + (wv >> 1) * IC + 32 * half + j;
   b0f16 acc[5];
-  auto compute_a = [&](const uint4* st, bool zero_g1, const WNext& nx) {
+  auto compute_a = [&](const uint4* st, const WNext& nx) {
     const uint4* base = st + a_base;
-    // channels 8..15 of a chunk past cin (cin % 16 in 1..8): zero operands, as the direct kernel's
-    // zero row (the stage holds the first group's records there)
-    const unsigned keep = zero_g1 && hh ? 0u : ~0u;
     b0h8 b[2][5];
     auto ld = [&](int t, int slot) {
       const int ky = t / 3, kx = t - 3 * (t / 3);
@@ -169,9 +177,7 @@ __global__ __launch_bounds__(256, 2) void conv_block0_h8_kernel(Block0Args a) {
       for (int i = 0; i < 5; ++i) {
         if constexpr ((RRIN_B0_ABL & 4) != 0)
           if (t > 0) continue;
-        uint4 r = base[(2 * i + ky) * IC + kx];
-        r.x &= keep, r.y &= keep, r.z &= keep, r.w &= keep;
-        b[slot][i] = __builtin_bit_cast(b0h8, r);
+        b[slot][i] = __builtin_bit_cast(b0h8, base[(2 * i + ky) * IC + kx]);
       }
     };
     ld(0, 0);
@@ -203,6 +209,7 @@ __global__ __launch_bounds__(256, 2) void conv_block0_h8_kernel(Block0Args a) {
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
+  zero_past(0, stX);
   bar();
   bool bad = false;  // a stored value fp16 cannot hold (range guard)
   for (;;) {
@@ -213,11 +220,12 @@ __global__ __launch_bounds__(256, 2) void conv_block0_h8_kernel(Block0Args a) {
     for (int c = 0; c < nch; ++c) {
       const bool more = c + 1 < nch;
       fence();
-      compute_a((c & 1) ? stY : stX, 2 * c + 1 >= a.ngroups, more ? WNext{0, c + 1} : WNext{1, 0});
+      compute_a((c & 1) ? stY : stX, more ? WNext{0, c + 1} : WNext{1, 0});
       fence();
       if (more) {
         // chunk c + 1 (DMA) landed; every wave done with this chunk's stage
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        zero_past(c + 1, ((c + 1) & 1) ? stY : stX);
         bar();
         if (c + 2 < nch) issue_chunk(ibase, c + 2, (c & 1) ? stY : stX);
       }
@@ -235,7 +243,10 @@ __global__ __launch_bounds__(256, 2) void conv_block0_h8_kernel(Block0Args a) {
       issue_chunk(nbase, 0, stX);
     }
 
-    // ---- conv a's epilogue into the LDS tile [4 groups][MR rows][MC cols]
+    // ---- conv a's epilogue into the LDS tile [4 groups][MR rows][MC cols].  No range check here:
+    // a value past the fp16 range rounds to +-inf and reaches every conv-b output of its window as
+    // +-inf or NaN (inf x 0 = NaN), which conv b's epilogue flags; only values in (65504, 65520),
+    // which round to 65504, go unflagged where the unfused conv a would flag them
     {
       const float4* bq = reinterpret_cast<const float4*>(sbias) + hh;  // channels 8 q + 4 hh ..
       const int x = x0 - 1 + 32 * half + j;
@@ -256,7 +267,6 @@ __global__ __launch_bounds__(256, 2) void conv_block0_h8_kernel(Block0Args a) {
             t = t * a.isa + bsa[e];
             v[e] = in ? leaky(t, a.slope) : 0.f;
           }
-          bad |= !(fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))) <= kB0F16Max);
           reinterpret_cast<uint2*>(smem4 + (q * MR + m) * MC + 32 * half + j)[hh] = b0_pack4(v);
         }
       }
@@ -366,6 +376,7 @@ __global__ __launch_bounds__(256, 2) void conv_block0_h8_kernel(Block0Args a) {
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+    zero_past(0, stX);
     bar();
     first_tile = false;
     tile = ntile;
@@ -391,7 +402,7 @@ static int block0_cus(hipStream_t st) {
 }
 
 #ifndef RRIN_BLOCK0_BPC
-#define RRIN_BLOCK0_BPC 2  // persistent workgroups per CU (the LDS holds two); 0: one tile per workgroup
+#define RRIN_BLOCK0_BPC 0  // persistent workgroups per CU (the LDS holds two); 0: one tile per workgroup
 #endif
 template <bool POOL>
 static int launch_block0_k(const Block0Args& a, hipStream_t st) {
