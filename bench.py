@@ -146,9 +146,9 @@ def parse():
     ap.add_argument("--no-wino", action="store_true",
                     help="A/B: the direct-form conv (one MFMA product per tap) instead of Winograd F(2x2,3x3), "
                          "exact fp32 and fp16")
-    ap.add_argument("--fuse-l0", type=int, default=None, choices=[0, 1],
-                    help="fp16: each level-0 UNetConvBlock as one fused launch (1) or two (0); "
-                         "default engine.FUSE_L0")
+    ap.add_argument("--fuse-l0", type=int, default=None, choices=[0, 1, 2],
+                    help="fp16: level-0 UNetConvBlocks as one fused launch: 0 none, 1 down_path[0], "
+                         "2 also the last up block's; default engine.FUSE_L0")
     ap.add_argument("--wino-persistent", type=int, default=None, choices=[0, 1],
                     help="A/B: exact fp32 kind 12 (kind 6 on a persistent grid) for the cout %% 64 convs (1) or "
                          "kind 6 (0); default engine.WINO_PERSISTENT")
@@ -411,7 +411,7 @@ def main():
     if args.wino_persistent is not None:
         engine_mod.WINO_PERSISTENT = bool(args.wino_persistent)
     if args.fuse_l0 is not None:
-        engine_mod.FUSE_L0 = bool(args.fuse_l0)
+        engine_mod.FUSE_L0 = args.fuse_l0
     if args.wino_f16_kind is not None:
         engine_mod.WINO_F16_KIND = args.wino_f16_kind
     if args.wino_f16_levels is not None:

@@ -289,10 +289,13 @@ WINO_F16_LEVELS = (4,)
 WINO_F16_KIND = 6
 
 
-# fp16: each level-0 UNetConvBlock (conv a: in -> 32, conv b: 32 -> 32, unet.py:59-63) as one
-# launch with conv a's output tile in LDS (conv_block0.hip, rrin_conv_block0_h8_fwd; bitwise the
-# two direct-form launches).  False: two launches (A/B, bench.py --fuse-l0 0).
-FUSE_L0 = False
+# fp16: level-0 UNetConvBlocks (conv a: in -> 32, conv b: 32 -> 32, unet.py:59-63) as one launch
+# with conv a's output tile in LDS (conv_block0.hip, rrin_conv_block0_h8_fwd; bitwise the two
+# direct-form launches).  0: two launches everywhere; 1: down_path[0] (conv a from the U-Net's
+# 6-16-channel input) fused; 2: also the last up block's conv_block (conv a 64 -> 32, whose
+# recomputed halo -- 1.29x conv a's MACs -- costs more than the HBM round trip it saves:
+# 159 vs 150 us at 1280x736 x 2, the down block 108 vs 121 us; profiles/r05/block0/).
+FUSE_L0 = 1
 
 
 def fused_pairs(convs) -> list:
@@ -599,6 +602,8 @@ class RRINEngine:
                 e.bias_raw = edge[1].data_ptr()
         if FUSE_L0 and self.prec == _lib.PREC_F16:
             for i in self._block0:  # both convs on direct-form packs (the fused kernel's weights)
+                if self._h8_convs[i][2] >= 32 and FUSE_L0 < 2:
+                    continue  # the up block's conv_block (cat input): unfused below FUSE_L0 = 2
                 if not (L.rrin_conv_h8_cfg_wino(cfgs[i]) or L.rrin_conv_h8_cfg_wino(cfgs[i + 1])):
                     table[i].fuse_next = 1
         p = (blob, bias_blob, table, cfgs)

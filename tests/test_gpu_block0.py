@@ -157,10 +157,11 @@ def test_block0_rejects(gpu):
     torch.cuda.synchronize(gpu)
 
 
-@pytest.mark.parametrize("h,w,n", [(256, 256, 1), (368, 640, 2)])
-def test_net_fused_blocks_bitwise(gpu, h, w, n):
-    """Net.forward at fp16 with every level-0 UNetConvBlock fused gives the unfused forward's
-    output bit for bit (8 fused launches per forward: 4 U-Nets x down_path[0] + last up block)."""
+@pytest.mark.parametrize("h,w,n,mode", [(256, 256, 1, 2), (368, 640, 2, 2), (368, 640, 2, 1)])
+def test_net_fused_blocks_bitwise(gpu, h, w, n, mode):
+    """Net.forward at fp16 with the level-0 UNetConvBlocks fused gives the unfused forward's
+    output bit for bit (engine.FUSE_L0 = 2: 8 fused launches per forward, 4 U-Nets x
+    down_path[0] + last up block; 1: the 4 down blocks)."""
     from rrin_amd import Net
     from rrin_amd.synthetic import keyed_state_dict, synthetic_batch
     net = Net()
@@ -187,17 +188,18 @@ def test_net_fused_blocks_bitwise(gpu, h, w, n):
     saved = engine_mod.FUSE_L0
     try:
         with torch.no_grad():
-            engine_mod.FUSE_L0 = False
+            engine_mod.FUSE_L0 = 0
             eng = net.engine()
             ref = eng.forward(i0, i1, 0.5, streams=1)
             n0, f0 = conv_launches(eng)
-            engine_mod.FUSE_L0 = True
+            engine_mod.FUSE_L0 = mode
             t = eng.conv_table_for(n, h, w)
-            assert sum(int(t[i].fuse_next) for i in range(eng.expected_convs)) == 8
+            nf = 8 if mode == 2 else 4
+            assert sum(int(t[i].fuse_next) for i in range(eng.expected_convs)) == nf
             out = eng.forward(i0, i1, 0.5, streams=1)
             n1, f1 = conv_launches(eng)
     finally:
         engine_mod.FUSE_L0 = saved
-    assert n1 == n0 - 8, (n0, n1)  # the fused launches ran (one per two convs)
+    assert n1 == n0 - nf, (n0, n1)  # the fused launches ran (one per two convs)
     assert abs(f1 - f0) <= 1e-9 * f0  # same algorithmic FLOPs counted
     assert torch.equal(out, ref)
