@@ -292,10 +292,12 @@ WINO_F16_KIND = 6
 # fp16: level-0 UNetConvBlocks (conv a: in -> 32, conv b: 32 -> 32, unet.py:59-63) as one launch
 # with conv a's output tile in LDS (conv_block0.hip, rrin_conv_block0_h8_fwd; bitwise the two
 # direct-form launches).  0: two launches everywhere; 1: down_path[0] (conv a from the U-Net's
-# 6-16-channel input) fused; 2: also the last up block's conv_block (conv a 64 -> 32, whose
-# recomputed halo -- 1.29x conv a's MACs -- costs more than the HBM round trip it saves:
-# 159 vs 150 us at 1280x736 x 2, the down block 108 vs 121 us; profiles/r05/block0/).
-FUSE_L0 = 1
+# 6-16-channel input) fused; 2: also the last up block's conv_block (conv a 64 -> 32).  In
+# isolation at 1280x736 x 2 the fused down block takes 108 vs 121 us, the fused up block 159 vs
+# 150 us (its recomputed halo, 1.29x conv a's MACs, costs more than the HBM round trip it saves;
+# profiles/r05/block0/); in the two-stream C3 forward mode 2 measured best: 480.0-481.7 pairs/s
+# vs 478.2-479.6 (mode 1) and 474.5-475.7 (unfused), C5 within noise (56.6-56.9).
+FUSE_L0 = 2
 
 
 def fused_pairs(convs) -> list:
