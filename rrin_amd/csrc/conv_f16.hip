@@ -225,31 +225,49 @@ __global__ void RRIN_PK_CONV_ATTR __launch_bounds__(64 * NW) conv3x3_h8_kernel(C
   uint4 rw[PLANES][DMA ? 1 : T::W_IT];
 
   // LDS-DMA staging of chunk c of tile tl: input piece `it` into buffer buf,
-  // weight piece `it` into weight slot `slot` (both planes)
-  auto issue_in = [&](const TileId& tl, int c, int buf, int it) {
-    const int idx = tid + NT * it;
-    if (idx < IN_REC) {
+  // weight piece `it` into weight slot `slot` (both planes).  buffer_load ... lds from a
+  // per-chunk base (scalar arithmetic) at a per-lane byte offset computed once per kernel:
+  // no vector address arithmetic in the chunk loop (it cost ~80 VALU per chunk beside 36
+  // MFMAs on the SPREAD tiles, each VALU stalling the MFMA pipe -- DESIGN.md §5e)
+  uint32_t in_off[DMA ? T::IN_IT : 1], in_zoff[DMA ? T::IN_IT : 1];
+  if constexpr (DMA) {
+#pragma unroll
+    for (int it = 0; it < T::IN_IT; ++it) {
+      const int idx = min(tid + NT * it, IN_REC - 1);
       const int g = idx / (ROWS * H8_LC);
       const int rem = idx - g * (ROWS * H8_LC);
       const int r = rem / H8_LC;
       const int col = rem - r * H8_LC;
-      const int gg = c * 2 + g;
-      // groups past cin read the zero top-padding row of group 0 instead
-      const int64_t off = (int64_t)tl.img * a.src_img +
-                          (gg * CPR < a.cin ? (int64_t)gg * a.src_gp + (int64_t)(tl.y0 + r) * a.src_wp : 0) +
-                          tl.x0 + (kH8PadLeft - 1) + col;
+      in_off[it] = (uint32_t)(g * a.src_gp + r * a.src_wp + col) * 16u;
+      in_zoff[it] = (uint32_t)col * 16u;  // the zero top-padding row of group 0 (groups past cin)
+    }
+  }
+  auto dma_rs = [&](const void* base, uint32_t voff, int soff, uint4* d) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000),
+        (__attribute__((address_space(3))) void*)d, 16, voff, soff, 0, 0);
+  };
+  auto issue_in = [&](const TileId& tl, int c, int buf, int it) {
+    // (a full piece needs no lane test: the condition folds for every piece but the last)
+    if (NT * (it + 1) <= IN_REC || tid + NT * it < IN_REC) {
       uint4* d = s_in + buf * PLANES * IN_REC + NT * it + (tid & ~63);
-      dma16(a.src_hi + off, d);
-      if constexpr (PLANES == 2) dma16(a.src_lo + off, d + IN_REC);
+      // one base per tile (scalar); the chunk's group pair and the tile row in the lane offset
+      const int64_t tb = (int64_t)tl.img * a.src_img + tl.x0 + (kH8PadLeft - 1);
+      const uint32_t c0 = (uint32_t)(2 * c) * (uint32_t)a.src_gp * 16u;
+      uint32_t vo = in_off[it] + c0 + (uint32_t)tl.y0 * (uint32_t)a.src_wp * 16u;
+      // the chunk's second group past cin: its lanes read the zero top-padding row of the
+      // chunk's first group instead (uniform test; a select only in that chunk)
+      if ((2 * c + 1) * CPR >= a.cin && tid + NT * it >= ROWS * H8_LC) vo = c0 + in_zoff[it];
+      dma_rs(a.src_hi + tb, vo, 0, d);
+      if constexpr (PLANES == 2) dma_rs(a.src_lo + tb, vo, 0, d + IN_REC);
     }
   };
   auto issue_w = [&](const TileId& tl, int c, int slot, int it) {
-    const int idx = tid + NT * it;
-    if (idx < W_REC) {
-      const int64_t off = ((int64_t)tl.cob * a.nchunks + c) * W_REC + idx;
+    if (NT * (it + 1) <= W_REC || tid + NT * it < W_REC) {
+      const int64_t off = ((int64_t)tl.cob * a.nchunks + c) * W_REC;
       uint4* d = s_w + slot * PLANES * W_REC + NT * it + (tid & ~63);
-      dma16(a.w_hi + off, d);
-      if constexpr (PLANES == 2) dma16(a.w_lo + off, d + W_REC);
+      dma_rs(a.w_hi + off, (uint32_t)tid * 16u, NT * it * 16, d);
+      if constexpr (PLANES == 2) dma_rs(a.w_lo + off, (uint32_t)tid * 16u, NT * it * 16, d + W_REC);
     }
   };
   auto issue_piece = [&](const TileId& tl, int c, int buf, int k) {
@@ -586,9 +604,11 @@ __global__ void RRIN_PK_CONV_ATTR __launch_bounds__(64 * NW) conv3x3_h8_kernel(C
         if constexpr (kSpread) {
           compute(buf, wslot, [&](int t) {
             if (t < kSpreadTaps && pre) {
+              // pieces [t NPIECE / kSpreadTaps, (t + 1) NPIECE / kSpreadTaps) with tap t; the piece
+              // index a compile-time constant (a runtime index put the per-piece offsets in scratch)
 #pragma unroll
-              for (int k = t * NPIECE / kSpreadTaps; k < (t + 1) * NPIECE / kSpreadTaps; ++k)
-                issue_piece(pt, pc, buf ^ 1, k);
+              for (int k = 0; k < NPIECE; ++k)
+                if (t * NPIECE / kSpreadTaps <= k && k < (t + 1) * NPIECE / kSpreadTaps) issue_piece(pt, pc, buf ^ 1, k);
             }
           });
         } else if constexpr (kStagger) {
