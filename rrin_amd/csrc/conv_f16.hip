@@ -1208,7 +1208,7 @@ struct HeadH8Args {
 // ~2^-22 and accumulate in fp32: the fp32 VALU head's result up to summation order.  Before this,
 // the head's 288 multiply-adds per pixel and output channel ran on the VALU (87 us per launch at
 // 1280x736 x 2, 8 % of the C3 step).
-constexpr int kHeadGStride = 18 * H8_LC;  // records per group in LDS (lane-linear LDS-DMA image)
+constexpr int kHeadGStride = 624;  // records per group in LDS (18 x 34 = 612, padded: conflict-free b128 reads)
 template <int COUT>
 __device__ inline void head_conv_mfma(const HeadH8Args& a, int img, int x0, int y0, float2v (&acc2)[COUT],
                                       uint4* s_rec, float* s_out) {
@@ -1216,24 +1216,12 @@ __device__ inline void head_conv_mfma(const HeadH8Args& a, int img, int x0, int 
   typedef float hf4 __attribute__((ext_vector_type(4)));
   constexpr int HROWS = 18, NREC = 4 * HROWS * H8_LC;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  // the tile's records: rows y0 - 1 .. y0 + 16, cols x0 - 1 .. x0 + 32 of the 4 groups, by
-  // LDS-DMA (every piece in flight at once; a register round trip per record serialised them)
-  {
-    const auto rs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint4*>(a.src_hi + img * a.src_img + (int64_t)y0 * a.src_wp + x0 + (kH8PadLeft - 1)), 0,
-        0x7fffffff, 0x00020000);
-#pragma unroll
-    for (int it = 0; it < (NREC + 255) / 256; ++it) {
-      const int idx = tid + 256 * it;
-      if (256 * (it + 1) <= NREC || idx < NREC) {
-        const int g = idx / (HROWS * H8_LC), rem = idx - g * (HROWS * H8_LC);
-        const int rr = rem / H8_LC, col = rem - rr * H8_LC;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            rs, (__attribute__((address_space(3))) void*)(s_rec + 256 * it + (tid & ~63)), 16,
-            (uint32_t)(g * a.src_gp + rr * a.src_wp + col) * 16u, 0, 0, 0);
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // the tile's records: rows y0 - 1 .. y0 + 16, cols x0 - 1 .. x0 + 32 of the 4 groups
+  for (int idx = tid; idx < NREC; idx += 256) {
+    const int g = idx / (HROWS * H8_LC), rem = idx - g * (HROWS * H8_LC);
+    const int rr = rem / H8_LC, col = rem - rr * H8_LC;
+    s_rec[g * kHeadGStride + rem] =
+        a.src_hi[img * a.src_img + (int64_t)g * a.src_gp + (int64_t)(y0 + rr) * a.src_wp + x0 + (kH8PadLeft - 1) + col];
   }
   // A operands: row co = lane & 15, channels 8 (lane >> 4) .. + 7 of tap t
   const int co = lane & 15, kg = lane >> 4;
