@@ -1201,78 +1201,11 @@ struct HeadH8Args {
   int* status;      // optional fp16 range flag: glue stores set it, FINAL poisons on it
 };
 
-// fp16 head conv on the matrix cores: one v_mfma_f32_16x16x32_f16 per tap and 16 pixels (A = the
-// weights, rows co < COUT of 16; B = the 32-channel records of 16 pixels of a row, as they lie in
-// memory: lane l supplies record group l >> 4 of pixel l & 15).  The fp32 weights enter as
-// w 2^10 = hi + lo (two fp16 values, two MFMAs per tap), so the products carry the weights to
-// ~2^-22 and accumulate in fp32: the fp32 VALU head's result up to summation order.  Before this,
-// the head's 288 multiply-adds per pixel and output channel ran on the VALU (87 us per launch at
-// 1280x736 x 2, 8 % of the C3 step).
-constexpr int kHeadGStride = 624;  // records per group in LDS (18 x 34 = 612, padded: conflict-free b128 reads)
-template <int COUT>
-__device__ inline void head_conv_mfma(const HeadH8Args& a, int img, int x0, int y0, float2v (&acc2)[COUT],
-                                      uint4* s_rec, float* s_out) {
-  typedef _Float16 hh8 __attribute__((ext_vector_type(8)));
-  typedef float hf4 __attribute__((ext_vector_type(4)));
-  constexpr int HROWS = 18, NREC = 4 * HROWS * H8_LC;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  // the tile's records: rows y0 - 1 .. y0 + 16, cols x0 - 1 .. x0 + 32 of the 4 groups
-  for (int idx = tid; idx < NREC; idx += 256) {
-    const int g = idx / (HROWS * H8_LC), rem = idx - g * (HROWS * H8_LC);
-    const int rr = rem / H8_LC, col = rem - rr * H8_LC;
-    s_rec[g * kHeadGStride + rem] =
-        a.src_hi[img * a.src_img + (int64_t)g * a.src_gp + (int64_t)(y0 + rr) * a.src_wp + x0 + (kH8PadLeft - 1) + col];
-  }
-  // A operands: row co = lane & 15, channels 8 (lane >> 4) .. + 7 of tap t
-  const int co = lane & 15, kg = lane >> 4;
-  hh8 whi[9], wlo[9];
-#pragma unroll
-  for (int t = 0; t < 9; ++t)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float v = co < COUT ? a.w[((co * 32) + 8 * kg + e) * 9 + t] * 1024.0f : 0.f;
-      const _Float16 h = (_Float16)v;
-      whi[t][e] = h;
-      wlo[t][e] = (_Float16)(v - (float)h);
-    }
-  __syncthreads();
-  // wave w: rows 4 w .. 4 w + 3 of the tile (its threads' pixels), two 16-pixel column blocks
-  hf4 d[8];
-#pragma unroll
-  for (int n = 0; n < 8; ++n) {
-    d[n] = hf4{0.f, 0.f, 0.f, 0.f};
-    const uint4* b0 = s_rec + kg * kHeadGStride + (4 * w + (n >> 1)) * H8_LC + 16 * (n & 1) + co;
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      const hh8 b = __builtin_bit_cast(hh8, b0[(t / 3) * H8_LC + t % 3]);
-      d[n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(whi[t], b, d[n], 0, 0, 0);
-      d[n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wlo[t], b, d[n], 0, 0, 0);
-    }
-  }
-  // D: lane l holds pixel l & 15 of its column block, rows (co) 4 (l >> 4) .. + 3: lanes 0-15
-  // carry co 0-3.  Through this wave's LDS area to the threads' pixel mapping (in-order LDS
-  // within a wave: no barrier)
-  float* so = s_out + w * (4 * 4 * 32);
-  if (lane < 16) {
-#pragma unroll
-    for (int n = 0; n < 8; ++n)
-#pragma unroll
-      for (int i = 0; i < COUT; ++i) so[(i * 4 + (n >> 1)) * 32 + 16 * (n & 1) + lane] = d[n][i] * (1.0f / 1024.0f);
-  }
-  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes done before its reads
-  const int rl = 2 * ((tid >> 5) & 1), xl = tid & 31;  // local rows of this thread's two pixels
-#pragma unroll
-  for (int i = 0; i < COUT; ++i)
-    acc2[i] = float2v{so[(i * 4 + rl) * 32 + xl] + a.bias[i], so[(i * 4 + rl + 1) * 32 + xl] + a.bias[i]};
-}
-
 template <int COUT, int MODE, int PLANES>
 __global__ void __launch_bounds__(256) head_h8_kernel(HeadH8Args a) {
   // tile 16 rows x 32 cols; thread = 2 vertically adjacent pixels (packed fp32 FMA)
   constexpr int CIN = 32, HROWS = 18, HLC = 40;
-  // fp16: MFMA path (head_conv_mfma: records + per-wave output exchange); split16: fp32 planar
-  constexpr size_t kSmemF = PLANES == 1 ? (4 * kHeadGStride * 16 + 4 * 4 * 4 * 32 * 4) / 4 : 8 * HROWS * HLC;
-  __shared__ __attribute__((aligned(16))) float s_in[kSmemF];
+  __shared__ __attribute__((aligned(16))) float s_in[8 * HROWS * HLC];
   const int tid = threadIdx.x;
   int bid = blockIdx.x;
   const int tx = bid % a.tiles_x;
@@ -1282,12 +1215,8 @@ __global__ void __launch_bounds__(256) head_h8_kernel(HeadH8Args a) {
   const int x0 = tx * 32, y0 = ty * 16;
   const int r2 = 2 * (tid >> 5), xl = tid & 31;
 
-  float2v acc2[COUT];
-  if constexpr (PLANES == 1) {
-    head_conv_mfma<COUT>(a, img, x0, y0, acc2, reinterpret_cast<uint4*>(s_in),
-                         s_in + 4 * kHeadGStride * 4);
-  } else {
   // weights are wave-uniform: scalar loads, no LDS traffic
+  float2v acc2[COUT];
 #pragma unroll
   for (int co = 0; co < COUT; ++co) acc2[co] = float2v{a.bias[co], a.bias[co]};
   // records of rows y0-1..y0+16, cols x0-1..x0+32 of one channel group, fetched
@@ -1345,7 +1274,6 @@ __global__ void __launch_bounds__(256) head_h8_kernel(HeadH8Args a) {
     }
     __syncthreads();
   }
-  }  // PLANES == 2
 
   for (int p = 0; p < 2; ++p) {
   float acc[COUT];
