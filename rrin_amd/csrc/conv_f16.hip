@@ -1838,20 +1838,24 @@ static const CfgH8 kCfgH8[] = {
     {64, 8, kWinoHP2Lds, (size_t)1 << 30, 0, true, 0, 0},
     // kWinoCPCfg: exact fp32, kind 6 on a persistent grid (conv3x3_winocp_kernel)
     {64, 4, kWinoCPLds, (size_t)1 << 30, 0, true, 0, 0},
+    // kWinoHLCfg: fp16 only, kind 6 on two patch tiles per workgroup, U shared through LDS
+    // (conv3x3_winohl_kernel, 8 waves, one block per CU)
+    {64, 8, kWinoHLLds, (size_t)1 << 30, 0, true, 0, 0},
 };
 static constexpr int kNumCfgH8 = sizeof(kCfgH8) / sizeof(kCfgH8[0]);
-static constexpr int kWinoCfg = kNumCfgH8 - 12;
-static constexpr int kWino64Cfg = kNumCfgH8 - 11;
-static constexpr int kWinoQCfg = kNumCfgH8 - 10;
-static constexpr int kWinoQ4Cfg = kNumCfgH8 - 9;
-static constexpr int kWino4Cfg = kNumCfgH8 - 8;
-static constexpr int kWinoC2Cfg = kNumCfgH8 - 7;
-static constexpr int kWinoC1Cfg = kNumCfgH8 - 6;
-static constexpr int kWinoPCfg = kNumCfgH8 - 5;
-static constexpr int kWinoH2Cfg = kNumCfgH8 - 4;
-static constexpr int kWinoHP1Cfg = kNumCfgH8 - 3;
-static constexpr int kWinoHP2Cfg = kNumCfgH8 - 2;
-static constexpr int kWinoCPCfg = kNumCfgH8 - 1;
+static constexpr int kWinoCfg = kNumCfgH8 - 13;
+static constexpr int kWino64Cfg = kNumCfgH8 - 12;
+static constexpr int kWinoQCfg = kNumCfgH8 - 11;
+static constexpr int kWinoQ4Cfg = kNumCfgH8 - 10;
+static constexpr int kWino4Cfg = kNumCfgH8 - 9;
+static constexpr int kWinoC2Cfg = kNumCfgH8 - 8;
+static constexpr int kWinoC1Cfg = kNumCfgH8 - 7;
+static constexpr int kWinoPCfg = kNumCfgH8 - 6;
+static constexpr int kWinoH2Cfg = kNumCfgH8 - 5;
+static constexpr int kWinoHP1Cfg = kNumCfgH8 - 4;
+static constexpr int kWinoHP2Cfg = kNumCfgH8 - 3;
+static constexpr int kWinoCPCfg = kNumCfgH8 - 2;
+static constexpr int kWinoHLCfg = kNumCfgH8 - 1;
 static_assert(kWinoCfg == 18, "the direct-form configs keep ids 0-17 (engine tile tables)");
 static inline bool is_winoc(int cfg) { return cfg == kWinoC2Cfg || cfg == kWinoC1Cfg || cfg == kWinoCPCfg; }
 // tiles whose kernels only the lab library builds (kind 2 wino64, kind 5 F(4x4), kind 8
@@ -1872,10 +1876,13 @@ static constexpr bool kLabBuild = false;
 #endif
 static inline bool is_wino(int cfg) {
   return cfg == kWinoCfg || cfg == kWino64Cfg || cfg == kWinoQCfg || cfg == kWinoQ4Cfg || cfg == kWino4Cfg ||
-         is_winoc(cfg) || cfg == kWinoPCfg || cfg == kWinoH2Cfg || cfg == kWinoHP1Cfg || cfg == kWinoHP2Cfg;
+         is_winoc(cfg) || cfg == kWinoPCfg || cfg == kWinoH2Cfg || cfg == kWinoHP1Cfg || cfg == kWinoHP2Cfg ||
+         cfg == kWinoHLCfg;
 }
-// fp16-only Winograd tiles: kind 9 and the persistent kinds 10, 11
-static inline bool f16_only(int cfg) { return cfg == kWinoH2Cfg || cfg == kWinoHP1Cfg || cfg == kWinoHP2Cfg; }
+// fp16-only Winograd tiles: kind 9, the persistent kinds 10, 11 and kind 13
+static inline bool f16_only(int cfg) {
+  return cfg == kWinoH2Cfg || cfg == kWinoHP1Cfg || cfg == kWinoHP2Cfg || cfg == kWinoHLCfg;
+}
 // the fp16 Winograd tiles (conv_winoh.hip): kind 6 and the fp16-only kinds
 static inline bool is_winoh(int cfg) { return cfg == kWinoC2Cfg || f16_only(cfg); }
 static constexpr size_t kMaxLds = 160 * 1024;
@@ -2154,6 +2161,7 @@ extern "C" int rrin_conv_h8_cfg_wino(int32_t cfg) {
          : cfg == kWinoHP1Cfg ? 10
          : cfg == kWinoHP2Cfg ? 11
          : cfg == kWinoCPCfg ? 12
+         : cfg == kWinoHLCfg ? 13
                              : 0;
 }
 // Fused level-0 UNetConvBlock (conv_block0.hip): validate and launch.
@@ -2246,6 +2254,7 @@ extern "C" int rrin_conv3x3_h8_fwd(const rrin_conv_h8_desc* d, void* stream) {
   if (d->cfg == kWino64Cfg) return launch_wino64(a, d->epi_mode, st);
   if (d->cfg == kWino4Cfg) return launch_wino4(a, d->epi_mode, st);
 #endif
+  if (d->cfg == kWinoHLCfg && d->prec == RRIN_PREC_F16) return launch_winohl(a, d->epi_mode, st);
   if (is_winoh(d->cfg) && d->prec == RRIN_PREC_F16)
     return launch_winoh(a, d->epi_mode, d->cfg == kWinoH2Cfg || d->cfg == kWinoHP2Cfg ? 2 : 1,
                         d->cfg == kWinoHP1Cfg || d->cfg == kWinoHP2Cfg, st);

@@ -411,6 +411,318 @@ __global__ __launch_bounds__(256, NT == 1 ? 2 : 1) void conv3x3_winoh_kernel(Con
   if (bad && a.status) *a.status = 1;
 }
 
+// ---- kind 13: the kind-6 tile on two patch tiles per workgroup, U shared through LDS.  At fp16
+// the kind-6 U stream (one 16-B U record per lane and MFMA, from L2 into registers) is its
+// structural limit: at the f16 MFMA rate a CU would pull 128 B/clk of U, twice its L2 share
+// (DESIGN.md §5e).  Here 8 waves (two per SIMD, one workgroup per CU) cover TH 8 = two patch
+// tiles: wave w owns B^T row w & 3 of patch tile w >> 2, so waves w and w + 4 use the same U
+// records; the chunk's U (2048 records) is staged by LDS-DMA with the raw tile (3 stages) and
+// each U record is fetched from L2 once per 64 patches instead of once per 32.  Same U, same
+// transforms, same accumulation and epilogue order as kind 6: bitwise its outputs.
+struct WinoHL {
+  static constexpr int NTH = 512;
+  static constexpr int TH = 8;
+  static constexpr int RG = (TH + 2) * 34;            // raw records per group
+  static constexpr int RAW = 2 * RG;                  // per chunk (two groups)
+  static constexpr int PR = (RAW + NTH - 1) / NTH;    // raw DMA pieces per thread
+  static constexpr int RAWS = PR * NTH;               // raw records per stage (the tail: dummy)
+  static constexpr int UREC = 16 * 2 * 64;            // U records per chunk: [point][hh][64 co]
+  static constexpr int PU = UREC / NTH;               // U DMA pieces per thread
+  static constexpr int STAGE = RAWS + UREC;
+  static constexpr int NS = 3;
+  static constexpr int XREC = 2 * 4 * 8 * 64;         // output-transform exchange, one co tile
+  static constexpr size_t LDS = (size_t)(NS * STAGE > XREC ? NS * STAGE : XREC) * 16;
+};
+static_assert(WinoHL::LDS == kWinoHLLds, "LDS size (common.hpp)");
+static_assert(WinoHL::UREC % WinoHL::NTH == 0, "whole U pieces");
+
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void conv3x3_winohl_kernel(ConvH8Args a) {
+  using G = WinoHL;
+  constexpr int CT = 2, BM = 64, TH = G::TH, RG = G::RG, STAGE = G::STAGE, PR = G::PR, PU = G::PU;
+  extern __shared__ __attribute__((aligned(16))) uint4 smem4[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int yw = wv & 3, ntw = wv >> 2;  // B^T row, patch tile of this wave
+  const int j = lane & 31, hh = lane >> 5;
+  int bid;
+  {  // XCD-aware bijective remap: an XCD's workgroups are consecutive tiles
+    const int nwg = gridDim.x, q = nwg >> 3, r = nwg & 7;
+    const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+  }
+  const int ntiles = a.co_blocks * a.tiles_x * a.tiles_y * a.n;
+  if (bid >= ntiles) return;
+  const int nch = a.nchunks;
+  int cob, x0, y0, img;
+  {  // kind 6's workgroup order (co-block groups whose U fits an XCD's L2)
+    const int cpg = a.cob_group > 0 ? a.cob_group : a.co_blocks;
+    const int gsz = cpg * (ntiles / a.co_blocks);
+    const int g = bid / gsz;
+    const int r = bid - g * gsz;
+    const int cg = min(cpg, a.co_blocks - g * cpg);
+    cob = g * cpg + r % cg;
+    int t = r / cg;
+    x0 = (t % a.tiles_x) * 32;
+    t /= a.tiles_x;
+    y0 = (t % a.tiles_y) * TH;
+    img = t / a.tiles_y;
+  }
+
+  // ---- raw tile (rows y0 - 1 .. y0 + TH, cols x0 - 1 .. x0 + 32 of the chunk's two groups) and
+  // the chunk's U, both by LDS-DMA into stage s
+  const uint4* tbase = a.src_hi + (int64_t)img * a.src_img + (int64_t)y0 * a.src_wp + x0 + (kH8PadLeft - 1);
+  uint32_t voff[PR];
+#pragma unroll
+  for (int it = 0; it < PR; ++it) {
+    const int idx = tid + G::NTH * it;
+    const int g = idx >= RG ? 1 : 0;
+    const int rem = idx < G::RAW ? idx - g * RG : 0;
+    const int r = rem / 34, pos = rem - r * 34;
+    const int col = pos < 17 ? 2 * pos : 2 * (pos - 17) + 1;
+    voff[it] = (uint32_t)((idx < G::RAW ? (int64_t)g * a.src_gp : 0) + (int64_t)r * a.src_wp + col) * 16u;
+  }
+  const int64_t chunk_stride = 2 * a.src_gp;
+  const uint4* ubase = a.w_hi + (int64_t)cob * nch * G::UREC;
+  auto issue_chunk = [&](int c, int s) {
+    const auto rs = wh_rsrc(tbase + c * chunk_stride);
+#pragma unroll
+    for (int it = 0; it < PR; ++it) wh_dma16(rs, smem4 + s * STAGE + G::NTH * it + 64 * wv, voff[it]);
+    const auto us = wh_rsrc(ubase + (int64_t)c * G::UREC);
+#pragma unroll
+    for (int it = 0; it < PU; ++it)
+      wh_dma16(us, smem4 + s * STAGE + G::RAWS + G::NTH * it + 64 * wv, (uint32_t)(tid + G::NTH * it) * 16u);
+  };
+
+  // ---- B operands (kind 6's lane mapping within this wave's patch tile)
+  const int jx = (j + 12 * (j >> 4)) & 15;
+  const int ra = yw == 0 ? 0 : (yw == 2 ? 2 : 1);
+  const int rb = yw == 0 ? 2 : (yw == 1 ? 2 : (yw == 2 ? 1 : 3));
+  const _Float16 sgh = yw == 1 ? (_Float16)1.0f : (_Float16)-1.0f;
+  const whx8 sg = {sgh, sgh, sgh, sgh, sgh, sgh, sgh, sgh};
+  unsigned m1w = 0xBC00BC00u;
+  asm volatile("" : "+v"(m1w));
+  const whx8 m1 = __builtin_bit_cast(whx8, make_uint4(m1w, m1w, m1w, m1w));
+  int pcol[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) pcol[k] = hh * RG + (2 * (j >> 4)) * 34 + wh_col(2 * jx + k);
+  const int oa = ra * 34 + ntw * 4 * 34, ob = rb * 34 + ntw * 4 * 34;
+  // U record of point x (of this wave's B^T row), co tile t, lane (j, hh) in a stage
+  const int ubase_l = G::RAWS + ((4 * yw) * 2 + hh) * 64 + j;
+
+  wfx16 acc[CT][4];
+#pragma unroll
+  for (int t = 0; t < CT; ++t)
+#pragma unroll
+    for (int x = 0; x < 4; ++x) acc[t][x] = wfx16{};
+  whx8 u[CT][4];
+  whx8 v[4];
+  whx8 d[8];
+  auto read_raw = [&](int s) {
+    const uint4* rw = smem4 + s * STAGE;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      d[2 * k] = __builtin_bit_cast(whx8, rw[oa + pcol[k]]);
+      d[2 * k + 1] = __builtin_bit_cast(whx8, rw[ob + pcol[k]]);
+    }
+  };
+  auto read_u = [&](int s) {
+    const uint4* us = smem4 + s * STAGE + ubase_l;
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+      for (int t = 0; t < CT; ++t) u[t][x] = __builtin_bit_cast(whx8, us[x * 128 + t * 32]);
+  };
+  auto transform = [&]() {
+    whx8 tr[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) tr[k] = __builtin_elementwise_fma(sg, d[2 * k + 1], d[2 * k]);
+    v[0] = __builtin_elementwise_fma(m1, tr[2], tr[0]);
+    v[1] = tr[1] + tr[2];
+    v[2] = __builtin_elementwise_fma(m1, tr[1], tr[2]);
+    v[3] = __builtin_elementwise_fma(m1, tr[3], tr[1]);
+  };
+  auto mfma_point = [&](int x) {
+#pragma unroll
+    for (int t = 0; t < CT; ++t) acc[t][x] = __builtin_amdgcn_mfma_f32_32x32x16_f16(u[t][x], v[x], acc[t][x], 0, 0, 0);
+  };
+  auto bar = [&]() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+  auto fence = [&]() { __builtin_amdgcn_sched_barrier(0); };
+
+  // chunk c (its U in u, its B operands in v): points 0-2; the wait for chunk c + 1's DMA (the
+  // only VMEM in flight); the barrier; chunk c + 2's DMA; chunk c + 1's window reads; point 3;
+  // chunk c + 1's transform and U reads
+  auto chunk = [&](int c, int s, const bool more) {
+#pragma unroll
+    for (int x = 0; x < 3; ++x) mfma_point(x);
+    fence();
+    const int s1 = s == 2 ? 0 : s + 1;
+    if (more) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      bar();
+      if (c + 2 < nch) issue_chunk(c + 2, s == 0 ? 2 : s - 1);
+      read_raw(s1);
+    }
+    fence();
+    mfma_point(3);
+    fence();
+    if (more) {
+      transform();
+      read_u(s1);
+    }
+  };
+
+  issue_chunk(0, 0);
+  if (nch > 1) {
+    issue_chunk(1, 1);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PR + PU) : "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  bar();
+  read_raw(0);
+  transform();
+  read_u(0);
+  {
+    int s = 0;
+    for (int c = 0; c + 1 < nch; ++c) {
+      chunk(c, s, true);
+      s = s == 2 ? 0 : s + 1;
+    }
+    chunk(nch - 1, s, false);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  float bsv[CT][16];
+#pragma unroll
+  for (int t = 0; t < CT; ++t)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) bsv[t][i] = a.bias[(CT * cob + t) * 32 + 8 * (i >> 2) + 4 * hh + (i & 3)];
+  __syncthreads();  // every read of the stages done before the exchange reuses the LDS
+
+  // ---- kind 6's output transform, exchanged per patch tile among its four waves
+  wfx4* X = reinterpret_cast<wfx4*>(smem4);
+  const int r = yw & 1, cc = yw >> 1;
+  uint4* dst = a.dst_hi + (int64_t)img * a.dst_img;
+  const float isc = a.inv_wscale;
+  bool bad = false;
+  auto store4 = [&](uint4* base, int64_t rec, const float* vv) {
+    bad |= !(fmaxf(fmaxf(fabsf(vv[0]), fabsf(vv[1])), fmaxf(fabsf(vv[2]), fabsf(vv[3]))) <= kWinoHF16Max);
+    reinterpret_cast<uint2*>(base + rec)[hh] = wh_pack4(vv);
+  };
+#pragma unroll
+  for (int t = 0; t < CT; ++t) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      wfx4 g;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int vi = 4 * k + e, c2 = vi >> 4, i = vi & 15;
+        const float q0 = acc[t][0][i], q1 = acc[t][1][i], q2 = acc[t][2][i], q3 = acc[t][3][i];
+        g[e] = c2 == 0 ? (q0 + q1) + q2 : (q1 - q2) - q3;
+      }
+      X[((ntw * 4 + yw) * 8 + k) * 64 + lane] = g;
+    }
+    __syncthreads();
+    float yv[16];
+#pragma unroll
+    for (int k4 = 0; k4 < 4; ++k4) {
+      const int k = 4 * cc + k4;
+      const wfx4 q0 = X[((ntw * 4 + 0) * 8 + k) * 64 + lane];
+      const wfx4 q1 = X[((ntw * 4 + 1) * 8 + k) * 64 + lane];
+      const wfx4 q2 = X[((ntw * 4 + 2) * 8 + k) * 64 + lane];
+      const wfx4 q3 = X[((ntw * 4 + 3) * 8 + k) * 64 + lane];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) yv[4 * k4 + e] = r == 0 ? (q0[e] + q1[e]) + q2[e] : (q1[e] - q2[e]) - q3[e];
+    }
+    __syncthreads();  // X is rewritten by the next co tile / the pool exchange
+    const int cobe = CT * cob + t;
+    const int pr = 2 * ntw + (j >> 4);
+    const int y = y0 + 2 * pr + r, x = x0 + 2 * jx + cc;
+    if constexpr (EPI == RRIN_EPI_SUBPIXEL) {
+      const int HH = 2 * a.h, WW = 2 * a.w, creal = a.cout >> 2;
+      if (cobe * 32 < a.cout && y < a.h && x < a.w) {
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          const int Y = 2 * y + (qq >> 1), XX = 2 * x + (qq & 1);
+          const int64_t ri = ring_index(Y, XX, HH, WW);
+          if (ri >= 0) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              a.edge[((int64_t)img * creal + cobe * 8 + 4 * hh + e) * a.ring + ri] = yv[4 * qq + e] * isc;
+          } else {
+            float vv[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) vv[e] = yv[4 * qq + e] * isc + bsv[t][4 * qq + e];
+            store4(dst, (int64_t)cobe * a.dst_gp + (int64_t)(Y + 1) * a.dst_wp + XX + kH8PadLeft, vv);
+          }
+        }
+      }
+    } else {
+      float vv[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        float tv = yv[i] * isc + bsv[t][i];
+        if constexpr (EPI != RRIN_EPI_LINEAR) tv = leaky(tv, a.slope);
+        vv[i] = tv;
+      }
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        if (cobe * 32 + 8 * qq < a.cout && y < a.h && x < a.w) {
+          const int64_t rec = (int64_t)(cobe * 4 + qq) * a.dst_gp + (int64_t)(y + 1) * a.dst_wp + x + kH8PadLeft;
+          store4(dst, rec, &vv[4 * qq]);
+          if constexpr (EPI == RRIN_EPI_LEAKY_REP) {
+            const int dy0 = y == 0 ? -1 : 0, dy1 = y == a.h - 1 ? 1 : 0;
+            const int dx0 = x == 0 ? -1 : 0, dx1 = x == a.w - 1 ? 1 : 0;
+            for (int dy = dy0; dy <= dy1; ++dy)
+              for (int dx = dx0; dx <= dx1; ++dx)
+                if (dy | dx) store4(dst, rec + (int64_t)dy * a.dst_wp + dx, &vv[4 * qq]);
+          }
+        }
+      }
+      if constexpr (EPI == RRIN_EPI_LEAKY_POOL) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          wfx4 g;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) g[e] = vv[4 * k + e];
+          X[((ntw * 4 + yw) * 4 + k) * 64 + lane] = g;
+        }
+        __syncthreads();
+        if (yw == 0) {
+          const int xp = x0 + 2 * jx, yp = y0 + 2 * pr;
+          uint4* pdst = a.pool_hi + (int64_t)img * a.pool_img;
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq) {
+            const wfx4 y00 = X[((ntw * 4 + 0) * 4 + qq) * 64 + lane];
+            const wfx4 y10 = X[((ntw * 4 + 1) * 4 + qq) * 64 + lane];
+            const wfx4 y01 = X[((ntw * 4 + 2) * 4 + qq) * 64 + lane];
+            const wfx4 y11 = X[((ntw * 4 + 3) * 4 + qq) * 64 + lane];
+            if (cobe * 32 + 8 * qq < a.cout && yp < a.h && xp < a.w) {
+              float s4[4];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) s4[e] = 0.25f * ((y00[e] + y10[e]) + (y01[e] + y11[e]));
+              store4(pdst, (int64_t)(cobe * 4 + qq) * a.pool_gp + (int64_t)(yp / 2 + 1) * a.pool_wp + xp / 2 + kH8PadLeft,
+                     s4);
+            }
+          }
+        }
+        __syncthreads();
+      }
+    }
+  }
+  if (bad && a.status) *a.status = 1;
+}
+
+template <int EPI>
+static int launch_winohl_k(const ConvH8Args& a, hipStream_t st) {
+  auto k = conv3x3_winohl_kernel<EPI>;
+  static LdsAttr attr;
+  if (int e = attr.ensure((const void*)k, (int)WinoHL::LDS, st)) return e;
+  const int64_t grid = (int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n;
+  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(WinoHL::NTH), WinoHL::LDS, st, a);
+  return hip_code(hipGetLastError());
+}
+
 #ifdef RRIN_LAB  // kinds 9-11 (one block per CU, persistent grids): lab library only
 // ---- persistent form (kinds 10 / 11): a workgroup walks tiles bid, bid + grid, ... and its
 // chunk pipeline runs on across tile boundaries.  At fp16 a tile's MFMAs take a few us, about
@@ -887,6 +1199,19 @@ static int launch_winoh_e(const ConvH8Args& b, int epi, hipStream_t st) {
     case RRIN_EPI_LEAKY_POOL: return launch_winoh_k<RRIN_EPI_LEAKY_POOL, NT>(b, st);
     case RRIN_EPI_LEAKY_REP: return launch_winoh_k<RRIN_EPI_LEAKY_REP, NT>(b, st);
     case RRIN_EPI_SUBPIXEL: return launch_winoh_k<RRIN_EPI_SUBPIXEL, NT>(b, st);
+  }
+  return RRIN_E_ARG;
+}
+
+int launch_winohl(const ConvH8Args& a, int epi, hipStream_t st) {
+  ConvH8Args b = a;
+  b.cob_group = winoh_cob_group(a);
+  switch (epi) {
+    case RRIN_EPI_LINEAR: return launch_winohl_k<RRIN_EPI_LINEAR>(b, st);
+    case RRIN_EPI_LEAKY: return launch_winohl_k<RRIN_EPI_LEAKY>(b, st);
+    case RRIN_EPI_LEAKY_POOL: return launch_winohl_k<RRIN_EPI_LEAKY_POOL>(b, st);
+    case RRIN_EPI_LEAKY_REP: return launch_winohl_k<RRIN_EPI_LEAKY_REP>(b, st);
+    case RRIN_EPI_SUBPIXEL: return launch_winohl_k<RRIN_EPI_SUBPIXEL>(b, st);
   }
   return RRIN_E_ARG;
 }

@@ -53,7 +53,7 @@ def assert_walks(n, cout_rows, h, w, th, slots_per_cu):
 
 def test_fp16_winograd_kinds_present():
     k = kinds()
-    assert set(k) in ({6}, {6, 9, 10, 11}), k
+    assert set(k) in ({6, 13}, {6, 9, 10, 11, 13}), k
     need_lab_kinds()
     lib = _lib.lib()
     for a, b in PAIRS:
@@ -238,3 +238,43 @@ def test_winograd_conv_bitwise_beside_side_stream_conv(gpu, prec, kind):
         torch.cuda.synchronize(gpu)
         bad += sum(int(not torch.equal(o.hi, ref.hi)) for o in outs)
     assert bad == 0, f"{bad}/32 convs differ from the serial result"
+
+
+@pytest.mark.parametrize("epi", [_lib.EPI_LINEAR, _lib.EPI_LEAKY, _lib.EPI_LEAKY_REP, _lib.EPI_LEAKY_POOL])
+@pytest.mark.parametrize("n,cin,cout,h,w", [(2, 64, 128, 48, 96), (1, 256, 256, 92, 160), (3, 32, 64, 22, 70),
+                                            (1, 16, 64, 46, 80)])
+def test_kind13_bitwise_kind6(gpu, epi, n, cin, cout, h, w):
+    """Kind 13 (two patch tiles per workgroup, U shared through LDS) gives kind 6's bits: the same
+    U, transforms and accumulation order -- ragged tile rows (h % 8), every epilogue."""
+    if epi == _lib.EPI_LEAKY_POOL and (h % 2 or w % 2):
+        pytest.skip("pool needs even sizes")
+    torch.manual_seed(n * cin + cout + h + epi)
+    x = torch.rand(n, cin, h, w, device=gpu) * 2 - 1
+    wt, b = keyed_conv(cin, cout, "winohl")
+    slope = None if epi == _lib.EPI_LINEAR else 0.1
+    ref = ref_conv(x, wt, b, slope)
+    outs = []
+    for kind in (6, 13):
+        kw = {}
+        if epi == _lib.EPI_LEAKY_POOL:
+            kw = dict(dst_off=cout, dst=H8Tensor(n, 2 * cout, h, w, gpu, F16))
+        dst, pool = conv_h8(H8Tensor.from_nchw(x, F16), wt, b, kind_cfg(kind, F16), F16, epi=epi, **kw)
+        got = dst.to_nchw(cout, cout) if epi == _lib.EPI_LEAKY_POOL else dst.to_nchw()
+        np.testing.assert_allclose(got.cpu().double().numpy(), ref.numpy(), **TOLF, err_msg=f"kind {kind}")
+        outs.append((dst, pool))
+    (d0, p0), (d1, p1) = outs
+    assert torch.equal(d0.hi, d1.hi)
+    if epi == _lib.EPI_LEAKY_POOL:
+        assert torch.equal(p0.hi, p1.hi)
+
+
+@pytest.mark.parametrize("n,cin,cout,sh,sw", [(2, 128, 64, 46, 80), (1, 256, 128, 92, 160)])
+def test_kind13_subpixel(gpu, n, cin, cout, sh, sw):
+    torch.manual_seed(cin + sh)
+    x = torch.rand(n, cin, sh, sw, device=gpu) * 2 - 1
+    wt, b = keyed_conv(cin, cout, "winohl_sub")
+    src = H8Tensor.from_nchw(x, F16)
+    replicate_ring(src)
+    d0 = subpixel_upconv(src, wt, b, kind_cfg(6, F16), F16, dst=H8Tensor(n, 2 * cout, 2 * sh, 2 * sw, gpu, F16))
+    d1 = subpixel_upconv(src, wt, b, kind_cfg(13, F16), F16, dst=H8Tensor(n, 2 * cout, 2 * sh, 2 * sw, gpu, F16))
+    assert torch.equal(d0.hi, d1.hi)

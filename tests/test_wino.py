@@ -95,21 +95,22 @@ def test_wino_config_entry():
     # for cout <= 32 (BM 32 x TH 8, 8 waves)
     # 9: the fp16-only register-U tile on 2 patch tiles (BM 64 x TH 8, one block per CU); 10, 11:
     # kinds 6 and 9 on a persistent grid (fp16 only; 9-11 are built into the lab library only)
-    # 12: kind 6 on a persistent grid (exact fp32)
-    assert sorted(lib.rrin_conv_h8_cfg_wino(c) for c in ids) == [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12]
+    # 12: kind 6 on a persistent grid (exact fp32); 13: kind 6 on two patch tiles per workgroup,
+    # U shared through LDS (fp16 only)
+    assert sorted(lib.rrin_conv_h8_cfg_wino(c) for c in ids) == [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13]
     assert min(ids) == 18  # the direct-form configs keep ids 0-17 (engine tile tables)
     assert {lib.rrin_conv_h8_cfg_wino(c): lib.rrin_conv_h8_cfg_bm(c) for c in ids} == {
-        1: 32, 2: 64, 3: 32, 4: 32, 5: 32, 6: 64, 7: 32, 8: 32, 9: 64, 10: 64, 11: 64, 12: 64}
+        1: 32, 2: 64, 3: 32, 4: 32, 5: 32, 6: 64, 7: 32, 8: 32, 9: 64, 10: 64, 11: 64, 12: 64, 13: 64}
     for c in ids:
         kind = lib.rrin_conv_h8_cfg_wino(c)
         assert lib.rrin_conv_h8_cfg_th(c) == {4: 4, 5: 16, 6: 4, 10: 4, 12: 4}.get(kind, 8)
         # kinds 2, 5 and 8 lost on every Net shape: their kernels are built only into the lab
         # library (make lab), so the product library reports them as not usable
-        assert lib.rrin_conv_h8_cfg_ok(c, _lib.PREC_F32R) == (0 if kind in (2, 5, 8, 9, 10, 11) else 1)
-        # split16 never runs a Winograd tile; fp16 runs kind 6 (conv_winoh.hip, ABI 13; the lab
-        # library also 9, 10, 11)
+        assert lib.rrin_conv_h8_cfg_ok(c, _lib.PREC_F32R) == (0 if kind in (2, 5, 8, 9, 10, 11, 13) else 1)
+        # split16 never runs a Winograd tile; fp16 runs kinds 6 and 13 (conv_winoh.hip, ABI 13; the
+        # lab library also 9, 10, 11)
         assert lib.rrin_conv_h8_cfg_ok(c, _lib.PREC_F16X3) == 0
-        assert lib.rrin_conv_h8_cfg_ok(c, _lib.PREC_F16) == (1 if kind == 6 else 0)
+        assert lib.rrin_conv_h8_cfg_ok(c, _lib.PREC_F16) == (1 if kind in (6, 13) else 0)
     assert lib.rrin_pack_conv3x3_wino_floats(33, 5) == 2 * 1 * 16 * 2 * 32 * 4
     assert lib.rrin_pack_conv3x3_wino_floats(0, 5) < 0
     assert lib.rrin_pack_conv3x3_wino_bm_floats(65, 9, 64) == 2 * 2 * 16 * 2 * 64 * 4
