@@ -273,8 +273,9 @@ int64_t rrin_conv_h8_ring_floats(const rrin_conv_h8_desc* d, int64_t* cnt_ints);
  * RRIN_PREC_F16 only (ABI 13: fp16 Winograd, packed by rrin_pack_conv3x3_wino_h8;
  * cin % 16 == 0 or tail_finite; no split-K, no ring fold); 10 and 11 = kinds 6 and 9 on
  * a persistent grid (workgroups walk tiles; bitwise equal; fp16 only).  12 = kind 6 on a
- * persistent grid at F32R (bitwise equal to kind 6).  Kinds 2, 5, 8, 9, 10 and 11 are
- * built only into the lab library: the product library reports them with
+ * persistent grid at F32R (bitwise equal to kind 6).  13 = kind 6 on two patch tiles per
+ * workgroup with U shared through LDS (fp16; bitwise equal to kind 6).  Kinds 2, 5, 8, 9, 10,
+ * 11 and 13 are built only into the lab library: the product library reports them with
  * rrin_conv_h8_cfg_ok == 0 and rrin_conv3x3_h8_fwd returns RRIN_E_CONFIG.
  * 0: direct form. */
 int rrin_conv_h8_cfg_wino(int32_t cfg);

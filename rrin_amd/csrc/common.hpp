@@ -271,7 +271,9 @@ int launch_winoh(const ConvH8Args& a, int epi, int nt, bool persistent, hipStrea
 constexpr size_t kWinoHP1Lds = (size_t)(3 * 512 + 2048 + 128) * 16;  // persistent TH 4: stages + exchange + bias
 // kind 13 (fp16): kind 6 on two patch tiles per workgroup (8 waves), U shared through LDS: 3 stages
 // of [raw 1024 | U 2048] records
+#ifdef RRIN_LAB
 int launch_winohl(const ConvH8Args& a, int epi, hipStream_t st);
+#endif
 constexpr size_t kWinoHLLds = (size_t)3 * (1024 + 2048) * 16;
 constexpr size_t kWinoHP2Lds = (size_t)(3 * 768 + 4096 + 128) * 16;  // persistent TH 8
 // fused level-0 UNetConvBlock at fp16 (conv_block0.hip): conv a (cin -> 32) + leaky, conv b

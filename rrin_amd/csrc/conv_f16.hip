@@ -1865,9 +1865,10 @@ static inline bool is_winoc(int cfg) { return cfg == kWinoC2Cfg || cfg == kWinoC
 // 6 / 9 on a persistent grid: slower in the two-stream forward, and an A/B build with one
 // workgroup per CU ran the C3 forward non-deterministically -- a race not found)
 // are lab-only too.
+// Kind 13 (U shared through LDS by two patch tiles) measured 1.0-1.3x kind 6's time per conv: lab-only.
 static inline bool lab_only(int cfg) {
   return cfg == kWino64Cfg || cfg == kWino4Cfg || cfg == kWinoPCfg || cfg == kWinoH2Cfg || cfg == kWinoHP1Cfg ||
-         cfg == kWinoHP2Cfg;
+         cfg == kWinoHP2Cfg || cfg == kWinoHLCfg;
 }
 #ifdef RRIN_LAB
 static constexpr bool kLabBuild = true;
@@ -2254,7 +2255,9 @@ extern "C" int rrin_conv3x3_h8_fwd(const rrin_conv_h8_desc* d, void* stream) {
   if (d->cfg == kWino64Cfg) return launch_wino64(a, d->epi_mode, st);
   if (d->cfg == kWino4Cfg) return launch_wino4(a, d->epi_mode, st);
 #endif
+#ifdef RRIN_LAB
   if (d->cfg == kWinoHLCfg && d->prec == RRIN_PREC_F16) return launch_winohl(a, d->epi_mode, st);
+#endif
   if (is_winoh(d->cfg) && d->prec == RRIN_PREC_F16)
     return launch_winoh(a, d->epi_mode, d->cfg == kWinoH2Cfg || d->cfg == kWinoHP2Cfg ? 2 : 1,
                         d->cfg == kWinoHP1Cfg || d->cfg == kWinoHP2Cfg, st);

@@ -411,6 +411,7 @@ __global__ __launch_bounds__(256, NT == 1 ? 2 : 1) void conv3x3_winoh_kernel(Con
   if (bad && a.status) *a.status = 1;
 }
 
+#ifdef RRIN_LAB  // kind 13: 1.0-1.3x kind 6's time per conv, lab library only
 // ---- kind 13: the kind-6 tile on two patch tiles per workgroup, U shared through LDS.  At fp16
 // the kind-6 U stream (one 16-B U record per lane and MFMA, from L2 into registers) is its
 // structural limit: at the f16 MFMA rate a CU would pull 128 B/clk of U, twice its L2 share
@@ -722,6 +723,7 @@ static int launch_winohl_k(const ConvH8Args& a, hipStream_t st) {
   hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(WinoHL::NTH), WinoHL::LDS, st, a);
   return hip_code(hipGetLastError());
 }
+#endif  // RRIN_LAB (kind 13)
 
 #ifdef RRIN_LAB  // kinds 9-11 (one block per CU, persistent grids): lab library only
 // ---- persistent form (kinds 10 / 11): a workgroup walks tiles bid, bid + grid, ... and its
@@ -1203,6 +1205,7 @@ static int launch_winoh_e(const ConvH8Args& b, int epi, hipStream_t st) {
   return RRIN_E_ARG;
 }
 
+#ifdef RRIN_LAB
 int launch_winohl(const ConvH8Args& a, int epi, hipStream_t st) {
   ConvH8Args b = a;
   b.cob_group = winoh_cob_group(a);
@@ -1215,6 +1218,7 @@ int launch_winohl(const ConvH8Args& a, int epi, hipStream_t st) {
   }
   return RRIN_E_ARG;
 }
+#endif
 
 int launch_winoh(const ConvH8Args& a, int epi, int nt, bool persistent, hipStream_t st) {
   ConvH8Args b = a;

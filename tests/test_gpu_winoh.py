@@ -39,8 +39,8 @@ PAIRS = [(6, 10), (9, 11)]  # one-tile kind -> its persistent kind
 
 
 def need_lab_kinds():
-    if not {9, 10, 11} <= set(kinds()):
-        pytest.skip("fp16 kinds 9-11: lab library only")
+    if not {9, 10, 11, 13} <= set(kinds()):
+        pytest.skip("fp16 kinds 9-11, 13: lab library only")
 
 
 def assert_walks(n, cout_rows, h, w, th, slots_per_cu):
@@ -53,7 +53,7 @@ def assert_walks(n, cout_rows, h, w, th, slots_per_cu):
 
 def test_fp16_winograd_kinds_present():
     k = kinds()
-    assert set(k) in ({6, 13}, {6, 9, 10, 11, 13}), k
+    assert set(k) in ({6}, {6, 9, 10, 11, 13}), k
     need_lab_kinds()
     lib = _lib.lib()
     for a, b in PAIRS:
@@ -244,8 +244,10 @@ def test_winograd_conv_bitwise_beside_side_stream_conv(gpu, prec, kind):
 @pytest.mark.parametrize("n,cin,cout,h,w", [(2, 64, 128, 48, 96), (1, 256, 256, 92, 160), (3, 32, 64, 22, 70),
                                             (1, 16, 64, 46, 80)])
 def test_kind13_bitwise_kind6(gpu, epi, n, cin, cout, h, w):
-    """Kind 13 (two patch tiles per workgroup, U shared through LDS) gives kind 6's bits: the same
-    U, transforms and accumulation order -- ragged tile rows (h % 8), every epilogue."""
+    """Kind 13 (two patch tiles per workgroup, U shared through LDS; lab library) gives kind 6's
+    bits: the same U, transforms and accumulation order -- ragged tile rows (h % 8), every
+    epilogue."""
+    need_lab_kinds()
     if epi == _lib.EPI_LEAKY_POOL and (h % 2 or w % 2):
         pytest.skip("pool needs even sizes")
     torch.manual_seed(n * cin + cout + h + epi)
@@ -270,6 +272,7 @@ def test_kind13_bitwise_kind6(gpu, epi, n, cin, cout, h, w):
 
 @pytest.mark.parametrize("n,cin,cout,sh,sw", [(2, 128, 64, 46, 80), (1, 256, 128, 92, 160)])
 def test_kind13_subpixel(gpu, n, cin, cout, sh, sw):
+    need_lab_kinds()
     torch.manual_seed(cin + sh)
     x = torch.rand(n, cin, sh, sw, device=gpu) * 2 - 1
     wt, b = keyed_conv(cin, cout, "winohl_sub")

@@ -107,10 +107,10 @@ def test_wino_config_entry():
         # kinds 2, 5 and 8 lost on every Net shape: their kernels are built only into the lab
         # library (make lab), so the product library reports them as not usable
         assert lib.rrin_conv_h8_cfg_ok(c, _lib.PREC_F32R) == (0 if kind in (2, 5, 8, 9, 10, 11, 13) else 1)
-        # split16 never runs a Winograd tile; fp16 runs kinds 6 and 13 (conv_winoh.hip, ABI 13; the
-        # lab library also 9, 10, 11)
+        # split16 never runs a Winograd tile; fp16 runs kind 6 (conv_winoh.hip, ABI 13; the lab
+        # library also 9, 10, 11, 13)
         assert lib.rrin_conv_h8_cfg_ok(c, _lib.PREC_F16X3) == 0
-        assert lib.rrin_conv_h8_cfg_ok(c, _lib.PREC_F16) == (1 if kind in (6, 13) else 0)
+        assert lib.rrin_conv_h8_cfg_ok(c, _lib.PREC_F16) == (1 if kind == 6 else 0)
     assert lib.rrin_pack_conv3x3_wino_floats(33, 5) == 2 * 1 * 16 * 2 * 32 * 4
     assert lib.rrin_pack_conv3x3_wino_floats(0, 5) < 0
     assert lib.rrin_pack_conv3x3_wino_bm_floats(65, 9, 64) == 2 * 2 * 16 * 2 * 64 * 4
