@@ -132,9 +132,10 @@ def parse():
     ap.add_argument("--cpu-pairs", type=int, default=2, help="pairs timed on the CPU baseline")
     ap.add_argument("--cpu-all-threads", action="store_true",
                     help="also time one CPU pair on os.cpu_count() threads (beyond the job's CPU quota)")
-    ap.add_argument("--streams", type=int, default=2,
+    ap.add_argument("--streams", type=int, default=None,
                     help="HIP streams the rank's pairs are split over (their kernels overlap, filling each "
-                         "other's launch gaps and last-wave tails; outputs are bitwise those of one stream)")
+                         "other's launch gaps and last-wave tails; outputs are bitwise those of one stream); "
+                         "default engine.default_streams: fp16 one pair per stream up to 4, else 2")
     ap.add_argument("--dist-init", action="store_true",
                     help="initialise torch.distributed and run the all-gather path even at WORLD_SIZE 1 "
                          "(exercises RCCL / the gather check on a single GPU)")
@@ -446,6 +447,8 @@ def main():
     split = [int(c) for c in args.split.split(",")] if args.split else None
     if split:
         args.streams = len(split)
+    elif args.streams is None:
+        args.streams = engine_mod.default_streams(args.precision, B)
 
     last_gather = [None]
 

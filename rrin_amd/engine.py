@@ -300,6 +300,14 @@ WINO_F16_KIND = 6
 FUSE_L0 = 2
 
 
+def default_streams(precision: str, batch: int) -> int:
+    """HIP streams a forward of `batch` pairs is split over by default: fp16 one pair per stream
+    up to 4 (C3 1280x736 x 4: 488.8-489.1 pairs/s on 4 streams vs 482.1-482.3 on 2), the other
+    precisions 2 (headline 1280x720 x 4 exact fp32: 143.0-143.4 on 2 vs 141.8-142.0 on 4;
+    profiles/r05/streams_ab.txt).  The output is bitwise that of one stream either way."""
+    return max(1, min(batch, 4 if precision == "fp16" else 2))
+
+
 def fused_pairs(convs) -> list:
     """Indices i of the (cin, cout, level, edge) list whose conv and conv i + 1 form a level-0
     UNetConvBlock: conv i (not an up conv) -> 32 channels at level 0, conv i + 1 32 -> 32 at
@@ -721,7 +729,7 @@ class RRINEngine:
         return self._sides[:k]
 
     def forward(self, i0: torch.Tensor, i1: torch.Tensor, t=0.5, prof=None, reuse_flow: bool = False,
-                streams: int = 1, split=None, taps: dict | None = None) -> torch.Tensor:
+                streams: int | None = 1, split=None, taps: dict | None = None) -> torch.Tensor:
         """One Net.forward.  ``reuse_flow=True`` promises that (i0, i1) is the pair
         of the previous call with the same shape: the Flow U-Net (t-independent,
         model.py:35, 30 % of the FLOPs) is skipped and its kept raw output is
@@ -729,7 +737,8 @@ class RRINEngine:
         into that many contiguous parts, each with its own workspace, enqueued
         on its own HIP stream: the parts' kernels overlap, filling each other's
         launch gaps and last-wave tails (pairs are independent, so the output is
-        bitwise the same).  ``split`` gives the part sizes explicitly.
+        bitwise the same).  ``split`` gives the part sizes explicitly.  ``streams=None``: the
+        precision's default (``default_streams``).
 
         ``taps`` (test / debug, one stream only): a dict that receives the four
         U-Nets' raw outputs (their ``last`` conv before the model.py glue,
@@ -745,6 +754,8 @@ class RRINEngine:
         if h % 16 or w % 16 or n < 1:
             raise RuntimeError(f"H and W must be multiples of 16 (the Flow U-Net pools 4 times); "
                                f"got {h}x{w} (reference fails at model.py:41)")
+        if streams is None:
+            streams = default_streams(self.precision, n)
         self._poll_range()
         i0 = i0.contiguous()
         i1 = i1.contiguous()

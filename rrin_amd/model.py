@@ -55,8 +55,9 @@ class Net(nn.Module):
         self.subpixel_max_level = 2
         # HIP streams a batch of N >= 2 pairs is split over (pairs are
         # independent: the output is bitwise that of one stream; the parts'
-        # kernels fill each other's launch gaps and tails)
-        self.streams = 2
+        # kernels fill each other's launch gaps and tails); None: by precision
+        # and batch (engine.default_streams: fp16 up to 4, else 2)
+        self.streams = None
         self.register_load_state_dict_post_hook(Net._on_load)
 
     # Packed weights are rebuilt after load_state_dict / .to() (version bump) and

@@ -121,7 +121,9 @@ def test_streams_split_is_bitwise(gpu, nets, precision):
         assert torch.equal(eng.forward(i0, i1, 0.5, split=[1, 4]), one)
         net.streams = 1
         assert torch.equal(net(i0, i1, 0.5), one)
-        net.streams = 2  # the module default
+        net.streams = 2
+        assert torch.equal(net(i0, i1, 0.5), one)
+        net.streams = None  # the module default: by precision and batch (engine.default_streams)
         assert torch.equal(net(i0, i1, 0.5), one)
     net.precision = "fp32"
 
