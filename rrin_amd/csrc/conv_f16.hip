@@ -2079,6 +2079,9 @@ static int h8_prepare(const rrin_conv_h8_desc* d, ConvH8Args& a, bool need_scrat
     // two record groups per K chunk; F(4x4): one
     a.nchunks = d->cfg == kWino4Cfg ? (d->cin + 3) / 4 : (d->cin + 7) / 8;
   }
+  // the Winograd tiles stage every record group of every chunk (past cin against zero
+  // weights): the source view must hold them, or the staging reads past the tensor
+  if (is_wino(d->cfg) && (d->cfg == kWino4Cfg ? a.nchunks : 2 * a.nchunks) > d->src.groups) return RRIN_E_SHAPE;
   a.n = d->n;
   if ((int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n > 0x7fffffff) return RRIN_E_SHAPE;
   a.ksplit = 1;

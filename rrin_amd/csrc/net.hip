@@ -491,7 +491,8 @@ int run_unet_h8(const Plan& p, const UNetSpec& u, const rrin_conv_weights* cw, c
   for (int L = 0; L < D; ++L) {
     const int C = chans(L);
     const int cin = L ? chans(L - 1) : u.in_ch;
-    const rrin_h8 in = L ? hview(p.X[L], 0, cin) : hview(p.G, 0, cin);
+    // level 0 views all 16 staged channels of G (zero past in_ch): Winograd tiles read whole chunks
+    const rrin_h8 in = L ? hview(p.X[L], 0, cin) : hview(p.G, 0, 16);
     const rrin_h8 t = hview(p.T[L], 0, C);
     if (L == 0 && D >= 2 && fused_block0(p, cw[k])) {  // down_path[0] in one launch
       const rrin_h8 bridge = hview(p.CAT[0], C, C);

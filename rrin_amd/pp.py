@@ -60,13 +60,15 @@ class H8Tensor:
     """Channel-record activation tensor (record layout, include/rrin_hip.h):
     ``hi`` (and for fp32_split16 ``lo``) are ``[n, ceil(c/8), hp, wp, 8]``
     half tensors (fp32 records, PREC_F32R: ``[n, ceil(c/4), hp, wp, 4]``
-    float), pixel (y,x) at ``[.., y+1, x+8, :]``; padding zero."""
+    float), pixel (y,x) at ``[.., y+1, x+8, :]``; padding zero.  The group count is
+    rounded up to whole 2-group chunks: the Winograd tiles stage both record groups of
+    every K chunk (``chunk_view``), past ``c`` against zero weights."""
 
     def __init__(self, n: int, c: int, h: int, w: int, device, prec: int):
         self.n, self.c, self.h, self.w, self.prec = n, c, h, w, prec
         self.g = _lib.geom_h8(h, w)
         self.cpr = _lib.chans_per_record(prec)
-        self.groups = (c + self.cpr - 1) // self.cpr
+        self.groups = (c + 2 * self.cpr - 1) // (2 * self.cpr) * 2
         shape = (n, self.groups, self.g.hp, self.g.wp, self.cpr)
         dt = torch.float32 if prec == _lib.PREC_F32R else torch.float16
         self.hi = torch.zeros(shape, dtype=dt, device=device)
@@ -83,6 +85,13 @@ class H8Tensor:
         v.g_off = ch_off // self.cpr
         v.groups = (channels + self.cpr - 1) // self.cpr
         v.g = self.g
+        return v
+
+    def chunk_view(self, ch_off: int = 0, channels: int | None = None) -> _lib.H8:
+        """``view`` widened to whole 2-group chunks (within the allocation): the source
+        view of a conv, which may stage groups past ``channels`` (conv_f16.hip h8_prepare)."""
+        v = self.view(ch_off, channels)
+        v.groups = min((v.groups + 1) // 2 * 2, self.groups - v.g_off)
         return v
 
     @classmethod

@@ -48,7 +48,7 @@ def block0(src, cin, wa, ba, cfg_a, wb, bb, cfg_b, pool, dst=None, dst_off=0, st
     d = _lib.Block0Desc()
     d.n, d.cin, d.cfg_a, d.cfg_b, d.slope = n, cin, cfg_a, cfg_b, 0.1
     d.inv_wscale_a, d.inv_wscale_b, d.tail_finite = inva, invb, tail_finite
-    d.src = src.view(0, cin)
+    d.src = src.chunk_view(0, cin)
     d.dst = dst.view(dst_off, 32)
     if pl is not None:
         d.pool = pl.view(0, 32)
@@ -141,7 +141,7 @@ def test_block0_rejects(gpu):
     def desc(**kw):
         d = _lib.Block0Desc()
         d.n, d.cin, d.cfg_a, d.cfg_b, d.slope, d.inv_wscale_a, d.inv_wscale_b = n, cin, cfg, cfg, 0.1, inv, inv
-        d.src, d.dst = src.view(0, cin), dst.view(0, 32)
+        d.src, d.dst = src.chunk_view(0, cin), dst.view(0, 32)
         d.whi_a = d.whi_b = wh.data_ptr()
         d.bias_a = d.bias_b = bp.data_ptr()
         for k, v in kw.items():

@@ -34,7 +34,7 @@ def side_conv(dev, prec):
     whi, wlo, bp, inv = pack_h8(wt, torch.zeros(cout), cfg, prec, dev)
     d = _lib.ConvH8Desc()
     d.n, d.cin, d.cout, d.cfg, d.prec, d.epi_mode, d.slope, d.inv_wscale = n, cin, cout, cfg, prec, 1, 0.1, inv
-    d.src, d.dst = x.view(0, cin), dst.view(0, cout)
+    d.src, d.dst = x.chunk_view(0, cin), dst.view(0, cout)
     d.whi, d.wlo, d.bias = whi.data_ptr(), wlo.data_ptr(), bp.data_ptr()
     return lib, d, (x, dst, whi, wlo, bp)
 

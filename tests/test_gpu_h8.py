@@ -161,7 +161,7 @@ def conv_h8(src: H8Tensor, w, b, cfg, prec, epi=_lib.EPI_LINEAR, dst=None, dst_o
     d = _lib.ConvH8Desc()
     d.n, d.cin, d.cout, d.cfg, d.prec, d.epi_mode, d.slope, d.inv_wscale = src.n, cin, cout, cfg, prec, epi, 0.1, inv
     d.tail_finite = tail_finite
-    d.src = src.view(0, cin)
+    d.src = src.chunk_view(0, cin)
     d.dst = dst.view(dst_off, cout)
     if pool is not None:
         d.pool = pool.view(0, cout)
@@ -258,9 +258,44 @@ def test_h8_conv_dma_finite_tail(gpu, prec, cin):
     x = torch.rand(2, 16, 32, 48, device=gpu) * 2 - 1
     wt, b = keyed_conv(cin, 32, "tail")
     ref = ref_conv(x[:, :cin], wt, b)
-    for cfg in (1, 6) + (wino_cfgs() if prec == R32 else ()):
+    for cfg in (1, 6) + (wino_cfgs() if prec == R32 else f16_wino_cfgs() if prec == F16 else ()):
         dst, _ = conv_h8(H8Tensor.from_nchw(x, prec), wt, b, cfg, prec, cin=cin, tail_finite=1)
         np.testing.assert_allclose(dst.to_nchw().cpu().double().numpy(), ref.numpy(), **tol(prec, cfg))
+        # a tensor of just cin channels: allocated in whole 2-group chunks, so the
+        # Winograd tiles' staging of the chunk's second group stays inside it
+        dst, _ = conv_h8(H8Tensor.from_nchw(x[:, :cin], prec), wt, b, cfg, prec, tail_finite=1)
+        np.testing.assert_allclose(dst.to_nchw().cpu().double().numpy(), ref.numpy(), **tol(prec, cfg))
+
+
+def f16_wino_cfgs():
+    lib = _lib.lib()
+    return tuple(c for c in range(lib.rrin_conv_h8_cfg_count())
+                 if lib.rrin_conv_h8_cfg_wino(c) and lib.rrin_conv_h8_cfg_ok(c, F16))
+
+
+@pytest.mark.parametrize("prec,cin", [(F16, 6), (F16, 20), (R32, 9)])
+def test_h8_wino_rejects_short_source_view(gpu, prec, cin):
+    """A Winograd F(2x2) tile stages both record groups of every K chunk: a source view
+    holding cin but not the chunk's last group is rejected (RRIN_E_SHAPE) instead of
+    read past."""
+    x = torch.rand(1, cin, 16, 32, device=gpu)
+    wt, b = keyed_conv(cin, 32, "tail")
+    t = H8Tensor.from_nchw(x, prec)
+    cfgs_ = [c for c in (f16_wino_cfgs() if prec == F16 else wino_cfgs()) if _lib.lib().rrin_conv_h8_cfg_wino(c) != 5]
+    assert cfgs_
+    for cfg in cfgs_:
+        whi, wlo, bp, inv = pack_h8(wt, b, cfg, prec, gpu)
+        dst = H8Tensor(1, 32, 16, 32, gpu, prec)
+        d = _lib.ConvH8Desc()
+        d.n, d.cin, d.cout, d.cfg, d.prec, d.epi_mode, d.inv_wscale = 1, cin, 32, cfg, prec, _lib.EPI_LINEAR, inv
+        d.slope, d.tail_finite = 0.1, 1
+        d.src, d.dst = t.view(0, cin), dst.view(0, 32)  # an odd group count: one short of the chunk
+        d.whi, d.wlo, d.bias = whi.data_ptr(), None, bp.data_ptr()
+        assert _lib.lib().rrin_conv3x3_h8_fwd(C.byref(d), H.stream(gpu)) == -1, f"cfg {cfg}"
+        d.src = t.chunk_view(0, cin)
+        _lib.check(_lib.lib().rrin_conv3x3_h8_fwd(C.byref(d), H.stream(gpu)), f"cfg {cfg}")
+        torch.cuda.synchronize()
+        np.testing.assert_allclose(dst.to_nchw().cpu().double().numpy(), ref_conv(x, wt, b).numpy(), **tol(prec, cfg))
 
 
 @pytest.mark.parametrize("prec", PRECS)
@@ -336,7 +371,7 @@ def subpixel_upconv(src: H8Tensor, w, b, cfg, prec, dst=None, ksplit=0, keep=Non
     d = _lib.ConvH8Desc()
     d.n, d.cin, d.cout, d.cfg, d.prec, d.epi_mode, d.slope, d.inv_wscale = (src.n, cin, 4 * cout, cfg, prec,
                                                                             _lib.EPI_SUBPIXEL, 0.1, inv)
-    d.src, d.dst = src.view(0, cin), dst.view(0, cout)
+    d.src, d.dst = src.chunk_view(0, cin), dst.view(0, cout)
     d.whi, d.wlo, d.bias = whi.data_ptr(), wlo.data_ptr() if prec == X3 else None, bp.data_ptr()
     d.edge = edge.data_ptr()
     keep = keep if keep is not None else []
@@ -358,7 +393,7 @@ def subpixel_upconv(src: H8Tensor, w, b, cfg, prec, dst=None, ksplit=0, keep=Non
     _lib.check(lib.rrin_conv3x3_h8_fwd(C.byref(d), H.stream(dev)), "rrin_conv3x3_h8_fwd(subpixel)")
     e = _lib.EdgeFixDesc()
     e.n, e.cin, e.cout, e.prec, e.epi_mode, e.slope = src.n, cin, cout, prec, _lib.EPI_LINEAR, 0.1
-    e.src, e.dst = src.view(0, cin), dst.view(0, cout)
+    e.src, e.dst = src.chunk_view(0, cin), dst.view(0, cout)
     e.edge, e.wedge, e.bias = edge.data_ptr(), wedge.data_ptr(), braw.data_ptr()
     if edge_split:  # cross-workgroup K split of the fix-up (fp32 records)
         nc = C.c_int64(-1)

@@ -139,7 +139,7 @@ def test_persistent_range_guard(gpu):
         status = torch.zeros(1, dtype=torch.int32, device=gpu)
         d = _lib.ConvH8Desc()
         d.n, d.cin, d.cout, d.cfg, d.prec, d.epi_mode, d.slope, d.inv_wscale = n, cin, cout, cfg, F16, 1, 0.1, inv
-        d.src, d.dst = src.view(0, cin), dst.view(0, cout)
+        d.src, d.dst = src.chunk_view(0, cin), dst.view(0, cout)
         d.whi, d.bias, d.status = whi.data_ptr(), bp.data_ptr(), status.data_ptr()
         _lib.check(_lib.lib().rrin_conv3x3_h8_fwd(C.byref(d), H.stream(gpu)))
         torch.cuda.synchronize(gpu)
@@ -224,7 +224,7 @@ def test_winograd_conv_bitwise_beside_side_stream_conv(gpu, prec, kind):
     for o in outs:
         e = _lib.ConvH8Desc()
         e.n, e.cin, e.cout, e.cfg, e.prec, e.epi_mode, e.slope, e.inv_wscale = n, cin, cout, cfg, prec, 1, 0.1, inv
-        e.src, e.dst = x.view(0, cin), o.view(0, cout)
+        e.src, e.dst = x.chunk_view(0, cin), o.view(0, cout)
         e.whi, e.wlo, e.bias = whi.data_ptr(), whi.data_ptr(), bp.data_ptr()
         dd.append(e)
     bad = 0

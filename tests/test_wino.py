@@ -245,7 +245,7 @@ def test_edge_fix_split_scratch_size():
         dst = H8Tensor(n, cout, 2 * h, 2 * w, torch.device("cpu"), prec)
         e = _lib.EdgeFixDesc()
         e.n, e.cin, e.cout, e.prec = n, cin, cout, prec
-        e.src, e.dst = src.view(0, cin), dst.view(0, cout)
+        e.src, e.dst = src.chunk_view(0, cin), dst.view(0, cout)
         tiles = (2 * -(-2 * w // 32) + 2 * -(-(2 * h - 2) // 32)) * -(-cout // 32) * n
         cnt = C.c_int64(-1)
         nf = lib.rrin_edge_fix_split_floats(C.byref(e), C.byref(cnt))

@@ -82,7 +82,7 @@ def main():
         d = _lib.Block0Desc()
         d.n, d.cin, d.cfg_a, d.cfg_b, d.slope = n, cin, cfg_a, cfg_b, 0.1
         d.inv_wscale_a, d.inv_wscale_b, d.tail_finite = pa[2], pb[2], 1
-        d.src, d.dst = src.view(0, cin), dst.view(0, 32)
+        d.src, d.dst = src.chunk_view(0, cin), dst.view(0, 32)
         if pl is not None:
             d.pool = pl.view(0, 32)
         d.whi_a, d.bias_a, d.whi_b, d.bias_b = pa[0].data_ptr(), pa[1].data_ptr(), pb[0].data_ptr(), pb[1].data_ptr()
@@ -91,7 +91,7 @@ def main():
             e = _lib.ConvH8Desc()
             e.n, e.cin, e.cout, e.cfg, e.prec, e.epi_mode, e.slope, e.inv_wscale = n, ci, 32, cfg, F16, epi, 0.1, p[2]
             e.tail_finite = 1
-            e.src, e.dst = s.view(0, ci), o.view(0, 32)
+            e.src, e.dst = s.chunk_view(0, ci), o.view(0, 32)
             if poolv is not None:
                 e.pool = poolv.view(0, 32)
             e.whi, e.bias = p[0].data_ptr(), p[1].data_ptr()

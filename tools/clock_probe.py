@@ -67,7 +67,7 @@ def main():
         d = _lib.ConvH8Desc()
         d.n, d.cin, d.cout, d.cfg, d.prec, d.epi_mode, d.slope, d.inv_wscale = n, cin, cout, a.cfg, prec, epi, 0.1, inv
         d.tail_finite = 1
-        d.src, d.dst = x.view(0, cin), dst.view(0, cout // 4 if epi == 4 else cout)
+        d.src, d.dst = x.chunk_view(0, cin), dst.view(0, cout // 4 if epi == 4 else cout)
         if pool is not None:
             d.pool = pool.view(0, cout)
         ring = None

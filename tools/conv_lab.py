@@ -162,7 +162,7 @@ def tune_h8(args):
             d = _lib.ConvH8Desc()
             d.n, d.cin, d.cout, d.cfg, d.prec, d.epi_mode, d.slope, d.inv_wscale = n, cin, kout, cfg, prec, epi, 0.1, inv
             d.tail_finite = 1  # channels past cin are zero (as the Net's g16 buffer): whole-record staging
-            d.src, d.dst = x.view(0, cin), dst.view(0, cout)
+            d.src, d.dst = x.chunk_view(0, cin), dst.view(0, cout)
             if edge is not None:
                 d.edge = edge.data_ptr()
             if pool is not None:
@@ -296,7 +296,7 @@ def single(args):
     whi, wlo, bp, inv = pack_h8(wt, torch.zeros(cout), cfg, prec, dev)
     d = _lib.ConvH8Desc()
     d.n, d.cin, d.cout, d.cfg, d.prec, d.epi_mode, d.slope, d.inv_wscale = n, cin, cout, cfg, prec, epi, 0.1, inv
-    d.src, d.dst = x.view(0, cin), dst.view(0, cout)
+    d.src, d.dst = x.chunk_view(0, cin), dst.view(0, cout)
     if pool is not None:
         d.pool = pool.view(0, cout)
     d.whi, d.wlo, d.bias = whi.data_ptr(), wlo.data_ptr(), bp.data_ptr()
@@ -372,7 +372,7 @@ def ablate(args):
         d = _lib.ConvH8Desc()
         d.n, d.cin, d.cout, d.cfg, d.prec, d.epi_mode, d.slope, d.inv_wscale = (n, cin, cout, cfg, prec,
                                                                                 _lib.EPI_LEAKY, 0.1, inv)
-        d.src, d.dst = x.view(0, cin), dst.view(0, cout)
+        d.src, d.dst = x.chunk_view(0, cin), dst.view(0, cout)
         d.whi, d.wlo, d.bias = whi.data_ptr(), wlo.data_ptr(), bp.data_ptr()
         _lib.check(lib.rrin_conv3x3_h8_fwd(C.byref(d), st))
         torch.cuda.synchronize()
@@ -506,7 +506,7 @@ def abconv(args):
             pool = H8Tensor(n, cout, h // 2, w // 2, dev, prec) if epi == 2 else None
             d = _lib.ConvH8Desc()
             d.n, d.cin, d.cout, d.cfg, d.prec, d.epi_mode, d.slope, d.inv_wscale = n, cin, cout, cfg, prec, epi, 0.1, inv
-            d.src, d.dst = x.view(0, cin), dst.view(0, cout // 4 if epi == 4 else cout)
+            d.src, d.dst = x.chunk_view(0, cin), dst.view(0, cout // 4 if epi == 4 else cout)
             if pool is not None:
                 d.pool = pool.view(0, cout)
             if epi == 4:
@@ -587,7 +587,7 @@ def cfgab(args):
             d = _lib.ConvH8Desc()
             d.n, d.cin, d.cout, d.cfg, d.prec, d.epi_mode, d.slope, d.inv_wscale = n, cin, cout, cfg, prec, epi, 0.1, inv
             d.tail_finite = 1  # channels past cin are zero (as the Net's g16 buffer)
-            d.src, d.dst = x.view(0, cin), dst.view(0, cout // 4 if epi == 4 else cout)
+            d.src, d.dst = x.chunk_view(0, cin), dst.view(0, cout // 4 if epi == 4 else cout)
             if pool is not None:
                 d.pool = pool.view(0, cout)
             ring = None
