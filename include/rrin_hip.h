@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define RRIN_ABI_VERSION 14
+#define RRIN_ABI_VERSION 15
 
 #define RRIN_OK 0
 #define RRIN_E_SHAPE (-1)     /* H or W not a multiple of 16, or N < 1          */
@@ -359,7 +359,12 @@ typedef struct rrin_edge_fix_desc {
   float* part;
   int32_t* cnt;
   int64_t part_floats;
-  int32_t cnt_len, pad_;
+  int32_t cnt_len;
+  /* ABI 15: 1 = the ring value from scratch (bias + the conv's in-image taps of the
+   * upsampled src, two staged lines per ring line; `edge` unused, may be NULL): it reads
+   * nothing the EPI_SUBPIXEL conv writes (that conv writes ring pixels only to `edge`), so
+   * the two may run concurrently.  0 = the correction of the conv's `edge` values. */
+  int32_t full;
 } rrin_edge_fix_desc;
 int rrin_subpixel_edge_fix_h8(const rrin_edge_fix_desc* d, void* stream);
 /* Scratch floats (return; 0 = this cin / precision does not split) and tickets

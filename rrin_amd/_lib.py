@@ -9,7 +9,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-ABI_VERSION = 14
+ABI_VERSION = 15
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "librrin_hip.so")
 # A/B sessions only (tools/sessions/): another build of the same library, e.g. ab/librrin_hip_X.so
 if os.environ.get("RRIN_LIB_AB"):
@@ -87,7 +87,7 @@ class EdgeFixDesc(C.Structure):
                 ("epi_mode", C.c_int32), ("slope", C.c_float), ("src", H8), ("dst", H8),
                 ("edge", C.c_void_p), ("wedge", C.c_void_p), ("bias", C.c_void_p), ("status", C.c_void_p),
                 ("part", C.c_void_p), ("cnt", C.c_void_p), ("part_floats", C.c_int64), ("cnt_len", C.c_int32),
-                ("pad_", C.c_int32)]
+                ("full", C.c_int32)]
 
 
 class HeadH8Desc(C.Structure):

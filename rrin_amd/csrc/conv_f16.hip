@@ -838,19 +838,28 @@ struct Up8 {
 // of the few blocks a small ring has (the deep levels: cin 128-256, 16-64
 // blocks at 640x368) and gives each CU more waves to hide LDS latency.
 constexpr int kFixSubFloats = kFixCi * (kFixPx + 2) + kFixCi * 4 + 7 * kFixCi * kFixCo;
+// FULL (rrin_edge_fix_desc.full): the ring value from scratch -- the conv's in-image taps over
+// two staged lines of U (the ring line and the next one inward, zero outside the image), plus
+// the bias -- instead of the conv's pre-bias ring value minus the outside taps.  It reads
+// nothing the sub-pixel conv writes, so it can run beside that conv (net.hip: side stream).
+constexpr int kFixFullFloats = 2 * kFixCi * (kFixPx + 2) + 6 * kFixCi * kFixCo;
+static_assert(kFixFullFloats <= kFixSubFloats, "FULL ring staging fits the K group's region");
 
-template <int PLANES, int KS, bool F32 = false>
+template <int PLANES, int KS, bool F32 = false, bool FULL = false>
 __global__ void RRIN_PK_EDGE_ATTR __launch_bounds__(256 * KS) edge_fix_h8_kernel(EdgeFixArgs a) {
   constexpr int CPR = F32 ? 4 : 8;            // channels per record
   constexpr int GPC = kFixCi / CPR;           // record groups per ci chunk
+  constexpr int NL = FULL ? 2 : 1;            // staged U lines
   extern __shared__ __attribute__((aligned(16))) float s_fix[];
   const int ks = threadIdx.x >> 8;  // K group (wave-uniform)
   float* s_base = s_fix + ks * kFixSubFloats;
+  // U: row ci * NL + l (l = 0 the ring line, 1 the next line inward)
   float(*s_u)[kFixPx + 2] = reinterpret_cast<float(*)[kFixPx + 2]>(s_base);
-  // corner extras: [left ky_a, left ky_b, right ky_a, right ky_b]
-  float(*s_ux)[4] = reinterpret_cast<float(*)[4]>(s_base + kFixCi * (kFixPx + 2));
-  // slots 0-2 line taps, 3-6 corner extras
-  float(*s_w)[kFixCi][kFixCo] = reinterpret_cast<float(*)[kFixCi][kFixCo]>(s_base + kFixCi * (kFixPx + 2) + kFixCi * 4);
+  // corner extras: [left ky_a, left ky_b, right ky_a, right ky_b] (not FULL)
+  float(*s_ux)[4] = reinterpret_cast<float(*)[4]>(s_base + NL * kFixCi * (kFixPx + 2));
+  // slots 0-2 line taps, 3-6 corner extras; FULL: slot 3 l + k = line l, tap k along the line
+  float(*s_w)[kFixCi][kFixCo] = reinterpret_cast<float(*)[kFixCi][kFixCo]>(
+      s_base + NL * kFixCi * (kFixPx + 2) + (FULL ? 0 : kFixCi * 4));
   const int tid = threadIdx.x & 255, px = tid & (kFixPx - 1), cg = tid / kFixPx;  // 8 groups of 4 channels
   // (fp16 records always run one K run in one workgroup: compile-time there)
   const bool cross = F32 && a.cross;
@@ -870,8 +879,9 @@ __global__ void RRIN_PK_EDGE_ATTR __launch_bounds__(256 * KS) edge_fix_h8_kernel
   const int out_k = (line == 0 || line == 2) ? 0 : 2;                          // outside row/col of the kernel
   // corner extras (row lines only): corner at X = 0 and/or X = W-1 inside this tile
   const bool has_l = row && pos0 == 0, has_r = row && pos0 <= W - 1 && W - 1 < pos0 + kFixPx;
-  const bool corners = has_l || has_r;
-  const int nslot = corners ? 7 : 3;
+  const bool corners = !FULL && (has_l || has_r);
+  const int nslot = FULL ? 6 : corners ? 7 : 3;
+  const int inner_d = (line == 0 || line == 2) ? 1 : -1;  // FULL: the second line, one step inward
   // extra slot s (0-1 left corner, 2-3 right): kernel row ky = the (s&1)-th of {0,1,2} minus out_k,
   // column 0 (left) or 2 (right); its U sits at row fixed + ky - 1 of that image column
   auto xky = [&](int sl) { return (sl & 1) + (out_k == 0 ? 1 : 0); };
@@ -879,9 +889,9 @@ __global__ void RRIN_PK_EDGE_ATTR __launch_bounds__(256 * KS) edge_fix_h8_kernel
   const uint4* rlo = PLANES == 2 ? a.s_lo + (int64_t)img * a.s_img : nullptr;
 
   // per-thread staging work of one ci chunk, fetched one chunk ahead
-  constexpr int kItems = GPC * (kFixPx + 2);  // U: record groups x line positions
+  constexpr int kItems = GPC * NL * (kFixPx + 2);  // U: record groups x lines x line positions
   constexpr int kUIt = (kItems + 255) / 256;
-  constexpr int kFixB = F32 ? 4 : 1;  // channels per batch of LDS reads (fp32 records only)
+  constexpr int kFixB = F32 ? (FULL ? 2 : 4) : 1;  // channels per batch of LDS reads (fp32 records only)
   Up8<PLANES, F32> ru[kUIt], rx;
   float4 rw[7];
   const int w_ci = tid >> 3, w_cq = (tid & 7) * 4;
@@ -890,9 +900,13 @@ __global__ void RRIN_PK_EDGE_ATTR __launch_bounds__(256 * KS) edge_fix_h8_kernel
     for (int it = 0; it < kUIt; ++it) {
       const int idx = tid + 256 * it;
       if (idx < kItems) {
-        const int u_gl = idx / (kFixPx + 2), u_j = idx - u_gl * (kFixPx + 2);
-        const int q = min(max(pos0 - 1 + u_j, 0), full - 1);
-        if (c0 + u_gl * CPR < a.cin) ru[it].fetch(a, rhi, rlo, c0 / CPR + u_gl, row ? fixed : q, row ? q : fixed);
+        const int u_gl = idx / (NL * (kFixPx + 2)), rem = idx - u_gl * (NL * (kFixPx + 2));
+        const int u_l = NL == 1 ? 0 : rem / (kFixPx + 2), u_j = rem - u_l * (kFixPx + 2);
+        // correction: positions past the line's ends clamp (the conv's replicate padding);
+        // FULL: they are the zero padding of the upsampled image
+        const int q = FULL ? pos0 - 1 + u_j : min(max(pos0 - 1 + u_j, 0), full - 1);
+        const int o = fixed + u_l * inner_d;
+        if (c0 + u_gl * CPR < a.cin && q >= 0 && q < full) ru[it].fetch(a, rhi, rlo, c0 / CPR + u_gl, row ? o : q, row ? q : o);
         else ru[it].zero();
       }
     }
@@ -906,7 +920,11 @@ __global__ void RRIN_PK_EDGE_ATTR __launch_bounds__(256 * KS) edge_fix_h8_kernel
     for (int sl = 0; sl < 7; ++sl) {
       rw[sl] = make_float4(0.f, 0.f, 0.f, 0.f);
       if (sl < nslot && ok) {
-        const int tap = sl < 3 ? (row ? out_k * 3 + sl : sl * 3 + out_k) : xky(sl - 3) * 3 + (sl < 5 ? 0 : 2);
+        // FULL: line l of slot sl is kernel row (row lines) / column (column lines) 1 for the
+        // ring line, 2 or 0 for the inner line below / above it; k runs along the line
+        const int kk = sl < 3 ? 1 : (inner_d > 0 ? 2 : 0), k3 = sl % 3;
+        const int tap = FULL ? (row ? kk * 3 + k3 : k3 * 3 + kk)
+                             : sl < 3 ? (row ? out_k * 3 + sl : sl * 3 + out_k) : xky(sl - 3) * 3 + (sl < 5 ? 0 : 2);
         rw[sl] = *reinterpret_cast<const float4*>(a.wedge + ((int64_t)(c0 + w_ci) * 9 + tap) * a.cout + co0 + w_cq);
       }
     }
@@ -916,9 +934,10 @@ __global__ void RRIN_PK_EDGE_ATTR __launch_bounds__(256 * KS) edge_fix_h8_kernel
     for (int it = 0; it < kUIt; ++it) {
       const int idx = tid + 256 * it;
       if (idx < kItems) {
-        const int u_gl = idx / (kFixPx + 2), u_j = idx - u_gl * (kFixPx + 2);
+        const int u_gl = idx / (NL * (kFixPx + 2)), rem = idx - u_gl * (NL * (kFixPx + 2));
+        const int u_l = NL == 1 ? 0 : rem / (kFixPx + 2), u_j = rem - u_l * (kFixPx + 2);
 #pragma unroll
-        for (int e = 0; e < CPR; ++e) s_u[u_gl * CPR + e][u_j] = ru[it].value(e);
+        for (int e = 0; e < CPR; ++e) s_u[(u_gl * CPR + e) * NL + u_l][u_j] = ru[it].value(e);
       }
     }
     if (corners && tid < 4 * GPC)
@@ -958,7 +977,7 @@ __global__ void RRIN_PK_EDGE_ATTR __launch_bounds__(256 * KS) edge_fix_h8_kernel
     for (int i = 0; i < 4; ++i) {
       const int co = co0 + cg * 4 + i;
       if (co < a.cout) {
-        pre[i] = a.edge[((int64_t)img * a.cout + co) * a.ring + e];
+        if constexpr (!FULL) pre[i] = a.edge[((int64_t)img * a.cout + co) * a.ring + e];
         bco[i] = a.bias[co];
       }
     }
@@ -991,27 +1010,27 @@ __global__ void RRIN_PK_EDGE_ATTR __launch_bounds__(256 * KS) edge_fix_h8_kernel
 #pragma unroll 4
         for (int ci = 0; ci < kFixCi; ++ci)
 #pragma unroll
-          for (int k = 0; k < 3; ++k) {
-            const float u = s_u[ci][px + k];
+          for (int k = 0; k < 3 * NL; ++k) {
+            const float u = s_u[ci * NL + k / 3][px + k % 3];
             const float4 w = *reinterpret_cast<const float4*>(&s_w[k][ci][cg * 4]);
             FIX_FMA(acc, w, u);
           }
       } else
 #pragma clang loop unroll(disable)
       for (int cb = 0; cb < kFixCi; cb += kFixB) {
-        float u[kFixB][3];
-        float4 w[kFixB][3];
+        float u[kFixB][3 * NL];
+        float4 w[kFixB][3 * NL];
 #pragma unroll
         for (int j = 0; j < kFixB; ++j)
 #pragma unroll
-          for (int k = 0; k < 3; ++k) {
-            u[j][k] = s_u[cb + j][px + k];
+          for (int k = 0; k < 3 * NL; ++k) {
+            u[j][k] = s_u[(cb + j) * NL + k / 3][px + k % 3];
             w[j][k] = *reinterpret_cast<const float4*>(&s_w[k][cb + j][cg * 4]);
           }
 #pragma unroll
         for (int j = 0; j < kFixB; ++j)
 #pragma unroll
-          for (int k = 0; k < 3; ++k) {
+          for (int k = 0; k < 3 * NL; ++k) {
             FIX_FMA(acc, w[j][k], u[j][k]);
           }
       }
@@ -1094,7 +1113,7 @@ __global__ void RRIN_PK_EDGE_ATTR __launch_bounds__(256 * KS) edge_fix_h8_kernel
   for (int i = 0; i < 4; ++i) {
     const int co = co0 + cg * 4 + i;
     if (co >= a.cout) break;
-    float v = (pre[i] - acc[i]) + bco[i];
+    float v = FULL ? acc[i] + bco[i] : (pre[i] - acc[i]) + bco[i];
     if (a.leaky) v = v > 0.f ? v : v * a.slope;
     const int64_t k = (((int64_t)img * a.d_img + (int64_t)(co / CPR) * a.d_gp + (int64_t)(Y + 1) * a.d_wp + X +
                         kH8PadLeft) * CPR) + (co % CPR);
@@ -2441,15 +2460,21 @@ extern "C" int rrin_subpixel_weights(const float* w, const float* b, int32_t cou
   return 0;
 }
 
-template <int PLANES, int KS, bool F32 = false>
-static int edge_fix_launch(const EdgeFixArgs& a, dim3 grid, hipStream_t st) {
+template <int PLANES, int KS, bool F32, bool FULL>
+static int edge_fix_launch_m(const EdgeFixArgs& a, dim3 grid, hipStream_t st) {
   constexpr size_t lds = (size_t)KS * kFixSubFloats * sizeof(float);
   static_assert(lds <= 160 * 1024, "edge fix LDS");
   static_assert(kFixSubFloats >= 4 * 256, "K-group sums fit a staging region");
   static LdsAttr attr;
-  if (int e = attr.ensure((const void*)edge_fix_h8_kernel<PLANES, KS, F32>, (int)lds, st)) return e;
-  hipLaunchKernelGGL((edge_fix_h8_kernel<PLANES, KS, F32>), grid, dim3(256 * KS), lds, st, a);
+  if (int e = attr.ensure((const void*)edge_fix_h8_kernel<PLANES, KS, F32, FULL>, (int)lds, st)) return e;
+  hipLaunchKernelGGL((edge_fix_h8_kernel<PLANES, KS, F32, FULL>), grid, dim3(256 * KS), lds, st, a);
   return hip_code(hipGetLastError());
+}
+
+template <int PLANES, int KS, bool F32 = false>
+static int edge_fix_launch(const EdgeFixArgs& a, dim3 grid, hipStream_t st, bool full) {
+  return full ? edge_fix_launch_m<PLANES, KS, F32, true>(a, grid, st)
+              : edge_fix_launch_m<PLANES, KS, F32, false>(a, grid, st);
 }
 
 // K groups and K runs of the ring fix-up, by cin and precision only (the
@@ -2470,8 +2495,9 @@ static void edge_fix_split(int cin, int prec, int* ks, int* nsl) {
 }
 
 extern "C" int rrin_subpixel_edge_fix_h8(const rrin_edge_fix_desc* d, void* stream) {
-  if (!d || !d->edge || !d->wedge || !d->bias) return RRIN_E_ARG;
+  if (!d || (!d->edge && !d->full) || !d->wedge || !d->bias || (d->full != 0 && d->full != 1)) return RRIN_E_ARG;
   if (!rec_prec(d->prec)) return RRIN_E_ARG;
+  const bool full = d->full == 1;
   if (d->n < 1 || d->cin < 8 || (d->cin & 7) || d->cout < 8 || (d->cout & 7)) return RRIN_E_ARG;
   if (d->epi_mode != RRIN_EPI_LINEAR && d->epi_mode != RRIN_EPI_LEAKY) return RRIN_E_ARG;
   if (!h8_ok(d->src, d->prec) || !h8_ok(d->dst, d->prec)) return RRIN_E_SHAPE;
@@ -2526,14 +2552,14 @@ extern "C" int rrin_subpixel_edge_fix_h8(const rrin_edge_fix_desc* d, void* stre
   }
   hipStream_t st = (hipStream_t)stream;
   if (d->prec == RRIN_PREC_F32R) {
-    return ks == 2 ? edge_fix_launch<1, 2, true>(a, g, st) : edge_fix_launch<1, 1, true>(a, g, st);
+    return ks == 2 ? edge_fix_launch<1, 2, true>(a, g, st, full) : edge_fix_launch<1, 1, true>(a, g, st, full);
   }
   switch (planes * 8 + ks) {
-    case 2 * 8 + 2: return edge_fix_launch<2, 2>(a, g, st);
-    case 2 * 8 + 1: return edge_fix_launch<2, 1>(a, g, st);
-    case 1 * 8 + 4: return edge_fix_launch<1, 4>(a, g, st);
-    case 1 * 8 + 2: return edge_fix_launch<1, 2>(a, g, st);
-    default: return edge_fix_launch<1, 1>(a, g, st);
+    case 2 * 8 + 2: return edge_fix_launch<2, 2>(a, g, st, full);
+    case 2 * 8 + 1: return edge_fix_launch<2, 1>(a, g, st, full);
+    case 1 * 8 + 4: return edge_fix_launch<1, 4>(a, g, st, full);
+    case 1 * 8 + 2: return edge_fix_launch<1, 2>(a, g, st, full);
+    default: return edge_fix_launch<1, 1>(a, g, st, full);
   }
 }
 

@@ -351,10 +351,13 @@ def test_h8_leaky_rep_writes_replicated_ring(gpu, prec):
         assert dst.hi[:, :, 0, 7:9 + dst.w].any() and dst.hi[:, :, 1:dst.h + 1, 7].any()
 
 
-def subpixel_upconv(src: H8Tensor, w, b, cfg, prec, dst=None, ksplit=0, keep=None, fold=False, edge_split=False):
+def subpixel_upconv(src: H8Tensor, w, b, cfg, prec, dst=None, ksplit=0, keep=None, fold=False, edge_split=False,
+                    full=False):
     """EPI_SUBPIXEL conv + ring fix-up through the C ABI (the Net's up.1 conv); fold: the
     ring in the conv launch (rrin_conv_h8_desc.ring_w, Winograd kind 3) instead of
-    rrin_subpixel_edge_fix_h8."""
+    rrin_subpixel_edge_fix_h8; full: the fix-up's from-scratch mode (rrin_edge_fix_desc.full,
+    no edge buffer), launched BEFORE the conv -- it must read nothing the conv writes, and the
+    conv must write no ring pixel."""
     lib = _lib.lib()
     dev = src.hi.device
     cout, cin = w.shape[:2]
@@ -390,11 +393,13 @@ def subpixel_upconv(src: H8Tensor, w, b, cfg, prec, dst=None, ksplit=0, keep=Non
         _lib.check(lib.rrin_conv3x3_h8_fwd(C.byref(d), H.stream(dev)), "rrin_conv3x3_h8_fwd(subpixel, fold)")
         torch.cuda.synchronize(dev)
         return dst
-    _lib.check(lib.rrin_conv3x3_h8_fwd(C.byref(d), H.stream(dev)), "rrin_conv3x3_h8_fwd(subpixel)")
+    if not full:
+        _lib.check(lib.rrin_conv3x3_h8_fwd(C.byref(d), H.stream(dev)), "rrin_conv3x3_h8_fwd(subpixel)")
     e = _lib.EdgeFixDesc()
     e.n, e.cin, e.cout, e.prec, e.epi_mode, e.slope = src.n, cin, cout, prec, _lib.EPI_LINEAR, 0.1
     e.src, e.dst = src.chunk_view(0, cin), dst.view(0, cout)
-    e.edge, e.wedge, e.bias = edge.data_ptr(), wedge.data_ptr(), braw.data_ptr()
+    e.edge, e.wedge, e.bias = (None if full else edge.data_ptr()), wedge.data_ptr(), braw.data_ptr()
+    e.full = int(full)
     if edge_split:  # cross-workgroup K split of the fix-up (fp32 records)
         nc = C.c_int64(-1)
         nf = lib.rrin_edge_fix_split_floats(C.byref(e), C.byref(nc))
@@ -405,6 +410,8 @@ def subpixel_upconv(src: H8Tensor, w, b, cfg, prec, dst=None, ksplit=0, keep=Non
             e.part, e.cnt, e.part_floats, e.cnt_len = part.data_ptr(), cnt.data_ptr(), nf, nc.value
             keep.extend([part, cnt])
     _lib.check(lib.rrin_subpixel_edge_fix_h8(C.byref(e), H.stream(dev)), "rrin_subpixel_edge_fix_h8")
+    if full:
+        _lib.check(lib.rrin_conv3x3_h8_fwd(C.byref(d), H.stream(dev)), "rrin_conv3x3_h8_fwd(subpixel)")
     torch.cuda.synchronize(dev)
     return dst
 
@@ -427,6 +434,34 @@ def test_h8_subpixel_upconv(gpu, prec, n, cin, cout, sh, sw):
                                    err_msg=f"cfg {cfg}")
         assert not dst.to_nchw(cout, cout).any()           # the bridge half of CAT is untouched
         assert not dst.hi[:, :, 0].any() and not dst.hi[:, :, :, :8].any()  # zero padding kept
+
+
+@pytest.mark.parametrize("prec", PRECS)
+@pytest.mark.parametrize("n,cin,cout,sh,sw", [(2, 64, 32, 20, 36), (1, 128, 64, 23, 40), (1, 256, 128, 5, 7),
+                                              (2, 512, 256, 3, 5), (1, 64, 32, 1, 1), (1, 256, 128, 1, 2),
+                                              (1, 1024, 512, 2, 3)])
+def test_h8_subpixel_ring_full(gpu, prec, n, cin, cout, sh, sw):
+    """The from-scratch ring (rrin_edge_fix_desc.full; what net.hip runs on a side stream
+    beside the sub-pixel conv) launched before the conv: the whole output within the
+    tolerance of upsample-then-conv in float64, the bridge half untouched, and every K split
+    of the fix-up (fp32 records: one workgroup per run) bit for bit the one-workgroup result."""
+    x = torch.rand(n, cin, sh, sw, device=gpu) * 2 - 1
+    wt, b = keyed_conv(cin, cout, "sub")
+    up = F.interpolate(x.double().cpu(), scale_factor=2, mode="bilinear", align_corners=False)
+    ref = F.conv2d(up, wt.double().cpu(), b.double().cpu(), padding=1)
+    src = H8Tensor.from_nchw(x, prec)
+    replicate_ring(src)
+    cfg = next(c for c in cfgs(prec, 4 * cout, cin) if prec != _lib.PREC_F32R or _lib.lib().rrin_conv_h8_cfg_wino(c))
+    dst = subpixel_upconv(src, wt, b, cfg, prec, full=True, dst=H8Tensor(n, 2 * cout, 2 * sh, 2 * sw, gpu, prec))
+    np.testing.assert_allclose(dst.to_nchw(0, cout).cpu().double().numpy(), ref.numpy(), **tol(prec, cfg))
+    assert not dst.to_nchw(cout, cout).any()
+    assert not dst.hi[:, :, 0].any() and not dst.hi[:, :, :, :8].any()
+    if prec == _lib.PREC_F32R:
+        keep = []
+        split = subpixel_upconv(src, wt, b, cfg, prec, full=True, keep=keep, edge_split=True,
+                                dst=H8Tensor(n, 2 * cout, 2 * sh, 2 * sw, gpu, prec))
+        assert torch.equal(split.hi, dst.hi)
+        assert not keep or not keep[1].any()
 
 
 @pytest.mark.parametrize("n,cin,cout,sh,sw", [(2, 128, 64, 20, 36), (1, 256, 128, 5, 7), (2, 512, 256, 3, 5),
