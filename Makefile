@@ -8,6 +8,9 @@ ARCH  ?= gfx950
 # packed code measured no faster.  The flag also reaches the host
 # compile, which ignores it (one "not a recognized feature" line per file).
 NOPK := -Xclang -target-feature -Xclang -packed-fp32-ops
+# Default machine scheduler only: the conv tiles' counted s_waitcnt vmcnt(N) waits (inline asm)
+# assume its VMEM issue order -- -mllvm -amdgpu-sched-strategy=max-ilp reorders loads between
+# them and produced wrong, nondeterministic results (profiles/r05/sched_strategy_ab.txt)
 CXXFLAGS := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function -Iinclude $(NOPK)
 SRC_DIR := rrin_amd/csrc
 OBJ_DIR := build/obj
