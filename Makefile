@@ -8,10 +8,15 @@ ARCH  ?= gfx950
 # packed code measured no faster.  The flag also reaches the host
 # compile, which ignores it (one "not a recognized feature" line per file).
 NOPK := -Xclang -target-feature -Xclang -packed-fp32-ops
-# Default machine scheduler only: the conv tiles' counted s_waitcnt vmcnt(N) waits (inline asm)
-# assume its VMEM issue order -- -mllvm -amdgpu-sched-strategy=max-ilp reorders loads between
-# them and produced wrong, nondeterministic results (profiles/r05/sched_strategy_ab.txt)
 CXXFLAGS := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function -Iinclude $(NOPK)
+# Machine scheduler (A/B: `make SCHED=max-ilp`).  The conv tiles' counted waits
+# (RRIN_VMWAIT, common.hpp) hold for any VMEM issue order the vm_fence()s allow; every build
+# checks that on its own gfx950 ISA (check-isa below) -- round 5's max-ilp build moved U loads
+# across a DMA issue group and ran wrong (profiles/r06/isa/).
+SCHED ?=
+ifneq ($(SCHED),)
+CXXFLAGS += -mllvm -amdgpu-sched-strategy=$(SCHED)
+endif
 SRC_DIR := rrin_amd/csrc
 OBJ_DIR := build/obj
 SRCS := $(wildcard $(SRC_DIR)/*.hip)
@@ -24,13 +29,27 @@ LAB32 := rrin_amd/librrin_lab32.so
 
 all: $(LIB)
 
+# check-isa: the device ISA of every product source (same flags), and tools/isa_vmcheck.py over
+# it -- each declared counted wait must see exactly its declared loads on every path.  A
+# prerequisite of the library, so a build whose compiler or flags reorder the staging loads fails
+# here instead of computing wrong tiles on the GPU.
+ISA_DIR := build/isa
+ISA_OK := $(patsubst $(SRC_DIR)/%.hip,$(ISA_DIR)/%.ok,$(SRCS))
+check-isa: $(ISA_OK)
+
+$(ISA_DIR)/%.ok: $(SRC_DIR)/%.hip $(SRC_DIR)/common.hpp include/rrin_hip.h tools/isa_vmcheck.py
+	@mkdir -p $(ISA_DIR)
+	$(HIPCC) $(CXXFLAGS) --cuda-device-only -S -o $(ISA_DIR)/$*.s $< 2>/dev/null
+	python3 tools/isa_vmcheck.py $(ISA_DIR)/$*.s
+	@touch $@
+
 lab: $(LAB) $(LAB32)
 
 $(OBJ_DIR)/%.o: $(SRC_DIR)/%.hip $(SRC_DIR)/common.hpp include/rrin_hip.h
 	@mkdir -p $(OBJ_DIR)
 	$(HIPCC) $(CXXFLAGS) -c $< -o $@
 
-$(LIB): $(OBJS)
+$(LIB): $(OBJS) $(ISA_OK)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(OBJS)
 
 LAB_SRCS := $(SRC_DIR)/conv_f16.hip $(SRC_DIR)/conv_block0.hip $(SRC_DIR)/conv_wino.hip $(SRC_DIR)/conv_wino4.hip $(SRC_DIR)/conv_winoc.hip $(SRC_DIR)/conv_winoh.hip $(SRC_DIR)/conv_winop.hip
@@ -67,4 +86,4 @@ resource: $(SRCS)
 clean:
 	rm -rf build $(LIB) $(LAB) $(LAB32) $(PKV)
 
-.PHONY: all lab clean resource pk-variants
+.PHONY: all lab clean resource pk-variants check-isa

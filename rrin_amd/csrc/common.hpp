@@ -7,6 +7,27 @@
 
 #include "../../include/rrin_hip.h"
 
+// Counted wait for LDS-DMA staging: s_waitcnt vmcnt(LDS + LD), declaring that the LDS + LD
+// youngest vector-memory loads at this point are LDS younger LDS-DMA pieces and LD register
+// loads (stores are not counted: they return out of order with loads and can only make the
+// wait stricter).  Loads return in issue order, so every load issued before those -- the
+// awaited stage -- has landed.  The count is right only for the VMEM order the source pins with
+// sched_barrier fences; `make check-isa` (tools/isa_vmcheck.py) walks every path of the
+// compiled gfx950 code back from each declared wait and fails the build on a mismatch.
+#define RRIN_VMWAIT(LDS, LD) \
+  asm volatile("s_waitcnt vmcnt(%0) ; rrin-vm lds=%1 ld=%2" ::"n"((LDS) + (LD)), "n"(LDS), "n"(LD) : "memory")
+
+// Pins the vector-memory issue order at this point (no VMEM instruction is scheduled across
+// it; ALU, MFMA and LDS instructions may move): the fence around each issue group a counted
+// RRIN_VMWAIT relies on.  sched_barrier's mask names the instruction classes allowed across --
+// here everything but VMEM (0x10 all, 0x20 read, 0x40 write).
+// (RRIN_NO_VMFENCE: a check build without the fences, tests/test_isa_check.py only.)
+#ifdef RRIN_NO_VMFENCE
+#define vm_fence() ((void)0)
+#else
+#define vm_fence() __builtin_amdgcn_sched_barrier(0x78F)
+#endif
+
 namespace rrin {
 
 constexpr int kPadRowsAlign = 16;  // hp = round_up(h,16) + 2

@@ -201,11 +201,14 @@ __global__ __launch_bounds__(256, 2) void conv_block0_h8_kernel(Block0Args a) {
   const uint4* ibase = a.src + (size_t)img * a.src_img;
   // prologue of the first tile: chunk 0 (DMA), its weights, chunk 1 (DMA); wait for the first two
   issue_chunk(ibase, 0, stX);
+  vm_fence();
 #pragma unroll
   for (int t = 0; t < 9; ++t) w[t] = b0_load16(rs_wa, wa_voff, t * wa_tap);
+  vm_fence();
   if (nch > 1) {
     issue_chunk(ibase, 1, stY);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P) : "memory");
+    vm_fence();
+    RRIN_VMWAIT(P, 0);
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
@@ -371,8 +374,10 @@ __global__ __launch_bounds__(256, 2) void conv_block0_h8_kernel(Block0Args a) {
     // order among themselves, not in order with the epilogue's stores)
     bar();
     if (nch > 1) {
+      vm_fence();
       issue_chunk(nbase, 1, stY);
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P) : "memory");
+      vm_fence();
+      RRIN_VMWAIT(P, 0);
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }

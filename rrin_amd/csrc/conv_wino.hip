@@ -1204,9 +1204,9 @@ __global__ __launch_bounds__(256 * PT, 2) void conv3x3_winoq_kernel(ConvH8Args a
     if (!next_in_flight) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else if (tail_wave) {
-      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      RRIN_VMWAIT(2, 0);
     } else {
-      asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+      RRIN_VMWAIT(1, 0);
     }
   };
   if constexpr ((ABL & 4) != 0) {

@@ -225,7 +225,7 @@ __global__ __launch_bounds__(256, NT == 1 ? 2 : 1) void conv3x3_winoh_kernel(Con
       fence();
     }
     if (more) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((RRIN_WINOH_ABL & 1) ? 0 : 4 * CT) : "memory");
+      RRIN_VMWAIT(0, (RRIN_WINOH_ABL & 1) ? 0 : 4 * CT);
       bar();
       if (!(RRIN_WINOH_ABL & 2)) issue_raw_at(raw_next, s == 0 ? 2 : s - 1);
       if (c + 3 < nch) raw_next += chunk_stride;
@@ -248,15 +248,15 @@ __global__ __launch_bounds__(256, NT == 1 ? 2 : 1) void conv3x3_winoh_kernel(Con
 
   // prologue in the steady state's VMEM order: raw(0), U(0) pts 0-2, raw(1), U(0) pt 3
   issue_raw_at(tbase, 0);
+  vm_fence();
 #pragma unroll
   for (int x = 0; x < 3; ++x) reload_u(0, x);
+  vm_fence();
   issue_raw_at(nch > 1 ? tbase + chunk_stride : tbase, 1);
+  vm_fence();
   reload_u(0, 3);
-  if constexpr (P == 2) {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * CT + 2) : "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * CT + 3) : "memory");
-  }
+  vm_fence();
+  RRIN_VMWAIT(P, 4 * CT);
   bar();
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) {
@@ -576,7 +576,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_winohl_kernel(ConvH8Args a) {
   issue_chunk(0, 0);
   if (nch > 1) {
     issue_chunk(1, 1);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PR + PU) : "memory");
+    RRIN_VMWAIT(PR + PU, 0);
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
@@ -911,9 +911,9 @@ __global__ __launch_bounds__(256, NT == 1 ? 2 : 1) void conv3x3_winohp_kernel(Co
       // LOADS of raw(c + 1) are U(c) pt 3, the bias DMA and U(c + 1) pts 0-2 (the epilogue's
       // stores in between are not counted -- a count that included them could pass with the
       // raw tile still in flight once the stores had completed)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * CT + 1) : "memory");
+      RRIN_VMWAIT(1, 4 * CT);
     } else {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * CT) : "memory");
+      RRIN_VMWAIT(0, 4 * CT);
     }
     bar();
     const int c2 = c + 2;
@@ -941,14 +941,18 @@ __global__ __launch_bounds__(256, NT == 1 ? 2 : 1) void conv3x3_winohp_kernel(Co
   int tp = 0;
   issue_bias(cur, tp);
   issue_raw_at(tb, 0);
+  vm_fence();
 #pragma unroll
   for (int x = 0; x < 3; ++x)
 #pragma unroll
     for (int t = 0; t < CT; ++t) u[t][x] = load_u(ur, 0, x, t);
+  vm_fence();
   issue_raw_at(tb + chunk_stride, 1);
+  vm_fence();
 #pragma unroll
   for (int t = 0; t < CT; ++t) u[t][3] = load_u(ur, 0, 3, t);
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * CT + P) : "memory");
+  vm_fence();
+  RRIN_VMWAIT(P, 4 * CT);
   bar();
   issue_bias(cur, tp);  // again, in the after-epilogue position: chunk 0 waits as after an epilogue
 #pragma unroll

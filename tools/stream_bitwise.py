@@ -60,3 +60,4 @@ with torch.no_grad():
     except RuntimeError as e:
         flag = str(e)[:60]
 print(f"differ {bad}/{2 * a.rounds} forwards from the first 1-stream one, max abs {worst:.3e}, range flag: {flag}")
+sys.exit(1 if bad or flag else 0)
