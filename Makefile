@@ -17,6 +17,10 @@ SCHED ?=
 ifneq ($(SCHED),)
 CXXFLAGS += -mllvm -amdgpu-sched-strategy=$(SCHED)
 endif
+# Per-source scheduler: the kind-6 tile (conv_winoc.hip) under max-ilp, 144.4-144.6 vs 143.6-144.0
+# pairs/s on one box interleaved, GPU suite and repeat-bitwise green (profiles/r06/sched/).
+SCHED_conv_winoc := max-ilp
+sched_of = $(if $(SCHED_$(1)),-mllvm -amdgpu-sched-strategy=$(SCHED_$(1)))
 SRC_DIR := rrin_amd/csrc
 OBJ_DIR := build/obj
 SRCS := $(wildcard $(SRC_DIR)/*.hip)
@@ -39,7 +43,7 @@ check-isa: $(ISA_OK)
 
 $(ISA_DIR)/%.ok: $(SRC_DIR)/%.hip $(SRC_DIR)/common.hpp include/rrin_hip.h tools/isa_vmcheck.py
 	@mkdir -p $(ISA_DIR)
-	$(HIPCC) $(CXXFLAGS) --cuda-device-only -S -o $(ISA_DIR)/$*.s $< 2>/dev/null
+	$(HIPCC) $(CXXFLAGS) $(call sched_of,$*) --cuda-device-only -S -o $(ISA_DIR)/$*.s $< 2>/dev/null
 	python3 tools/isa_vmcheck.py $(ISA_DIR)/$*.s
 	@touch $@
 
@@ -47,12 +51,12 @@ lab: $(LAB) $(LAB32)
 
 $(OBJ_DIR)/%.o: $(SRC_DIR)/%.hip $(SRC_DIR)/common.hpp include/rrin_hip.h
 	@mkdir -p $(OBJ_DIR)
-	$(HIPCC) $(CXXFLAGS) -c $< -o $@
+	$(HIPCC) $(CXXFLAGS) $(call sched_of,$*) -c $< -o $@
 
 $(LIB): $(OBJS) $(ISA_OK)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(OBJS)
 
-LAB_SRCS := $(SRC_DIR)/conv_f16.hip $(SRC_DIR)/conv_block0.hip $(SRC_DIR)/conv_wino.hip $(SRC_DIR)/conv_wino4.hip $(SRC_DIR)/conv_winoc.hip $(SRC_DIR)/conv_winoh.hip $(SRC_DIR)/conv_winop.hip
+LAB_SRCS := $(SRC_DIR)/conv_f16.hip $(SRC_DIR)/conv_block0.hip $(SRC_DIR)/conv_wino.hip $(SRC_DIR)/conv_winoc.hip $(SRC_DIR)/conv_winoh.hip
 $(LAB): $(LAB_SRCS) $(SRC_DIR)/common.hpp include/rrin_hip.h
 	$(HIPCC) $(CXXFLAGS) -DRRIN_LAB -shared -o $@ $(LAB_SRCS)
 

@@ -72,14 +72,9 @@ WINO_KERNELS = {1: "conv3x3_wino_kernel (BM 32 x TH 8, 4 waves of 8 accumulators
                 3: "conv3x3_winoq_kernel (BM 32 x TH 8, 8 waves of 4 accumulators)",
                 4: "conv3x3_winoq_kernel (BM 32 x TH 4, 4 waves)",
                 6: "conv3x3_winoc_kernel (register-U, BM 64 x TH 4, 4 waves of 2 co tiles)",
-                7: "conv3x3_winoc_kernel (register-U, BM 32 x TH 8, 4 waves of 2 patch tiles)",
-                8: "conv3x3_winop_kernel (persistent register-U, BM 32 x TH 8, 8 waves)",
-                12: "conv3x3_winocp_kernel (register-U, BM 64 x TH 4, persistent grid)"}
+                7: "conv3x3_winoc_kernel (register-U, BM 32 x TH 8, 4 waves of 2 patch tiles)"}
 # fp16 Winograd tiles (conv_winoh.hip)
-WINO_KERNELS_F16 = {6: "conv3x3_winoh_kernel (register-U, BM 64 x TH 4)",
-                    9: "conv3x3_winoh_kernel (register-U, BM 64 x TH 8, U on 2 patch tiles)",
-                    10: "conv3x3_winohp_kernel (register-U, BM 64 x TH 4, persistent grid)",
-                    11: "conv3x3_winohp_kernel (register-U, BM 64 x TH 8, persistent grid)"}
+WINO_KERNELS_F16 = {6: "conv3x3_winoh_kernel (register-U, BM 64 x TH 4)"}
 
 
 def kernel_wino(eng, n, h, w):
@@ -150,11 +145,6 @@ def parse():
     ap.add_argument("--fuse-l0", type=int, default=None, choices=[0, 1, 2],
                     help="fp16: level-0 UNetConvBlocks as one fused launch: 0 none, 1 down_path[0], "
                          "2 also the last up block's; default engine.FUSE_L0")
-    ap.add_argument("--wino-persistent", type=int, default=None, choices=[0, 1],
-                    help="A/B: exact fp32 kind 12 (kind 6 on a persistent grid) for the cout %% 64 convs (1) or "
-                         "kind 6 (0); default engine.WINO_PERSISTENT")
-    ap.add_argument("--wino-f16-kind", type=int, default=None,
-                    help="A/B: fp16 Winograd tile kind (6, 9, 10, 11; engine.WINO_F16_KIND)")
     ap.add_argument("--wino-f16-levels", default=None,
                     help="A/B: grid levels of the fp16 Winograd convs, e.g. '2,3,4' (engine.WINO_F16_LEVELS)")
     ap.add_argument("--wino-kind", type=int, default=None,
@@ -167,7 +157,7 @@ def parse():
                     help="A/B: run the sub-pixel ring fix-up as its own launch (engine.RING_FOLD = False)")
     ap.add_argument("--wino-kind32", type=int, default=None,
                     help="A/B: Winograd kind of the 32-output-channel convs in the auto mode "
-                         "(engine.WINO_KIND32: 3, or 8 the persistent register-U tile)")
+                         "(engine.WINO_KIND32: 3 or 7)")
     ap.add_argument("--no-wino-th4", action="store_true",
                     help="A/B: no TH-4 Winograd tiles on the deep convs (engine.WINO_TH4)")
     ap.add_argument("--split", default=None,
@@ -409,12 +399,8 @@ def main():
     if args.no_wino:
         engine_mod.WINO = False
         engine_mod.WINO_F16 = False
-    if args.wino_persistent is not None:
-        engine_mod.WINO_PERSISTENT = bool(args.wino_persistent)
     if args.fuse_l0 is not None:
         engine_mod.FUSE_L0 = args.fuse_l0
-    if args.wino_f16_kind is not None:
-        engine_mod.WINO_F16_KIND = args.wino_f16_kind
     if args.wino_f16_levels is not None:
         engine_mod.WINO_F16_LEVELS = tuple(int(v) for v in args.wino_f16_levels.split(",") if v)
     if args.wino_kind is not None:

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define RRIN_ABI_VERSION 15
+#define RRIN_ABI_VERSION 16
 
 #define RRIN_OK 0
 #define RRIN_E_SHAPE (-1)     /* H or W not a multiple of 16, or N < 1          */
@@ -258,26 +258,18 @@ int64_t rrin_conv_h8_split_floats(const rrin_conv_h8_desc* d, int64_t* cnt_ints)
  * d->ring_corr and stores the ints of d->ring_cnt; < 0: the error code (RRIN_E_CONFIG:
  * the config cannot fold -- run rrin_subpixel_edge_fix_h8 instead) */
 int64_t rrin_conv_h8_ring_floats(const rrin_conv_h8_desc* d, int64_t* cnt_ints);
-/* Nonzero if cfg is a Winograd exact-fp32 config (F32R only, not packed by
- * rrin_pack_conv3x3_r32): the tile kind.  F(2x2,3x3), packed by
- * rrin_pack_conv3x3_wino_bm with the config's BM: 1 = BM 32 x TH 8 on 4 waves,
- * 2 = BM 64 x TH 8 on 8 waves, 3 = BM 32 x TH 8 on 8 waves of 4 accumulators
- * (4 waves per SIMD), 4 = kind 3 on TH 4 tiles (4 waves); all four give
- * bitwise-equal outputs.  5 = F(4x4,3x3), BM 32 x TH 16 on 6 waves, packed by
- * rrin_pack_conv3x3_wino4 (a different rounding: 36 transform points).  Kinds
- * 3 and 4 take a split-K (rrin_conv_h8_desc.ksplit).  6 = BM 64 x TH 4 and 7 =
- * BM 32 x TH 8 on 4 waves with the U operands loaded straight into registers
- * (ABI 12; bitwise equal to kinds 1-4; cin % 8 == 0 or tail_finite).  8 = a
- * persistent register-U tile for cout <= 32 (BM 32 x TH 8, 8 waves).  Kind 6 also
- * runs at RRIN_PREC_F16, and 9 = BM 64 x TH 8 (4 waves, one block per CU) at
- * RRIN_PREC_F16 only (ABI 13: fp16 Winograd, packed by rrin_pack_conv3x3_wino_h8;
- * cin % 16 == 0 or tail_finite; no split-K, no ring fold); 10 and 11 = kinds 6 and 9 on
- * a persistent grid (workgroups walk tiles; bitwise equal; fp16 only).  12 = kind 6 on a
- * persistent grid at F32R (bitwise equal to kind 6).  13 = kind 6 on two patch tiles per
- * workgroup with U shared through LDS (fp16; bitwise equal to kind 6).  Kinds 2, 5, 8, 9, 10,
- * 11 and 13 are built only into the lab library: the product library reports them with
- * rrin_conv_h8_cfg_ok == 0 and rrin_conv3x3_h8_fwd returns RRIN_E_CONFIG.
- * 0: direct form. */
+/* Nonzero if cfg is a Winograd config (not packed by rrin_pack_conv3x3_r32 /
+ * rrin_pack_conv3x3_h8): the tile kind.  F(2x2,3x3), packed by
+ * rrin_pack_conv3x3_wino_bm with the config's BM (F32R): 1 = BM 32 x TH 8 on 4
+ * waves, 3 = BM 32 x TH 8 on 8 waves of 4 accumulators (4 waves per SIMD), 4 =
+ * kind 3 on TH 4 tiles (4 waves), 6 = BM 64 x TH 4 and 7 = BM 32 x TH 8 on 4 waves
+ * with the U operands loaded straight into registers (cin % 8 == 0 or
+ * tail_finite); all give bitwise-equal outputs.  Kinds 3 and 4 take a split-K
+ * (rrin_conv_h8_desc.ksplit).  Kind 6 also runs at RRIN_PREC_F16 (packed by
+ * rrin_pack_conv3x3_wino_h8; cin % 16 == 0 or tail_finite; no split-K, no ring
+ * fold).  0: direct form.  -1: a retired id (19, 22: ABI 16 removed the rejected
+ * kinds 2, 5 and 8-13 and their configs 25-30; rrin_conv_h8_cfg_ok reports 0 and
+ * rrin_conv3x3_h8_fwd returns RRIN_E_CONFIG). */
 int rrin_conv_h8_cfg_wino(int32_t cfg);
 
 /* F32R packing: [co_block][chunk of 8 ci][tap][half][bm][4] fp32 (half hh holds
@@ -299,16 +291,6 @@ int rrin_pack_conv3x3_wino_bm(const float* w, const float* b, int32_t cout, int3
 int64_t rrin_pack_conv3x3_wino_floats(int32_t cout, int32_t cin);
 int rrin_pack_conv3x3_wino(const float* w, const float* b, int32_t cout, int32_t cin, const int32_t* perm,
                            float* wpack, float* bpack);
-/* Winograd F(4x4,3x3) packing (kind 5): U = G g G^T, G = [1/2 0 0; 1/6 1/6 1/6;
- * 1/6 -1/6 1/6; 16/15 8/15 4/15; 1/30 -1/15 2/15; 0 0 1/2] (interpolation points
- * 0, 1, -1, 1/2, -2, inf with B^T scaled to integers), in double, rounded once,
- * laid out [co_block of 32][chunk of 4 ci][xi 36][half 2][co 32][2 ci] (xi =
- * 6*row + col; half hh holds channels chunk*4 + 2*hh, +1).  bpack:
- * rrin_pack_bias_floats(cout, 32) floats. */
-int64_t rrin_pack_conv3x3_wino4_floats(int32_t cout, int32_t cin);
-int rrin_pack_conv3x3_wino4(const float* w, const float* b, int32_t cout, int32_t cin, const int32_t* perm,
-                            float* wpack, float* bpack);
-
 /* fp16 Winograd packing (ABI 13; kind 6 at RRIN_PREC_F16): U = G g G^T per (co, ci)
  * in double, times a power of two that puts max|U| in [2^12, 2^13), rounded once to
  * fp16, laid out [co_block of 64][chunk of 16 ci][xi 16][half 2][co 64][8 ci] (half hh
@@ -363,7 +345,8 @@ typedef struct rrin_edge_fix_desc {
   /* ABI 15: 1 = the ring value from scratch (bias + the conv's in-image taps of the
    * upsampled src, two staged lines per ring line; `edge` unused, may be NULL): it reads
    * nothing the EPI_SUBPIXEL conv writes (that conv writes ring pixels only to `edge`), so
-   * the two may run concurrently.  0 = the correction of the conv's `edge` values. */
+   * the two may run concurrently (the Net measured both orders slower than the
+   * correction, DESIGN.md §5e, and uses 0).  0 = the correction of the conv's `edge` values. */
   int32_t full;
 } rrin_edge_fix_desc;
 int rrin_subpixel_edge_fix_h8(const rrin_edge_fix_desc* d, void* stream);

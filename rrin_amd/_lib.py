@@ -9,7 +9,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-ABI_VERSION = 15
+ABI_VERSION = 16
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "librrin_hip.so")
 # A/B sessions only (tools/sessions/): another build of the same library, e.g. ab/librrin_hip_X.so
 if os.environ.get("RRIN_LIB_AB"):
@@ -169,9 +169,6 @@ SIGNATURES = {
     "rrin_edge_fix_split_floats": (C.c_int64, [C.c_void_p, C.c_void_p]),
     "rrin_pack_conv3x3_wino_floats": (C.c_int64, [C.c_int32, C.c_int32]),
     "rrin_pack_conv3x3_wino_bm_floats": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32]),
-    "rrin_pack_conv3x3_wino4_floats": (C.c_int64, [C.c_int32, C.c_int32]),
-    "rrin_pack_conv3x3_wino4": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p,
-                                          C.c_void_p]),
     "rrin_pack_conv3x3_wino_bm": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p,
                                             C.c_void_p, C.c_void_p]),
     "rrin_pack_conv3x3_wino": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p,

@@ -257,46 +257,21 @@ constexpr size_t kWinoLds = (size_t)(2 * 704 + 2 * 16 * 2 * 32) * 16;
 int launch_wino(const ConvH8Args& a, int epi, hipStream_t st);
 // zero channels [c0, c1) of a record-layout view (conv_f16.hip)
 int clear_channels_h8(const rrin_h8* v, int32_t n, int32_t c0, int32_t c1, int32_t prec, hipStream_t st);
-// 64-channel tile (8 waves, one block per CU): two stages of raw tile + 64-co U slab
-// (kind 2: built only into the lab library)
-constexpr size_t kWino64Lds = (size_t)2 * (704 + 16 * 2 * 64) * 16;
-#ifdef RRIN_LAB
-int launch_wino64(const ConvH8Args& a, int epi, hipStream_t st);
-#endif
 // cfg 18's tile on 8 waves of 4 accumulators (<= 128 VGPRs: 4 waves per SIMD),
 // two stages of [raw 680 | U 1024] records (three in A/B builds: two blocks per
 // CU would fill 163,584 B)
 constexpr size_t kWinoQLds = (size_t)3 * (680 + 1024) * 16;
 // th = 8 (cfg 20: 8 waves) or 4 (cfg 21: 4 waves, the same arithmetic on half-height tiles)
 int launch_winoq(const ConvH8Args& a, int epi, int th, hipStream_t st);
-// Winograd F(4x4,3x3) (conv_wino4.hip): BM 32 x TH 16, 6 waves, 4-channel K chunks
-// (kind 5: built only into the lab library)
-constexpr size_t kWino4Lds = (size_t)2 * (612 + 1152) * 16;
-#ifdef RRIN_LAB
-int launch_wino4(const ConvH8Args& a, int epi, hipStream_t st);
-int launch_wino4_lab(const ConvH8Args& a, int abl, hipStream_t st);
-#endif
 // register-U Winograd tiles (conv_winoc.hip): 4 waves, two blocks per CU, the U operands
 // loaded straight into registers; ct = 2: BM 64 x TH 4 (kind 6), ct = 1: BM 32 x TH 8 (kind 7).
 // LDS: max(3 raw stages, the output-transform exchange)
 constexpr size_t kWinoCLds1 = (size_t)2048 * 16;  // TH 4: 3 x 512 stage records < 2048 exchange
 constexpr size_t kWinoCLds2 = (size_t)4096 * 16;  // TH 8: 3 x 768 < 4096
-// persistent: kind 12 (kind 6 on a persistent grid, conv3x3_winocp_kernel; same bits)
-int launch_winoc(const ConvH8Args& a, int epi, int ct, bool persistent, hipStream_t st);
-constexpr size_t kWinoCPLds = (size_t)(3 * 512 + 2048 + 128) * 16;  // stages + exchange + bias
+int launch_winoc(const ConvH8Args& a, int epi, int ct, hipStream_t st);
 // the kind-6 tile at fp16 (conv_winoh.hip): H8 records, v_mfma_f32_32x32x16_f16, packed-f16
 // input transform; same LDS as kWinoCLds1
-// nt = 1 (kind 6: BM 64 x TH 4, two blocks per CU) or 2 (kind 9: BM 64 x TH 8, one block per CU);
-// persistent: the tile-walking form (kinds 10 / 11), same bits
-int launch_winoh(const ConvH8Args& a, int epi, int nt, bool persistent, hipStream_t st);
-constexpr size_t kWinoHP1Lds = (size_t)(3 * 512 + 2048 + 128) * 16;  // persistent TH 4: stages + exchange + bias
-// kind 13 (fp16): kind 6 on two patch tiles per workgroup (8 waves), U shared through LDS: 3 stages
-// of [raw 1024 | U 2048] records
-#ifdef RRIN_LAB
-int launch_winohl(const ConvH8Args& a, int epi, hipStream_t st);
-#endif
-constexpr size_t kWinoHLLds = (size_t)3 * (1024 + 2048) * 16;
-constexpr size_t kWinoHP2Lds = (size_t)(3 * 768 + 4096 + 128) * 16;  // persistent TH 8
+int launch_winoh(const ConvH8Args& a, int epi, hipStream_t st);
 // fused level-0 UNetConvBlock at fp16 (conv_block0.hip): conv a (cin -> 32) + leaky, conv b
 // (32 -> 32) + leaky (+ pool), conv a's output tile in LDS.  Tile kB0TH x kB0TW outputs; conv a
 // runs on (kB0TH + 2) x (kB0TW + 2) positions from a (kB0TH + 4) x (kB0TW + 4) input tile
@@ -335,12 +310,6 @@ constexpr size_t kB0Lds = (size_t)(kB0Mid + kB0Stage + 16) * 16;
 static_assert(kB0Stage <= kB0Mid, "stage Y inside the conv-a tile");
 static_assert(2 * kB0Lds <= 160 * 1024, "two fused-block workgroups per CU");
 int launch_block0(const Block0Args& a, hipStream_t st);
-// persistent register-U tile for cout <= 32 (conv_winop.hip, kind 8): 8 waves, two raw
-// stages + a separate exchange area + 32 bias floats
-constexpr size_t kWinoPLds = (size_t)(2 * 680 + 2048) * 16 + 128;
-#ifdef RRIN_LAB
-int launch_winop(const ConvH8Args& a, int epi, hipStream_t st);
-#endif
 #ifdef RRIN_LAB
 int launch_wino_lab(const ConvH8Args& a, int abl, hipStream_t st);  // ablation bits (conv_wino.hip)
 #endif

@@ -1826,6 +1826,7 @@ struct CfgH8 {
   bool pool_ok;
   int sched, persist;
 };
+static constexpr size_t kRetiredLds = (size_t)1 << 30;  // > kMaxLds: never usable
 static const CfgH8 kCfgH8[] = {
 #define X(id, nw, wm, wn, sc, pe)                                                                               \
   {TileH8<nw, wm, wn, 1>::BM, TileH8<nw, wm, wn, 1>::TH, h8_lds_bytes<nw, wm, wn, 1>((sc & SCHED_WRES) != 0, 2), \
@@ -1835,76 +1836,39 @@ static const CfgH8 kCfgH8[] = {
 #undef X
     // kWinoCfg: Winograd F(2x2,3x3) on fp32 records (conv_wino.hip), BM 32 x TH 8
     {32, 8, kWinoLds, (size_t)1 << 30, 0, true, 0, 0},
-    // kWino64Cfg: the same, BM 64 x TH 8, 8 waves (conv3x3_wino64_kernel)
-    {64, 8, kWino64Lds, (size_t)1 << 30, 0, true, 0, 0},
+    // config 19, retired in round 6: the kind-2 Winograd tile (BM 64, 8 waves, one block per CU)
+    // lost to kinds 3 and 6 and was removed; the id stays reserved so ids 20-24 keep their meaning
+    {64, 8, kRetiredLds, kRetiredLds, 0, true, 0, 0},
     // kWinoQCfg: cfg 18's tile and packing, 8 waves of 4 accumulators (conv3x3_winoq_kernel)
     {32, 8, (size_t)2 * (680 + 1024) * 16, (size_t)1 << 30, 0, true, 0, 0},
     // kWinoQ4Cfg: the same on half-height tiles (TH 4, 4 waves): twice the tiles
     {32, 4, (size_t)2 * (408 + 1024) * 16, (size_t)1 << 30, 0, true, 0, 0},
-    // kWino4Cfg: Winograd F(4x4,3x3), BM 32 x TH 16, 6 waves (conv_wino4.hip)
-    {32, 16, kWino4Lds, (size_t)1 << 30, 0, true, 0, 0},
-    // kWinoC2Cfg: register-U tile, BM 64 x TH 4, 4 waves of 2 co tiles (conv_winoc.hip)
+    // config 22, retired in round 6: Winograd F(4x4,3x3) (kind 5), 1.28-1.58x kind 3's time
+    {32, 16, kRetiredLds, kRetiredLds, 0, true, 0, 0},
+    // kWinoC2Cfg: register-U tile, BM 64 x TH 4, 4 waves of 2 co tiles (conv_winoc.hip); at fp16
+    // the same tile with f16 MFMAs (conv_winoh.hip)
     {64, 4, kWinoCLds1, (size_t)1 << 30, 0, true, 0, 0},
     // kWinoC1Cfg: register-U tile, BM 32 x TH 8, 4 waves of 2 patch tiles
     {32, 8, kWinoCLds2, (size_t)1 << 30, 0, true, 0, 0},
-    // kWinoPCfg: persistent register-U tile, BM 32 x TH 8, 8 waves (conv_winop.hip; cout <= 32)
-    {32, 8, kWinoPLds, (size_t)1 << 30, 0, true, 0, 0},
-    // kWinoH2Cfg: fp16 only, the register-U tile on 2 patch tiles, BM 64 x TH 8, 4 waves, one
-    // block per CU (conv_winoh.hip)
-    {64, 8, kWinoCLds2, (size_t)1 << 30, 0, true, 0, 0},
-    // kWinoHP1Cfg / kWinoHP2Cfg: fp16 only, kinds 6 / 9 on a persistent grid (tile-walking workgroups)
-    {64, 4, kWinoHP1Lds, (size_t)1 << 30, 0, true, 0, 0},
-    {64, 8, kWinoHP2Lds, (size_t)1 << 30, 0, true, 0, 0},
-    // kWinoCPCfg: exact fp32, kind 6 on a persistent grid (conv3x3_winocp_kernel)
-    {64, 4, kWinoCPLds, (size_t)1 << 30, 0, true, 0, 0},
-    // kWinoHLCfg: fp16 only, kind 6 on two patch tiles per workgroup, U shared through LDS
-    // (conv3x3_winohl_kernel, 8 waves, one block per CU)
-    {64, 8, kWinoHLLds, (size_t)1 << 30, 0, true, 0, 0},
 };
 static constexpr int kNumCfgH8 = sizeof(kCfgH8) / sizeof(kCfgH8[0]);
-static constexpr int kWinoCfg = kNumCfgH8 - 13;
-static constexpr int kWino64Cfg = kNumCfgH8 - 12;
-static constexpr int kWinoQCfg = kNumCfgH8 - 11;
-static constexpr int kWinoQ4Cfg = kNumCfgH8 - 10;
-static constexpr int kWino4Cfg = kNumCfgH8 - 9;
-static constexpr int kWinoC2Cfg = kNumCfgH8 - 8;
-static constexpr int kWinoC1Cfg = kNumCfgH8 - 7;
-static constexpr int kWinoPCfg = kNumCfgH8 - 6;
-static constexpr int kWinoH2Cfg = kNumCfgH8 - 5;
-static constexpr int kWinoHP1Cfg = kNumCfgH8 - 4;
-static constexpr int kWinoHP2Cfg = kNumCfgH8 - 3;
-static constexpr int kWinoCPCfg = kNumCfgH8 - 2;
-static constexpr int kWinoHLCfg = kNumCfgH8 - 1;
+static constexpr int kWinoCfg = kNumCfgH8 - 7;
+static constexpr int kRetired19Cfg = kNumCfgH8 - 6;
+static constexpr int kWinoQCfg = kNumCfgH8 - 5;
+static constexpr int kWinoQ4Cfg = kNumCfgH8 - 4;
+static constexpr int kRetired22Cfg = kNumCfgH8 - 3;
+static constexpr int kWinoC2Cfg = kNumCfgH8 - 2;
+static constexpr int kWinoC1Cfg = kNumCfgH8 - 1;
 static_assert(kWinoCfg == 18, "the direct-form configs keep ids 0-17 (engine tile tables)");
-static inline bool is_winoc(int cfg) { return cfg == kWinoC2Cfg || cfg == kWinoC1Cfg || cfg == kWinoCPCfg; }
-// tiles whose kernels only the lab library builds (kind 2 wino64, kind 5 F(4x4), kind 8
-// the persistent register-U tile):
-// the product library reports them as not usable (rrin_conv_h8_cfg_ok 0)
-// Round 5: the fp16 kinds 9 (one wave per SIMD: 1.2-2.3x kind 6's time per conv) and 10 / 11 (kinds
-// 6 / 9 on a persistent grid: slower in the two-stream forward, and an A/B build with one
-// workgroup per CU ran the C3 forward non-deterministically -- a race not found)
-// are lab-only too.
-// Kind 13 (U shared through LDS by two patch tiles) measured 1.0-1.3x kind 6's time per conv: lab-only.
-static inline bool lab_only(int cfg) {
-  return cfg == kWino64Cfg || cfg == kWino4Cfg || cfg == kWinoPCfg || cfg == kWinoH2Cfg || cfg == kWinoHP1Cfg ||
-         cfg == kWinoHP2Cfg || cfg == kWinoHLCfg;
-}
-#ifdef RRIN_LAB
-static constexpr bool kLabBuild = true;
-#else
-static constexpr bool kLabBuild = false;
-#endif
+static inline bool is_winoc(int cfg) { return cfg == kWinoC2Cfg || cfg == kWinoC1Cfg; }
+// Round 6 removed the rejected Winograd tiles (kinds 2, 5, 8-13; DESIGN.md §5b-§5e keep their
+// measurements): ids 19 and 22 stay reserved (rrin_conv_h8_cfg_ok 0, RRIN_E_CONFIG), 25-30 are gone.
+static inline bool retired(int cfg) { return cfg == kRetired19Cfg || cfg == kRetired22Cfg; }
 static inline bool is_wino(int cfg) {
-  return cfg == kWinoCfg || cfg == kWino64Cfg || cfg == kWinoQCfg || cfg == kWinoQ4Cfg || cfg == kWino4Cfg ||
-         is_winoc(cfg) || cfg == kWinoPCfg || cfg == kWinoH2Cfg || cfg == kWinoHP1Cfg || cfg == kWinoHP2Cfg ||
-         cfg == kWinoHLCfg;
+  return cfg == kWinoCfg || cfg == kWinoQCfg || cfg == kWinoQ4Cfg || is_winoc(cfg);
 }
-// fp16-only Winograd tiles: kind 9, the persistent kinds 10, 11 and kind 13
-static inline bool f16_only(int cfg) {
-  return cfg == kWinoH2Cfg || cfg == kWinoHP1Cfg || cfg == kWinoHP2Cfg || cfg == kWinoHLCfg;
-}
-// the fp16 Winograd tiles (conv_winoh.hip): kind 6 and the fp16-only kinds
-static inline bool is_winoh(int cfg) { return cfg == kWinoC2Cfg || f16_only(cfg); }
+// the fp16 Winograd tile (conv_winoh.hip): kind 6
+static inline bool is_winoh(int cfg) { return cfg == kWinoC2Cfg; }
 static constexpr size_t kMaxLds = 160 * 1024;
 static constexpr int kMaxKSplit = 16;
 
@@ -2021,7 +1985,7 @@ static int h8_prepare(const rrin_conv_h8_desc* d, ConvH8Args& a, bool need_scrat
   if (!d || !d->whi || !d->bias) return RRIN_E_ARG;
   if (!rec_prec(d->prec)) return RRIN_E_ARG;
   if (d->prec == RRIN_PREC_F16X3 && !d->wlo) return RRIN_E_ARG;
-  if (d->cfg < 0 || d->cfg >= kNumCfgH8 || (lab_only(d->cfg) && !kLabBuild) ||
+  if (d->cfg < 0 || d->cfg >= kNumCfgH8 || retired(d->cfg) ||
       (planes_of(d->prec) == 2 ? kCfgH8[d->cfg].lds2 : kCfgH8[d->cfg].lds1) > kMaxLds)
     return RRIN_E_CONFIG;
   if (d->n < 1 || d->cin < 1 || d->cout < 8 || (d->cout & 7)) return RRIN_E_ARG;
@@ -2087,20 +2051,25 @@ static int h8_prepare(const rrin_conv_h8_desc* d, ConvH8Args& a, bool need_scrat
     if (!is_winoh(d->cfg) || d->ksplit > 1 || d->ring_w) return RRIN_E_CONFIG;
     if ((d->cin & 15) && !d->tail_finite) return RRIN_E_CONFIG;
   } else if (is_wino(d->cfg)) {
-    if (d->prec != RRIN_PREC_F32R || f16_only(d->cfg)) return RRIN_E_CONFIG;
+    if (d->prec != RRIN_PREC_F32R) return RRIN_E_CONFIG;
     if ((d->cin & 3) && !d->tail_finite) return RRIN_E_CONFIG;  // stages whole records only
     // the register-U tiles stage both record groups of every chunk: they must exist
     if (is_winoc(d->cfg) && (d->cin & 7) && !d->tail_finite) return RRIN_E_CONFIG;
-    // kind 8: one co block, no sub-pixel / replicate epilogue, no split
-    if (d->cfg == kWinoPCfg && (d->cout > 32 || d->epi_mode == RRIN_EPI_SUBPIXEL || d->epi_mode == RRIN_EPI_LEAKY_REP ||
-                                d->ksplit > 1))
-      return RRIN_E_CONFIG;
-    // two record groups per K chunk; F(4x4): one
-    a.nchunks = d->cfg == kWino4Cfg ? (d->cin + 3) / 4 : (d->cin + 7) / 8;
+    a.nchunks = (d->cin + 7) / 8;  // two record groups per K chunk
   }
   // the Winograd tiles stage every record group of every chunk (past cin against zero
   // weights): the source view must hold them, or the staging reads past the tensor
-  if (is_wino(d->cfg) && (d->cfg == kWino4Cfg ? a.nchunks : 2 * a.nchunks) > d->src.groups) return RRIN_E_SHAPE;
+  if (is_wino(d->cfg) && 2 * a.nchunks > d->src.groups) return RRIN_E_SHAPE;
+  {
+    // LDS-DMA staging addresses the source through buffer resources (num_records 2^31 - 1) with
+    // 32-bit byte offsets: the direct-form tiles from one base per image (every staged record
+    // group of the image), the Winograd tiles from one base per tile and chunk (two groups).  A
+    // larger span would stage zeros past the range -- a wrong result with no error -- so it is
+    // rejected (a 64-channel fp16 view passes 2 GB near 6144x3456).
+    const bool dma = is_wino(d->cfg) || d->cin % 8 == 0 || d->tail_finite;
+    const int64_t span_groups = is_wino(d->cfg) ? 3 : 2 * (int64_t)a.nchunks;
+    if (dma && span_groups * d->src.g.plane * 16 >= ((int64_t)1 << 31)) return RRIN_E_SHAPE;
+  }
   a.n = d->n;
   if ((int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n > 0x7fffffff) return RRIN_E_SHAPE;
   a.ksplit = 1;
@@ -2168,23 +2137,16 @@ extern "C" int rrin_conv_h8_cfg_bm(int32_t cfg) {
 extern "C" int rrin_conv_h8_cfg_th(int32_t cfg) {
   return (cfg >= 0 && cfg < kNumCfgH8) ? kCfgH8[cfg].th : RRIN_E_CONFIG;
 }
-// 0: direct form; Winograd tile kind: 1 BM 32 / 4 waves, 2 BM 64 / 8 waves, 3 BM 32 / 8 waves,
-// 4 BM 32 x TH 4 / 4 waves; 5 Winograd F(4x4,3x3), BM 32 x TH 16 / 6 waves (its own packing,
-// rrin_pack_conv3x3_wino4); 6 BM 64 x TH 4 and 7 BM 32 x TH 8, register-U tiles (conv_winoc.hip)
+// 0: direct form; Winograd tile kind: 1 BM 32 / 4 waves, 3 BM 32 / 8 waves, 4 BM 32 x TH 4 / 4 waves;
+// 6 BM 64 x TH 4 and 7 BM 32 x TH 8, register-U tiles (conv_winoc.hip; kind 6 also at fp16,
+// conv_winoh.hip).  The retired ids (19, 22) report -1.
 extern "C" int rrin_conv_h8_cfg_wino(int32_t cfg) {
   return cfg == kWinoCfg     ? 1
-         : cfg == kWino64Cfg ? 2
          : cfg == kWinoQCfg  ? 3
          : cfg == kWinoQ4Cfg ? 4
-         : cfg == kWino4Cfg  ? 5
          : cfg == kWinoC2Cfg ? 6
          : cfg == kWinoC1Cfg ? 7
-         : cfg == kWinoPCfg  ? 8
-         : cfg == kWinoH2Cfg ? 9
-         : cfg == kWinoHP1Cfg ? 10
-         : cfg == kWinoHP2Cfg ? 11
-         : cfg == kWinoCPCfg ? 12
-         : cfg == kWinoHLCfg ? 13
+         : retired(cfg)      ? -1
                              : 0;
 }
 // Fused level-0 UNetConvBlock (conv_block0.hip): validate and launch.
@@ -2247,11 +2209,9 @@ extern "C" int rrin_conv_block0_h8_fwd(const rrin_block0_h8_desc* d, void* strea
 
 extern "C" int rrin_conv_h8_cfg_ok(int32_t cfg, int32_t prec) {
   if (cfg < 0 || cfg >= kNumCfgH8) return 0;
-  if (!rec_prec(prec) || (lab_only(cfg) && !kLabBuild)) return 0;
-  // Winograd tiles: exact fp32 records (kinds 1-8); the register-U kind 6 also at fp16 and
-  // kind 9 at fp16 only (conv_winoh.hip)
-  if (is_wino(cfg) && (prec == RRIN_PREC_F16 ? !is_winoh(cfg) : prec != RRIN_PREC_F32R || f16_only(cfg)))
-    return 0;
+  if (!rec_prec(prec) || retired(cfg)) return 0;
+  // Winograd tiles: exact fp32 records; the register-U kind 6 also at fp16 (conv_winoh.hip)
+  if (is_wino(cfg) && (prec == RRIN_PREC_F16 ? !is_winoh(cfg) : prec != RRIN_PREC_F32R)) return 0;
   return (planes_of(prec) == 2 ? kCfgH8[cfg].lds2 : kCfgH8[cfg].lds1) <= kMaxLds ? 1 : 0;
 }
 
@@ -2273,22 +2233,9 @@ extern "C" int rrin_conv3x3_h8_fwd(const rrin_conv_h8_desc* d, void* stream) {
   if (d->cfg == kWinoCfg) return launch_wino(a, d->epi_mode, st);
   if (d->cfg == kWinoQCfg) return launch_winoq(a, d->epi_mode, 8, st);
   if (d->cfg == kWinoQ4Cfg) return launch_winoq(a, d->epi_mode, 4, st);
-#ifdef RRIN_LAB
-  if (d->cfg == kWino64Cfg) return launch_wino64(a, d->epi_mode, st);
-  if (d->cfg == kWino4Cfg) return launch_wino4(a, d->epi_mode, st);
-#endif
-#ifdef RRIN_LAB
-  if (d->cfg == kWinoHLCfg && d->prec == RRIN_PREC_F16) return launch_winohl(a, d->epi_mode, st);
-#endif
-  if (is_winoh(d->cfg) && d->prec == RRIN_PREC_F16)
-    return launch_winoh(a, d->epi_mode, d->cfg == kWinoH2Cfg || d->cfg == kWinoHP2Cfg ? 2 : 1,
-                        d->cfg == kWinoHP1Cfg || d->cfg == kWinoHP2Cfg, st);
-  if (d->cfg == kWinoC2Cfg) return launch_winoc(a, d->epi_mode, 2, false, st);
-  if (d->cfg == kWinoCPCfg) return launch_winoc(a, d->epi_mode, 2, true, st);
-  if (d->cfg == kWinoC1Cfg) return launch_winoc(a, d->epi_mode, 1, false, st);
-#ifdef RRIN_LAB
-  if (d->cfg == kWinoPCfg) return launch_winop(a, d->epi_mode, st);
-#endif
+  if (is_winoh(d->cfg) && d->prec == RRIN_PREC_F16) return launch_winoh(a, d->epi_mode, st);
+  if (d->cfg == kWinoC2Cfg) return launch_winoc(a, d->epi_mode, 2, st);
+  if (d->cfg == kWinoC1Cfg) return launch_winoc(a, d->epi_mode, 1, st);
   switch (d->cfg) {
 #define X(id, nw, wm, wn, sc, pe) \
   case id:                        \
@@ -2322,7 +2269,6 @@ extern "C" int rrin_conv3x3_h8_lab(const rrin_conv_h8_desc* d, int32_t sched, in
     ConvH8Args a;
     const int rc = h8_prepare(d, a);
     if (rc) return rc;
-    if (d->cfg == kWino4Cfg) return launch_wino4_lab(a, sched, (hipStream_t)stream);
     return launch_wino_lab(a, sched, (hipStream_t)stream);
   }
   if (!d || (d->prec != RRIN_PREC_F16X3 && d->prec != RRIN_PREC_F32R) || d->epi_mode != RRIN_EPI_LEAKY ||

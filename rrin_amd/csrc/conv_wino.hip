@@ -455,297 +455,6 @@ int launch_wino(const ConvH8Args& a, int epi, hipStream_t st) {
 }
 
 
-#ifdef RRIN_LAB  // kind 2 (BM 64, 8 waves, one block per CU): lost to kinds 3 and 6, lab library only
-// ============================================================================
-// 64-channel tile (config kWino64Cfg): 8 waves = 2 per SIMD, one block per CU.
-// Tile = 64 output channels (two MFMA co tiles) x 32 px x 8 rows (64 patches).
-// Wave (yw, pt) owns B^T row yw (transform points 4 yw .. 4 yw + 3) of patch
-// rows 2 pt, 2 pt + 1 for BOTH co tiles: each transformed B operand feeds two
-// MFMAs (one per co tile), so the input-transform VALU and the window reads per
-// MFMA are half those of the 32-channel tile, and the per-chunk staging (U slab
-// 32 KB + raw 10.9 KB for 256 MFMAs) is 2/3 of its DMA pieces per MFMA.  Same
-// arithmetic in the same order as the 32-channel kernel (bitwise equal outputs).
-// Loop: one phase per chunk, the barrier at its top (chunk c + 1 landed, chunk
-// c's buffers free for chunk c + 2's DMA); the phase's 32 MFMAs (point-major)
-// run while chunk c + 1's operands are read and transformed point by point.
-// ============================================================================
-constexpr int kW6U = 16 * 2 * 64;                      // U records per chunk: [xi][half][64 co]
-constexpr int kW6Stage = kWnRawStride + kW6U;          // records per LDS stage
-static_assert(kWino64Lds == (size_t)2 * kW6Stage * 16, "LDS size");
-
-template <int EPI>
-__global__ __launch_bounds__(512, 1) void conv3x3_wino64_kernel(ConvH8Args a) {
-  extern __shared__ __attribute__((aligned(16))) uint4 smem4[];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int yw = wv & 3, pt = wv >> 2, j = lane & 31, hh = lane >> 5;
-  int bid;
-  {  // XCD-aware bijective remap
-    const int nwg = gridDim.x, q = nwg >> 3, r = nwg & 7;
-    const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
-    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
-  }
-  const int ntiles = a.co_blocks * a.tiles_x * a.tiles_y * a.n;
-  if (bid >= ntiles) return;
-  const int nch = a.nchunks;
-  int cob, x0, y0, img;
-  {
-    int t = bid;
-    cob = t % a.co_blocks;
-    t /= a.co_blocks;
-    x0 = (t % a.tiles_x) * 32;
-    t /= a.tiles_x;
-    y0 = (t % a.tiles_y) * 8;
-    img = t / a.tiles_y;
-  }
-  const uint4* tsrc = a.src_hi + (int64_t)img * a.src_img + (int64_t)y0 * a.src_wp + x0 + (kH8PadLeft - 1);
-  const uint4* wsrc = a.w_hi + (int64_t)cob * nch * kW6U + tid;
-
-  // ---- staging: raw pieces (680 records: 512 + 168) and U pieces (2048 = 4 x 512)
-  int64_t p_off[2];
-  int p_g[2], p_zero[2];
-#pragma unroll
-  for (int it = 0; it < 2; ++it) {
-    const int idx = tid + 512 * it;
-    const int g = idx >= kWnRawG ? 1 : 0;
-    const int rem = idx - g * kWnRawG;
-    const int r = rem / kWnRawCols, pos = rem - r * kWnRawCols;
-    const int col = pos < 17 ? 2 * pos : 2 * (pos - 17) + 1;
-    p_g[it] = g;
-    p_off[it] = (int64_t)g * a.src_gp + r * a.src_wp + col;
-    p_zero[it] = col - y0 * a.src_wp;
-  }
-  auto issue = [&](int c, int stg) {
-    uint4* base = smem4 + stg * kW6Stage;
-#pragma unroll
-    for (int it = 0; it < 2; ++it) {
-      if (it == 0 || tid < kWnRaw - 512) {
-        const int gg = 2 * c + p_g[it];
-        const int64_t off = gg * 4 < a.cin ? (int64_t)(2 * c) * a.src_gp + p_off[it] : (int64_t)p_zero[it];
-        dma16(tsrc + off, base + 512 * it + (tid & ~63));
-      }
-    }
-#pragma unroll
-    for (int it = 0; it < 4; ++it)
-      dma16(wsrc + (int64_t)c * kW6U + 512 * it, base + kWnRawStride + 512 * it + (tid & ~63));
-  };
-
-  // MFMA column j -> patch (row pr, column jx), second row rotated by 12 (bank spread)
-  const int pr = 2 * pt + (j >> 4), jx = (j + 12 * (j >> 4)) & 15;
-  // B^T row yw of the window: t = d[ra] + sg d[rb]  (0: d0 - d2, 1: d1 + d2, 2: d2 - d1, 3: d1 - d3)
-  const int ra = yw == 0 ? 0 : (yw == 2 ? 2 : 1);
-  const int rb = yw == 0 ? 2 : (yw == 1 ? 2 : (yw == 2 ? 1 : 3));
-  const float sg = yw == 1 ? 1.f : -1.f;
-  const int rw0 = hh * kWnRawG + (2 * pr) * kWnRawCols;
-  const int oa = ra * kWnRawCols, ob = rb * kWnRawCols;
-  int pc[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) pc[k] = wn_col(2 * jx + k);
-  const int su0 = kWnRawStride + (8 * yw) * 64 + hh * 64 + j;  // U of point 4 yw + x, co tile t: + x * 128 + t * 32
-
-  wfloatx16 acc[2][4];
-  wfloatx4 u[2][4], v[4];
-  auto read_u = [&](int stg, int t, int x) {
-    return __builtin_bit_cast(wfloatx4, smem4[stg * kW6Stage + su0 + x * 128 + t * 32]);
-  };
-  auto read_raw = [&](int stg, wfloatx4* d) {
-    const uint4* rw = smem4 + stg * kW6Stage + rw0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      d[2 * k] = __builtin_bit_cast(wfloatx4, rw[oa + pc[k]]);
-      d[2 * k + 1] = __builtin_bit_cast(wfloatx4, rw[ob + pc[k]]);
-    }
-  };
-  auto row_t = [&](const wfloatx4* d, int k) {
-    wfloatx4 t;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) t[e] = fmaf(sg, d[2 * k + 1][e], d[2 * k][e]);
-    return t;
-  };
-  auto mfma_point = [&](int x, bool first) {
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const wfloatx16 c = (first && e == 0) ? wfloatx16{} : acc[t][x];
-        acc[t][x] = __builtin_amdgcn_mfma_f32_32x32x2f32(u[t][x][e], v[x][e], c, 0, 0, 0);
-      }
-  };
-  // phase: the MFMAs of the chunk in u / v while the next chunk (stage sn) is
-  // read and transformed into u / v point by point
-  auto phase = [&](int sn, bool first) {
-    wfloatx4 d[8], t[4];
-    read_raw(sn, d);
-    mfma_point(0, first);
-    u[0][0] = read_u(sn, 0, 0);
-    u[1][0] = read_u(sn, 1, 0);
-    t[0] = row_t(d, 0);
-    t[2] = row_t(d, 2);
-    mfma_point(1, first);
-    v[0] = t[0] - t[2];
-    u[0][1] = read_u(sn, 0, 1);
-    u[1][1] = read_u(sn, 1, 1);
-    t[1] = row_t(d, 1);
-    mfma_point(2, first);
-    v[1] = t[1] + t[2];
-    u[0][2] = read_u(sn, 0, 2);
-    u[1][2] = read_u(sn, 1, 2);
-    t[3] = row_t(d, 3);
-    mfma_point(3, first);
-    v[2] = t[2] - t[1];
-    v[3] = t[1] - t[3];
-    u[0][3] = read_u(sn, 0, 3);
-    u[1][3] = read_u(sn, 1, 3);
-  };
-
-  // ---- prologue: chunk 0 staged, its operands in u / v; chunk 1 in flight
-  issue(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (nch > 1) issue(1, 1);
-  {
-    wfloatx4 d[8], t[4];
-    read_raw(0, d);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) t[k] = row_t(d, k);
-    v[0] = t[0] - t[2];
-    v[1] = t[1] + t[2];
-    v[2] = t[2] - t[1];
-    v[3] = t[1] - t[3];
-#pragma unroll
-    for (int x = 0; x < 4; ++x) {
-      u[0][x] = read_u(0, 0, x);
-      u[1][x] = read_u(0, 1, x);
-    }
-  }
-  // phase c: chunk c + 1 landed everywhere and every read of chunk c's stage
-  // consumed (it was read during phase c - 1), so that stage takes chunk c + 2.
-  // After the last chunk the "next chunk" reads fetch stale records; never used.
-  auto step = [&](int c, bool first) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (c + 2 < nch) issue(c + 2, c & 1);
-    phase((c + 1) & 1, first);
-  };
-  step(0, true);
-  for (int c = 1; c < nch; ++c) step(c, false);
-  __syncthreads();  // stale reads done before the exchange reuses the LDS
-
-  // ---- output transform.  Q[t][c] = sum_x M[t][x] A[x][c] of this wave's B^T row;
-  // Y[0][c] = (Q0 + Q1) + Q2, Y[1][c] = (Q1 - Q2) - Q3 over the four yw waves of
-  // a patch-row pair, exchanged through LDS one co tile at a time; wave (yw, pt)
-  // then finishes output row r = yw & 1, column c = yw >> 1 of its patches.
-  wfloatx4* X = reinterpret_cast<wfloatx4*>(smem4);
-  const int r = yw & 1, cc = yw >> 1;
-  const int y = y0 + 2 * pr + r, x = x0 + 2 * jx + cc;
-  uint4* dst = a.dst_hi + (int64_t)img * a.dst_img;
-  auto store4 = [&](int64_t rec, const float* vv) {
-    dst[rec] = make_uint4(__float_as_uint(vv[0]), __float_as_uint(vv[1]), __float_as_uint(vv[2]), __float_as_uint(vv[3]));
-  };
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      wfloatx4 g;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int vi = 4 * k + e, c2 = vi >> 4, i = vi & 15;
-        const float m0 = acc[t][0][i], m1 = acc[t][1][i], m2 = acc[t][2][i], m3 = acc[t][3][i];
-        g[e] = c2 == 0 ? (m0 + m1) + m2 : (m1 - m2) - m3;
-      }
-      X[((pt * 4 + yw) * 8 + k) * 64 + lane] = g;
-    }
-    __syncthreads();
-    float yv[16];
-#pragma unroll
-    for (int k4 = 0; k4 < 4; ++k4) {
-      const int k = 4 * cc + k4;
-      const wfloatx4 q0 = X[((pt * 4 + 0) * 8 + k) * 64 + lane];
-      const wfloatx4 q1 = X[((pt * 4 + 1) * 8 + k) * 64 + lane];
-      const wfloatx4 q2 = X[((pt * 4 + 2) * 8 + k) * 64 + lane];
-      const wfloatx4 q3 = X[((pt * 4 + 3) * 8 + k) * 64 + lane];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) yv[4 * k4 + e] = r == 0 ? (q0[e] + q1[e]) + q2[e] : (q1[e] - q2[e]) - q3[e];
-    }
-    __syncthreads();  // X is rewritten by the next co tile / the pool exchange
-    const int cobe = 2 * cob + t;  // 32-channel block of this co tile
-    if constexpr (EPI == RRIN_EPI_SUBPIXEL) {
-      const int HH = 2 * a.h, WW = 2 * a.w, creal = a.cout >> 2;
-      if (cobe * 32 < a.cout && y < a.h && x < a.w) {
-#pragma unroll
-        for (int qq = 0; qq < 4; ++qq) {
-          const int Y = 2 * y + (qq >> 1), XX = 2 * x + (qq & 1);
-          const int64_t ri = ring_index(Y, XX, HH, WW);
-          if (ri >= 0) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-              a.edge[((int64_t)img * creal + cobe * 8 + 4 * hh + e) * a.ring + ri] = yv[4 * qq + e];
-          } else {
-            float vv[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) vv[e] = yv[4 * qq + e] + a.bias[cobe * 32 + 8 * qq + 4 * hh + e];
-            store4((int64_t)(2 * cobe + hh) * a.dst_gp + (int64_t)(Y + 1) * a.dst_wp + XX + kH8PadLeft, vv);
-          }
-        }
-      }
-    } else {
-      float vv[16];
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        float tv = yv[i] + a.bias[cobe * 32 + 8 * (i >> 2) + 4 * hh + (i & 3)];
-        if constexpr (EPI != RRIN_EPI_LINEAR) tv = leaky(tv, a.slope);
-        vv[i] = tv;
-      }
-#pragma unroll
-      for (int qq = 0; qq < 4; ++qq) {
-        if (cobe * 32 + 8 * qq < a.cout && y < a.h && x < a.w) {
-          const int64_t rec = (int64_t)(cobe * 8 + 2 * qq + hh) * a.dst_gp + (int64_t)(y + 1) * a.dst_wp + x + kH8PadLeft;
-          store4(rec, &vv[4 * qq]);
-          if constexpr (EPI == RRIN_EPI_LEAKY_REP) {
-            const int dy0 = y == 0 ? -1 : 0, dy1 = y == a.h - 1 ? 1 : 0;
-            const int dx0 = x == 0 ? -1 : 0, dx1 = x == a.w - 1 ? 1 : 0;
-            for (int dy = dy0; dy <= dy1; ++dy)
-              for (int dx = dx0; dx <= dx1; ++dx)
-                if (dy | dx) store4(rec + (int64_t)dy * a.dst_wp + dx, &vv[4 * qq]);
-          }
-        }
-      }
-      if constexpr (EPI == RRIN_EPI_LEAKY_POOL) {
-        // the patch's four outputs (yw = (r, c)) meet in LDS; wave yw 0 writes
-        // avg = 0.25 ((Y00 + Y10) + (Y01 + Y11)), the 32-channel kernel's order
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          wfloatx4 g;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) g[e] = vv[4 * k + e];
-          X[((pt * 4 + yw) * 4 + k) * 64 + lane] = g;
-        }
-        __syncthreads();
-        if (yw == 0) {
-          const int xp = x0 + 2 * jx, yp = y0 + 2 * pr;
-          uint4* pdst = a.pool_hi + (int64_t)img * a.pool_img;
-#pragma unroll
-          for (int qq = 0; qq < 4; ++qq) {
-            const wfloatx4 y00 = X[((pt * 4 + 0) * 4 + qq) * 64 + lane];
-            const wfloatx4 y10 = X[((pt * 4 + 1) * 4 + qq) * 64 + lane];
-            const wfloatx4 y01 = X[((pt * 4 + 2) * 4 + qq) * 64 + lane];
-            const wfloatx4 y11 = X[((pt * 4 + 3) * 4 + qq) * 64 + lane];
-            if (cobe * 32 + 8 * qq < a.cout && yp < a.h && xp < a.w) {
-              float s4[4];
-#pragma unroll
-              for (int e = 0; e < 4; ++e) s4[e] = 0.25f * ((y00[e] + y10[e]) + (y01[e] + y11[e]));
-              const int64_t rec =
-                  (int64_t)(cobe * 8 + 2 * qq + hh) * a.pool_gp + (int64_t)(yp / 2 + 1) * a.pool_wp + xp / 2 + kH8PadLeft;
-              pdst[rec] = make_uint4(__float_as_uint(s4[0]), __float_as_uint(s4[1]), __float_as_uint(s4[2]),
-                                     __float_as_uint(s4[3]));
-            }
-          }
-        }
-        __syncthreads();
-      }
-    }
-  }
-}
-#endif  // RRIN_LAB (wino64)
 
 
 // ============================================================================
@@ -1546,27 +1255,6 @@ int launch_winoq(const ConvH8Args& a0, int epi, int th, hipStream_t st) {
 }
 
 #ifdef RRIN_LAB
-template <int EPI>
-static int launch_wino64_k(const ConvH8Args& a, hipStream_t st) {
-  auto k = conv3x3_wino64_kernel<EPI>;
-  static LdsAttr attr;
-  if (int e = attr.ensure((const void*)k, (int)kWino64Lds, st)) return e;
-  const int64_t grid = (int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n;
-  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(512), kWino64Lds, st, a);
-  return hip_code(hipGetLastError());
-}
-
-int launch_wino64(const ConvH8Args& a, int epi, hipStream_t st) {
-  switch (epi) {
-    case RRIN_EPI_LINEAR: return launch_wino64_k<RRIN_EPI_LINEAR>(a, st);
-    case RRIN_EPI_LEAKY: return launch_wino64_k<RRIN_EPI_LEAKY>(a, st);
-    case RRIN_EPI_LEAKY_POOL: return launch_wino64_k<RRIN_EPI_LEAKY_POOL>(a, st);
-    case RRIN_EPI_LEAKY_REP: return launch_wino64_k<RRIN_EPI_LEAKY_REP>(a, st);
-    case RRIN_EPI_SUBPIXEL: return launch_wino64_k<RRIN_EPI_SUBPIXEL>(a, st);
-  }
-  return RRIN_E_ARG;
-}
-
 // kernel lab (librrin_lab.so only): the LEAKY conv with ablation bits
 int launch_wino_lab(const ConvH8Args& a, int abl, hipStream_t st) {
   switch (abl) {  // 1024 + bits: the 4-waves-per-SIMD tile (cfg 20)

@@ -441,390 +441,6 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winoc_kernel(ConvH8Args a) {
 #endif
 }
 
-// ---- persistent kind 6 (kind 12): the workgroup walks tiles bid, bid + grid, ... with its chunk
-// pipeline running on across tile boundaries, as conv_winoh.hip's persistent fp16 tiles: the
-// next tile's chunk 0 (raw tile, U) and chunk 1 (raw tile) load during the current tile's last
-// chunks; the exchange area is separate from the raw stages; the epilogue's barriers are bare;
-// every epilogue store is an unconditional buffer store (an out-of-image position gets an offset
-// past the buffer: dropped); the first chunk after an epilogue waits for its raw tile by counting
-// the younger loads only (stores complete out of order with loads); the tile's bias is staged
-// into LDS by LDS-DMA.
-// The cin 32-64 convs (4-8 chunks per tile) spend ~40 % of a one-tile workgroup's life outside
-// its main loop; here that part overlaps the next tile's loads.  Same arithmetic
-// in the same order as kinds 1-7: bitwise equal outputs.
-template <int EPI>
-struct WinoCP {
-  using G = WinoC<1>;
-  static constexpr int XOFF = G::NS * G::STAGE;
-  static constexpr int BOFF = XOFF + G::XREC;  // bias areas: 2 x 64 records (16 used), by tile parity
-  static constexpr size_t LDS = (size_t)(BOFF + 128) * 16;
-  static constexpr int PER = EPI == RRIN_EPI_LEAKY_REP ? 4
-                             : EPI == RRIN_EPI_LEAKY_POOL ? 2
-                             : EPI == RRIN_EPI_SUBPIXEL  ? 5
-                                                         : 1;
-  static constexpr int S = 2 * 4 * PER;  // stores per wave and epilogue: 2 co tiles x 4 record pairs
-};
-static_assert(WinoCP<RRIN_EPI_LEAKY>::LDS == kWinoCPLds, "LDS (common.hpp)");
-static_assert(2 * kWinoCPLds <= 160 * 1024, "two blocks per CU");
-
-template <int EPI>
-__global__ __launch_bounds__(256, 2) void conv3x3_winocp_kernel(ConvH8Args a) {
-  using G = WinoC<1>;
-  using PP = WinoCP<EPI>;
-  constexpr int CT = 2, BM = 64, TH = G::TH, RG = G::RG, STAGE = G::STAGE, P = G::PIECES;
-  constexpr uint32_t kOOB = 0x80000000u;
-  extern __shared__ __attribute__((aligned(16))) uint4 smem4[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int yw = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int j = lane & 31, hh = lane >> 5;
-  const int grid = gridDim.x;
-  int bid;
-  {
-    const int q = grid >> 3, r = grid & 7;
-    const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
-    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
-  }
-  const int ntiles = a.co_blocks * a.tiles_x * a.tiles_y * a.n;
-  if (bid >= ntiles) return;
-  const int nch = a.nchunks;  // >= 2 (launch_winoc)
-  struct Tile {
-    int cob, x0, y0, img;
-  };
-  auto coords = [&](int t) {
-    Tile o;
-    const int cpg = a.cob_group > 0 ? a.cob_group : a.co_blocks;
-    const int gsz = cpg * (ntiles / a.co_blocks);
-    const int g = t / gsz;
-    const int r = t - g * gsz;
-    const int cg = min(cpg, a.co_blocks - g * cpg);
-    o.cob = g * cpg + r % cg;
-    int u = r / cg;
-    o.x0 = (u % a.tiles_x) * 32;
-    u /= a.tiles_x;
-    o.y0 = (u % a.tiles_y) * TH;
-    o.img = u / a.tiles_y;
-    return o;
-  };
-  auto tile_base = [&](const Tile& t) {
-    return a.src_hi + (int64_t)t.img * a.src_img + (int64_t)t.y0 * a.src_wp + t.x0 + (kH8PadLeft - 1);
-  };
-  auto u_base = [&](const Tile& t) { return buf_rsrc(a.w_hi + (int64_t)t.cob * nch * 32 * BM); };
-
-  uint32_t voff[P];
-#pragma unroll
-  for (int it = 0; it < P; ++it) {
-    const int idx = tid + 256 * it;
-    const int g = idx >= RG ? 1 : 0;
-    const int rem = idx < G::RAW ? idx - g * RG : 0;
-    const int r = rem / 34, pos = rem - r * 34;
-    const int col = pos < 17 ? 2 * pos : 2 * (pos - 17) + 1;
-    voff[it] = (uint32_t)((idx < G::RAW ? (int64_t)g * a.src_gp : 0) + (int64_t)r * a.src_wp + col) * 16u;
-  }
-  const int64_t chunk_stride = 2 * a.src_gp;
-  auto issue_raw_at = [&](const uint4* base, int s) {
-    const auto rs = buf_rsrc(base);
-#pragma unroll
-    for (int it = 0; it < P; ++it) buf_dma16(rs, smem4 + s * STAGE + 256 * it + 64 * yw, voff[it]);
-  };
-  auto issue_bias = [&](const Tile& t, int tp) {
-    const auto rs = buf_rsrc(a.bias + (int64_t)t.cob * BM);
-    buf_dma16(rs, smem4 + PP::BOFF + 64 * tp, (uint32_t)(lane & 15) * 16u);
-  };
-  const uint32_t uvoff = (uint32_t)(hh * BM + j) * 16u;
-  auto load_u = [&](__amdgpu_buffer_rsrc_t ur, int c, int x, int t) {
-    const int soff = c * (32 * BM * 16) + (4 * yw + (x & 2)) * (2 * BM * 16);
-    const int imm = (x & 1) * 2048 + t * 512;
-    return buf_load16(ur, uvoff + imm, soff);
-  };
-
-  const int jx = (j + 12 * (j >> 4)) & 15;
-  const int ra = yw == 0 ? 0 : (yw == 2 ? 2 : 1);
-  const int rb = yw == 0 ? 2 : (yw == 1 ? 2 : (yw == 2 ? 1 : 3));
-  const float sg = yw == 1 ? 1.f : -1.f;
-  int pcol[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) pcol[k] = hh * RG + (2 * (j >> 4)) * 34 + wc_col(2 * jx + k);
-  const int oa = ra * 34, ob = rb * 34;
-
-  cfloatx16 acc[CT][4];
-  cfloatx4 u[CT][4];
-  cfloatx4 v[4];
-  cfloatx4 d[8];
-  auto zero_acc = [&]() {
-#pragma unroll
-    for (int t = 0; t < CT; ++t)
-#pragma unroll
-      for (int x = 0; x < 4; ++x) acc[t][x] = cfloatx16{};
-  };
-  auto read_raw = [&](int s) {
-    const uint4* rw = smem4 + s * STAGE;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      d[2 * k] = __builtin_bit_cast(cfloatx4, rw[oa + pcol[k]]);
-      d[2 * k + 1] = __builtin_bit_cast(cfloatx4, rw[ob + pcol[k]]);
-    }
-  };
-  auto transform = [&]() {
-    cfloatx4 tr[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) tr[k][e] = fmaf(sg, d[2 * k + 1][e], d[2 * k][e]);
-    v[0] = tr[0] - tr[2];
-    v[1] = tr[1] + tr[2];
-    v[2] = tr[2] - tr[1];
-    v[3] = tr[1] - tr[3];
-  };
-  auto mfma_point = [&](int x) {
-#pragma unroll
-    for (int t = 0; t < CT; ++t)
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        acc[t][x] = __builtin_amdgcn_mfma_f32_32x32x2f32(u[t][x][e], v[x][e], acc[t][x], 0, 0, 0);
-  };
-  auto bar = [&]() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
-  auto fence = [&]() { __builtin_amdgcn_sched_barrier(0); };
-
-  int tile = bid;
-  Tile cur = coords(tile);
-  bool has_next = tile + grid < ntiles;
-  Tile nxt = has_next ? coords(tile + grid) : cur;
-  auto ur = u_base(cur), urn = u_base(nxt);
-  const uint4* tb = tile_base(cur);
-  const uint4* tbn = tile_base(nxt);
-
-  // chunk c (see conv_winoh.hip's persistent chunk): FIRST = chunk 0 of a tile (an epilogue's
-  // stores and one bias DMA before its loads), LAST = a tile's last chunk (loads the next
-  // tile's chunk 0 U and chunk 1 raw tile, does not transform)
-  auto chunk = [&](int c, int s, const bool first, const bool last) {
-    const auto un = last ? urn : ur;
-    const int cn = last ? 0 : c + 1;
-#pragma unroll
-    for (int x = 0; x < 3; ++x) {
-      mfma_point(x);
-#pragma unroll
-      for (int t = 0; t < CT; ++t) u[t][x] = load_u(un, cn, x, t);
-      fence();
-    }
-    if (first) {
-      // loads complete in order among themselves, stores not in order with them: the younger
-      // LOADS of raw(c + 1) are U(c) pt 3, the bias DMA and U(c + 1) pts 0-2 (the epilogue's
-      // stores in between are not counted -- a count that included them could pass with the
-      // raw tile still in flight once the stores had completed)
-      RRIN_VMWAIT(1, 4 * CT);
-    } else {
-      RRIN_VMWAIT(0, 4 * CT);
-    }
-    bar();
-    const int c2 = c + 2;
-    const uint4* rp = c2 < nch ? tb + c2 * chunk_stride : tbn + (c2 - nch) * chunk_stride;
-    issue_raw_at(rp, s == 0 ? 2 : s - 1);
-    const int s1 = s == 2 ? 0 : s + 1;
-    if (!last) read_raw(s1);
-    fence();
-    mfma_point(3);
-    fence();
-    if (!last) transform();
-#pragma unroll
-    for (int t = 0; t < CT; ++t) u[t][3] = load_u(un, cn, 3, t);
-  };
-
-  int tp = 0;
-  issue_bias(cur, tp);
-  issue_raw_at(tb, 0);
-  vm_fence();
-#pragma unroll
-  for (int x = 0; x < 3; ++x)
-#pragma unroll
-    for (int t = 0; t < CT; ++t) u[t][x] = load_u(ur, 0, x, t);
-  vm_fence();
-  issue_raw_at(tb + chunk_stride, 1);
-  vm_fence();
-#pragma unroll
-  for (int t = 0; t < CT; ++t) u[t][3] = load_u(ur, 0, 3, t);
-  vm_fence();
-  RRIN_VMWAIT(P, 4 * CT);
-  bar();
-  issue_bias(cur, tp);  // again, in the after-epilogue position: chunk 0 waits as after an epilogue
-  read_raw(0);
-  transform();
-
-  cfloatx4* X = reinterpret_cast<cfloatx4*>(smem4 + PP::XOFF);
-  const int r = yw & 1, cc = yw >> 1;
-  // one fp32 record (4 channels) at byte offset off of rs (invalid: dropped)
-  auto st16 = [&](__amdgpu_buffer_rsrc_t rs, uint32_t off, const float* vv, bool valid) {
-    __builtin_amdgcn_raw_buffer_store_b128(
-        (unsigned __attribute__((ext_vector_type(4)))){__float_as_uint(vv[0]), __float_as_uint(vv[1]),
-                                                      __float_as_uint(vv[2]), __float_as_uint(vv[3])},
-        rs, valid ? off : kOOB, 0, 0);
-  };
-  int s = 0;
-  for (;;) {
-    chunk(0, s, true, false);
-    s = s == 2 ? 0 : s + 1;
-    for (int c = 1; c + 1 < nch; ++c) {
-      chunk(c, s, false, false);
-      s = s == 2 ? 0 : s + 1;
-    }
-    chunk(nch - 1, s, false, true);
-    s = s == 2 ? 0 : s + 1;
-
-    const auto drs = buf_rsrc(a.dst_hi + (int64_t)cur.img * a.dst_img);
-#pragma unroll
-    for (int t = 0; t < CT; ++t) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        cfloatx4 g;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int vi = 4 * k + e, c2 = vi >> 4, i = vi & 15;
-          const float m0 = acc[t][0][i], m1 = acc[t][1][i], m2 = acc[t][2][i], m3 = acc[t][3][i];
-          g[e] = c2 == 0 ? (m0 + m1) + m2 : (m1 - m2) - m3;
-        }
-        X[(yw * 8 + k) * 64 + lane] = g;
-      }
-      bar();
-      float yv[16];
-#pragma unroll
-      for (int k4 = 0; k4 < 4; ++k4) {
-        const int k = 4 * cc + k4;
-        const cfloatx4 q0 = X[(0 * 8 + k) * 64 + lane];
-        const cfloatx4 q1 = X[(1 * 8 + k) * 64 + lane];
-        const cfloatx4 q2 = X[(2 * 8 + k) * 64 + lane];
-        const cfloatx4 q3 = X[(3 * 8 + k) * 64 + lane];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) yv[4 * k4 + e] = r == 0 ? (q0[e] + q1[e]) + q2[e] : (q1[e] - q2[e]) - q3[e];
-      }
-      bar();
-      const cfloatx4* Bs = reinterpret_cast<const cfloatx4*>(smem4 + PP::BOFF + 64 * tp);
-      auto bias4 = [&](int qq) { return Bs[t * 8 + 2 * qq + hh]; };
-      const int cobe = CT * cur.cob + t;
-      const int pr = j >> 4;
-      const int y = cur.y0 + 2 * pr + r, x = cur.x0 + 2 * jx + cc;
-      const bool in = y < a.h && x < a.w;
-      if constexpr (EPI == RRIN_EPI_SUBPIXEL) {
-        const int HH = 2 * a.h, WW = 2 * a.w, creal = a.cout >> 2;
-        const bool blk = cobe * 32 < a.cout && in;
-        const auto ers = buf_rsrc(a.edge + (int64_t)cur.img * creal * a.ring);
-#pragma unroll
-        for (int qq = 0; qq < 4; ++qq) {
-          const int Y = 2 * y + (qq >> 1), XX = 2 * x + (qq & 1);
-          const int64_t ri = ring_index(Y, XX, HH, WW);
-          const bool ring = blk && ri >= 0;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const uint32_t eo = (uint32_t)(((int64_t)(cobe * 8 + 4 * hh + e) * a.ring + (ring ? ri : 0)) * 4);
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(yv[4 * qq + e]), ers, ring ? eo : kOOB, 0, 0);
-          }
-          float vv[4];
-          const cfloatx4 bq = bias4(qq);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) vv[e] = yv[4 * qq + e] + bq[e];
-          const int64_t rec = (int64_t)(2 * cobe + hh) * a.dst_gp + (int64_t)(Y + 1) * a.dst_wp + XX + kH8PadLeft;
-          st16(drs, (uint32_t)(rec * 16), vv, blk && ri < 0);
-        }
-      } else {
-        float vv[16];
-#pragma unroll
-        for (int qq = 0; qq < 4; ++qq) {
-          const cfloatx4 bq = bias4(qq);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            float tv = yv[4 * qq + e] + bq[e];
-            if constexpr (EPI != RRIN_EPI_LINEAR) tv = leaky(tv, a.slope);
-            vv[4 * qq + e] = tv;
-          }
-        }
-#pragma unroll
-        for (int qq = 0; qq < 4; ++qq) {
-          const bool ok = cobe * 32 + 8 * qq < a.cout && in;
-          const int64_t rec = (int64_t)(cobe * 8 + 2 * qq + hh) * a.dst_gp + (int64_t)(y + 1) * a.dst_wp + x + kH8PadLeft;
-          st16(drs, (uint32_t)(rec * 16), &vv[4 * qq], ok);
-          if constexpr (EPI == RRIN_EPI_LEAKY_REP) {
-            const int dy = y == 0 ? -1 : (y == a.h - 1 ? 1 : 0);
-            const int dx = x == 0 ? -1 : (x == a.w - 1 ? 1 : 0);
-            st16(drs, (uint32_t)((rec + (int64_t)dy * a.dst_wp) * 16), &vv[4 * qq], ok && dy != 0);
-            st16(drs, (uint32_t)((rec + dx) * 16), &vv[4 * qq], ok && dx != 0);
-            st16(drs, (uint32_t)((rec + (int64_t)dy * a.dst_wp + dx) * 16), &vv[4 * qq], ok && dy != 0 && dx != 0);
-          }
-        }
-        if constexpr (EPI == RRIN_EPI_LEAKY_POOL) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            cfloatx4 g;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) g[e] = vv[4 * k + e];
-            X[(yw * 4 + k) * 64 + lane] = g;
-          }
-          bar();
-          const int xp = cur.x0 + 2 * jx, yp = cur.y0 + 2 * pr;
-          const auto prs = buf_rsrc(a.pool_hi + (int64_t)cur.img * a.pool_img);
-#pragma unroll
-          for (int qq = 0; qq < 4; ++qq) {
-            const cfloatx4 y00 = X[(0 * 4 + qq) * 64 + lane];
-            const cfloatx4 y10 = X[(1 * 4 + qq) * 64 + lane];
-            const cfloatx4 y01 = X[(2 * 4 + qq) * 64 + lane];
-            const cfloatx4 y11 = X[(3 * 4 + qq) * 64 + lane];
-            float s4[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) s4[e] = 0.25f * ((y00[e] + y10[e]) + (y01[e] + y11[e]));
-            const bool ok = yw == 0 && cobe * 32 + 8 * qq < a.cout && yp < a.h && xp < a.w;
-            const int64_t rec =
-                (int64_t)(cobe * 8 + 2 * qq + hh) * a.pool_gp + (int64_t)(yp / 2 + 1) * a.pool_wp + xp / 2 + kH8PadLeft;
-            st16(prs, (uint32_t)(rec * 16), s4, ok);
-          }
-          bar();
-        }
-      }
-    }
-    if (!has_next) break;
-    tile += grid;
-    cur = nxt;
-    ur = urn;
-    tb = tbn;
-    has_next = tile + grid < ntiles;
-    nxt = has_next ? coords(tile + grid) : cur;
-    urn = u_base(nxt);
-    tbn = tile_base(nxt);
-    zero_acc();
-    tp ^= 1;
-    issue_bias(cur, tp);
-    read_raw(s);
-    transform();
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-// CUs of the stream's device (cached per device)
-static int winoc_cus(hipStream_t st) {
-  static std::atomic<int> cus[kMaxDevices];
-  const int dev = stream_device(st);
-  int ncu = cus[dev].load(std::memory_order_relaxed);
-  if (ncu <= 0) {
-    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
-    cus[dev].store(ncu, std::memory_order_relaxed);
-  }
-  return ncu;
-}
-
-// persistent workgroups per CU (A/B builds: 1 leaves the other slot of every CU to the other
-// stream's kernels)
-#ifndef RRIN_WINOCP_BPC
-#define RRIN_WINOCP_BPC 2
-#endif
-template <int EPI>
-static int launch_winocp_k(const ConvH8Args& a, int ncu, hipStream_t st) {
-  auto k = conv3x3_winocp_kernel<EPI>;
-  static LdsAttr attr;
-  constexpr size_t lds = WinoCP<EPI>::LDS;
-  if (int e = attr.ensure((const void*)k, (int)lds, st)) return e;
-  const int64_t tiles = (int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n;
-  const int64_t slots = (int64_t)RRIN_WINOCP_BPC * ncu;
-  const int64_t grid = tiles < slots ? tiles : slots;
-  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256), lds, st, a);
-  return hip_code(hipGetLastError());
-}
-
 template <int EPI, int CT, int NT>
 static int launch_winoc_k(const ConvH8Args& a, hipStream_t st) {
   auto k = conv3x3_winoc_kernel<EPI, CT, NT>;
@@ -866,34 +482,9 @@ static int winoc_cob_group(const ConvH8Args& a, int bm) {
   return g;
 }
 
-#ifndef RRIN_WINOCP_MIN_WALK
-#define RRIN_WINOCP_MIN_WALK 2
-#endif
-int launch_winoc(const ConvH8Args& a, int epi, int ct, bool persistent, hipStream_t st) {
+int launch_winoc(const ConvH8Args& a, int epi, int ct, hipStream_t st) {
   ConvH8Args b = a;
   b.cob_group = winoc_cob_group(a, 32 * ct);
-  // the persistent form (kind 12: ct 2) needs 2+ chunks, 32-bit byte offsets within an image of
-  // every output view, and 2+ pixels each way for the replicate epilogue; and it pays only where
-  // workgroups walk tiles: from RRIN_WINOCP_MIN_WALK tiles per workgroup slot (two per CU) on
-  // average (a grid of 1.1 tiles per slot -- the 720p level-4 convs -- ran 26 % slower, its few
-  // two-tile workgroups serialising the tail).  Otherwise kind 6: the same bits.
-  const int64_t lim = (int64_t)1 << 31;
-  const int ncu = winoc_cus(st);
-  const int64_t tiles = (int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n;
-  const bool fits = a.nchunks >= 2 && a.dst_img * 16 < lim && (!a.pool_hi || a.pool_img * 16 < lim) &&
-                    (epi != RRIN_EPI_SUBPIXEL || (int64_t)(a.cout >> 2) * a.ring * 4 < lim) &&
-                    (epi != RRIN_EPI_LEAKY_REP || (a.h >= 2 && a.w >= 2)) &&
-                    tiles >= (int64_t)RRIN_WINOCP_MIN_WALK * RRIN_WINOCP_BPC * ncu;
-  if (ct == 2 && persistent && fits) {
-    switch (epi) {
-      case RRIN_EPI_LINEAR: return launch_winocp_k<RRIN_EPI_LINEAR>(b, ncu, st);
-      case RRIN_EPI_LEAKY: return launch_winocp_k<RRIN_EPI_LEAKY>(b, ncu, st);
-      case RRIN_EPI_LEAKY_POOL: return launch_winocp_k<RRIN_EPI_LEAKY_POOL>(b, ncu, st);
-      case RRIN_EPI_LEAKY_REP: return launch_winocp_k<RRIN_EPI_LEAKY_REP>(b, ncu, st);
-      case RRIN_EPI_SUBPIXEL: return launch_winocp_k<RRIN_EPI_SUBPIXEL>(b, ncu, st);
-    }
-    return RRIN_E_ARG;
-  }
   return ct == 2 ? launch_winoc_e<2, 1>(b, epi, st) : launch_winoc_e<1, 2>(b, epi, st);
 }
 

@@ -80,9 +80,9 @@ struct WinoH {
 };
 static_assert(WinoH<1>::LDS == kWinoCLds1 && WinoH<2>::LDS == kWinoCLds2, "LDS sizes (common.hpp)");
 
-// NT 1 (kind 6 at fp16): 128 accumulator registers, two blocks per CU.  NT 2 (kind 9): TH 8, each
-// U record on 2 patch tiles (half the U loads per MFMA), 256 accumulators (AGPRs): one block of
-// 4 waves per CU, one wave per SIMD
+// NT 1 (kind 6 at fp16, the one the library launches): 128 accumulator registers, two blocks per
+// CU.  (NT 2, round 5's kind 9 -- each U record on 2 patch tiles, one wave per SIMD -- ran 1.2-2.3x
+// kind 6's time per conv and was removed in round 6 with the other rejected kinds)
 template <int EPI, int NT>
 __global__ __launch_bounds__(256, NT == 1 ? 2 : 1) void conv3x3_winoh_kernel(ConvH8Args a) {
   using G = WinoH<NT>;
@@ -411,726 +411,6 @@ __global__ __launch_bounds__(256, NT == 1 ? 2 : 1) void conv3x3_winoh_kernel(Con
   if (bad && a.status) *a.status = 1;
 }
 
-#ifdef RRIN_LAB  // kind 13: 1.0-1.3x kind 6's time per conv, lab library only
-// ---- kind 13: the kind-6 tile on two patch tiles per workgroup, U shared through LDS.  At fp16
-// the kind-6 U stream (one 16-B U record per lane and MFMA, from L2 into registers) is its
-// structural limit: at the f16 MFMA rate a CU would pull 128 B/clk of U, twice its L2 share
-// (DESIGN.md §5e).  Here 8 waves (two per SIMD, one workgroup per CU) cover TH 8 = two patch
-// tiles: wave w owns B^T row w & 3 of patch tile w >> 2, so waves w and w + 4 use the same U
-// records; the chunk's U (2048 records) is staged by LDS-DMA with the raw tile (3 stages) and
-// each U record is fetched from L2 once per 64 patches instead of once per 32.  Same U, same
-// transforms, same accumulation and epilogue order as kind 6: bitwise its outputs.
-struct WinoHL {
-  static constexpr int NTH = 512;
-  static constexpr int TH = 8;
-  static constexpr int RG = (TH + 2) * 34;            // raw records per group
-  static constexpr int RAW = 2 * RG;                  // per chunk (two groups)
-  static constexpr int PR = (RAW + NTH - 1) / NTH;    // raw DMA pieces per thread
-  static constexpr int RAWS = PR * NTH;               // raw records per stage (the tail: dummy)
-  static constexpr int UREC = 16 * 2 * 64;            // U records per chunk: [point][hh][64 co]
-  static constexpr int PU = UREC / NTH;               // U DMA pieces per thread
-  static constexpr int STAGE = RAWS + UREC;
-  static constexpr int NS = 3;
-  static constexpr int XREC = 2 * 4 * 8 * 64;         // output-transform exchange, one co tile
-  static constexpr size_t LDS = (size_t)(NS * STAGE > XREC ? NS * STAGE : XREC) * 16;
-};
-static_assert(WinoHL::LDS == kWinoHLLds, "LDS size (common.hpp)");
-static_assert(WinoHL::UREC % WinoHL::NTH == 0, "whole U pieces");
-
-template <int EPI>
-__global__ __launch_bounds__(512, 1) void conv3x3_winohl_kernel(ConvH8Args a) {
-  using G = WinoHL;
-  constexpr int CT = 2, BM = 64, TH = G::TH, RG = G::RG, STAGE = G::STAGE, PR = G::PR, PU = G::PU;
-  extern __shared__ __attribute__((aligned(16))) uint4 smem4[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int yw = wv & 3, ntw = wv >> 2;  // B^T row, patch tile of this wave
-  const int j = lane & 31, hh = lane >> 5;
-  int bid;
-  {  // XCD-aware bijective remap: an XCD's workgroups are consecutive tiles
-    const int nwg = gridDim.x, q = nwg >> 3, r = nwg & 7;
-    const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
-    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
-  }
-  const int ntiles = a.co_blocks * a.tiles_x * a.tiles_y * a.n;
-  if (bid >= ntiles) return;
-  const int nch = a.nchunks;
-  int cob, x0, y0, img;
-  {  // kind 6's workgroup order (co-block groups whose U fits an XCD's L2)
-    const int cpg = a.cob_group > 0 ? a.cob_group : a.co_blocks;
-    const int gsz = cpg * (ntiles / a.co_blocks);
-    const int g = bid / gsz;
-    const int r = bid - g * gsz;
-    const int cg = min(cpg, a.co_blocks - g * cpg);
-    cob = g * cpg + r % cg;
-    int t = r / cg;
-    x0 = (t % a.tiles_x) * 32;
-    t /= a.tiles_x;
-    y0 = (t % a.tiles_y) * TH;
-    img = t / a.tiles_y;
-  }
-
-  // ---- raw tile (rows y0 - 1 .. y0 + TH, cols x0 - 1 .. x0 + 32 of the chunk's two groups) and
-  // the chunk's U, both by LDS-DMA into stage s
-  const uint4* tbase = a.src_hi + (int64_t)img * a.src_img + (int64_t)y0 * a.src_wp + x0 + (kH8PadLeft - 1);
-  uint32_t voff[PR];
-#pragma unroll
-  for (int it = 0; it < PR; ++it) {
-    const int idx = tid + G::NTH * it;
-    const int g = idx >= RG ? 1 : 0;
-    const int rem = idx < G::RAW ? idx - g * RG : 0;
-    const int r = rem / 34, pos = rem - r * 34;
-    const int col = pos < 17 ? 2 * pos : 2 * (pos - 17) + 1;
-    voff[it] = (uint32_t)((idx < G::RAW ? (int64_t)g * a.src_gp : 0) + (int64_t)r * a.src_wp + col) * 16u;
-  }
-  const int64_t chunk_stride = 2 * a.src_gp;
-  const uint4* ubase = a.w_hi + (int64_t)cob * nch * G::UREC;
-  auto issue_chunk = [&](int c, int s) {
-    const auto rs = wh_rsrc(tbase + c * chunk_stride);
-#pragma unroll
-    for (int it = 0; it < PR; ++it) wh_dma16(rs, smem4 + s * STAGE + G::NTH * it + 64 * wv, voff[it]);
-    const auto us = wh_rsrc(ubase + (int64_t)c * G::UREC);
-#pragma unroll
-    for (int it = 0; it < PU; ++it)
-      wh_dma16(us, smem4 + s * STAGE + G::RAWS + G::NTH * it + 64 * wv, (uint32_t)(tid + G::NTH * it) * 16u);
-  };
-
-  // ---- B operands (kind 6's lane mapping within this wave's patch tile)
-  const int jx = (j + 12 * (j >> 4)) & 15;
-  const int ra = yw == 0 ? 0 : (yw == 2 ? 2 : 1);
-  const int rb = yw == 0 ? 2 : (yw == 1 ? 2 : (yw == 2 ? 1 : 3));
-  const _Float16 sgh = yw == 1 ? (_Float16)1.0f : (_Float16)-1.0f;
-  const whx8 sg = {sgh, sgh, sgh, sgh, sgh, sgh, sgh, sgh};
-  unsigned m1w = 0xBC00BC00u;
-  asm volatile("" : "+v"(m1w));
-  const whx8 m1 = __builtin_bit_cast(whx8, make_uint4(m1w, m1w, m1w, m1w));
-  int pcol[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) pcol[k] = hh * RG + (2 * (j >> 4)) * 34 + wh_col(2 * jx + k);
-  const int oa = ra * 34 + ntw * 4 * 34, ob = rb * 34 + ntw * 4 * 34;
-  // U record of point x (of this wave's B^T row), co tile t, lane (j, hh) in a stage
-  const int ubase_l = G::RAWS + ((4 * yw) * 2 + hh) * 64 + j;
-
-  wfx16 acc[CT][4];
-#pragma unroll
-  for (int t = 0; t < CT; ++t)
-#pragma unroll
-    for (int x = 0; x < 4; ++x) acc[t][x] = wfx16{};
-  whx8 u[CT][4];
-  whx8 v[4];
-  whx8 d[8];
-  auto read_raw = [&](int s) {
-    const uint4* rw = smem4 + s * STAGE;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      d[2 * k] = __builtin_bit_cast(whx8, rw[oa + pcol[k]]);
-      d[2 * k + 1] = __builtin_bit_cast(whx8, rw[ob + pcol[k]]);
-    }
-  };
-  auto read_u = [&](int s) {
-    const uint4* us = smem4 + s * STAGE + ubase_l;
-#pragma unroll
-    for (int x = 0; x < 4; ++x)
-#pragma unroll
-      for (int t = 0; t < CT; ++t) u[t][x] = __builtin_bit_cast(whx8, us[x * 128 + t * 32]);
-  };
-  auto transform = [&]() {
-    whx8 tr[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) tr[k] = __builtin_elementwise_fma(sg, d[2 * k + 1], d[2 * k]);
-    v[0] = __builtin_elementwise_fma(m1, tr[2], tr[0]);
-    v[1] = tr[1] + tr[2];
-    v[2] = __builtin_elementwise_fma(m1, tr[1], tr[2]);
-    v[3] = __builtin_elementwise_fma(m1, tr[3], tr[1]);
-  };
-  auto mfma_point = [&](int x) {
-#pragma unroll
-    for (int t = 0; t < CT; ++t) acc[t][x] = __builtin_amdgcn_mfma_f32_32x32x16_f16(u[t][x], v[x], acc[t][x], 0, 0, 0);
-  };
-  auto bar = [&]() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
-  auto fence = [&]() { __builtin_amdgcn_sched_barrier(0); };
-
-  // chunk c (its U in u, its B operands in v): points 0-2; the wait for chunk c + 1's DMA (the
-  // only VMEM in flight); the barrier; chunk c + 2's DMA; chunk c + 1's window reads; point 3;
-  // chunk c + 1's transform and U reads
-  auto chunk = [&](int c, int s, const bool more) {
-#pragma unroll
-    for (int x = 0; x < 3; ++x) mfma_point(x);
-    fence();
-    const int s1 = s == 2 ? 0 : s + 1;
-    if (more) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      bar();
-      if (c + 2 < nch) issue_chunk(c + 2, s == 0 ? 2 : s - 1);
-      read_raw(s1);
-    }
-    fence();
-    mfma_point(3);
-    fence();
-    if (more) {
-      transform();
-      read_u(s1);
-    }
-  };
-
-  issue_chunk(0, 0);
-  if (nch > 1) {
-    issue_chunk(1, 1);
-    RRIN_VMWAIT(PR + PU, 0);
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  bar();
-  read_raw(0);
-  transform();
-  read_u(0);
-  {
-    int s = 0;
-    for (int c = 0; c + 1 < nch; ++c) {
-      chunk(c, s, true);
-      s = s == 2 ? 0 : s + 1;
-    }
-    chunk(nch - 1, s, false);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  float bsv[CT][16];
-#pragma unroll
-  for (int t = 0; t < CT; ++t)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) bsv[t][i] = a.bias[(CT * cob + t) * 32 + 8 * (i >> 2) + 4 * hh + (i & 3)];
-  __syncthreads();  // every read of the stages done before the exchange reuses the LDS
-
-  // ---- kind 6's output transform, exchanged per patch tile among its four waves
-  wfx4* X = reinterpret_cast<wfx4*>(smem4);
-  const int r = yw & 1, cc = yw >> 1;
-  uint4* dst = a.dst_hi + (int64_t)img * a.dst_img;
-  const float isc = a.inv_wscale;
-  bool bad = false;
-  auto store4 = [&](uint4* base, int64_t rec, const float* vv) {
-    bad |= !(fmaxf(fmaxf(fabsf(vv[0]), fabsf(vv[1])), fmaxf(fabsf(vv[2]), fabsf(vv[3]))) <= kWinoHF16Max);
-    reinterpret_cast<uint2*>(base + rec)[hh] = wh_pack4(vv);
-  };
-#pragma unroll
-  for (int t = 0; t < CT; ++t) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      wfx4 g;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int vi = 4 * k + e, c2 = vi >> 4, i = vi & 15;
-        const float q0 = acc[t][0][i], q1 = acc[t][1][i], q2 = acc[t][2][i], q3 = acc[t][3][i];
-        g[e] = c2 == 0 ? (q0 + q1) + q2 : (q1 - q2) - q3;
-      }
-      X[((ntw * 4 + yw) * 8 + k) * 64 + lane] = g;
-    }
-    __syncthreads();
-    float yv[16];
-#pragma unroll
-    for (int k4 = 0; k4 < 4; ++k4) {
-      const int k = 4 * cc + k4;
-      const wfx4 q0 = X[((ntw * 4 + 0) * 8 + k) * 64 + lane];
-      const wfx4 q1 = X[((ntw * 4 + 1) * 8 + k) * 64 + lane];
-      const wfx4 q2 = X[((ntw * 4 + 2) * 8 + k) * 64 + lane];
-      const wfx4 q3 = X[((ntw * 4 + 3) * 8 + k) * 64 + lane];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) yv[4 * k4 + e] = r == 0 ? (q0[e] + q1[e]) + q2[e] : (q1[e] - q2[e]) - q3[e];
-    }
-    __syncthreads();  // X is rewritten by the next co tile / the pool exchange
-    const int cobe = CT * cob + t;
-    const int pr = 2 * ntw + (j >> 4);
-    const int y = y0 + 2 * pr + r, x = x0 + 2 * jx + cc;
-    if constexpr (EPI == RRIN_EPI_SUBPIXEL) {
-      const int HH = 2 * a.h, WW = 2 * a.w, creal = a.cout >> 2;
-      if (cobe * 32 < a.cout && y < a.h && x < a.w) {
-#pragma unroll
-        for (int qq = 0; qq < 4; ++qq) {
-          const int Y = 2 * y + (qq >> 1), XX = 2 * x + (qq & 1);
-          const int64_t ri = ring_index(Y, XX, HH, WW);
-          if (ri >= 0) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-              a.edge[((int64_t)img * creal + cobe * 8 + 4 * hh + e) * a.ring + ri] = yv[4 * qq + e] * isc;
-          } else {
-            float vv[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) vv[e] = yv[4 * qq + e] * isc + bsv[t][4 * qq + e];
-            store4(dst, (int64_t)cobe * a.dst_gp + (int64_t)(Y + 1) * a.dst_wp + XX + kH8PadLeft, vv);
-          }
-        }
-      }
-    } else {
-      float vv[16];
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        float tv = yv[i] * isc + bsv[t][i];
-        if constexpr (EPI != RRIN_EPI_LINEAR) tv = leaky(tv, a.slope);
-        vv[i] = tv;
-      }
-#pragma unroll
-      for (int qq = 0; qq < 4; ++qq) {
-        if (cobe * 32 + 8 * qq < a.cout && y < a.h && x < a.w) {
-          const int64_t rec = (int64_t)(cobe * 4 + qq) * a.dst_gp + (int64_t)(y + 1) * a.dst_wp + x + kH8PadLeft;
-          store4(dst, rec, &vv[4 * qq]);
-          if constexpr (EPI == RRIN_EPI_LEAKY_REP) {
-            const int dy0 = y == 0 ? -1 : 0, dy1 = y == a.h - 1 ? 1 : 0;
-            const int dx0 = x == 0 ? -1 : 0, dx1 = x == a.w - 1 ? 1 : 0;
-            for (int dy = dy0; dy <= dy1; ++dy)
-              for (int dx = dx0; dx <= dx1; ++dx)
-                if (dy | dx) store4(dst, rec + (int64_t)dy * a.dst_wp + dx, &vv[4 * qq]);
-          }
-        }
-      }
-      if constexpr (EPI == RRIN_EPI_LEAKY_POOL) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          wfx4 g;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) g[e] = vv[4 * k + e];
-          X[((ntw * 4 + yw) * 4 + k) * 64 + lane] = g;
-        }
-        __syncthreads();
-        if (yw == 0) {
-          const int xp = x0 + 2 * jx, yp = y0 + 2 * pr;
-          uint4* pdst = a.pool_hi + (int64_t)img * a.pool_img;
-#pragma unroll
-          for (int qq = 0; qq < 4; ++qq) {
-            const wfx4 y00 = X[((ntw * 4 + 0) * 4 + qq) * 64 + lane];
-            const wfx4 y10 = X[((ntw * 4 + 1) * 4 + qq) * 64 + lane];
-            const wfx4 y01 = X[((ntw * 4 + 2) * 4 + qq) * 64 + lane];
-            const wfx4 y11 = X[((ntw * 4 + 3) * 4 + qq) * 64 + lane];
-            if (cobe * 32 + 8 * qq < a.cout && yp < a.h && xp < a.w) {
-              float s4[4];
-#pragma unroll
-              for (int e = 0; e < 4; ++e) s4[e] = 0.25f * ((y00[e] + y10[e]) + (y01[e] + y11[e]));
-              store4(pdst, (int64_t)(cobe * 4 + qq) * a.pool_gp + (int64_t)(yp / 2 + 1) * a.pool_wp + xp / 2 + kH8PadLeft,
-                     s4);
-            }
-          }
-        }
-        __syncthreads();
-      }
-    }
-  }
-  if (bad && a.status) *a.status = 1;
-}
-
-template <int EPI>
-static int launch_winohl_k(const ConvH8Args& a, hipStream_t st) {
-  auto k = conv3x3_winohl_kernel<EPI>;
-  static LdsAttr attr;
-  if (int e = attr.ensure((const void*)k, (int)WinoHL::LDS, st)) return e;
-  const int64_t grid = (int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n;
-  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(WinoHL::NTH), WinoHL::LDS, st, a);
-  return hip_code(hipGetLastError());
-}
-#endif  // RRIN_LAB (kind 13)
-
-#ifdef RRIN_LAB  // kinds 9-11 (one block per CU, persistent grids): lab library only
-// ---- persistent form (kinds 10 / 11): a workgroup walks tiles bid, bid + grid, ... and its
-// chunk pipeline runs on across tile boundaries.  At fp16 a tile's MFMAs take a few us, about
-// what its prologue (raw tile and U from memory) and epilogue (output-transform exchange,
-// stores) cost, so the one-tile-per-workgroup grid loses most of its time there:
-// here the next tile's chunk 0 (raw tile, U) and chunk 1 (raw tile) are loaded during the
-// current tile's last chunks, and its B operands transformed, before the epilogue runs.  The
-// exchange area is separate from the raw stages; the epilogue's barriers are bare (no vmcnt
-// drain); every epilogue store is an unconditional buffer store (an out-of-image position gets
-// an offset past the buffer: the store is dropped).  The first chunk after an epilogue waits for
-// its raw tile by counting the younger loads only: loads complete in order among themselves, but
-// not in order with stores (LLVM's waitcnt pass treats mixed pending reads and writes the same
-// way), so a count that included the epilogue's stores could pass early.  The bias
-// of a tile is staged into LDS by LDS-DMA at the tile's start.  Same arithmetic, in the same
-// order, as conv3x3_winoh_kernel: the outputs are bitwise those of kinds 6 / 9.
-template <int EPI, int NT>
-struct WinoHP {
-  using G = WinoH<NT>;
-  static constexpr int XOFF = G::NS * G::STAGE;        // exchange area (records) after the raw stages
-  static constexpr int BOFF = XOFF + G::XREC;          // bias areas: 2 x 64 records (16 used), by tile parity
-  static constexpr size_t LDS = (size_t)(BOFF + 128) * 16;
-  // buffer stores per wave and tile epilogue, per (co tile, N tile, 8-channel block)
-  static constexpr int PER = EPI == RRIN_EPI_LEAKY_REP ? 4
-                             : EPI == RRIN_EPI_LEAKY_POOL ? 2
-                             : EPI == RRIN_EPI_SUBPIXEL  ? 5
-                                                         : 1;
-  static constexpr int S = 2 * NT * 4 * PER;
-};
-static_assert(WinoHP<RRIN_EPI_LEAKY, 1>::LDS <= 80 * 1024, "two persistent BM 64 x TH 4 blocks per CU");
-
-template <int EPI, int NT>
-__global__ __launch_bounds__(256, NT == 1 ? 2 : 1) void conv3x3_winohp_kernel(ConvH8Args a) {
-  using G = WinoH<NT>;
-  using PP = WinoHP<EPI, NT>;
-  constexpr int CT = 2, BM = 64, TH = G::TH, RG = G::RG, STAGE = G::STAGE, P = G::PIECES;
-  constexpr uint32_t kOOB = 0x80000000u;  // buffer offset past num_records: the store is dropped
-  extern __shared__ __attribute__((aligned(16))) uint4 smem4[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int yw = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int j = lane & 31, hh = lane >> 5;
-  const int grid = gridDim.x;
-  int bid;
-  {  // XCD-aware bijective remap: an XCD's workgroups are consecutive tiles at every step
-    const int q = grid >> 3, r = grid & 7;
-    const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
-    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
-  }
-  const int ntiles = a.co_blocks * a.tiles_x * a.tiles_y * a.n;
-  if (bid >= ntiles) return;
-  const int nch = a.nchunks;  // >= 2 (launch_winohp)
-  struct Tile {
-    int cob, x0, y0, img;
-  };
-  auto coords = [&](int t) {
-    Tile o;
-    const int cpg = a.cob_group > 0 ? a.cob_group : a.co_blocks;
-    const int gsz = cpg * (ntiles / a.co_blocks);
-    const int g = t / gsz;
-    const int r = t - g * gsz;
-    const int cg = min(cpg, a.co_blocks - g * cpg);
-    o.cob = g * cpg + r % cg;
-    int u = r / cg;
-    o.x0 = (u % a.tiles_x) * 32;
-    u /= a.tiles_x;
-    o.y0 = (u % a.tiles_y) * TH;
-    o.img = u / a.tiles_y;
-    return o;
-  };
-  auto tile_base = [&](const Tile& t) {
-    return a.src_hi + (int64_t)t.img * a.src_img + (int64_t)t.y0 * a.src_wp + t.x0 + (kH8PadLeft - 1);
-  };
-  auto u_base = [&](const Tile& t) { return wh_rsrc(a.w_hi + (int64_t)t.cob * nch * 32 * BM); };
-
-  uint32_t voff[P];
-#pragma unroll
-  for (int it = 0; it < P; ++it) {
-    const int idx = tid + 256 * it;
-    const int g = idx >= RG ? 1 : 0;
-    const int rem = idx < G::RAW ? idx - g * RG : 0;
-    const int r = rem / 34, pos = rem - r * 34;
-    const int col = pos < 17 ? 2 * pos : 2 * (pos - 17) + 1;
-    voff[it] = (uint32_t)((idx < G::RAW ? (int64_t)g * a.src_gp : 0) + (int64_t)r * a.src_wp + col) * 16u;
-  }
-  const int64_t chunk_stride = 2 * a.src_gp;
-  auto issue_raw_at = [&](const uint4* base, int s) {
-    const auto rs = wh_rsrc(base);
-#pragma unroll
-    for (int it = 0; it < P; ++it) wh_dma16(rs, smem4 + s * STAGE + 256 * it + 64 * yw, voff[it]);
-  };
-  // the tile's 64 biases -> bias area tp of LDS (every wave loads the same 16 records: one VMEM op
-  // each); two areas by tile parity, so a slow wave may still read the previous tile's
-  auto issue_bias = [&](const Tile& t, int tp) {
-    const auto rs = wh_rsrc(a.bias + (int64_t)t.cob * BM);
-    wh_dma16(rs, smem4 + PP::BOFF + 64 * tp, (uint32_t)(lane & 15) * 16u);
-  };
-  const uint32_t uvoff = (uint32_t)(hh * BM + j) * 16u;
-  auto load_u = [&](__amdgpu_buffer_rsrc_t ur, int c, int x, int t) {
-    const int soff = c * (32 * BM * 16) + (4 * yw + (x & 2)) * (2 * BM * 16);
-    const int imm = (x & 1) * 2048 + t * 512;
-    return wh_load16(ur, uvoff + imm, soff);
-  };
-
-  const int jx = (j + 12 * (j >> 4)) & 15;
-  const int ra = yw == 0 ? 0 : (yw == 2 ? 2 : 1);
-  const int rb = yw == 0 ? 2 : (yw == 1 ? 2 : (yw == 2 ? 1 : 3));
-  const _Float16 sgh = yw == 1 ? (_Float16)1.0f : (_Float16)-1.0f;
-  const whx8 sg = {sgh, sgh, sgh, sgh, sgh, sgh, sgh, sgh};
-  unsigned m1w = 0xBC00BC00u;
-  asm volatile("" : "+v"(m1w));
-  const whx8 m1 = __builtin_bit_cast(whx8, make_uint4(m1w, m1w, m1w, m1w));
-  int pcol[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) pcol[k] = hh * RG + (2 * (j >> 4)) * 34 + wh_col(2 * jx + k);
-  const int oa = ra * 34, ob = rb * 34;
-
-  wfx16 acc[CT][NT][4];
-  whx8 u[CT][4];
-  whx8 v[NT][4];
-  whx8 d[NT][8];
-  auto zero_acc = [&]() {
-#pragma unroll
-    for (int t = 0; t < CT; ++t)
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-        for (int x = 0; x < 4; ++x) acc[t][nt][x] = wfx16{};
-  };
-  auto read_raw = [&](int s, int nt) {
-    const uint4* rw = smem4 + s * STAGE + nt * 4 * 34;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      d[nt][2 * k] = __builtin_bit_cast(whx8, rw[oa + pcol[k]]);
-      d[nt][2 * k + 1] = __builtin_bit_cast(whx8, rw[ob + pcol[k]]);
-    }
-  };
-  auto transform = [&](int nt) {
-    whx8 tr[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) tr[k] = __builtin_elementwise_fma(sg, d[nt][2 * k + 1], d[nt][2 * k]);
-    v[nt][0] = __builtin_elementwise_fma(m1, tr[2], tr[0]);
-    v[nt][1] = tr[1] + tr[2];
-    v[nt][2] = __builtin_elementwise_fma(m1, tr[1], tr[2]);
-    v[nt][3] = __builtin_elementwise_fma(m1, tr[3], tr[1]);
-  };
-  auto mfma_point = [&](int x, int nt) {
-#pragma unroll
-    for (int t = 0; t < CT; ++t)
-      acc[t][nt][x] = __builtin_amdgcn_mfma_f32_32x32x16_f16(u[t][x], v[nt][x], acc[t][nt][x], 0, 0, 0);
-  };
-  auto bar = [&]() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
-  auto fence = [&]() { __builtin_amdgcn_sched_barrier(0); };
-
-  // the tile being computed and the workgroup's next tile
-  int tile = bid;
-  Tile cur = coords(tile);
-  bool has_next = tile + grid < ntiles;
-  Tile nxt = has_next ? coords(tile + grid) : cur;
-  auto ur = u_base(cur), urn = u_base(nxt);
-  const uint4* tb = tile_base(cur);
-  const uint4* tbn = tile_base(nxt);
-
-  // Chunk c of the current tile (U(c) in u, its B operands in v, stage s): conv3x3_winoh_kernel's
-  // chunk.  Its successor is chunk c + 1 of this tile or (LAST, a tile's last chunk) chunk 0 of
-  // the next tile; raw(c + 2) is this tile's chunk c + 2 or the next tile's chunk c + 2 - nch.
-  // Without a next tile the loads re-read this tile's (a dummy raw tile into the free stage, U
-  // of chunk 0 into registers no MFMA reads again), so every chunk issues the same VMEM.
-  // FIRST (chunk 0 of a tile): the epilogue's stores and one bias DMA sit between raw(c + 1) and
-  // this chunk's loads (the first tile's prologue issues the same bias DMA).
-  // A tile's last chunk does not transform: the next tile's chunk 0 is read and transformed
-  // after the epilogue, so its B operands are not live across it.
-  auto chunk = [&](int c, int s, const bool first, const bool last) {
-    const auto un = last ? urn : ur;
-    const int cn = last ? 0 : c + 1;
-#pragma unroll
-    for (int x = 0; x < 3; ++x) {
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) mfma_point(x, nt);
-#pragma unroll
-      for (int t = 0; t < CT; ++t) u[t][x] = load_u(un, cn, x, t);
-      fence();
-    }
-    if (first) {
-      // loads complete in order among themselves, stores not in order with them: the younger
-      // LOADS of raw(c + 1) are U(c) pt 3, the bias DMA and U(c + 1) pts 0-2 (the epilogue's
-      // stores in between are not counted -- a count that included them could pass with the
-      // raw tile still in flight once the stores had completed)
-      RRIN_VMWAIT(1, 4 * CT);
-    } else {
-      RRIN_VMWAIT(0, 4 * CT);
-    }
-    bar();
-    const int c2 = c + 2;
-    const uint4* rp = c2 < nch ? tb + c2 * chunk_stride : tbn + (c2 - nch) * chunk_stride;
-    issue_raw_at(rp, s == 0 ? 2 : s - 1);
-    const int s1 = s == 2 ? 0 : s + 1;
-    if (!last) {
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) read_raw(s1, nt);
-    }
-    fence();
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) mfma_point(3, nt);
-    fence();
-    if (!last) {
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) transform(nt);
-    }
-#pragma unroll
-    for (int t = 0; t < CT; ++t) u[t][3] = load_u(un, cn, 3, t);
-  };
-
-  // prologue (first tile): bias, raw(0), U(0) pts 0-2, raw(1), U(0) pt 3; wait for raw(0); the
-  // bias DMA again, so that chunk 0 waits as after an epilogue
-  int tp = 0;
-  issue_bias(cur, tp);
-  issue_raw_at(tb, 0);
-  vm_fence();
-#pragma unroll
-  for (int x = 0; x < 3; ++x)
-#pragma unroll
-    for (int t = 0; t < CT; ++t) u[t][x] = load_u(ur, 0, x, t);
-  vm_fence();
-  issue_raw_at(tb + chunk_stride, 1);
-  vm_fence();
-#pragma unroll
-  for (int t = 0; t < CT; ++t) u[t][3] = load_u(ur, 0, 3, t);
-  vm_fence();
-  RRIN_VMWAIT(P, 4 * CT);
-  bar();
-  issue_bias(cur, tp);  // again, in the after-epilogue position: chunk 0 waits as after an epilogue
-#pragma unroll
-  for (int nt = 0; nt < NT; ++nt) {
-    read_raw(0, nt);
-    transform(nt);
-  }
-
-  wfx4* X = reinterpret_cast<wfx4*>(smem4 + PP::XOFF);
-  const int r = yw & 1, cc = yw >> 1;
-  const float isc = a.inv_wscale;
-  bool bad = false;
-  // one 8-B half record (4 channels) at byte offset off of rs (off = kOOB: dropped)
-  auto st8 = [&](__amdgpu_buffer_rsrc_t rs, uint32_t off, const float* vv, bool valid) {
-    bad |= valid && !(fmaxf(fmaxf(fabsf(vv[0]), fabsf(vv[1])), fmaxf(fabsf(vv[2]), fabsf(vv[3]))) <= kWinoHF16Max);
-    const uint2 pk = wh_pack4(vv);
-    __builtin_amdgcn_raw_buffer_store_b64((unsigned __attribute__((ext_vector_type(2)))){pk.x, pk.y}, rs,
-                                          valid ? off : kOOB, 0, 0);
-  };
-  int s = 0;
-  for (;;) {
-    chunk(0, s, true, false);  // nch >= 2
-    s = s == 2 ? 0 : s + 1;
-    for (int c = 1; c + 1 < nch; ++c) {
-      chunk(c, s, false, false);
-      s = s == 2 ? 0 : s + 1;
-    }
-    chunk(nch - 1, s, false, true);
-    s = s == 2 ? 0 : s + 1;
-
-    // ---- epilogue of tile cur (kind 6's output transform and order), stores unconditional
-    const auto drs = wh_rsrc(a.dst_hi + (int64_t)cur.img * a.dst_img);
-#pragma unroll
-    for (int t = 0; t < CT; ++t) {
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          wfx4 g;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int vi = 4 * k + e, c2 = vi >> 4, i = vi & 15;
-            const float q0 = acc[t][nt][0][i], q1 = acc[t][nt][1][i], q2 = acc[t][nt][2][i], q3 = acc[t][nt][3][i];
-            g[e] = c2 == 0 ? (q0 + q1) + q2 : (q1 - q2) - q3;
-          }
-          X[((nt * 4 + yw) * 8 + k) * 64 + lane] = g;
-        }
-      bar();
-      float yv[NT][16];
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-        for (int k4 = 0; k4 < 4; ++k4) {
-          const int k = 4 * cc + k4;
-          const wfx4 q0 = X[((nt * 4 + 0) * 8 + k) * 64 + lane];
-          const wfx4 q1 = X[((nt * 4 + 1) * 8 + k) * 64 + lane];
-          const wfx4 q2 = X[((nt * 4 + 2) * 8 + k) * 64 + lane];
-          const wfx4 q3 = X[((nt * 4 + 3) * 8 + k) * 64 + lane];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) yv[nt][4 * k4 + e] = r == 0 ? (q0[e] + q1[e]) + q2[e] : (q1[e] - q2[e]) - q3[e];
-        }
-      bar();  // X is rewritten by the next co tile / the pool exchange
-      // bias of lane half hh, 8-channel block qq of this co tile: 4 floats in LDS
-      const wfx4* Bs = reinterpret_cast<const wfx4*>(smem4 + PP::BOFF + 64 * tp);
-      auto bias4 = [&](int qq) { return Bs[t * 8 + 2 * qq + hh]; };
-      const int cobe = CT * cur.cob + t;
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        const int pr = 2 * nt + (j >> 4);
-        const int y = cur.y0 + 2 * pr + r, x = cur.x0 + 2 * jx + cc;
-        const bool in = y < a.h && x < a.w;
-        if constexpr (EPI == RRIN_EPI_SUBPIXEL) {
-          const int HH = 2 * a.h, WW = 2 * a.w, creal = a.cout >> 2;
-          const bool blk = cobe * 32 < a.cout && in;
-          const auto ers = wh_rsrc(a.edge + (int64_t)cur.img * creal * a.ring);
-#pragma unroll
-          for (int qq = 0; qq < 4; ++qq) {
-            const int Y = 2 * y + (qq >> 1), XX = 2 * x + (qq & 1);
-            const int64_t ri = ring_index(Y, XX, HH, WW);
-            const bool ring = blk && ri >= 0;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const uint32_t eo = (uint32_t)(((int64_t)(cobe * 8 + 4 * hh + e) * a.ring + (ring ? ri : 0)) * 4);
-              __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(yv[nt][4 * qq + e] * isc), ers, ring ? eo : kOOB,
-                                                    0, 0);
-            }
-            float vv[4];
-            const wfx4 bq = bias4(qq);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) vv[e] = yv[nt][4 * qq + e] * isc + bq[e];
-            const bool inner = blk && ri < 0;
-            const int64_t rec = (int64_t)cobe * a.dst_gp + (int64_t)(Y + 1) * a.dst_wp + XX + kH8PadLeft;
-            st8(drs, (uint32_t)(rec * 16 + hh * 8), vv, inner);
-          }
-        } else {
-          float vv[16];
-#pragma unroll
-          for (int qq = 0; qq < 4; ++qq) {
-            const wfx4 bq = bias4(qq);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              float tv = yv[nt][4 * qq + e] * isc + bq[e];
-              if constexpr (EPI != RRIN_EPI_LINEAR) tv = leaky(tv, a.slope);
-              vv[4 * qq + e] = tv;
-            }
-          }
-#pragma unroll
-          for (int qq = 0; qq < 4; ++qq) {
-            const bool ok = cobe * 32 + 8 * qq < a.cout && in;
-            const int64_t rec = (int64_t)(cobe * 4 + qq) * a.dst_gp + (int64_t)(y + 1) * a.dst_wp + x + kH8PadLeft;
-            st8(drs, (uint32_t)(rec * 16 + hh * 8), &vv[4 * qq], ok);
-            if constexpr (EPI == RRIN_EPI_LEAKY_REP) {
-              // the ring replicas of an edge pixel (h, w >= 2: one row side, one column side)
-              const int dy = y == 0 ? -1 : (y == a.h - 1 ? 1 : 0);
-              const int dx = x == 0 ? -1 : (x == a.w - 1 ? 1 : 0);
-              st8(drs, (uint32_t)((rec + (int64_t)dy * a.dst_wp) * 16 + hh * 8), &vv[4 * qq], ok && dy != 0);
-              st8(drs, (uint32_t)((rec + dx) * 16 + hh * 8), &vv[4 * qq], ok && dx != 0);
-              st8(drs, (uint32_t)((rec + (int64_t)dy * a.dst_wp + dx) * 16 + hh * 8), &vv[4 * qq],
-                  ok && dy != 0 && dx != 0);
-            }
-          }
-          if constexpr (EPI == RRIN_EPI_LEAKY_POOL) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-              wfx4 g;
-#pragma unroll
-              for (int e = 0; e < 4; ++e) g[e] = vv[4 * k + e];
-              X[(yw * 4 + k) * 64 + lane] = g;
-            }
-            bar();
-            // every wave stores (wave 0's values; the other waves' stores are dropped): no
-            // wave-dependent branch around stores
-            const int xp = cur.x0 + 2 * jx, yp = cur.y0 + 2 * pr;
-            const auto prs = wh_rsrc(a.pool_hi + (int64_t)cur.img * a.pool_img);
-#pragma unroll
-            for (int qq = 0; qq < 4; ++qq) {
-              const wfx4 y00 = X[(0 * 4 + qq) * 64 + lane];
-              const wfx4 y10 = X[(1 * 4 + qq) * 64 + lane];
-              const wfx4 y01 = X[(2 * 4 + qq) * 64 + lane];
-              const wfx4 y11 = X[(3 * 4 + qq) * 64 + lane];
-              float s4[4];
-#pragma unroll
-              for (int e = 0; e < 4; ++e) s4[e] = 0.25f * ((y00[e] + y10[e]) + (y01[e] + y11[e]));
-              const bool ok = yw == 0 && cobe * 32 + 8 * qq < a.cout && yp < a.h && xp < a.w;
-              const int64_t rec = (int64_t)(cobe * 4 + qq) * a.pool_gp + (int64_t)(yp / 2 + 1) * a.pool_wp + xp / 2 +
-                                  kH8PadLeft;
-              st8(prs, (uint32_t)(rec * 16 + hh * 8), s4, ok);
-            }
-            bar();
-          }
-        }
-      }
-    }
-    if (!has_next) break;
-    // ---- advance: the next tile's chunk 0 is staged (stage s) and transformed (v), its U(0)
-    // loaded; its chunk 1 is in flight to stage s + 1
-    tile += grid;
-    cur = nxt;
-    ur = urn;
-    tb = tbn;
-    has_next = tile + grid < ntiles;
-    nxt = has_next ? coords(tile + grid) : cur;
-    urn = u_base(nxt);
-    tbn = tile_base(nxt);
-    zero_acc();
-    tp ^= 1;
-    issue_bias(cur, tp);  // lands before the next chunk's wait (AFTER_EPI counts it)
-    // chunk 0's B operands from stage s (staged and made visible during the last chunk)
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-      read_raw(s, nt);
-      transform(nt);
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every LDS-DMA has landed before the workgroup ends
-  if (bad && a.status) *a.status = 1;
-}
-#endif  // RRIN_LAB (conv3x3_winohp_kernel)
 
 template <int EPI, int NT>
 static int launch_winoh_k(const ConvH8Args& a, hipStream_t st) {
@@ -1155,47 +435,6 @@ static int winoh_cob_group(const ConvH8Args& a) {
   return g;
 }
 
-#ifdef RRIN_LAB
-static int winoh_cus(hipStream_t st) {
-  static std::atomic<int> cus[kMaxDevices];
-  const int dev = stream_device(st);
-  int ncu = cus[dev].load(std::memory_order_relaxed);
-  if (ncu <= 0) {
-    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
-    cus[dev].store(ncu, std::memory_order_relaxed);
-  }
-  return ncu;
-}
-
-// persistent workgroups per CU of kind 10 (A/B builds: 1 leaves a slot per CU to the other stream)
-#ifndef RRIN_WINOHP_BPC
-#define RRIN_WINOHP_BPC 2
-#endif
-template <int EPI, int NT>
-static int launch_winohp_k(const ConvH8Args& a, hipStream_t st) {
-  auto k = conv3x3_winohp_kernel<EPI, NT>;
-  static LdsAttr attr;
-  constexpr size_t lds = WinoHP<EPI, NT>::LDS;
-  if (int e = attr.ensure((const void*)k, (int)lds, st)) return e;
-  const int ncu = winoh_cus(st);
-  const int64_t tiles = (int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n;
-  const int64_t grid = std::min<int64_t>(tiles, (int64_t)ncu * (NT == 1 ? RRIN_WINOHP_BPC : 1));
-  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256), lds, st, a);
-  return hip_code(hipGetLastError());
-}
-
-template <int NT>
-static int launch_winohp_e(const ConvH8Args& b, int epi, hipStream_t st) {
-  switch (epi) {
-    case RRIN_EPI_LINEAR: return launch_winohp_k<RRIN_EPI_LINEAR, NT>(b, st);
-    case RRIN_EPI_LEAKY: return launch_winohp_k<RRIN_EPI_LEAKY, NT>(b, st);
-    case RRIN_EPI_LEAKY_POOL: return launch_winohp_k<RRIN_EPI_LEAKY_POOL, NT>(b, st);
-    case RRIN_EPI_LEAKY_REP: return launch_winohp_k<RRIN_EPI_LEAKY_REP, NT>(b, st);
-    case RRIN_EPI_SUBPIXEL: return launch_winohp_k<RRIN_EPI_SUBPIXEL, NT>(b, st);
-  }
-  return RRIN_E_ARG;
-}
-#endif  // RRIN_LAB
 
 template <int NT>
 static int launch_winoh_e(const ConvH8Args& b, int epi, hipStream_t st) {
@@ -1209,43 +448,11 @@ static int launch_winoh_e(const ConvH8Args& b, int epi, hipStream_t st) {
   return RRIN_E_ARG;
 }
 
-#ifdef RRIN_LAB
-int launch_winohl(const ConvH8Args& a, int epi, hipStream_t st) {
-  ConvH8Args b = a;
-  b.cob_group = winoh_cob_group(a);
-  switch (epi) {
-    case RRIN_EPI_LINEAR: return launch_winohl_k<RRIN_EPI_LINEAR>(b, st);
-    case RRIN_EPI_LEAKY: return launch_winohl_k<RRIN_EPI_LEAKY>(b, st);
-    case RRIN_EPI_LEAKY_POOL: return launch_winohl_k<RRIN_EPI_LEAKY_POOL>(b, st);
-    case RRIN_EPI_LEAKY_REP: return launch_winohl_k<RRIN_EPI_LEAKY_REP>(b, st);
-    case RRIN_EPI_SUBPIXEL: return launch_winohl_k<RRIN_EPI_SUBPIXEL>(b, st);
-  }
-  return RRIN_E_ARG;
-}
-#endif
 
-int launch_winoh(const ConvH8Args& a, int epi, int nt, bool persistent, hipStream_t st) {
+int launch_winoh(const ConvH8Args& a, int epi, hipStream_t st) {
   ConvH8Args b = a;
   b.cob_group = winoh_cob_group(a);
-  // the persistent form needs 2+ chunks (its pipeline crosses tiles two chunks ahead), 32-bit
-  // byte offsets within an image of every output view (its stores are buffer stores), and a
-  // grid of 2+ pixels each way for the replicate epilogue (one row side, one column side per
-  // edge pixel); otherwise the one-tile-per-workgroup form of the same tile (same bits)
-#ifdef RRIN_LAB
-  const int64_t lim = (int64_t)1 << 31;
-  // ... and it pays only where workgroups walk tiles (as conv_winoc.hip's kind 12): from 2 tiles
-  // per workgroup slot on average
-  const int64_t tiles = (int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n;
-  const bool fits = a.nchunks >= 2 && a.dst_img * 16 < lim && (!a.pool_hi || a.pool_img * 16 < lim) &&
-                    (epi != RRIN_EPI_SUBPIXEL || (int64_t)(a.cout >> 2) * a.ring * 4 < lim) &&
-                    (epi != RRIN_EPI_LEAKY_REP || (a.h >= 2 && a.w >= 2)) &&
-                    tiles >= (int64_t)2 * winoh_cus(st) * (nt == 1 ? RRIN_WINOHP_BPC : 1);
-  if (persistent && fits) return nt == 2 ? launch_winohp_e<2>(b, epi, st) : launch_winohp_e<1>(b, epi, st);
-  return nt == 2 ? launch_winoh_e<2>(b, epi, st) : launch_winoh_e<1>(b, epi, st);
-#else
-  if (persistent || nt != 1) return RRIN_E_CONFIG;  // kinds 9-11: lab library only
   return launch_winoh_e<1>(b, epi, st);
-#endif
 }
 
 }  // namespace rrin

@@ -104,10 +104,6 @@ constexpr int64_t kScratchTickets = 4096;  // minimum ints at the head of the sc
 #define RRIN_EDGE_CROSS_MAX 256
 #endif
 constexpr int64_t kEdgeCrossMaxGroups = RRIN_EDGE_CROSS_MAX;
-#ifndef RRIN_RING_MODE_DEFAULT
-#define RRIN_RING_MODE_DEFAULT 0
-#endif
-constexpr int kRingModeDefault = RRIN_RING_MODE_DEFAULT;
 
 int64_t align256(int64_t b) { return (b + 255) & ~(int64_t)255; }
 
@@ -434,69 +430,19 @@ int block0_h8(const Plan& p, const rrin_conv_weights& ca, const rrin_conv_weight
   return rrin_conv_block0_h8_fwd(&d, st);
 }
 
-// Ring fix-up mode of the sub-pixel up convs (RRIN_RING_MODE, read once; A/B): 0 = the
-// correction of the conv's pre-bias ring values, after the conv on its stream; 1 = the ring
-// from scratch (rrin_edge_fix_desc.full) on a side stream beside the conv -- it reads only the
-// conv's input, and the conv writes no ring pixel of dst; 2 = from scratch, after the conv.
-static int ring_mode() {
-  static const int m = [] {
-    const char* e = getenv("RRIN_RING_MODE");
-    return e && e[0] >= '0' && e[0] <= '2' && !e[1] ? e[0] - '0' : kRingModeDefault;
-  }();
-  return m;
-}
-
-// The side stream of a forward stream (one per device and stream, made on first use, highest
-// priority so the short ring launches are not queued behind the conv's tiles) and the two
-// events of a fork / join.  Events are re-recorded per fork: a wait binds to the record
-// before it.
-struct SideStream {
-  hipStream_t main, side;
-  hipEvent_t fork, join;
-  int dev;
-};
-static std::mutex g_side_mu;
-static std::vector<SideStream> g_side;
-
-static int side_stream(hipStream_t st, SideStream* out) {
-  int dev = 0;
-  if (hipError_t e = hipGetDevice(&dev)) return (int)e;
-  std::lock_guard<std::mutex> lk(g_side_mu);
-  for (const SideStream& s : g_side)
-    if (s.main == st && s.dev == dev) {
-      *out = s;
-      return 0;
-    }
-  SideStream s{st, nullptr, nullptr, nullptr, dev};
-  int lo = 0, hi = 0;
-  if (hipError_t e = hipDeviceGetStreamPriorityRange(&lo, &hi)) return (int)e;
-  if (hipError_t e = hipStreamCreateWithPriority(&s.side, hipStreamNonBlocking, hi)) return (int)e;
-  if (hipError_t e = hipEventCreateWithFlags(&s.fork, hipEventDisableTiming)) return (int)e;
-  if (hipError_t e = hipEventCreateWithFlags(&s.join, hipEventDisableTiming)) return (int)e;
-  g_side.push_back(s);
-  *out = s;
-  return 0;
-}
-
 // up.1 conv of the up block at level L on the sub-pixel path: low-res x (2C ch,
-// edge-replicated) -> CAT[L][0, C), and the ring fix-up (ring_mode()).
+// edge-replicated) -> CAT[L][0, C), then the ring fix-up on the same stream: the correction of
+// the conv's pre-bias ring values (the outside taps of the zero-padded upsampled image).  Round 5
+// measured the two alternatives the ABI allows (rrin_edge_fix_desc.full, the ring from scratch:
+// beside the conv on a side stream, or after it) and both lost; the product has
+// this one mode.
 int upconv_subpixel(const Plan& p, const rrin_conv_weights& cw, int C, const rrin_h8& x, const rrin_h8& up,
                     hipStream_t st) {
   if (cw.subpixel == 2) {  // ring folded into the conv (Winograd kind 3, no split)
     if (!p.RCORR || rrin_conv_h8_cfg_wino(cw.cfg) != 3 || cw.ksplit > 1) return RRIN_E_CONFIG;
     return conv_h8(p, cw, 2 * C, 4 * C, RRIN_EPI_SUBPIXEL, x, up, nullptr, st, p.EDGE, true);
   }
-  const int mode = ring_mode();
-  SideStream ss{};
-  hipStream_t fst = st;  // the fix-up's stream
-  if (mode == 1 && !p.dry) {
-    RRIN_TRY(side_stream(st, &ss));
-    fst = ss.side;
-    if (hipError_t e = hipEventRecord(ss.fork, st)) return (int)e;  // x is complete here
-    if (hipError_t e = hipStreamWaitEvent(fst, ss.fork, 0)) return (int)e;
-  } else {
-    RRIN_TRY(conv_h8(p, cw, 2 * C, 4 * C, RRIN_EPI_SUBPIXEL, x, up, nullptr, st, p.EDGE));
-  }
+  RRIN_TRY(conv_h8(p, cw, 2 * C, 4 * C, RRIN_EPI_SUBPIXEL, x, up, nullptr, st, p.EDGE));
   rrin_edge_fix_desc e;
   memset(&e, 0, sizeof(e));
   e.n = p.n;
@@ -510,14 +456,13 @@ int upconv_subpixel(const Plan& p, const rrin_conv_weights& cw, int C, const rri
   e.wedge = cw.wedge;
   e.bias = cw.bias_raw;
   e.status = p.status;
-  e.full = mode != 0;
+  e.full = 0;
   // F32R plans: the cross-workgroup K split (the same result bit for bit) where the
   // split grid is at most one workgroup per CU -- the latency-bound small grids
   // (640x368 x 1: fix-up 195 -> 129 us per forward); larger grids keep one
   // workgroup per tile, whose extra workgroups only queue behind the other
   // stream's convs (720p x 4 on 2 streams: fix-up span 1.4 -> 3.5 ms per step).
-  // Not beside the conv: its split-K uses the same scratch.
-  if (p.prec == RRIN_PREC_F32R && mode != 1) {
+  if (p.prec == RRIN_PREC_F32R) {
     int64_t tk = 0;
     const int64_t nf = rrin_edge_fix_split_floats(&e, &tk);
     if (nf > 0 && nf / 1024 <= kEdgeCrossMaxGroups) {
@@ -531,17 +476,9 @@ int upconv_subpixel(const Plan& p, const rrin_conv_weights& cw, int C, const rri
       }
     }
   }
-  if (p.dry) return mode == 1 ? conv_h8(p, cw, 2 * C, 4 * C, RRIN_EPI_SUBPIXEL, x, up, nullptr, st, p.EDGE) : 0;
-  {
-    ProfScope ps(p.prof, fst, RRIN_KIND_EDGE, 0.0);
-    RRIN_TRY(rrin_subpixel_edge_fix_h8(&e, fst));
-  }
-  if (mode == 1) {
-    RRIN_TRY(conv_h8(p, cw, 2 * C, 4 * C, RRIN_EPI_SUBPIXEL, x, up, nullptr, st, p.EDGE));
-    if (hipError_t r = hipEventRecord(ss.join, fst)) return (int)r;
-    if (hipError_t r = hipStreamWaitEvent(st, ss.join, 0)) return (int)r;  // the ring is in place
-  }
-  return 0;
+  if (p.dry) return 0;
+  ProfScope ps(p.prof, st, RRIN_KIND_EDGE, 0.0);
+  return rrin_subpixel_edge_fix_h8(&e, st);
 }
 
 // conv cw (a level-0 conv a) runs fused with the next conv: fp16, asked for by the table

@@ -183,24 +183,18 @@ WINO_DIRECT = {(6, 32, 0): 13}
 WINO_KIND = 0
 
 
-# the kind of the auto mode's 32-output-channel convs (the level-0 convs): 3, or the
-# persistent register-U tile 8 (conv_winop.hip)
+# the kind of the auto mode's 32-output-channel convs (the level-0 convs).  Round 4-5 measured
+# the alternatives (kind 7, the persistent kind 8, register U inside kind 3) slower; the
+# rejected kinds 2, 5 and 8-13 (kind 12: kind 6 on a persistent grid, slower in the
+# two-stream forward) were removed in round 6 -- DESIGN.md §5b-§5e keep the numbers.
 WINO_KIND32 = 3
-
-
-# Kind 12 (round 5): kind 6 on a persistent grid (conv3x3_winocp_kernel: workgroups walk tiles,
-# the next tile's first chunks load during the current tile's last ones; bitwise kind 6).  Per
-# conv at 1280x720 x 2 (profiles/r05/cfgab32_persistent.log): 0.86-0.96 of kind 6's time on the
-# cin 32-128 convs, 0.99-1.00 on the deep ones; the library runs kind 6 itself where a grid has
-# fewer than 2 tiles per workgroup slot (the 720p level-4 convs: 1.26x there).  False: kind 6.
-WINO_PERSISTENT = False  # measured slower in the two-stream forward
 
 
 def wino_kind_for(cout: int) -> int:
     if WINO_KIND != 0:
         return WINO_KIND
     if cout % 64 == 0:
-        return 12 if WINO_PERSISTENT else 6
+        return 6
     return WINO_KIND32 if cout <= 32 else 3
 # ... and kind 4 (the same arithmetic on TH 4 tiles of 4 waves: twice the
 # workgroups) on the few-tile deep convs where that wins, (cin, cout rows, grid
@@ -300,12 +294,15 @@ WINO_F16_KIND = 6
 FUSE_L0 = 2
 
 
+MAX_DEFAULT_STREAMS = 4
+
+
 def default_streams(precision: str, batch: int) -> int:
     """HIP streams a forward of `batch` pairs is split over by default: fp16 one pair per stream
     up to 4 (C3 1280x736 x 4: 488.8-489.1 pairs/s on 4 streams vs 482.1-482.3 on 2), the other
     precisions 2 (headline 1280x720 x 4 exact fp32: 143.0-143.4 on 2 vs 141.8-142.0 on 4;
     profiles/r05/streams_ab.txt).  The output is bitwise that of one stream either way."""
-    return max(1, min(batch, 4 if precision == "fp16" else 2))
+    return max(1, min(batch, MAX_DEFAULT_STREAMS if precision == "fp16" else 2))
 
 
 def fused_pairs(convs) -> list:
@@ -379,7 +376,11 @@ def t_coefficients(t, n: int) -> torch.Tensor:
 
 
 class RRINEngine:
-    MAX_WORKSPACES = 4
+    # cached workspaces (one per forward part: (pairs, h, w, stream slot)): two shapes at the
+    # largest default stream count stay resident together -- an fp16 4-stream forward alone fills 4
+    # slots, and evicting one forces a zero-filled reallocation and drops its reuse_flow state
+    # (ADVICE r05).  Eviction is by shape: every part of the least recently used (h, w) goes at once.
+    MAX_WORKSPACES = 2 * MAX_DEFAULT_STREAMS
 
     def __init__(self, net, precision: str = "fp32", subpixel_max_level: int = 2, units=None):
         """``units``: the U-Nets to pack, as (name, UNet, first-conv input permutation);
@@ -542,11 +543,7 @@ class RRINEngine:
             if f32:  # fp32 records: unscaled fp32 weights (offsets in floats)
                 bp = np.empty(L.rrin_pack_bias_floats(cout, bm), np.float32)
                 pa = perm_arr.ctypes.data if perm_arr is not None else None
-                if L.rrin_conv_h8_cfg_wino(cfg) == 5:  # Winograd F(4x4,3x3): 36-point transformed weights
-                    wp = np.empty(L.rrin_pack_conv3x3_wino4_floats(cout, cin), np.float32)
-                    _lib.check(L.rrin_pack_conv3x3_wino4(w.ctypes.data, b.ctypes.data, cout, cin, pa,
-                                                         wp.ctypes.data, bp.ctypes.data), "rrin_pack_conv3x3_wino4")
-                elif L.rrin_conv_h8_cfg_wino(cfg):  # Winograd F(2x2,3x3): transformed weights
+                if L.rrin_conv_h8_cfg_wino(cfg) > 0:  # Winograd F(2x2,3x3): transformed weights
                     wp = np.empty(L.rrin_pack_conv3x3_wino_bm_floats(cout, cin, bm), np.float32)
                     _lib.check(L.rrin_pack_conv3x3_wino_bm(w.ctypes.data, b.ctypes.data, cout, cin, bm, pa,
                                                            wp.ctypes.data, bp.ctypes.data), "rrin_pack_conv3x3_wino_bm")
@@ -560,7 +557,7 @@ class RRINEngine:
                 biases.append(bp)
                 boff += bp.size
                 continue
-            if L.rrin_conv_h8_cfg_wino(cfg):  # fp16 Winograd: U = G g G^T in fp16 (conv_winoh.hip)
+            if L.rrin_conv_h8_cfg_wino(cfg) > 0:  # fp16 Winograd: U = G g G^T in fp16 (conv_winoh.hip)
                 nh = L.rrin_pack_conv3x3_wino_h8_halves(cout, cin, bm)
                 whi = np.empty(nh, np.uint16)
                 bp = np.empty(L.rrin_pack_bias_floats(cout, bm), np.float32)
@@ -688,10 +685,12 @@ class RRINEngine:
             if nbytes < 0:
                 _lib.check(int(nbytes), "rrin_net_workspace_bytes")
             while len(self._ws) >= self.MAX_WORKSPACES:
-                old, _ = self._ws.popitem(last=False)
-                self._flow_valid.pop(old, None)
-                for sk in [k for k in self._scratch if k[0] == old]:
-                    del self._scratch[sk]
+                lru = next(iter(self._ws))   # least recently used part: evict its whole shape
+                for old in [k for k in self._ws if k[1:3] == lru[1:3]]:
+                    del self._ws[old]
+                    self._flow_valid.pop(old, None)
+                    for sk in [k for k in self._scratch if k[0] == old]:
+                        del self._scratch[sk]
             ws = torch.zeros(int(nbytes), dtype=torch.uint8, device=self.device)
             self._ws[key] = ws
             self._flow_valid[key] = False

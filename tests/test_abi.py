@@ -144,3 +144,38 @@ def test_h8_geometry_and_cfgs():
         assert lib.rrin_conv_h8_cfg_fits(c, 1, 16) == ok[c]
     assert lib.rrin_conv_h8_cfg_fits(9, 1, 64) == 1 and lib.rrin_conv_h8_cfg_fits(9, 1, 128) == 0
     assert lib.rrin_conv_h8_cfg_fits(8, 1, 512) == 0 and lib.rrin_conv_h8_cfg_fits(0, 1, 512) == 1
+
+
+def _h8_view(h, w, groups, base=1 << 30):
+    hp, wp = (h + 15) // 16 * 16 + 2, (w + 31) // 32 * 32 + 16
+    g = _lib.Geom(h, w, hp, wp, hp * wp)
+    return _lib.H8(base, None, groups * hp * wp, 0, groups, g)
+
+
+@pytest.mark.parametrize("wino", [False, True])
+def test_h8_dma_source_span_limit(wino):
+    """the LDS-DMA staging addresses a source through buffer resources with
+    32-bit byte offsets, so a source whose staged span reaches 2 GB must be rejected (RRIN_E_SHAPE)
+    instead of staging zeros.  Host-only size query: nothing is launched or dereferenced."""
+    lib = _lib.lib()
+    ncfg = lib.rrin_conv_h8_cfg_count()
+    if wino:   # kind 6 at fp16 (conv_winoh.hip)
+        cfg = next(c for c in range(ncfg) if lib.rrin_conv_h8_cfg_wino(c) == 6)
+    else:      # a direct-form LDS-DMA tile
+        cfg = next(c for c in range(ncfg)
+                   if lib.rrin_conv_h8_cfg_wino(c) == 0 and lib.rrin_conv_h8_cfg_ok(c, _lib.PREC_F16) == 1)
+
+    def query(h, w, cin=64):
+        d = _lib.ConvH8Desc()
+        d.n, d.cin, d.cout, d.cfg, d.prec = 1, cin, 64, cfg, _lib.PREC_F16
+        d.epi_mode, d.slope, d.inv_wscale = _lib.EPI_LEAKY, 0.1, 1.0
+        d.src, d.dst = _h8_view(h, w, cin // 8), _h8_view(h, w, 8)
+        d.whi = d.bias = 1 << 30
+        return lib.rrin_conv_h8_split_floats(C.byref(d), None)
+
+    ok = query(736, 1280)
+    assert ok >= 0, ok
+    # 64 fp16 channels = 8 record groups: the direct form stages all 8 (2.2 GB at 6144x3456)
+    assert query(3456, 6144) == (ok if wino else -1)
+    # the Winograd tiles stage from one base per tile and chunk: 3 planes must stay below 2 GB
+    assert query(11776, 11776) == -1

@@ -2,9 +2,7 @@
 (R32, the default "fp32" precision), split-fp16 (fp32_split16) and fp16.
 
 R32 is exact fp32 arithmetic (fp32 storage, v_mfma_f32_32x32x2_f32 products,
-fp32 accumulation): held to 1e-5 against float64; the Winograd F(4x4,3x3)
-config (tile kind 5) to 5e-5 -- its 6x6 transforms carry about 6x the rounding
-error of F(2x2) (still every operation an IEEE fp32 operation).
+fp32 accumulation): held to 1e-5 against float64, the Winograd F(2x2,3x3) tiles too.
 
 fp32_split16 holds each fp32 value as fp16 hi+lo and forms each product from
 three exact fp16 products with fp32 accumulation (error ~2^-21 relative per
@@ -28,12 +26,11 @@ pytestmark = pytest.mark.gpu
 X3, F16, R32 = _lib.PREC_F16X3, _lib.PREC_F16, _lib.PREC_F32R
 PRECS = [R32, X3, F16]
 TOL = {X3: dict(rtol=1e-4, atol=1e-4), F16: dict(rtol=2e-2, atol=2e-2), R32: dict(rtol=1e-5, atol=1e-5)}
-TOL_W4 = dict(rtol=5e-5, atol=5e-5)
 
 
 def tol(prec, cfg):
-    """Tolerance of config cfg at prec (the F(4x4) Winograd tile: TOL_W4)."""
-    return TOL_W4 if prec == R32 and _lib.lib().rrin_conv_h8_cfg_wino(cfg) == 5 else TOL[prec]
+    """Tolerance of config cfg at prec."""
+    return TOL[prec]
 
 
 def ref_conv(x, w, b, slope=None):
@@ -52,21 +49,11 @@ NO_POOL_CFGS = (4, 16)
 
 
 def wino_cfgs(cout=32, epi=None):
-    """Ids of the Winograd exact-fp32 configs the library builds (R32 only): F(2x2,3x3)
-    kinds 1, 3, 4, the register-U kinds 6-7 and the persistent register-U kind 8 (cout
-    <= 32, epilogues LINEAR / LEAKY / LEAKY_POOL); kind 2 and the F(4x4,3x3) kind 5
-    only in the lab library."""
+    """Ids of the Winograd exact-fp32 configs (R32 only): F(2x2,3x3) kinds 1, 3, 4 and the
+    register-U kinds 6-7 (every epilogue, any cout)."""
     lib = _lib.lib()
     return tuple(c for c in range(lib.rrin_conv_h8_cfg_count())
-                 if lib.rrin_conv_h8_cfg_wino(c) and lib.rrin_conv_h8_cfg_ok(c, R32)  # kinds 2, 5: lab only
-                 and kind8_ok(c, cout, epi))
-
-
-def kind8_ok(cfg, cout, epi=None):
-    """Kind 8 (conv_winop.hip) takes one co block and no sub-pixel / replicate epilogue."""
-    if _lib.lib().rrin_conv_h8_cfg_wino(cfg) != 8:
-        return True
-    return cout <= 32 and epi not in (_lib.EPI_LEAKY_REP, _lib.EPI_SUBPIXEL)
+                 if lib.rrin_conv_h8_cfg_wino(c) > 0 and lib.rrin_conv_h8_cfg_ok(c, R32))
 
 
 def cfgs(prec, cout, cin):
@@ -77,8 +64,7 @@ def cfgs(prec, cout, cin):
             if lib.rrin_conv_h8_cfg_fits(c, prec, cin) and lib.rrin_conv_h8_cfg_bm(c) <= max(32, 2 * cout)
             and not (lib.rrin_conv_h8_cfg_wino(c) and cin % 4)
             and not (lib.rrin_conv_h8_cfg_wino(c) in (6, 7) and cin % 8)
-            and not (prec == F16 and lib.rrin_conv_h8_cfg_wino(c) and cin % 16)  # fp16 kind 6: 16-ch chunks
-            and kind8_ok(c, cout)]
+            and not (prec == F16 and lib.rrin_conv_h8_cfg_wino(c) and cin % 16)]  # fp16 kind 6: 16-ch chunks
 
 
 def pack_h8(w, b, cfg, prec, dev, perm=None):
@@ -88,14 +74,6 @@ def pack_h8(w, b, cfg, prec, dev, perm=None):
     cout, cin = w.shape[:2]
     bm = lib.rrin_conv_h8_cfg_bm(cfg)
     pa = np.asarray(perm, np.int32) if perm is not None else None
-    if prec == R32 and lib.rrin_conv_h8_cfg_wino(cfg) == 5:  # Winograd F(4x4): 36 points
-        wp = np.zeros(lib.rrin_pack_conv3x3_wino4_floats(cout, cin), np.float32)
-        bp = np.zeros(lib.rrin_pack_bias_floats(cout, 32), np.float32)
-        _lib.check(lib.rrin_pack_conv3x3_wino4(w.ctypes.data, b.ctypes.data, cout, cin,
-                                               pa.ctypes.data if pa is not None else None, wp.ctypes.data,
-                                               bp.ctypes.data))
-        wt = torch.from_numpy(wp).to(dev)
-        return wt, wt, torch.from_numpy(bp).to(dev), 1.0
     if prec == R32 and lib.rrin_conv_h8_cfg_wino(cfg):  # Winograd: U = G g G^T per point
         wp = np.zeros(lib.rrin_pack_conv3x3_wino_bm_floats(cout, cin, bm), np.float32)
         bp = np.zeros(lib.rrin_pack_bias_floats(cout, bm), np.float32)
@@ -270,7 +248,7 @@ def test_h8_conv_dma_finite_tail(gpu, prec, cin):
 def f16_wino_cfgs():
     lib = _lib.lib()
     return tuple(c for c in range(lib.rrin_conv_h8_cfg_count())
-                 if lib.rrin_conv_h8_cfg_wino(c) and lib.rrin_conv_h8_cfg_ok(c, F16))
+                 if lib.rrin_conv_h8_cfg_wino(c) > 0 and lib.rrin_conv_h8_cfg_ok(c, F16))
 
 
 @pytest.mark.parametrize("prec,cin", [(F16, 6), (F16, 20), (R32, 9)])
@@ -281,7 +259,7 @@ def test_h8_wino_rejects_short_source_view(gpu, prec, cin):
     x = torch.rand(1, cin, 16, 32, device=gpu)
     wt, b = keyed_conv(cin, 32, "tail")
     t = H8Tensor.from_nchw(x, prec)
-    cfgs_ = [c for c in (f16_wino_cfgs() if prec == F16 else wino_cfgs()) if _lib.lib().rrin_conv_h8_cfg_wino(c) != 5]
+    cfgs_ = list(f16_wino_cfgs() if prec == F16 else wino_cfgs())
     assert cfgs_
     for cfg in cfgs_:
         whi, wlo, bp, inv = pack_h8(wt, b, cfg, prec, gpu)

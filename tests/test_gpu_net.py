@@ -268,3 +268,30 @@ def test_size_class_tables_bitwise_fp32_planar(gpu, nets):
         del eng.conv_table_for
     net.precision = "fp32"
     assert torch.equal(small, large)
+
+
+def test_workspace_cache_holds_two_shapes_at_four_streams(gpu):
+    """an fp16 4-pair forward takes 4 workspaces (one per stream part); forwards
+    alternating between two shapes must keep both shapes' workspaces (no zero-filled
+    reallocation, reuse_flow state kept), and a third shape evicts the least recently used
+    shape as a whole."""
+    net = make_net(gpu)
+    net.precision = "fp16"
+    eng = net.engine()
+    shapes = [(64, 96), (96, 128)]
+    with torch.no_grad():
+        for h, w in shapes:
+            i0, i1 = synthetic_batch(4, h, w, first_index=3)
+            eng.forward(i0.to(gpu), i1.to(gpu), 0.5, streams=4)
+        ids = {k: v.data_ptr() for k, v in eng._ws.items()}
+        assert len(ids) == 8
+        for _ in range(2):
+            for h, w in shapes:
+                i0, i1 = synthetic_batch(4, h, w, first_index=3)
+                eng.forward(i0.to(gpu), i1.to(gpu), 0.5, streams=4)
+        assert {k: v.data_ptr() for k, v in eng._ws.items()} == ids
+        assert all(eng._flow_valid[k] for k in ids)
+        i0, i1 = synthetic_batch(4, 32, 64, first_index=3)   # a third shape: (64, 96) goes, whole
+        eng.forward(i0.to(gpu), i1.to(gpu), 0.5, streams=4)
+        assert sorted({k[1:3] for k in eng._ws}) == [(32, 64), (96, 128)]
+    torch.cuda.synchronize(gpu)

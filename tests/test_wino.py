@@ -8,7 +8,6 @@ padding, reference unet.py:29) of the same weights.  The GPU tests
 (tests/test_gpu_h8.py, the Winograd config in every config sweep) check the
 kernel itself against float64."""
 import ctypes as C
-import os
 
 import numpy as np
 import pytest
@@ -89,27 +88,23 @@ def test_wino_packing_layout_and_perm():
 
 def test_wino_config_entry():
     lib = _lib.lib()
-    ids = [c for c in range(lib.rrin_conv_h8_cfg_count()) if lib.rrin_conv_h8_cfg_wino(c)]
-    # kinds 1 (BM 32, 4 waves), 2 (BM 64, 8 waves), 3 (BM 32, 8 waves of 4 accumulators), TH 8;
-    # 4 (kind 3's arithmetic on TH 4 tiles, 4 waves); 5 F(4x4,3x3) on TH 16 tiles; the register-U
-    # tiles 6 (BM 64 x TH 4) and 7 (BM 32 x TH 8), 4 waves; 8 the persistent register-U tile
-    # for cout <= 32 (BM 32 x TH 8, 8 waves)
-    # 9: the fp16-only register-U tile on 2 patch tiles (BM 64 x TH 8, one block per CU); 10, 11:
-    # kinds 6 and 9 on a persistent grid (fp16 only; 9-11 are built into the lab library only)
-    # 12: kind 6 on a persistent grid (exact fp32); 13: kind 6 on two patch tiles per workgroup,
-    # U shared through LDS (fp16 only)
-    assert sorted(lib.rrin_conv_h8_cfg_wino(c) for c in ids) == [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13]
+    ids = [c for c in range(lib.rrin_conv_h8_cfg_count()) if lib.rrin_conv_h8_cfg_wino(c) > 0]
+    # kinds 1 (BM 32, 4 waves), 3 (BM 32, 8 waves of 4 accumulators), TH 8; 4 (kind 3's
+    # arithmetic on TH 4 tiles, 4 waves); the register-U tiles 6 (BM 64 x TH 4) and 7 (BM 32 x
+    # TH 8), 4 waves.  Round 6 removed the rejected kinds 2, 5 and 8-13: ids 19 and 22 stay
+    # reserved (kind -1, never usable), 25-30 are gone.
+    assert sorted(lib.rrin_conv_h8_cfg_wino(c) for c in ids) == [1, 3, 4, 6, 7]
     assert min(ids) == 18  # the direct-form configs keep ids 0-17 (engine tile tables)
+    assert lib.rrin_conv_h8_cfg_count() == 25
+    assert [lib.rrin_conv_h8_cfg_wino(c) for c in (19, 22)] == [-1, -1]
+    assert all(lib.rrin_conv_h8_cfg_ok(c, p) == 0 for c in (19, 22) for p in range(4))
     assert {lib.rrin_conv_h8_cfg_wino(c): lib.rrin_conv_h8_cfg_bm(c) for c in ids} == {
-        1: 32, 2: 64, 3: 32, 4: 32, 5: 32, 6: 64, 7: 32, 8: 32, 9: 64, 10: 64, 11: 64, 12: 64, 13: 64}
+        1: 32, 3: 32, 4: 32, 6: 64, 7: 32}
     for c in ids:
         kind = lib.rrin_conv_h8_cfg_wino(c)
-        assert lib.rrin_conv_h8_cfg_th(c) == {4: 4, 5: 16, 6: 4, 10: 4, 12: 4}.get(kind, 8)
-        # kinds 2, 5 and 8 lost on every Net shape: their kernels are built only into the lab
-        # library (make lab), so the product library reports them as not usable
-        assert lib.rrin_conv_h8_cfg_ok(c, _lib.PREC_F32R) == (0 if kind in (2, 5, 8, 9, 10, 11, 13) else 1)
-        # split16 never runs a Winograd tile; fp16 runs kind 6 (conv_winoh.hip, ABI 13; the lab
-        # library also 9, 10, 11, 13)
+        assert lib.rrin_conv_h8_cfg_th(c) == {4: 4, 6: 4}.get(kind, 8)
+        assert lib.rrin_conv_h8_cfg_ok(c, _lib.PREC_F32R) == 1
+        # split16 never runs a Winograd tile; fp16 runs kind 6 (conv_winoh.hip)
         assert lib.rrin_conv_h8_cfg_ok(c, _lib.PREC_F16X3) == 0
         assert lib.rrin_conv_h8_cfg_ok(c, _lib.PREC_F16) == (1 if kind == 6 else 0)
     assert lib.rrin_pack_conv3x3_wino_floats(33, 5) == 2 * 1 * 16 * 2 * 32 * 4
@@ -147,57 +142,6 @@ def test_pack_wino_h8_layout(cout, cin):
     np.testing.assert_array_equal(got, want.astype(np.float16).astype(np.float64))
     np.testing.assert_array_equal(bp[:cout], b)
     assert not bp[cout:].any()
-
-
-# F(4x4,3x3), interpolation points 0, 1, -1, 1/2, -2, inf; B^T scaled to integers
-BT4 = np.array([[2, -3, -4, 3, 2, 0], [0, -2, 1, 5, 2, 0], [0, -2, 5, -1, -2, 0],
-                [0, 2, 1, -2, -1, 0], [0, 1, -2, -1, 2, 0], [0, 2, -3, -4, 3, 2]], np.float64)
-G4 = np.array([[1 / 2, 0, 0], [1 / 6, 1 / 6, 1 / 6], [1 / 6, -1 / 6, 1 / 6], [16 / 15, 8 / 15, 4 / 15],
-               [1 / 30, -1 / 15, 2 / 15], [0, 0, 1 / 2]])
-AT4 = np.array([[1, 1, 1, 1, 1, 0], [0, 1, -1, 1 / 2, -2, 0], [0, 1, 1, 1 / 4, 4, 0], [0, 1, -1, 1 / 8, -8, 1]])
-
-
-def test_wino4_matrices_are_exact():
-    """A^T[(G g) * (B^T d)] is the 1-D correlation of the 6-sample window d with the
-    3-tap g (in exact arithmetic), so the 2-D nesting is the 3x3 conv of a 6x6 window."""
-    rng = np.random.default_rng(3)
-    d, g = rng.standard_normal(6), rng.standard_normal(3)
-    y = AT4 @ ((G4 @ g) * (BT4 @ d))
-    np.testing.assert_allclose(y, [d[i:i + 3] @ g for i in range(4)], rtol=0, atol=1e-12)
-    d2, g2 = rng.standard_normal((6, 6)), rng.standard_normal((3, 3))
-    y2 = AT4 @ ((G4 @ g2 @ G4.T) * (BT4 @ d2 @ BT4.T)) @ AT4.T
-    ref = np.array([[np.sum(d2[r:r + 3, c:c + 3] * g2) for c in range(4)] for r in range(4)])
-    np.testing.assert_allclose(y2, ref, rtol=0, atol=1e-11)
-
-
-def test_pack_wino4_layout():
-    lib = _lib.lib()
-    cout, cin = 40, 7
-    rng = np.random.default_rng(4)
-    w = rng.standard_normal((cout, cin, 3, 3)).astype(np.float32)
-    b = rng.standard_normal(cout).astype(np.float32)
-    n = lib.rrin_pack_conv3x3_wino4_floats(cout, cin)
-    assert n == 2 * 2 * 36 * 2 * 32 * 2
-    wp = np.empty(n, np.float32)
-    bp = np.empty(lib.rrin_pack_bias_floats(cout, 32), np.float32)
-    assert lib.rrin_pack_conv3x3_wino4(w.ctypes.data, b.ctypes.data, cout, cin, None, wp.ctypes.data,
-                                       bp.ctypes.data) == 0
-    u = wp.reshape(2, 2, 36, 2, 32, 2)  # [cob][chunk][xi][half][co][e]
-    ref = np.einsum("ak,oikl,bl->oiab", G4, w.astype(np.float64), G4)  # [co][ci][6][6]
-    for cob in range(2):
-        for c in range(2):
-            for hh in range(2):
-                for e in range(2):
-                    ci = 4 * c + 2 * hh + e
-                    for col in range(32):
-                        co = 32 * cob + col
-                        got = u[cob, c, :, hh, col, e]
-                        want = ref[co, ci].reshape(36) if co < cout and ci < cin else np.zeros(36)
-                        # the double sum is rounded once: within 1 ulp of the einsum order's rounding
-                        np.testing.assert_array_max_ulp(got, want.astype(np.float32), maxulp=1)
-    np.testing.assert_array_equal(bp[:cout], b)
-    assert not bp[cout:].any()
-    assert lib.rrin_pack_conv3x3_wino4_floats(0, 3) < 0
 
 
 def test_split_scratch_size():
@@ -297,10 +241,7 @@ def test_net_scratch_bytes():
 
     assert need(4, 720, 1280) == 0
     base = need(1, 368, 640)
-    if os.environ.get("RRIN_RING_MODE", "0") == "1":
-        assert base == 0  # the ring fix-ups run beside their convs (net.hip ring_mode 1): no K split
-    else:
-        assert base > 16 * 1024 and base <= 16 * 1024 + 256 * 1024 * 4
+    assert base > 16 * 1024 and base <= 16 * 1024 + 256 * 1024 * 4
     split = need(1, 368, 640, ks={3: 2, 4: 4})
     assert split > base
     assert need(3, 368, 640, ks={3: 2, 4: 4}) > split  # the slabs scale with the batch

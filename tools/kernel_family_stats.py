@@ -15,7 +15,16 @@ stream part) / P (= bench --streams, default 2).  A profiled `bench.py --steps K
 counts them all.  With --ms-per-step (the bench line's own ms_per_step), a family
 whose union per step exceeds it is an error (exit 2): a union longer than the step
 means the step count is wrong.
+
+--profiled-log LOG: the log of the profiled command itself (a bench.py JSON line): its own
+ms_per_step and launch_overlap are printed beside the trace's, and an all-kernel union per step
+above that step (5 % slack for the warm-up steps) is an error (exit 2) -- the step count or the
+trace is wrong.  --live-log LOG: the unprofiled bench line the numbers are quoted for; its step
+and launch_overlap are printed beside the profiled ones, and a profiled step more than 15 %
+slower is flagged ("profile not of the benched regime": per-kernel averages from such a trace do
+not describe the benched forward).
 """
+import json
 import argparse
 import csv
 import re
@@ -61,6 +70,8 @@ def main():
     ap.add_argument("--parts", type=int, default=2, help="forward parts per step (bench --streams)")
     ap.add_argument("--ms-per-step", type=float, default=None,
                     help="the bench line's ms_per_step: a family union above it is an error")
+    ap.add_argument("--profiled-log", default=None, help="bench.py log of the profiled command")
+    ap.add_argument("--live-log", default=None, help="bench.py log of the unprofiled (quoted) run")
     a = ap.parse_args()
     stats(a.stats)
     if not a.trace:
@@ -97,8 +108,43 @@ def main():
             print(f"ERROR: {fam_name} union {per:.3f} ms per step > the bench's {a.ms_per_step:.3f} ms per step")
             bad += 1
     allspans = [(s, e) for _, s, e in rows]
-    print(f"all kernels: busy (union) {union_ns(allspans) / 1e6 / steps:.3f} ms per step")
+    all_union = union_ns(allspans) / 1e6 / steps
+    conv = [(s, e) for f, s, e in rows if f in fams]
+    conv_overlap = sum(e - s for s, e in conv) / max(union_ns(conv), 1) if conv else float("nan")
+    print(f"all kernels: busy (union) {all_union:.3f} ms per step; trace overlap of {','.join(fams)}: "
+          f"{conv_overlap:.3f}")
+    prof = bench_line(a.profiled_log) if a.profiled_log else None
+    live = bench_line(a.live_log) if a.live_log else None
+    if prof:
+        print(f"profiled run: {prof.get('ms_per_step')} ms per step, launch_overlap "
+              f"{prof.get('launch_overlap')} (trace: union {all_union:.3f} ms per step, overlap {conv_overlap:.3f})")
+        if prof.get("ms_per_step") and all_union > 1.05 * prof["ms_per_step"]:
+            print(f"ERROR: all-kernel union {all_union:.3f} ms per step > the profiled run's own "
+                  f"{prof['ms_per_step']:.3f} ms per step: the step count or the trace is wrong")
+            bad += 1
+    if live:
+        print(f"live (quoted) run: {live.get('ms_per_step')} ms per step, launch_overlap {live.get('launch_overlap')}")
+        if prof and prof.get("ms_per_step") and live.get("ms_per_step") and \
+                prof["ms_per_step"] > 1.15 * live["ms_per_step"]:
+            print(f"WARNING: profile not of the benched regime: profiled {prof['ms_per_step']:.3f} vs live "
+                  f"{live['ms_per_step']:.3f} ms per step -- per-kernel averages here do not describe the "
+                  f"benched forward")
     return 2 if bad else 0
+
+
+def bench_line(path):
+    """The last bench.py JSON line of a log, with the roofline's launch_overlap lifted up."""
+    line = None
+    for ln in open(path, errors="replace"):
+        ln = ln.strip()
+        if ln.startswith("{") and '"ms_per_step"' in ln:
+            line = ln
+    if line is None:
+        return None
+    d = json.loads(line)
+    rf = d.get("roofline") or {}
+    d.setdefault("launch_overlap", rf.get("launch_overlap"))
+    return d
 
 
 if __name__ == "__main__":

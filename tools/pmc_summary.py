@@ -56,6 +56,9 @@ def main():
     ap.add_argument("--family", default=None,
                     help="conv kernel family, comma-separated kernels summed (default by precision)")
     ap.add_argument("--key", default=None, help="table key prefix (default: --precision)")
+    ap.add_argument("--build", default=None,
+                    help="build id of the profiled library (default: the in-tree librrin_hip.so; set it when "
+                         "re-deriving an entry from counter files of an earlier build)")
     a = ap.parse_args()
     fetch = load(a.fetch, "FETCH_SIZE")
     write = load(a.write, "WRITE_SIZE")
@@ -81,10 +84,11 @@ def main():
         # the conv family = every body-conv kernel (bench.py's roofline covers all 77 body
         # convs of a forward part): exact fp32 runs the Winograd tiles (kinds 3/4:
         # conv3x3_winoq_kernel, 6/7: conv3x3_winoc_kernel) and the direct-form first conv
+        # (fp16: the fused level-0 UNetConvBlock kernel runs 2 body convs per launch -- omitting it
+        # dropped a third of the C3 conv bytes from the round-5 line)
         fam_name = a.family or {"fp32_planar": "conv3x3_mfma_kernel",
-                                "fp32": "conv3x3_winoq_kernel,conv3x3_winoc_kernel,conv3x3_winocp_kernel,"
-                                        "conv3x3_winop_kernel,conv3x3_h8_kernel",
-                                "fp16": "conv3x3_h8_kernel,conv3x3_winoh_kernel,conv3x3_winohp_kernel"}.get(
+                                "fp32": "conv3x3_winoq_kernel,conv3x3_winoc_kernel,conv3x3_h8_kernel",
+                                "fp16": "conv3x3_h8_kernel,conv3x3_winoh_kernel,conv_block0_h8_kernel"}.get(
             a.precision, "conv3x3_h8_kernel")
         names = [n for n in fam_name.split(",") if n in res]
         if not names:
@@ -100,7 +104,7 @@ def main():
             "correction": "hbm = (2*FETCH_SIZE + WRITE_SIZE) KiB, separate --pmc passes",
             "source": os.path.basename(os.path.normpath(a.fetch)) + " + " + os.path.basename(os.path.normpath(a.write)),
             # the library the profiled runs loaded (bench.py reports this entry only for that build)
-            "build": build_id()}
+            "build": a.build or build_id()}
         json.dump(tab, open(a.table, "w"), indent=1, sort_keys=True)
 
 

@@ -4,7 +4,7 @@ share CUs)?  Runs the Net at --height x --width x --batch in --precision with en
 rounds of (1-stream, 2-stream) forwards, and reports how many 2-stream outputs differ from the
 1-stream one, the max abs difference and whether the fp16 range flag fired.
 
-  python tools/stream_bitwise.py --precision fp16 --wino-f16-kind 10 --wino-f16-levels 3,4
+  python tools/stream_bitwise.py --precision fp16 --wino-f16-levels 3,4
 """
 import argparse
 import os
@@ -22,19 +22,13 @@ ap.add_argument("--height", type=int, default=736)
 ap.add_argument("--width", type=int, default=1280)
 ap.add_argument("--batch", type=int, default=4)
 ap.add_argument("--rounds", type=int, default=6)
-ap.add_argument("--wino-f16-kind", type=int, default=None)
 ap.add_argument("--wino-f16-levels", default=None)
 ap.add_argument("--no-wino", action="store_true")
-ap.add_argument("--wino-persistent", type=int, default=None)
 a = ap.parse_args()
-if a.wino_f16_kind is not None:
-    engine.WINO_F16_KIND = a.wino_f16_kind
 if a.wino_f16_levels is not None:
     engine.WINO_F16_LEVELS = tuple(int(v) for v in a.wino_f16_levels.split(","))
 if a.no_wino:
     engine.WINO = engine.WINO_F16 = False
-if a.wino_persistent is not None:
-    engine.WINO_PERSISTENT = bool(a.wino_persistent)
 dev = torch.device("cuda:0")
 net = Net()
 net.load_state_dict(keyed_state_dict(net.state_dict()), strict=True)
