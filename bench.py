@@ -162,6 +162,10 @@ def parse():
                     help="A/B: no TH-4 Winograd tiles on the deep convs (engine.WINO_TH4)")
     ap.add_argument("--split", default=None,
                     help="explicit pairs per stream, e.g. 1,3 (overrides --streams' even split)")
+    ap.add_argument("--graph", action="store_true",
+                    help="time HIP-graph replays of the forward (RRINEngine.graph: one captured graph per part "
+                         "split, static inputs / t coefficients / output); the roofline then comes from an "
+                         "eager profiled pass of the same K steps (per-launch events cannot be read per replay)")
     ap.add_argument("--train", action="store_true",
                     help="training step instead (SURVEY §8f f4, train.py:98,142-145): Net.forward under "
                          "autograd on the HIP training kernels + charbonnier loss + backward + AdamW step; "
@@ -437,10 +441,20 @@ def main():
         args.streams = engine_mod.default_streams(args.precision, B)
 
     last_gather = [None]
+    ngraph = None
+    if args.graph:
+        ngraph = eng.graph(B, H, W, streams=args.streams, split=split)
+        ngraph.i0.copy_(i0)
+        ngraph.i1.copy_(i1)
 
     def step(prof=None):
         with torch.no_grad():
-            out = eng.forward(i0, i1, args.t, prof=prof, streams=args.streams, split=split)
+            if ngraph is not None and prof is None:
+                out = ngraph.replay(args.t)
+                if gather is not None:
+                    out = out.clone()  # the next replay rewrites the static output
+            else:
+                out = eng.forward(i0, i1, args.t, prof=prof, streams=args.streams, split=split)
             if gather is not None:
                 last_gather[0] = (out, gather.submit(out)[0])
         return out
@@ -465,7 +479,7 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        last[0] = step(prof)
+        last[0] = step(None if ngraph is not None else prof)
     if gather is not None:
         gather.drain()  # every step's gather is inside the timed region
     torch.cuda.synchronize(dev)
@@ -486,7 +500,7 @@ def main():
         torch.cuda.synchronize(dev)
         u0 = time.perf_counter()
         for _ in range(args.steps):
-            step()
+            step(prof if ngraph is not None else None)
         if gather is not None:
             gather.drain()
         torch.cuda.synchronize(dev)
@@ -500,6 +514,10 @@ def main():
         unprofiled = {"value": round(world * B * args.steps / uel, 3),
                       "ms_per_step": round(1e3 * uel / args.steps, 3),
                       "note": "same K steps, no per-launch HIP events"}
+        if ngraph is not None:
+            unprofiled["note"] = ("the same K steps as eager forwards with the per-launch HIP events the "
+                                  "roofline is read from (value: HIP-graph replays, no events)")
+            unprofiled = {"eager_profiled": unprofiled}
 
     roofline = None
     conv_ms_step = head_ms_step = None
@@ -610,6 +628,17 @@ def main():
         if not gather_check["ok"]:
             raise RuntimeError("all-gathered output does not match the ranks' shards")
 
+    graph_info = None
+    if ngraph is not None:
+        # the replayed output against an eager forward of the same inputs (bit for bit)
+        with torch.no_grad():
+            eager = eng.forward(i0, i1, args.t, streams=args.streams, split=split)
+            torch.cuda.synchronize(dev)
+            graph_info = {"mode": "HIP graph replay (RRINEngine.graph: one captured forward, static inputs, "
+                                  "device-resident t coefficients)",
+                          "bitwise_equal_eager": bool(torch.equal(last[0], eager))}
+        if not graph_info["bitwise_equal_eager"]:
+            raise RuntimeError("graph replay output differs from the eager forward")
     pairs = world * B * args.steps
     value = pairs / elapsed
     res = {
@@ -634,6 +663,7 @@ def main():
                                                for u in ("Flow", "refine_flow", "Mask", "final")) / 1e9, 1)},
         "roofline": roofline,
         "unprofiled": unprofiled,
+        "graph": graph_info,
         "gather_check": gather_check,
         "cpu_baseline": None,
         "parity": None,

@@ -459,6 +459,7 @@ class RRINEngine:
         self._sides = []
         self._status = {}
         self._pending_status = []
+        self._graphs = {}
 
     def _init_h8(self, net):
         """Pack for the split-fp16 (F16X3) or fp16 (F16) path: [cob][16-ch chunk][tap][half][bm][8]
@@ -507,6 +508,7 @@ class RRINEngine:
         self._ws = OrderedDict()
         self._flow_valid = {}
         self._sides = []
+        self._graphs = {}
         self._status = {}           # slot -> device int32 range flag (fp16-stored precisions)
         self._pending_status = []   # (event, pinned host copy) of flags not checked yet
 
@@ -760,18 +762,8 @@ class RRINEngine:
         i1 = i1.contiguous()
         out = torch.empty_like(i0)
         coef = t_coefficients(t, n).to(self.device, non_blocking=True)
-        if split is not None:  # explicit part sizes (pairs per stream)
-            split = [int(c) for c in split]
-            if sum(split) != n or min(split) < 1:
-                raise ValueError(f"split {split} does not partition a batch of {n}")
-            cuts = [0]
-            for c in split:
-                cuts.append(cuts[-1] + c)
-            bounds = list(zip(cuts[:-1], cuts[1:]))
-            k = len(bounds)
-        else:
-            k = max(1, min(int(streams), n))
-            bounds = [(n * j // k, n * (j + 1) // k) for j in range(k)]
+        bounds = self._bounds(n, streams, split)
+        k = len(bounds)
         tapbuf = None
         if taps is not None:
             if len(bounds) != 1:
@@ -838,10 +830,42 @@ class RRINEngine:
                 self._pending_status.append((ev, host))
         return y
 
-    def _forward_part(self, i0, i1, out, coef, slot, ws, stream, prof, reuse_flow, tapbuf=None):
+    def _bounds(self, n: int, streams, split):
+        """Contiguous (lo, hi) pair ranges of the forward parts (one per HIP stream)."""
+        if split is not None:  # explicit part sizes (pairs per stream)
+            split = [int(c) for c in split]
+            if sum(split) != n or min(split) < 1:
+                raise ValueError(f"split {split} does not partition a batch of {n}")
+            cuts = [0]
+            for c in split:
+                cuts.append(cuts[-1] + c)
+            return list(zip(cuts[:-1], cuts[1:]))
+        k = max(1, min(int(streams), n))
+        return [(n * j // k, n * (j + 1) // k) for j in range(k)]
+
+    def graph(self, n: int, h: int, w: int, streams: int | None = None, split=None) -> "NetGraph":
+        """The forward of n pairs at h x w captured as one HIP graph and cached per (n, h, w, part
+        split) on this engine -- the engine is rebuilt when the weights, precision or schedule
+        change, so a graph never outlives the packing it captured.  Replaying it enqueues every
+        kernel of the forward with one call (no per-launch host work): the launch gaps of a
+        small forward part (C2 640x368 x 1: ~150 launches in ~2.9 ms) shrink.  Its inputs, t
+        coefficients and output live in static device buffers (``NetGraph.i0 / i1 / out``); the
+        bits are those of :meth:`forward` (same launches, same buffers' layout;
+        ``tests/test_gpu_graph.py``).  reuse_flow and taps are eager-only."""
+        if h % 16 or w % 16 or n < 1:
+            raise RuntimeError(f"H and W must be multiples of 16, got {h}x{w}")
+        if streams is None:
+            streams = default_streams(self.precision, n)
+        bounds = self._bounds(n, streams, split)
+        key = (n, h, w, tuple(bounds))
+        g = self._graphs.get(key)
+        if g is None:
+            g = NetGraph(self, n, h, w, bounds)
+            self._graphs[key] = g
+        return g
+
+    def _net_desc(self, i0, i1, out, coef, ws, sc, status, skip, prof, tapbuf):
         n, _, h, w = i0.shape
-        key = (n, h, w, slot)
-        skip = bool(reuse_flow) and self._flow_valid.get(key, False)
         d = _lib.NetDesc()
         d.n, d.h, d.w = n, h, w
         d.i0, d.i1, d.out, d.coef = i0.data_ptr(), i1.data_ptr(), out.data_ptr(), coef.data_ptr()
@@ -853,20 +877,35 @@ class RRINEngine:
         d.prec = self.prec
         d.prof = prof
         d.taps = tapbuf.data_ptr() if tapbuf is not None else None
-        sc = self._net_scratch(n, h, w, slot)  # allocated (and zero-filled) before the fork
         if sc is not None:
             d.scratch, d.scratch_bytes = sc.data_ptr(), sc.numel()
+        d.status = status.data_ptr() if status is not None else None
+        return d
+
+    def _queue_status(self, slot, stream):
+        """Copy part `slot`'s fp16 range flag to the host behind the work enqueued on `stream`
+        (checked by the next forward / check_range without a sync)."""
+        st = self._status.get(slot)
+        if st is None:
+            return
+        host = torch.empty(1, dtype=torch.int32, pin_memory=True)
+        with torch.cuda.stream(stream):
+            host.copy_(st, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+        self._pending_status.append((ev, host))
+
+    def _forward_part(self, i0, i1, out, coef, slot, ws, stream, prof, reuse_flow, tapbuf=None):
+        n, _, h, w = i0.shape
+        key = (n, h, w, slot)
+        skip = bool(reuse_flow) and self._flow_valid.get(key, False)
+        sc = self._net_scratch(n, h, w, slot)  # allocated (and zero-filled) before the fork
         st = self._status_of(slot) if self.prec in (_lib.PREC_F16X3, _lib.PREC_F16) else None
-        d.status = st.data_ptr() if st is not None else None
+        d = self._net_desc(i0, i1, out, coef, ws, sc, st, skip, prof, tapbuf)
         _lib.check(self.lib.rrin_net_fwd(C.byref(d), C.c_void_p(stream.cuda_stream)), "rrin_net_fwd")
         self._flow_valid[key] = True
         if st is not None:
-            host = torch.empty(1, dtype=torch.int32, pin_memory=True)
-            with torch.cuda.stream(stream):
-                host.copy_(st, non_blocking=True)
-                ev = torch.cuda.Event()
-                ev.record(stream)
-            self._pending_status.append((ev, host))
+            self._queue_status(slot, stream)
 
     # ---- fp16 range guard (fp32_split16 / fp16) ---------------------------------
     # Activations of these precisions are stored as fp16; a value beyond 65504
@@ -898,3 +937,66 @@ class RRINEngine:
     def check_range(self):
         """Wait for every forward issued so far and raise if one overflowed fp16."""
         self._poll_range(wait=True)
+
+
+class NetGraph:
+    """One captured forward (RRINEngine.graph): static inputs ``i0`` / ``i1`` [n,3,h,w], output
+    ``out``, device t coefficients.  :meth:`replay` writes the coefficients of t (only when t
+    changes: a pinned host row, copied stream-ordered before the graph) and replays the graph on
+    the current stream; ``out`` then holds the frames until the next replay."""
+
+    def __init__(self, eng: RRINEngine, n: int, h: int, w: int, bounds):
+        dev = eng.device
+        self.eng, self.n, self.h, self.w, self.bounds = eng, n, h, w, bounds
+        self.i0 = torch.zeros((n, 3, h, w), dtype=torch.float32, device=dev)
+        self.i1 = torch.zeros_like(self.i0)
+        self.out = torch.zeros_like(self.i0)
+        self.coef = torch.zeros((n, 8), dtype=torch.float32, device=dev)
+        self._coef_host = torch.zeros((n, 8), dtype=torch.float32, pin_memory=True)
+        self._coef_ev = None
+        self._t = None
+        with torch.no_grad(), torch.cuda.device(dev):
+            # an eager forward of the same parts first: workspaces, scratch, range flags, side
+            # streams and the packing are allocated outside the capture (nothing allocates inside)
+            eng.forward(self.i0, self.i1, 0.5, split=[hi - lo for lo, hi in bounds])
+            eng._poll_range(wait=True)
+            torch.cuda.synchronize(dev)
+            self.ws = [eng.workspace(hi - lo, h, w, j) for j, (lo, hi) in enumerate(bounds)]
+            self.sc = [eng._net_scratch(hi - lo, h, w, j) for j, (lo, hi) in enumerate(bounds)]
+            prec16 = eng.prec in (_lib.PREC_F16X3, _lib.PREC_F16)
+            self.status = [eng._status_of(j) if prec16 else None for j in range(len(bounds))]
+            sides = eng._side_streams(len(bounds) - 1)
+            self.graph = torch.cuda.CUDAGraph()
+            cap = torch.cuda.Stream(dev)
+            cap.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.graph(self.graph, stream=cap):
+                main = torch.cuda.current_stream(dev)
+                for s in sides:
+                    s.wait_stream(main)
+                for j, (lo, hi) in enumerate(bounds):
+                    st = main if j == 0 else sides[j - 1]
+                    d = eng._net_desc(self.i0[lo:hi], self.i1[lo:hi], self.out[lo:hi], self.coef[lo:hi],
+                                      self.ws[j], self.sc[j], self.status[j], False, None, None)
+                    _lib.check(eng.lib.rrin_net_fwd(C.byref(d), C.c_void_p(st.cuda_stream)), "rrin_net_fwd (capture)")
+                for s in sides:
+                    main.wait_stream(s)
+            torch.cuda.current_stream(dev).wait_stream(cap)
+
+    def replay(self, t=0.5) -> torch.Tensor:
+        eng = self.eng
+        eng._poll_range()
+        st = torch.cuda.current_stream(eng.device)
+        key = t.detach().cpu().numpy().tobytes() if isinstance(t, torch.Tensor) else float(t)
+        if key != self._t:
+            if self._coef_ev is not None:
+                self._coef_ev.synchronize()  # the previous upload has read the pinned row
+            self._coef_host.copy_(t_coefficients(t, self.n))
+            self.coef.copy_(self._coef_host, non_blocking=True)
+            self._coef_ev = torch.cuda.Event()
+            self._coef_ev.record(st)
+            self._t = key
+        self.graph.replay()
+        for j, s in enumerate(self.status):
+            if s is not None:
+                eng._queue_status(j, st)
+        return self.out
