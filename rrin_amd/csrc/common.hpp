@@ -108,6 +108,18 @@ struct LdsAttr {
   }
 };
 
+// Two 8-B record halves per lane -> one whole 16-B record per lane (gfx950 v_permlane32_swap):
+// lane (j, hh) holds half hh (channels 4 hh .. 4 hh + 3) of 8-channel block q0 in x and of block
+// q1 in y -- the MFMA output layout of the H8 epilogues; returns to lane (j, 0) the whole record
+// of block q0 and to lane (j, 1) that of block q1 (dwords in channel order).  Two VALU ops per
+// record, no LDS: a 16-lane group of ds_write_b64 half-records at a 16-B stride is a 2-way bank
+// conflict, and whole records halve the store instructions.
+__device__ inline uint4 halves_to_record(uint2 x, uint2 y) {
+  const auto a = __builtin_amdgcn_permlane32_swap(x.x, y.x, false, false);
+  const auto b = __builtin_amdgcn_permlane32_swap(x.y, y.y, false, false);
+  return make_uint4(a[0], b[0], a[1], b[1]);
+}
+
 // ---- H8 (channel-blocked fp16 records) geometry -----------------------------
 constexpr int kH8PadLeft = 8;  // records: pixel x at record x+8 (128-B aligned rows)
 

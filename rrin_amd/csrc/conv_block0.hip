@@ -260,17 +260,25 @@ __global__ __launch_bounds__(256, 2) void conv_block0_h8_kernel(Block0Args a) {
         const int y = y0 - 1 + m;
         const bool in = xin && y >= 0 && y < a.h;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float4 bs = bq[2 * q];
-          const float bsa[4] = {bs.x, bs.y, bs.z, bs.w};
-          float v[4];
+        for (int qp = 0; qp < 2; ++qp) {  // 8-channel blocks 2 qp, 2 qp + 1
+          uint2 pk[2];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            float t = acc[i][4 * q + e];
-            t = t * a.isa + bsa[e];
-            v[e] = in ? leaky(t, a.slope) : 0.f;
+          for (int k = 0; k < 2; ++k) {
+            const int q = 2 * qp + k;
+            const float4 bs = bq[2 * q];
+            const float bsa[4] = {bs.x, bs.y, bs.z, bs.w};
+            float v[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              float t = acc[i][4 * q + e];
+              t = t * a.isa + bsa[e];
+              v[e] = in ? leaky(t, a.slope) : 0.f;
+            }
+            pk[k] = b0_pack4(v);
           }
-          reinterpret_cast<uint2*>(smem4 + (q * MR + m) * MC + 32 * half + j)[hh] = b0_pack4(v);
+          // whole records: lane (j, hh) writes block 2 qp + hh of its pixel (ds_write_b128, 8
+          // contiguous lanes per LDS cycle: no bank conflict; the half-record ds_write_b64 was 2-way)
+          smem4[((2 * qp + hh) * MR + m) * MC + 32 * half + j] = halves_to_record(pk[0], pk[1]);
         }
       }
     }
@@ -313,7 +321,7 @@ __global__ __launch_bounds__(256, 2) void conv_block0_h8_kernel(Block0Args a) {
     fence();
 
     // ---- conv b's epilogue (conv3x3_h8_kernel's EPI_LEAKY / EPI_LEAKY_POOL expressions); buffer
-    // stores of 8-B record halves, an invalid position's offset past the buffer (dropped)
+    // whole-record (16-B) stores, an invalid position's offset past the buffer (dropped)
     {
       constexpr uint32_t kOOB = 0x80000000u;
       const float4* bq = reinterpret_cast<const float4*>(sbias + 32) + hh;
@@ -323,47 +331,62 @@ __global__ __launch_bounds__(256, 2) void conv_block0_h8_kernel(Block0Args a) {
       const auto rs_d = b0_rsrc(a.dst + (size_t)img * a.dst_img);
       const auto rs_p = b0_rsrc(POOL ? a.pool + (size_t)img * a.pool_img : a.dst);
       const int yb = y0 + (wv >> 1) * 4;
-      const uint32_t d0 = (uint32_t)((yb + 1) * a.dst_wp + x + kH8PadLeft) * 16u + hh * 8u;
-      const uint32_t p0 = (uint32_t)((yb / 2 + 1) * a.pool_wp + x / 2 + kH8PadLeft) * 16u + hh * 8u;
+      const uint32_t d0 = (uint32_t)((yb + 1) * a.dst_wp + x + kH8PadLeft) * 16u;
+      const uint32_t p0 = (uint32_t)((yb / 2 + 1) * a.pool_wp + x / 2 + kH8PadLeft) * 16u;
+      auto st16 = [&](__amdgpu_buffer_rsrc_t rs, uint4 r, uint32_t off) {
+        if constexpr ((RRIN_B0_ABL & 8) == 0)
+          __builtin_amdgcn_raw_buffer_store_b128((unsigned __attribute__((ext_vector_type(4)))){r.x, r.y, r.z, r.w},
+                                                 rs, off, 0, 0);
+      };
+      // 8-channel blocks in pairs (2 qp, 2 qp + 1): each lane's two half-records become one whole
+      // record (halves_to_record), lane (j, hh) storing block 2 qp + hh: 16-B stores, half as many
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float4 bs = bq[2 * q];
-        const float bsb[4] = {bs.x, bs.y, bs.z, bs.w};
-        float v[4][4];
+      for (int qp = 0; qp < 2; ++qp) {
+        float v[2][4][4];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const int q = 2 * qp + k;
+          const float4 bs = bq[2 * q];
+          const float bsb[4] = {bs.x, bs.y, bs.z, bs.w};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              float t = acc2[i][4 * q + e];
+              t = t * a.isb + bsb[e];
+              v[k][i][e] = leaky(t, a.slope);
+            }
+            if (xok && yb + i < a.h)
+              bad |= !(fmaxf(fmaxf(fabsf(v[k][i][0]), fabsf(v[k][i][1])), fmaxf(fabsf(v[k][i][2]), fabsf(v[k][i][3]))) <=
+                       kB0F16Max);
+          }
+        }
+        const int qo = 2 * qp + hh;  // the block this lane stores
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            float t = acc2[i][4 * q + e];
-            t = t * a.isb + bsb[e];
-            v[i][e] = leaky(t, a.slope);
-          }
           const bool ok = xok && yb + i < a.h;
-          if (ok)
-            bad |= !(fmaxf(fmaxf(fabsf(v[i][0]), fabsf(v[i][1])), fmaxf(fabsf(v[i][2]), fabsf(v[i][3]))) <=
-                     kB0F16Max);
-          const uint2 pk = b0_pack4(v[i]);
-          if constexpr ((RRIN_B0_ABL & 8) == 0)
-            __builtin_amdgcn_raw_buffer_store_b64((unsigned __attribute__((ext_vector_type(2)))){pk.x, pk.y}, rs_d,
-                                                ok ? d0 + (uint32_t)(q * a.dst_gp + i * a.dst_wp) * 16u : kOOB, 0, 0);
+          const uint4 rec = halves_to_record(b0_pack4(v[0][i]), b0_pack4(v[1][i]));
+          st16(rs_d, rec, ok ? d0 + (uint32_t)(qo * a.dst_gp + i * a.dst_wp) * 16u : kOOB);
         }
         if constexpr (POOL) {
 #pragma unroll
           for (int p2 = 0; p2 < 2; ++p2) {
-            float s4[4];
+            float s4[2][4];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float s = v[2 * p2][e] + v[2 * p2 + 1][e];
-              s4[e] = 0.25f * (s + __shfl_xor(s, 1));
-            }
+            for (int k = 0; k < 2; ++k)
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const float s = v[k][2 * p2][e] + v[k][2 * p2 + 1][e];
+                s4[k][e] = 0.25f * (s + __shfl_xor(s, 1));
+              }
             const bool ok = !(j & 1) && xok && yb + 2 * p2 < a.h;
-            if (ok)
-              bad |= !(fmaxf(fmaxf(fabsf(s4[0]), fabsf(s4[1])), fmaxf(fabsf(s4[2]), fabsf(s4[3]))) <= kB0F16Max);
-            const uint2 pk = b0_pack4(s4);
-            if constexpr ((RRIN_B0_ABL & 8) == 0)
-              __builtin_amdgcn_raw_buffer_store_b64((unsigned __attribute__((ext_vector_type(2)))){pk.x, pk.y}, rs_p,
-                                                  ok ? p0 + (uint32_t)(q * a.pool_gp + p2 * a.pool_wp) * 16u : kOOB,
-                                                  0, 0);
+#pragma unroll
+            for (int k = 0; k < 2; ++k)
+              if (ok)
+                bad |= !(fmaxf(fmaxf(fabsf(s4[k][0]), fabsf(s4[k][1])), fmaxf(fabsf(s4[k][2]), fabsf(s4[k][3]))) <=
+                         kB0F16Max);
+            const uint4 rec = halves_to_record(b0_pack4(s4[0]), b0_pack4(s4[1]));
+            st16(rs_p, rec, ok ? p0 + (uint32_t)(qo * a.pool_gp + p2 * a.pool_wp) * 16u : kOOB);
           }
         }
       }

@@ -148,6 +148,9 @@ __device__ inline uint4 mask_halves(uint4 v, int nvalid) {
 // (profiles/r04/h8_bias/): 2 where the accumulators are small (WM WN <= 2: the level-0
 // and level-4 tiles, 6-14 % faster per conv), 1 on the other unspread tiles (cfg 0 -8 %,
 // cfg 5 -3 %), 0 on the SPREAD tiles (cfg 10 / 11, which lose 1-7 % with either).
+#ifndef RRIN_H8_WIDE
+#define RRIN_H8_WIDE 1
+#endif
 #ifndef RRIN_H8_BIAS
 #define RRIN_H8_BIAS -1
 #endif
@@ -187,6 +190,8 @@ __global__ void RRIN_PK_CONV_ATTR __launch_bounds__(64 * NW) conv3x3_h8_kernel(C
   constexpr bool kWRes = DMA && (SCHED & SCHED_WRES) != 0;
   constexpr bool kMfma16 = (SCHED & SCHED_MFMA16) != 0;
   constexpr int kBias = RRIN_H8_BIAS >= 0 ? RRIN_H8_BIAS : (WM * WN <= 2 ? 2 : (SCHED & SCHED_SPREAD) ? 0 : 1);
+  // whole-record epilogue stores on H8 records (epi_pair; RRIN_H8_WIDE=0: per-piece half-records)
+  constexpr bool kWide = RRIN_H8_WIDE && !F32 && EPI != RRIN_EPI_SUBPIXEL;
   // DMA pieces (one 16-B record per thread and plane) of one chunk: input tile, then weight slab
   constexpr int NPIECE = T::IN_IT + (kWRes ? 0 : T::W_IT);
 
@@ -534,6 +539,93 @@ __global__ void RRIN_PK_CONV_ATTR __launch_bounds__(64 * NW) conv3x3_h8_kernel(C
       }
     }
   };
+  // ---- epilogue pieces (mt, 2 qp) and (mt, 2 qp + 1) together, H8 records (kWide): each lane
+  // forms its two 8-B half-records, halves_to_record (v_permlane32_swap) turns them into one whole
+  // 16-B record -- lane (j, hh) stores 8-channel block 2 qp + hh of its pixel -- and the wave
+  // stores whole records: half the store instructions of epi_piece, the same bytes and bits.
+  // (Not the sub-pixel epilogue: its ring pixels go to the fp32 edge scratch per channel.)
+  auto epi_pair = [&](const TileId& tl, const auto& V, int mt, int qp, const float* bs0, const float* bs1) {
+    const int cob = tl.cob, x0 = tl.x0, img = tl.img;
+    const int yb = tl.y0 + wn * WN;
+    const int x = x0 + j;
+    uint4* dst[2] = {a.dst_hi + img * a.dst_img, PLANES == 2 ? a.dst_lo + img * a.dst_img : nullptr};
+    const int cq0 = cob * BM + mt * 32 + 16 * qp;  // first channel of block 2 qp
+    const int col = cq0 + 8 * hh;                  // first channel of the block this lane stores
+    float v[2][WN][4];
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+      for (int nt = 0; nt < WN; ++nt)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float t = V[mt][nt][4 * (2 * qp + k) + e];
+          t = t * a.inv_wscale + (k ? bs1 : bs0)[e];
+          if constexpr (EPI != RRIN_EPI_LINEAR) t = leaky(t, a.slope);
+          v[k][nt][e] = t;
+        }
+    // range guard on each lane's own values (as store4: only where that block is stored)
+    auto guard = [&](const float* u) {
+      if (a.status && !(fmaxf(fmaxf(fabsf(u[0]), fabsf(u[1])), fmaxf(fabsf(u[2]), fabsf(u[3]))) <= kF16Max))
+        *a.status = 1;
+    };
+    auto store_rec = [&](uint4* const* d, int64_t rec, const uint4* r) {
+      d[0][rec] = r[0];
+      if constexpr (PLANES == 2) d[1][rec] = r[1];
+    };
+    // both blocks' halves -> this lane's whole record (hi, and lo for two planes)
+    auto records = [&](const float* u0, const float* u1, uint4* r) {
+      uint2 h0, l0, h1, l1;
+      split4(u0, h0, l0);
+      split4(u1, h1, l1);
+      r[0] = halves_to_record(h0, h1);
+      if constexpr (PLANES == 2) r[1] = halves_to_record(l0, l1);
+    };
+#pragma unroll
+    for (int nt = 0; nt < WN; ++nt) {
+      const int y = yb + nt;
+      const bool pix = y < a.h && x < a.w;
+#pragma unroll
+      for (int k = 0; k < 2; ++k)
+        if (pix && cq0 + 8 * k < a.cout) guard(v[k][nt]);
+      uint4 r[2];
+      records(v[0][nt], v[1][nt], r);  // every lane: the swap reads the partner lane
+      if (pix && col < a.cout) {
+        const int64_t rec = (int64_t)(col >> 3) * a.dst_gp + (int64_t)(y + 1) * a.dst_wp + x + kH8PadLeft;
+        store_rec(dst, rec, r);
+        if constexpr (EPI == RRIN_EPI_LEAKY_REP) {
+          // edge replicate into the padding ring (read only by a sub-pixel up conv)
+          const int dy0 = y == 0 ? -1 : 0, dy1 = y == a.h - 1 ? 1 : 0;
+          const int dx0 = x == 0 ? -1 : 0, dx1 = x == a.w - 1 ? 1 : 0;
+          for (int dy = dy0; dy <= dy1; ++dy)
+            for (int dx = dx0; dx <= dx1; ++dx)
+              if (dy | dx) store_rec(dst, rec + (int64_t)dy * a.dst_wp + dx, r);
+        }
+      }
+    }
+    if constexpr (EPI == RRIN_EPI_LEAKY_POOL) {
+      uint4* pdst[2] = {a.pool_hi + img * a.pool_img, PLANES == 2 ? a.pool_lo + img * a.pool_img : nullptr};
+#pragma unroll
+      for (int p2 = 0; p2 < WN / 2; ++p2) {
+        float s4[2][4];
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float s = v[k][2 * p2][e] + v[k][2 * p2 + 1][e];
+            s4[k][e] = 0.25f * (s + __shfl_xor(s, 1));
+          }
+        const int y = yb + 2 * p2;
+        const bool pix = !(j & 1) && y < a.h && x < a.w;
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+          if (pix && cq0 + 8 * k < a.cout) guard(s4[k]);
+        uint4 r[2];
+        records(s4[0], s4[1], r);
+        if (pix && col < a.cout)
+          store_rec(pdst, (int64_t)(col >> 3) * a.pool_gp + (int64_t)(y / 2 + 1) * a.pool_wp + x / 2 + kH8PadLeft, r);
+      }
+    }
+  };
   // combined accumulators: V = acc + accx 2^-11 (F16X3), V = acc (F16)
   auto combine = [&](floatx16 (&V)[WM][WN]) {
 #pragma unroll
@@ -674,14 +766,29 @@ __global__ void RRIN_PK_CONV_ATTR __launch_bounds__(64 * NW) conv3x3_h8_kernel(C
       // compiler sees, so that it does not wait out each piece's stores before the next
       // piece's bias (vmcnt(0), as s_waitcnt's 16-bit immediate)
       if constexpr (kBias != 0) __builtin_amdgcn_s_waitcnt(0x0F70);
+      if constexpr (kWide) {
 #pragma unroll
-      for (int p = 0; p < NPIECE_EPI; ++p) {
-        if constexpr (kBias == 0) {
-          float bq[4];
-          load_bias_piece(cur.cob, p / 4, p % 4, bq);
-          epi_piece(cur, V, p / 4, p % 4, bq);
-        } else {
-          epi_piece(cur, V, p / 4, p % 4, bsv[p / 4][p % 4]);
+        for (int pp = 0; pp < NPIECE_EPI / 2; ++pp) {
+          const int mt = pp / 2, qp = pp % 2;
+          if constexpr (kBias == 0) {
+            float b0[4], b1[4];
+            load_bias_piece(cur.cob, mt, 2 * qp, b0);
+            load_bias_piece(cur.cob, mt, 2 * qp + 1, b1);
+            epi_pair(cur, V, mt, qp, b0, b1);
+          } else {
+            epi_pair(cur, V, mt, qp, bsv[mt][2 * qp], bsv[mt][2 * qp + 1]);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int p = 0; p < NPIECE_EPI; ++p) {
+          if constexpr (kBias == 0) {
+            float bq[4];
+            load_bias_piece(cur.cob, p / 4, p % 4, bq);
+            epi_piece(cur, V, p / 4, p % 4, bq);
+          } else {
+            epi_piece(cur, V, p / 4, p % 4, bsv[p / 4][p % 4]);
+          }
         }
       }
     }
