@@ -435,6 +435,9 @@ __global__ void RRIN_PK_CONV_ATTR __launch_bounds__(64 * NW) conv3x3_h8_kernel(C
     }
   };
 
+  // fp16 range guard of the stored values, accumulated per lane over the workgroup's tiles and
+  // written once at its end (one conditional store instead of one per epilogue piece)
+  bool bad = false;
   // ---- epilogue piece (mt, q) of tile tl: V = the combined accumulators
   // (acc + accx 2^-11, weight scale still applied): scale, bias, leaky, split,
   // 8-B half-record stores (+ pool / edge-replicate / sub-pixel ring scratch).
@@ -448,8 +451,7 @@ __global__ void RRIN_PK_CONV_ATTR __launch_bounds__(64 * NW) conv3x3_h8_kernel(C
       // fp16 range guard: a value fp16 cannot hold would become inf / NaN and
       // could end as a finite but wrong pixel (e.g. a warp of an inf flow
       // samples zeros); flag it (the FINAL head then poisons the output)
-      if (a.status && !(fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))) <= kF16Max))
-        *a.status = 1;
+      bad |= !(fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))) <= kF16Max);
       uint2 hv, lv;
       split4(v, hv, lv);
       reinterpret_cast<uint2*>(d[0] + rec)[hh] = hv;
@@ -565,8 +567,7 @@ __global__ void RRIN_PK_CONV_ATTR __launch_bounds__(64 * NW) conv3x3_h8_kernel(C
         }
     // range guard on each lane's own values (as store4: only where that block is stored)
     auto guard = [&](const float* u) {
-      if (a.status && !(fmaxf(fmaxf(fabsf(u[0]), fabsf(u[1])), fmaxf(fabsf(u[2]), fabsf(u[3]))) <= kF16Max))
-        *a.status = 1;
+      bad |= !(fmaxf(fmaxf(fabsf(u[0]), fabsf(u[1])), fmaxf(fabsf(u[2]), fabsf(u[3]))) <= kF16Max);
     };
     auto store_rec = [&](uint4* const* d, int64_t rec, const uint4* r) {
       d[0][rec] = r[0];
@@ -796,6 +797,7 @@ __global__ void RRIN_PK_CONV_ATTR __launch_bounds__(64 * NW) conv3x3_h8_kernel(C
     tile = ntile;
     cur = nxt;
   }
+  if (bad && a.status) *a.status = 1;
 }
 
 // ---- bilinear x2 upsample pass (unet.py:77, align_corners=False) -------------
