@@ -16,6 +16,10 @@ step c3_new2 timeout -k 10 200 python bench.py $C3
 step c3_r06d2 env RRIN_LIB_AB=ab/librrin_hip_r06d.so timeout -k 10 200 python bench.py $C3
 step c3_new3 timeout -k 10 200 python bench.py $C3
 step c3_r06d3 env RRIN_LIB_AB=ab/librrin_hip_r06d.so timeout -k 10 200 python bench.py $C3
+# upper bound of the ring fix-up's cost: the same build without the fix-up launches (ring pixels wrong)
+step c3_noring1 env RRIN_LIB_AB=ab/librrin_hip_noring.so timeout -k 10 200 python bench.py $C3
+step c3_new4 timeout -k 10 200 python bench.py $C3
+step c3_noring2 env RRIN_LIB_AB=ab/librrin_hip_noring.so timeout -k 10 200 python bench.py $C3
 C3P="python3 bench.py --height 736 --width 1280 --batch 4 --precision fp16 --steps 2 --warmup 1 --cpu-baseline off --no-prof --no-alt"
 step sq1 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAVE_CYCLES --output-format csv -d $O/sq1 -o run -- $C3P
 step sq2 timeout -s KILL 120 rocprofv3 --pmc SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM SQ_INSTS_SALU GRBM_GUI_ACTIVE --output-format csv -d $O/sq2 -o run -- $C3P
