@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define RRIN_ABI_VERSION 16
+#define RRIN_ABI_VERSION 17
 
 #define RRIN_OK 0
 #define RRIN_E_SHAPE (-1)     /* H or W not a multiple of 16, or N < 1          */
@@ -219,6 +219,13 @@ typedef struct rrin_conv_h8_desc {
   float* ring_corr;            /* rrin_conv_h8_ring_floats() floats, any contents */
   int32_t* ring_cnt;           /* rrin_conv_h8_ring_floats() ints, zero before the first call;
                                   every call leaves it zero again */
+  /* ABI 17, EPI_SUBPIXEL: the ring pixels from scratch in the same call -- a rrin_edge_fix_desc
+     with full = 1 for this conv's src / dst (its own weights, bias, epi_mode, status); edge is
+     still written.  The direct-form tiles of 256 or 512 threads run it in extra workgroups at
+     the head of the conv's grid (they read only src and write only dst's ring pixels, which the
+     sub-pixel conv never writes) with threads / 256 K groups; other configs launch it after the
+     conv.  NULL: the caller runs rrin_subpixel_edge_fix_h8 itself. */
+  const struct rrin_edge_fix_desc* ring_full;
 } rrin_conv_h8_desc;
 
 /* Fused level-0 UNetConvBlock at fp16 (unet.py:59-63, and :46 for down_path[0]): conv a

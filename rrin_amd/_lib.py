@@ -9,7 +9,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-ABI_VERSION = 16
+ABI_VERSION = 17
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "librrin_hip.so")
 # A/B sessions only (tools/sessions/): another build of the same library, e.g. ab/librrin_hip_X.so
 if os.environ.get("RRIN_LIB_AB"):
@@ -72,7 +72,8 @@ class ConvH8Desc(C.Structure):
                 ("tail_finite", C.c_int32), ("pad_", C.c_int32), ("src", H8), ("dst", H8), ("pool", H8), ("whi", C.c_void_p), ("wlo", C.c_void_p),
                 ("bias", C.c_void_p), ("edge", C.c_void_p), ("status", C.c_void_p), ("ksplit", C.c_int32),
                 ("pad2_", C.c_int32), ("part", C.c_void_p), ("cnt", C.c_void_p), ("ring_w", C.c_void_p),
-                ("ring_bias", C.c_void_p), ("ring_corr", C.c_void_p), ("ring_cnt", C.c_void_p)]
+                ("ring_bias", C.c_void_p), ("ring_corr", C.c_void_p), ("ring_cnt", C.c_void_p),
+                ("ring_full", C.c_void_p)]
 
 
 class Block0Desc(C.Structure):

@@ -201,6 +201,38 @@ __device__ inline float warp_apply_f(const WarpTaps& t, F get) {
 // LeakyReLU for 0 <= slope <= 1 (h8_prepare checks): one mul + one max
 __device__ inline float leaky(float t, float slope) { return fmaxf(t, t * slope); }
 
+// sub-pixel ring fix-up (conv_f16.hip edge_fix_*): tiles of kFixPx line pixels x kFixCo output
+// channels, input channels staged kFixCi at a time
+constexpr int kFixPx = 32, kFixCo = 32, kFixCi = 32;
+
+struct EdgeFixArgs {
+  const uint4* s_hi;
+  const uint4* s_lo;
+  int64_t s_img, s_gp;  // records
+  int s_wp, sh, sw, cin;
+  _Float16* d_hi;
+  _Float16* d_lo;
+  float* d_f32;  // F32R output (d_hi / d_lo unused)
+  int64_t d_img, d_gp;
+  int d_wp, cout;
+  const float* edge;
+  const float* wedge;  // [cin][9][cout]
+  const float* bias;
+  int64_t ring;
+  float slope;
+  int leaky;
+  int tiles_row, tiles_col;  // tiles per row line / per column line
+  int* status;               // optional fp16 range flag
+  // K slices: the cin chunks in nslices runs of KS chunks (one per K group) or,
+  // fp16, one run; a run's group sums are added in group order, the runs' sums
+  // in run order.  cross: one workgroup per (tile, run), partial sums through
+  // part (1024 floats per run) and the last workgroup (cnt ticket) adds them in
+  // run order -- the same arithmetic as one workgroup looping over the runs.
+  int nslices, cross;
+  float* part;
+  int* cnt;
+};
+
 struct ConvH8Args {
   const uint4* src_hi;
   const uint4* src_lo;
@@ -243,6 +275,13 @@ struct ConvH8Args {
   // co blocks (0: one group of all co blocks), tile positions within a group, the
   // group's co blocks fastest -- see launch_winoc
   int cob_group;
+  // EPI_SUBPIXEL, the ring from scratch in the same launch (rrin_conv_h8_desc.ring_full): the
+  // first nfix workgroups of the grid (a multiple of 8: the conv tiles keep their XCD remap) run
+  // the FULL ring fix-up over fix (fix_real of them do work; workgroup r covers ring tile
+  // r % fix_gx, co block (r / fix_gx) % fix_gy, image r / (fix_gx fix_gy)); they read only the
+  // conv's input and write only the ring pixels of dst, which the conv does not write
+  EdgeFixArgs fix;
+  int nfix, fix_real, fix_gx, fix_gy;
 };
 
 // Ring index of pixel (y, x) of an H x W image (rrin_ring_pixels order: top
@@ -281,6 +320,9 @@ int launch_winoq(const ConvH8Args& a, int epi, int th, hipStream_t st);
 constexpr size_t kWinoCLds1 = (size_t)2048 * 16;  // TH 4: 3 x 512 stage records < 2048 exchange
 constexpr size_t kWinoCLds2 = (size_t)4096 * 16;  // TH 8: 3 x 768 < 4096
 int launch_winoc(const ConvH8Args& a, int epi, int ct, hipStream_t st);
+// whether rrin_conv3x3_h8_fwd runs a ring_full fix-up inside the conv's launch for tile config
+// cfg and cin input channels (else it launches it after the conv) -- conv_f16.hip
+bool ring_in_launch_ok(int cfg, int cin);
 // the kind-6 tile at fp16 (conv_winoh.hip): H8 records, v_mfma_f32_32x32x16_f16, packed-f16
 // input transform; same LDS as kWinoCLds1
 int launch_winoh(const ConvH8Args& a, int epi, hipStream_t st);

@@ -176,9 +176,23 @@ constexpr int kSpreadTaps = 6, kStaggerTap = 3;
 // v_mfma_f32_32x32x2_f32 (product e: lanes 0-31 channel e, lanes 32-63 channel
 // 4+e of the chunk; one ds_read_b128 per operand feeds all 4).  Same tiles,
 // LDS images and DMA as the fp16 kernel; weights unscaled; whole-record stores.
+template <int PLANES, int KS, bool F32, bool FULL>
+__device__ inline void edge_fix_body(const EdgeFixArgs& a, int bx, int by, int bz);
+
 template <int NW, int WM, int WN, int PLANES, int EPI, bool DMA, int SCHED = 0, bool F32 = false>
 __global__ void RRIN_PK_CONV_ATTR __launch_bounds__(64 * NW) conv3x3_h8_kernel(ConvH8Args a) {
   using T = TileH8<NW, WM, WN, PLANES>;
+  // EPI_SUBPIXEL with the ring from scratch in this launch: workgroups [0, nfix) run the FULL
+  // fix-up (NW / 4 K groups of 256 threads) and leave; the conv tiles follow
+  if constexpr (EPI == RRIN_EPI_SUBPIXEL && NW >= 4) {
+    if ((int)blockIdx.x < a.nfix) {
+      const int r = blockIdx.x;
+      if (r < a.fix_real)
+        edge_fix_body<PLANES, NW / 4, F32, true>(a.fix, r % a.fix_gx, (r / a.fix_gx) % a.fix_gy, r / (a.fix_gx * a.fix_gy));
+      return;
+    }
+  }
+  const int cgrid = (int)gridDim.x - a.nfix, cblk = (int)blockIdx.x - a.nfix;  // the conv's part of the grid
   static_assert(!F32 || PLANES == 1, "fp32 records: one plane");
   constexpr int CPR = F32 ? 4 : 8;  // channels per record
   constexpr int NT = T::NT, BM = T::BM, TH = T::TH, ROWS = T::ROWS;
@@ -206,9 +220,9 @@ __global__ void RRIN_PK_CONV_ATTR __launch_bounds__(64 * NW) conv3x3_h8_kernel(C
   const int hh = lane >> 5;
 
   int bid;
-  {  // XCD-aware bijective remap (see conv_mfma.hip)
-    const int nwg = gridDim.x, q = nwg >> 3, r = nwg & 7;
-    const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+  {  // XCD-aware bijective remap (see conv_mfma.hip); nfix is a multiple of 8
+    const int nwg = cgrid, q = nwg >> 3, r = nwg & 7;
+    const int xcd = cblk & 7, slot = cblk >> 3;
     bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
   }
   const int ntiles = a.co_blocks * a.tiles_x * a.tiles_y * a.n;
@@ -671,7 +685,7 @@ __global__ void RRIN_PK_CONV_ATTR __launch_bounds__(64 * NW) conv3x3_h8_kernel(C
   __syncthreads();
   int buf = 0;
   for (;;) {
-    const int ntile = tile + (int)gridDim.x;
+    const int ntile = tile + cgrid;
     const bool more = ntile < ntiles;
     const TileId nxt = tile_id(more ? ntile : tile);
 #pragma unroll
@@ -863,35 +877,6 @@ __global__ void up2x_h8_kernel(const uint4* __restrict__ s_hi, const uint4* __re
 // up2x_h8_kernel does) and the weights staged in LDS.  A corner also has the
 // two other taps of its outside column ("extra" slots).  Lines: top row and
 // bottom row (corners included), left and right columns without the corners.
-constexpr int kFixPx = 32, kFixCo = 32, kFixCi = 32;
-
-struct EdgeFixArgs {
-  const uint4* s_hi;
-  const uint4* s_lo;
-  int64_t s_img, s_gp;  // records
-  int s_wp, sh, sw, cin;
-  _Float16* d_hi;
-  _Float16* d_lo;
-  float* d_f32;  // F32R output (d_hi / d_lo unused)
-  int64_t d_img, d_gp;
-  int d_wp, cout;
-  const float* edge;
-  const float* wedge;  // [cin][9][cout]
-  const float* bias;
-  int64_t ring;
-  float slope;
-  int leaky;
-  int tiles_row, tiles_col;  // tiles per row line / per column line
-  int* status;               // optional fp16 range flag
-  // K slices: the cin chunks in nslices runs of KS chunks (one per K group) or,
-  // fp16, one run; a run's group sums are added in group order, the runs' sums
-  // in run order.  cross: one workgroup per (tile, run), partial sums through
-  // part (1024 floats per run) and the last workgroup (cnt ticket) adds them in
-  // run order -- the same arithmetic as one workgroup looping over the runs.
-  int nslices, cross;
-  float* part;
-  int* cnt;
-};
 
 // The 4 low-res records (8 halves / 4 floats, both planes) that bilinear x2
 // (align_corners = False, edge clamp) blends into U(Y, X), and the blend weights.
@@ -954,8 +939,11 @@ constexpr int kFixSubFloats = kFixCi * (kFixPx + 2) + kFixCi * 4 + 7 * kFixCi * 
 constexpr int kFixFullFloats = 2 * kFixCi * (kFixPx + 2) + 6 * kFixCi * kFixCo;
 static_assert(kFixFullFloats <= kFixSubFloats, "FULL ring staging fits the K group's region");
 
-template <int PLANES, int KS, bool F32 = false, bool FULL = false>
-__global__ void RRIN_PK_EDGE_ATTR __launch_bounds__(256 * KS) edge_fix_h8_kernel(EdgeFixArgs a) {
+// The fix-up of one ring workgroup (bx: ring tile, by: co block, bz: image [x K run]); the kernel
+// below runs it per block, and the sub-pixel conv can run it in extra workgroups of its own
+// launch (conv3x3_h8_kernel, ConvH8Args.nfix) -- KS 256-thread K groups, threadIdx.x < 256 KS
+template <int PLANES, int KS, bool F32, bool FULL>
+__device__ inline void edge_fix_body(const EdgeFixArgs& a, const int bx, const int by, const int bz) {
   constexpr int CPR = F32 ? 4 : 8;            // channels per record
   constexpr int GPC = kFixCi / CPR;           // record groups per ci chunk
   constexpr int NL = FULL ? 2 : 1;            // staged U lines
@@ -972,12 +960,12 @@ __global__ void RRIN_PK_EDGE_ATTR __launch_bounds__(256 * KS) edge_fix_h8_kernel
   const int tid = threadIdx.x & 255, px = tid & (kFixPx - 1), cg = tid / kFixPx;  // 8 groups of 4 channels
   // (fp16 records always run one K run in one workgroup: compile-time there)
   const bool cross = F32 && a.cross;
-  const int nsl = F32 ? a.nslices : 1, img = cross ? blockIdx.z / nsl : blockIdx.z, co0 = blockIdx.y * kFixCo;
-  const int sl0 = cross ? blockIdx.z - img * nsl : 0, sl1 = cross ? sl0 + 1 : nsl;
+  const int nsl = F32 ? a.nslices : 1, img = cross ? bz / nsl : bz, co0 = by * kFixCo;
+  const int sl0 = cross ? bz - img * nsl : 0, sl1 = cross ? sl0 + 1 : nsl;
   const int csl = a.cin / nsl;  // channels per run (a multiple of KS * kFixCi)
   const int H = 2 * a.sh, W = 2 * a.sw;
   // line of this tile: 0 top, 1 bottom, 2 left, 3 right
-  int t = blockIdx.x, line;
+  int t = bx, line;
   if (t < 2 * a.tiles_row) { line = t / a.tiles_row; t -= line * a.tiles_row; }
   else { t -= 2 * a.tiles_row; line = 2 + t / a.tiles_col; t -= (line - 2) * a.tiles_col; }
   const bool row = line < 2;
@@ -1185,7 +1173,7 @@ __global__ void RRIN_PK_EDGE_ATTR __launch_bounds__(256 * KS) edge_fix_h8_kernel
     // split-K seam, sc1 form (as conv3x3_winoq_kernel's SK path): write-through run
     // sums, drain, barrier, one relaxed ticket; the last workgroup reads every run's
     // sums with sc1 loads and adds them in run order
-    const int64_t tile = ((int64_t)img * gridDim.x + blockIdx.x) * gridDim.y + blockIdx.y;
+    const int64_t tile = ((int64_t)img * (2 * a.tiles_row + 2 * a.tiles_col) + bx) * ((a.cout + kFixCo - 1) / kFixCo) + by;
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(a.part + tile * nsl * 1024, 0, nsl * 1024 * 4, 0x00020000);
     if (ks == 0) {
@@ -1235,6 +1223,11 @@ __global__ void RRIN_PK_EDGE_ATTR __launch_bounds__(256 * KS) edge_fix_h8_kernel
       if constexpr (PLANES == 2) a.d_lo[k] = lo_of(v, vh);
     }
   }
+}
+
+template <int PLANES, int KS, bool F32 = false, bool FULL = false>
+__global__ void RRIN_PK_EDGE_ATTR __launch_bounds__(256 * KS) edge_fix_h8_kernel(EdgeFixArgs a) {
+  edge_fix_body<PLANES, KS, F32, FULL>(a, blockIdx.x, blockIdx.y, blockIdx.z);
 }
 
 // ---- layout kernels ------------------------------------------------------------
@@ -1934,13 +1927,14 @@ struct CfgH8 {
   size_t wslab;       // bytes of one weight slab per plane (WRES: one more per chunk past 2)
   bool pool_ok;
   int sched, persist;
+  int nt;  // threads per workgroup (the direct-form tiles; 0: Winograd configs)
 };
 static constexpr size_t kRetiredLds = (size_t)1 << 30;  // > kMaxLds: never usable
 static const CfgH8 kCfgH8[] = {
 #define X(id, nw, wm, wn, sc, pe)                                                                               \
   {TileH8<nw, wm, wn, 1>::BM, TileH8<nw, wm, wn, 1>::TH, h8_lds_bytes<nw, wm, wn, 1>((sc & SCHED_WRES) != 0, 2), \
    h8_lds_bytes<nw, wm, wn, 2>((sc & SCHED_WRES) != 0, 2), (size_t)TileH8<nw, wm, wn, 1>::W_REC * 16,     \
-   (wn % 2) == 0, sc, pe},
+   (wn % 2) == 0, sc, pe, 64 * nw},
     RRIN_H8_CFGS(X)
 #undef X
     // kWinoCfg: Winograd F(2x2,3x3) on fp32 records (conv_wino.hip), BM 32 x TH 8
@@ -2021,6 +2015,18 @@ static int launch_h8_k(const ConvH8Args& args, int persist, hipStream_t st) {
     if (g < args.co_blocks) g = args.co_blocks;
     if (g < grid) grid = g;
   }
+  if constexpr (EPI == RRIN_EPI_SUBPIXEL && T::NT >= 256) {
+    if (args.fix_real > 0) {  // the FULL ring fix-up in workgroups [0, nfix) of this launch
+      constexpr int KS = T::NT / 256;
+      ConvH8Args b = args;
+      b.nfix = (args.fix_real + 7) & ~7;
+      b.fix.nslices = F32 ? b.fix.cin / (KS * kFixCi) : 1;  // runs of KS chunks, added in run order
+      b.fix.cross = 0;
+      const size_t flds = (size_t)KS * kFixSubFloats * sizeof(float);
+      hipLaunchKernelGGL(k, dim3((unsigned)(grid + b.nfix)), dim3(T::NT), lds > flds ? lds : flds, st, b);
+      return hip_code(hipGetLastError());
+    }
+  }
   hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(T::NT), lds, st, args);
   return hip_code(hipGetLastError());
 }
@@ -2090,6 +2096,13 @@ static inline bool rec_prec(int prec) {
 static inline int chans_per_rec(int prec) { return prec == RRIN_PREC_F32R ? 4 : 8; }
 
 // Validate a conv descriptor and turn it into kernel arguments.
+}  // namespace rrin
+// the ring fix-up's host side (defined with its kernels below, at file scope)
+static int edge_fix_prepare(const rrin_edge_fix_desc* d, rrin::EdgeFixArgs& a, dim3& grid);
+static int edge_fix_run(rrin::EdgeFixArgs a, dim3 grid, int prec, bool full, const rrin_edge_fix_desc* d,
+                        hipStream_t st);
+namespace rrin {
+
 static int h8_prepare(const rrin_conv_h8_desc* d, ConvH8Args& a, bool need_scratch = true) {
   if (!d || !d->whi || !d->bias) return RRIN_E_ARG;
   if (!rec_prec(d->prec)) return RRIN_E_ARG;
@@ -2204,6 +2217,19 @@ static int h8_prepare(const rrin_conv_h8_desc* d, ConvH8Args& a, bool need_scrat
     a.bias_raw = d->ring_bias;
     a.corr = d->ring_corr;
     a.rcnt = d->ring_cnt;
+  }
+  if (d->ring_full) {  // the ring from scratch with this conv (ABI 17)
+    const rrin_edge_fix_desc* e = d->ring_full;
+    if (!sub || d->ring_w || e->full != 1 || e->prec != d->prec || e->n != d->n || e->cout * 4 != d->cout)
+      return RRIN_E_ARG;
+    dim3 g;
+    if (int rc = edge_fix_prepare(e, a.fix, g)) return rc;
+    if (a.fix.s_hi != a.src_hi || a.fix.sh != h || a.fix.sw != w) return RRIN_E_ARG;  // this conv's input
+    a.fix_gx = (int)g.x;
+    a.fix_gy = (int)g.y;
+    const int64_t nf = (int64_t)g.x * g.y * g.z;
+    if (nf + (int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n + 8 > 0x7fffffff) return RRIN_E_SHAPE;
+    a.fix_real = (int)nf;
   }
   return 0;
 }
@@ -2334,11 +2360,34 @@ extern "C" int rrin_conv_h8_cfg_fits(int32_t cfg, int32_t prec, int32_t cin) {
   return lds <= kMaxLds ? 1 : 0;
 }
 
+static int conv3x3_h8_launch(const rrin_conv_h8_desc* d, const ConvH8Args& a, hipStream_t st);
+
+bool rrin::ring_in_launch_ok(int cfg, int cin) {
+  if (cfg < 0 || cfg >= kNumCfgH8 || is_wino(cfg) || retired(cfg)) return false;
+  const int nt = kCfgH8[cfg].nt;
+  return nt >= 256 && cin % ((nt / 256) * kFixCi) == 0;
+}
+
 extern "C" int rrin_conv3x3_h8_fwd(const rrin_conv_h8_desc* d, void* stream) {
   ConvH8Args a;
   const int rc = h8_prepare(d, a);
   if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;
+  if (a.fix_real > 0) {
+    // in the conv's launch: a direct-form tile of 256 or 512 threads whose K groups split the
+    // input channels evenly; otherwise the conv, then the FULL fix-up as its own launch
+    if (!ring_in_launch_ok(d->cfg, a.fix.cin)) {
+      ConvH8Args b = a;
+      b.fix_real = 0;
+      if (int e = conv3x3_h8_launch(d, b, st)) return e;
+      dim3 g((unsigned)a.fix_gx, (unsigned)a.fix_gy, (unsigned)d->n);
+      return edge_fix_run(a.fix, g, d->prec, true, nullptr, st);
+    }
+  }
+  return conv3x3_h8_launch(d, a, st);
+}
+
+static int conv3x3_h8_launch(const rrin_conv_h8_desc* d, const ConvH8Args& a, hipStream_t st) {
   if (d->cfg == kWinoCfg) return launch_wino(a, d->epi_mode, st);
   if (d->cfg == kWinoQCfg) return launch_winoq(a, d->epi_mode, 8, st);
   if (d->cfg == kWinoQ4Cfg) return launch_winoq(a, d->epi_mode, 4, st);
@@ -2549,10 +2598,10 @@ static void edge_fix_split(int cin, int prec, int* ks, int* nsl) {
   if (planes_of(prec) == 1 && cin % (4 * kFixCi) == 0 && cin >= 8 * kFixCi) *ks = 4;
 }
 
-extern "C" int rrin_subpixel_edge_fix_h8(const rrin_edge_fix_desc* d, void* stream) {
+// validate d and fill a (everything but the K split); grid: ring tiles x co blocks x images
+static int edge_fix_prepare(const rrin_edge_fix_desc* d, EdgeFixArgs& a, dim3& grid) {
   if (!d || (!d->edge && !d->full) || !d->wedge || !d->bias || (d->full != 0 && d->full != 1)) return RRIN_E_ARG;
   if (!rec_prec(d->prec)) return RRIN_E_ARG;
-  const bool full = d->full == 1;
   if (d->n < 1 || d->cin < 8 || (d->cin & 7) || d->cout < 8 || (d->cout & 7)) return RRIN_E_ARG;
   if (d->epi_mode != RRIN_EPI_LINEAR && d->epi_mode != RRIN_EPI_LEAKY) return RRIN_E_ARG;
   if (!h8_ok(d->src, d->prec) || !h8_ok(d->dst, d->prec)) return RRIN_E_SHAPE;
@@ -2560,7 +2609,6 @@ extern "C" int rrin_subpixel_edge_fix_h8(const rrin_edge_fix_desc* d, void* stre
   const int cpr = chans_per_rec(d->prec);
   if (d->cin > cpr * d->src.groups || d->cout > cpr * d->dst.groups) return RRIN_E_ARG;
   const int planes = planes_of(d->prec);
-  EdgeFixArgs a;
   memset(&a, 0, sizeof(a));
   const int64_t sg = (int64_t)d->src.g_off * d->src.g.plane, dg = (int64_t)d->dst.g_off * d->dst.g.plane;
   a.s_hi = static_cast<const uint4*>(d->src.hi) + sg;
@@ -2591,31 +2639,47 @@ extern "C" int rrin_subpixel_edge_fix_h8(const rrin_edge_fix_desc* d, void* stre
   const int H = d->dst.g.h, W = d->dst.g.w;
   a.tiles_row = (W + kFixPx - 1) / kFixPx;
   a.tiles_col = (H - 2 + kFixPx - 1) / kFixPx;
-  const dim3 grid((unsigned)(2 * a.tiles_row + 2 * a.tiles_col), (unsigned)((d->cout + kFixCo - 1) / kFixCo),
-                  (unsigned)d->n);
+  grid = dim3((unsigned)(2 * a.tiles_row + 2 * a.tiles_col), (unsigned)((d->cout + kFixCo - 1) / kFixCo),
+              (unsigned)d->n);
+  a.nslices = 1;
+  a.cross = 0;
+  return 0;
+}
+
+// the fix-up as its own launch: K groups / runs by edge_fix_split; the cross-workgroup K split
+// where the caller passed its scratch (fp32 records)
+static int edge_fix_run(EdgeFixArgs a, dim3 grid, int prec, bool full, const rrin_edge_fix_desc* d,
+                        hipStream_t st) {
   int ks, nsl;
-  edge_fix_split(d->cin, d->prec, &ks, &nsl);
+  edge_fix_split(a.cin, prec, &ks, &nsl);
   a.nslices = nsl;
   a.cross = 0;
   dim3 g = grid;
-  const int64_t tiles = (int64_t)grid.x * grid.y * d->n;
-  if (nsl > 1 && d->part && d->cnt && tiles * nsl * 1024 <= d->part_floats && tiles <= d->cnt_len) {
+  const int n = (int)grid.z;
+  const int64_t tiles = (int64_t)grid.x * grid.y * n;
+  if (d && nsl > 1 && d->part && d->cnt && tiles * nsl * 1024 <= d->part_floats && tiles <= d->cnt_len) {
     a.cross = 1;  // one workgroup per K run (same arithmetic as the loop over runs)
     a.part = d->part;
     a.cnt = d->cnt;
-    g.z = (unsigned)(d->n * nsl);
+    g.z = (unsigned)(n * nsl);
   }
-  hipStream_t st = (hipStream_t)stream;
-  if (d->prec == RRIN_PREC_F32R) {
+  if (prec == RRIN_PREC_F32R) {
     return ks == 2 ? edge_fix_launch<1, 2, true>(a, g, st, full) : edge_fix_launch<1, 1, true>(a, g, st, full);
   }
-  switch (planes * 8 + ks) {
+  switch (planes_of(prec) * 8 + ks) {
     case 2 * 8 + 2: return edge_fix_launch<2, 2>(a, g, st, full);
     case 2 * 8 + 1: return edge_fix_launch<2, 1>(a, g, st, full);
     case 1 * 8 + 4: return edge_fix_launch<1, 4>(a, g, st, full);
     case 1 * 8 + 2: return edge_fix_launch<1, 2>(a, g, st, full);
     default: return edge_fix_launch<1, 1>(a, g, st, full);
   }
+}
+
+extern "C" int rrin_subpixel_edge_fix_h8(const rrin_edge_fix_desc* d, void* stream) {
+  EdgeFixArgs a;
+  dim3 grid;
+  if (int e = edge_fix_prepare(d, a, grid)) return e;
+  return edge_fix_run(a, grid, d->prec, d->full == 1, d, (hipStream_t)stream);
 }
 
 extern "C" int64_t rrin_edge_fix_split_floats(const rrin_edge_fix_desc* d, int64_t* cnt) {

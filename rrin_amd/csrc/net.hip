@@ -104,6 +104,12 @@ constexpr int64_t kScratchTickets = 4096;  // minimum ints at the head of the sc
 #define RRIN_EDGE_CROSS_MAX 256
 #endif
 constexpr int64_t kEdgeCrossMaxGroups = RRIN_EDGE_CROSS_MAX;
+// sub-pixel up convs on the direct-form tiles of 256 / 512 threads (fp16, split16): the ring from
+// scratch inside the conv's launch (RRIN_RING_INLAUNCH=0: the separate correction launch, A/B)
+#ifndef RRIN_RING_INLAUNCH
+#define RRIN_RING_INLAUNCH 1
+#endif
+constexpr bool kRingInLaunch = RRIN_RING_INLAUNCH != 0;
 
 int64_t align256(int64_t b) { return (b + 255) & ~(int64_t)255; }
 
@@ -350,7 +356,8 @@ int run_unet(const Plan& p, const UNetSpec& u, const rrin_conv_weights* cw, cons
 }
 
 int conv_h8(const Plan& p, const rrin_conv_weights& cw, int cin, int cout, int epi, const rrin_h8& src,
-            const rrin_h8& dst, const rrin_h8* pool, hipStream_t st, float* edge = nullptr, bool ring_fold = false) {
+            const rrin_h8& dst, const rrin_h8* pool, hipStream_t st, float* edge = nullptr, bool ring_fold = false,
+            const rrin_edge_fix_desc* ring_full = nullptr) {
   // algorithmic FLOPs of the conv (a sub-pixel conv has 4 phase rows per real channel): 9
   // multiply-adds per output and input channel in the direct form, 4 in Winograd F(2x2,3x3)
   // (16 per 2x2 patch)
@@ -376,6 +383,7 @@ int conv_h8(const Plan& p, const rrin_conv_weights& cw, int cin, int cout, int e
   d.bias = cw.bias;
   d.edge = edge;
   d.status = p.status;
+  d.ring_full = ring_full;
   if (ring_fold) {
     d.ring_w = cw.wedge;
     d.ring_bias = cw.bias_raw;
@@ -442,10 +450,6 @@ int upconv_subpixel(const Plan& p, const rrin_conv_weights& cw, int C, const rri
     if (!p.RCORR || rrin_conv_h8_cfg_wino(cw.cfg) != 3 || cw.ksplit > 1) return RRIN_E_CONFIG;
     return conv_h8(p, cw, 2 * C, 4 * C, RRIN_EPI_SUBPIXEL, x, up, nullptr, st, p.EDGE, true);
   }
-  RRIN_TRY(conv_h8(p, cw, 2 * C, 4 * C, RRIN_EPI_SUBPIXEL, x, up, nullptr, st, p.EDGE));
-#ifdef RRIN_SKIP_RING_FIX  // ablation build only (the ring pixels stay wrong): the fix-ups' cost bound
-  return 0;
-#endif
   rrin_edge_fix_desc e;
   memset(&e, 0, sizeof(e));
   e.n = p.n;
@@ -460,6 +464,19 @@ int upconv_subpixel(const Plan& p, const rrin_conv_weights& cw, int C, const rri
   e.bias = cw.bias_raw;
   e.status = p.status;
   e.full = 0;
+#ifndef RRIN_SKIP_RING_FIX
+  if (kRingInLaunch && ring_in_launch_ok(cw.cfg, 2 * C)) {
+    // the ring from scratch in extra workgroups of the conv's own launch (ABI 17 ring_full):
+    // no separate fix-up launch and no dependency step on this stream (C3: the separate
+    // fix-ups cost ~3.5 %, profiles/r06/ring/)
+    e.full = 1;
+    return conv_h8(p, cw, 2 * C, 4 * C, RRIN_EPI_SUBPIXEL, x, up, nullptr, st, p.EDGE, false, &e);
+  }
+#endif
+  RRIN_TRY(conv_h8(p, cw, 2 * C, 4 * C, RRIN_EPI_SUBPIXEL, x, up, nullptr, st, p.EDGE));
+#ifdef RRIN_SKIP_RING_FIX  // ablation build only (the ring pixels stay wrong): the fix-ups' cost bound
+  return 0;
+#endif
   // F32R plans: the cross-workgroup K split (the same result bit for bit) where the
   // split grid is at most one workgroup per CU -- the latency-bound small grids
   // (640x368 x 1: fix-up 195 -> 129 us per forward); larger grids keep one

@@ -330,7 +330,7 @@ def test_h8_leaky_rep_writes_replicated_ring(gpu, prec):
 
 
 def subpixel_upconv(src: H8Tensor, w, b, cfg, prec, dst=None, ksplit=0, keep=None, fold=False, edge_split=False,
-                    full=False):
+                    full=False, inlaunch=False):
     """EPI_SUBPIXEL conv + ring fix-up through the C ABI (the Net's up.1 conv); fold: the
     ring in the conv launch (rrin_conv_h8_desc.ring_w, Winograd kind 3) instead of
     rrin_subpixel_edge_fix_h8; full: the fix-up's from-scratch mode (rrin_edge_fix_desc.full,
@@ -371,13 +371,18 @@ def subpixel_upconv(src: H8Tensor, w, b, cfg, prec, dst=None, ksplit=0, keep=Non
         _lib.check(lib.rrin_conv3x3_h8_fwd(C.byref(d), H.stream(dev)), "rrin_conv3x3_h8_fwd(subpixel, fold)")
         torch.cuda.synchronize(dev)
         return dst
-    if not full:
-        _lib.check(lib.rrin_conv3x3_h8_fwd(C.byref(d), H.stream(dev)), "rrin_conv3x3_h8_fwd(subpixel)")
     e = _lib.EdgeFixDesc()
     e.n, e.cin, e.cout, e.prec, e.epi_mode, e.slope = src.n, cin, cout, prec, _lib.EPI_LINEAR, 0.1
     e.src, e.dst = src.chunk_view(0, cin), dst.view(0, cout)
-    e.edge, e.wedge, e.bias = (None if full else edge.data_ptr()), wedge.data_ptr(), braw.data_ptr()
-    e.full = int(full)
+    e.edge, e.wedge, e.bias = (None if full or inlaunch else edge.data_ptr()), wedge.data_ptr(), braw.data_ptr()
+    e.full = int(full or inlaunch)
+    if inlaunch:  # ABI 17: the ring from scratch with the conv (rrin_conv_h8_desc.ring_full)
+        d.ring_full = C.addressof(e)
+        _lib.check(lib.rrin_conv3x3_h8_fwd(C.byref(d), H.stream(dev)), "rrin_conv3x3_h8_fwd(subpixel, ring_full)")
+        torch.cuda.synchronize(dev)
+        return dst
+    if not full:
+        _lib.check(lib.rrin_conv3x3_h8_fwd(C.byref(d), H.stream(dev)), "rrin_conv3x3_h8_fwd(subpixel)")
     if edge_split:  # cross-workgroup K split of the fix-up (fp32 records)
         nc = C.c_int64(-1)
         nf = lib.rrin_edge_fix_split_floats(C.byref(e), C.byref(nc))
@@ -440,6 +445,41 @@ def test_h8_subpixel_ring_full(gpu, prec, n, cin, cout, sh, sw):
                                 dst=H8Tensor(n, 2 * cout, 2 * sh, 2 * sw, gpu, prec))
         assert torch.equal(split.hi, dst.hi)
         assert not keep or not keep[1].any()
+
+
+@pytest.mark.parametrize("prec", PRECS)
+@pytest.mark.parametrize("n,cin,cout,sh,sw", [(2, 64, 32, 20, 36), (1, 128, 64, 23, 40), (2, 256, 128, 5, 7),
+                                              (1, 512, 256, 3, 5), (1, 64, 32, 1, 1), (3, 128, 64, 46, 80)])
+def test_h8_subpixel_ring_in_launch(gpu, prec, n, cin, cout, sh, sw):
+    """ABI 17 ring_full: the ring from scratch in extra workgroups of the sub-pixel conv's own
+    launch (direct-form tiles of 256 / 512 threads; other configs -- the Winograd tiles, 128-thread
+    tiles -- run it as a second launch): every config within the tolerance of upsample-then-conv in
+    float64, the bridge half and the padding untouched, repeat launches bitwise equal, and the
+    second-launch fallback bit for bit the separate FULL fix-up."""
+    x = torch.rand(n, cin, sh, sw, device=gpu) * 2 - 1
+    wt, b = keyed_conv(cin, cout, "sub")
+    up = F.interpolate(x.double().cpu(), scale_factor=2, mode="bilinear", align_corners=False)
+    ref = F.conv2d(up, wt.double().cpu(), b.double().cpu(), padding=1)
+    src = H8Tensor.from_nchw(x, prec)
+    replicate_ring(src)
+    lib = _lib.lib()
+    tested = 0
+    # the sub-pixel configs of the Net's tables (10-13: 512 / 256 threads), a 128-thread tile (7, 17:
+    # second launch) and, exact fp32, the Winograd tiles (second launch)
+    for cfg in [c for c in cfgs(prec, 4 * cout, cin) if c in (7, 10, 11, 12, 13, 17) or lib.rrin_conv_h8_cfg_wino(c) > 0]:
+        out = [subpixel_upconv(src, wt, b, cfg, prec, inlaunch=True, dst=H8Tensor(n, 2 * cout, 2 * sh, 2 * sw, gpu, prec))
+               for _ in range(2)]
+        dst = out[0]
+        np.testing.assert_allclose(dst.to_nchw(0, cout).cpu().double().numpy(), ref.numpy(), **tol(prec, cfg),
+                                   err_msg=f"cfg {cfg}")
+        assert not dst.to_nchw(cout, cout).any()
+        assert not dst.hi[:, :, 0].any() and not dst.hi[:, :, :, :8].any()
+        assert torch.equal(out[0].hi, out[1].hi)
+        if prec == _lib.PREC_F32R and lib.rrin_conv_h8_cfg_wino(cfg) > 0:  # second-launch fallback
+            sep = subpixel_upconv(src, wt, b, cfg, prec, full=True, dst=H8Tensor(n, 2 * cout, 2 * sh, 2 * sw, gpu, prec))
+            assert torch.equal(sep.hi, dst.hi)
+        tested += 1
+    assert tested
 
 
 @pytest.mark.parametrize("n,cin,cout,sh,sw", [(2, 128, 64, 20, 36), (1, 256, 128, 5, 7), (2, 512, 256, 3, 5),
