@@ -24,6 +24,7 @@ sched_of = $(if $(SCHED_$(1)),-mllvm -amdgpu-sched-strategy=$(SCHED_$(1)))
 SRC_DIR := rrin_amd/csrc
 OBJ_DIR := build/obj
 SRCS := $(wildcard $(SRC_DIR)/*.hip)
+HDRS := $(wildcard $(SRC_DIR)/*.hpp) include/rrin_hip.h
 OBJS := $(patsubst $(SRC_DIR)/%.hip,$(OBJ_DIR)/%.o,$(SRCS))
 LIB := rrin_amd/librrin_hip.so
 # kernel lab (tools/conv_lab.py ablate): the split16 conv with schedule knobs / ablations
@@ -41,7 +42,7 @@ ISA_DIR := build/isa
 ISA_OK := $(patsubst $(SRC_DIR)/%.hip,$(ISA_DIR)/%.ok,$(SRCS))
 check-isa: $(ISA_OK)
 
-$(ISA_DIR)/%.ok: $(SRC_DIR)/%.hip $(SRC_DIR)/common.hpp include/rrin_hip.h tools/isa_vmcheck.py
+$(ISA_DIR)/%.ok: $(SRC_DIR)/%.hip $(HDRS) tools/isa_vmcheck.py
 	@mkdir -p $(ISA_DIR)
 	$(HIPCC) $(CXXFLAGS) $(call sched_of,$*) --cuda-device-only -S -o $(ISA_DIR)/$*.s $< 2>/dev/null
 	python3 tools/isa_vmcheck.py $(ISA_DIR)/$*.s
@@ -49,7 +50,7 @@ $(ISA_DIR)/%.ok: $(SRC_DIR)/%.hip $(SRC_DIR)/common.hpp include/rrin_hip.h tools
 
 lab: $(LAB) $(LAB32)
 
-$(OBJ_DIR)/%.o: $(SRC_DIR)/%.hip $(SRC_DIR)/common.hpp include/rrin_hip.h
+$(OBJ_DIR)/%.o: $(SRC_DIR)/%.hip $(HDRS)
 	@mkdir -p $(OBJ_DIR)
 	$(HIPCC) $(CXXFLAGS) $(call sched_of,$*) -c $< -o $@
 

@@ -252,7 +252,9 @@ def lib():
             f = getattr(h, name)
             f.restype = res
             f.argtypes = args
-        if h.rrin_abi_version() != ABI_VERSION:
+        # an A/B build of an earlier ABI whose changes since are appends only (RRIN_LIB_AB_ABI=16)
+        ok = {ABI_VERSION} | ({int(os.environ.get("RRIN_LIB_AB_ABI", ABI_VERSION))} if os.environ.get("RRIN_LIB_AB") else set())
+        if h.rrin_abi_version() not in ok:
             raise RRINError(f"librrin_hip ABI {h.rrin_abi_version()} != expected {ABI_VERSION}")
         _LIB = h
     return _LIB

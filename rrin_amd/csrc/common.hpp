@@ -321,8 +321,8 @@ constexpr size_t kWinoCLds1 = (size_t)2048 * 16;  // TH 4: 3 x 512 stage records
 constexpr size_t kWinoCLds2 = (size_t)4096 * 16;  // TH 8: 3 x 768 < 4096
 int launch_winoc(const ConvH8Args& a, int epi, int ct, hipStream_t st);
 // whether rrin_conv3x3_h8_fwd runs a ring_full fix-up inside the conv's launch for tile config
-// cfg and cin input channels (else it launches it after the conv) -- conv_f16.hip
-bool ring_in_launch_ok(int cfg, int cin);
+// cfg, cin input channels and precision prec (else it launches it after the conv) -- conv_f16.hip
+bool ring_in_launch_ok(int cfg, int cin, int prec);
 // the kind-6 tile at fp16 (conv_winoh.hip): H8 records, v_mfma_f32_32x32x16_f16, packed-f16
 // input transform; same LDS as kWinoCLds1
 int launch_winoh(const ConvH8Args& a, int epi, hipStream_t st);

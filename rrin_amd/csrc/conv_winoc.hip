@@ -31,6 +31,7 @@
 // (j, hh): patch j of a 32-patch MFMA tile, record half hh (channels 4 hh .. + 3
 // of the chunk; MFMA product e contracts channels e and 4 + e).
 #include "common.hpp"
+#include "edge_fix.hpp"
 
 #ifndef RRIN_WINOC_AGPR
 #define RRIN_WINOC_AGPR 0
@@ -99,10 +100,22 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winoc_kernel(ConvH8Args a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int yw = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int j = lane & 31, hh = lane >> 5;
+  if constexpr (EPI == RRIN_EPI_SUBPIXEL) {
+    // the ring from scratch in this launch (rrin_conv_h8_desc.ring_full): workgroups [0, nfix)
+    // run the FULL fix-up (one K group of 256 threads, fp32 records) and leave
+    if ((int)blockIdx.x < a.nfix) {
+      const int rr = blockIdx.x;
+      if (rr < a.fix_real)
+        edge_fix_body<1, 1, true, true>(a.fix, rr % a.fix_gx, (rr / a.fix_gx) % a.fix_gy, rr / (a.fix_gx * a.fix_gy));
+      return;
+    }
+  }
   int bid;
   {  // XCD-aware bijective remap (conv_mfma.hip): an XCD's workgroups are consecutive tiles
-    const int nwg = gridDim.x, q = nwg >> 3, r = nwg & 7;
-    const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+     // (nfix, a multiple of 8, keeps each conv workgroup's XCD)
+    const int nwg = (int)gridDim.x - a.nfix, q = nwg >> 3, r = nwg & 7;
+    const int cb = (int)blockIdx.x - a.nfix;
+    const int xcd = cb & 7, slot = cb >> 3;
     bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
   }
   const int ntiles = a.co_blocks * a.tiles_x * a.tiles_y * a.n;
@@ -446,8 +459,20 @@ static int launch_winoc_k(const ConvH8Args& a, hipStream_t st) {
   auto k = conv3x3_winoc_kernel<EPI, CT, NT>;
   static LdsAttr attr;
   constexpr size_t lds = WinoC<NT>::LDS;
-  if (int e = attr.ensure((const void*)k, (int)lds, st)) return e;
+  constexpr size_t flds = (size_t)kFixSubFloats * sizeof(float);  // the FULL fix-up's staging (one K group)
+  constexpr size_t lmax = EPI == RRIN_EPI_SUBPIXEL && flds > lds ? flds : lds;
+  if (int e = attr.ensure((const void*)k, (int)lmax, st)) return e;
   const int64_t grid = (int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n;
+  if constexpr (EPI == RRIN_EPI_SUBPIXEL) {
+    if (a.fix_real > 0) {  // ring workgroups at the head of the grid; runs of one 32-channel chunk
+      ConvH8Args b = a;
+      b.nfix = (a.fix_real + 7) & ~7;
+      b.fix.nslices = b.fix.cin / kFixCi;
+      b.fix.cross = 0;
+      hipLaunchKernelGGL(k, dim3((unsigned)(grid + b.nfix)), dim3(256), lmax, st, b);
+      return hip_code(hipGetLastError());
+    }
+  }
   hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256), lds, st, a);
   return hip_code(hipGetLastError());
 }

@@ -104,8 +104,9 @@ constexpr int64_t kScratchTickets = 4096;  // minimum ints at the head of the sc
 #define RRIN_EDGE_CROSS_MAX 256
 #endif
 constexpr int64_t kEdgeCrossMaxGroups = RRIN_EDGE_CROSS_MAX;
-// sub-pixel up convs on the direct-form tiles of 256 / 512 threads (fp16, split16): the ring from
-// scratch inside the conv's launch (RRIN_RING_INLAUNCH=0: the separate correction launch, A/B)
+// sub-pixel up convs: the ring from scratch inside the conv's launch where the tile allows it (the
+// exact-fp32 register-U Winograd tiles, the fp16 / split16 direct-form tiles of 256 / 512
+// threads; rrin_amd ring_in_launch_ok) -- RRIN_RING_INLAUNCH=0: the separate correction launch (A/B)
 #ifndef RRIN_RING_INLAUNCH
 #define RRIN_RING_INLAUNCH 1
 #endif
@@ -465,7 +466,7 @@ int upconv_subpixel(const Plan& p, const rrin_conv_weights& cw, int C, const rri
   e.status = p.status;
   e.full = 0;
 #ifndef RRIN_SKIP_RING_FIX
-  if (kRingInLaunch && ring_in_launch_ok(cw.cfg, 2 * C)) {
+  if (kRingInLaunch && ring_in_launch_ok(cw.cfg, 2 * C, p.prec)) {
     // the ring from scratch in extra workgroups of the conv's own launch (ABI 17 ring_full):
     // no separate fix-up launch and no dependency step on this stream (C3: the separate
     // fix-ups cost ~3.5 %, profiles/r06/ring/)
