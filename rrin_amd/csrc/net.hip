@@ -104,9 +104,12 @@ constexpr int64_t kScratchTickets = 4096;  // minimum ints at the head of the sc
 #define RRIN_EDGE_CROSS_MAX 256
 #endif
 constexpr int64_t kEdgeCrossMaxGroups = RRIN_EDGE_CROSS_MAX;
-// sub-pixel up convs: the ring from scratch inside the conv's launch where the tile allows it (the
-// exact-fp32 register-U Winograd tiles, the fp16 / split16 direct-form tiles of 256 / 512
-// threads; rrin_amd ring_in_launch_ok) -- RRIN_RING_INLAUNCH=0: the separate correction launch (A/B)
+// fp16 / split16 sub-pixel up convs: the ring from scratch (ABI 17 ring_full), inside the conv's
+// launch where the tile allows it (direct-form tiles of 256 / 512 threads; ring_in_launch_ok),
+// else as a second launch in the same summation order: every size class gets the same ring bits.
+// Exact fp32 keeps the correction launch (its K-split form on small grids: C2 339.6-339.7 vs
+// 334.4-334.6 pairs/s with the ring in the Winograd launch, headline +0.3 %; profiles/r06/ring/).
+// RRIN_RING_INLAUNCH=0: the correction launch at every precision (A/B)
 #ifndef RRIN_RING_INLAUNCH
 #define RRIN_RING_INLAUNCH 1
 #endif
@@ -440,11 +443,11 @@ int block0_h8(const Plan& p, const rrin_conv_weights& ca, const rrin_conv_weight
 }
 
 // up.1 conv of the up block at level L on the sub-pixel path: low-res x (2C ch,
-// edge-replicated) -> CAT[L][0, C), then the ring fix-up on the same stream: the correction of
-// the conv's pre-bias ring values (the outside taps of the zero-padded upsampled image).  Round 5
-// measured the two alternatives the ABI allows (rrin_edge_fix_desc.full, the ring from scratch:
-// beside the conv on a side stream, or after it) and both lost; the product has
-// this one mode.
+// edge-replicated) -> CAT[L][0, C), and the ring pixels: fp16 / split16 from scratch in the conv's
+// own launch (ring_full), exact fp32 by the correction of the conv's pre-bias ring values (the
+// outside taps of the zero-padded upsampled image) as a second launch on the same stream.  Round 5
+// measured the ring from scratch beside the conv on a side stream and after it: both lost
+// (DESIGN.md §5e).
 int upconv_subpixel(const Plan& p, const rrin_conv_weights& cw, int C, const rrin_h8& x, const rrin_h8& up,
                     hipStream_t st) {
   if (cw.subpixel == 2) {  // ring folded into the conv (Winograd kind 3, no split)
@@ -466,10 +469,10 @@ int upconv_subpixel(const Plan& p, const rrin_conv_weights& cw, int C, const rri
   e.status = p.status;
   e.full = 0;
 #ifndef RRIN_SKIP_RING_FIX
-  if (kRingInLaunch && ring_in_launch_ok(cw.cfg, 2 * C, p.prec)) {
-    // the ring from scratch in extra workgroups of the conv's own launch (ABI 17 ring_full):
-    // no separate fix-up launch and no dependency step on this stream (C3: the separate
-    // fix-ups cost ~3.5 %, profiles/r06/ring/)
+  if (kRingInLaunch && p.prec != RRIN_PREC_F32R && (2 * C) % kFixCi == 0) {
+    // the ring from scratch (ABI 17 ring_full): where the tile allows, extra workgroups of the
+    // conv's own launch -- no separate fix-up launch and no dependency step on this stream (C3:
+    // the separate fix-ups cost ~3.5 %, profiles/r06/ring/)
     e.full = 1;
     return conv_h8(p, cw, 2 * C, 4 * C, RRIN_EPI_SUBPIXEL, x, up, nullptr, st, p.EDGE, false, &e);
   }

@@ -228,7 +228,8 @@ def test_net_scratch_bytes():
     """rrin_net_scratch_bytes (ABI 12): the split-K / ring fix-up scratch lives outside the
     workspace, sized by the conv table -- none for an unsplit 720p x 4 forward (its ring
     fix-up grids exceed the cross-split limit), the ring fix-up's K split alone for
-    640x368 x 1, more with split-K convs; zero for the other precisions."""
+    640x368 x 1, more with split-K convs; zero for the other precisions (their ring runs
+    from scratch in the conv launch, ABI 17)."""
     import ctypes as C
     lib = _lib.lib()
     assert lib.rrin_net_conv_count() == 77
