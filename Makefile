@@ -57,7 +57,7 @@ $(OBJ_DIR)/%.o: $(SRC_DIR)/%.hip $(HDRS)
 $(LIB): $(OBJS) $(ISA_OK)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(OBJS)
 
-LAB_SRCS := $(SRC_DIR)/conv_f16.hip $(SRC_DIR)/conv_block0.hip $(SRC_DIR)/conv_wino.hip $(SRC_DIR)/conv_winoc.hip $(SRC_DIR)/conv_winoh.hip
+LAB_SRCS := $(SRC_DIR)/conv_f16.hip $(SRC_DIR)/conv_block0.hip $(SRC_DIR)/conv_wino.hip $(SRC_DIR)/conv_winoc.hip $(SRC_DIR)/conv_winoc42.hip $(SRC_DIR)/conv_winoh.hip
 $(LAB): $(LAB_SRCS) $(SRC_DIR)/common.hpp include/rrin_hip.h
 	$(HIPCC) $(CXXFLAGS) -DRRIN_LAB -shared -o $@ $(LAB_SRCS)
 

@@ -72,7 +72,8 @@ WINO_KERNELS = {1: "conv3x3_wino_kernel (BM 32 x TH 8, 4 waves of 8 accumulators
                 3: "conv3x3_winoq_kernel (BM 32 x TH 8, 8 waves of 4 accumulators)",
                 4: "conv3x3_winoq_kernel (BM 32 x TH 4, 4 waves)",
                 6: "conv3x3_winoc_kernel (register-U, BM 64 x TH 4, 4 waves of 2 co tiles)",
-                7: "conv3x3_winoc_kernel (register-U, BM 32 x TH 8, 4 waves of 2 patch tiles)"}
+                7: "conv3x3_winoc_kernel (register-U, BM 32 x TH 8, 4 waves of 2 patch tiles)",
+                14: "conv3x3_winoc42_kernel (register-U, Winograd F(4,3) x F(2,3), BM 32 x TH 8, 4 waves)"}
 # fp16 Winograd tiles (conv_winoh.hip)
 WINO_KERNELS_F16 = {6: "conv3x3_winoh_kernel (register-U, BM 64 x TH 4)"}
 
@@ -155,6 +156,9 @@ def parse():
                          "(engine.WINO_SPLIT_LEVELS, replaces the geometry rule); 'none' disables split-K (engine.GEOM_SPLIT)")
     ap.add_argument("--no-ring-fold", action="store_true",
                     help="A/B: run the sub-pixel ring fix-up as its own launch (engine.RING_FOLD = False)")
+    ap.add_argument("--wino42-levels", default=None,
+                    help="exact fp32: grid levels whose convs run Winograd F(4,3) x F(2,3) (kind 14), e.g. "
+                         "'2,3' or 'none' (engine.WINO42_LEVELS)")
     ap.add_argument("--wino-kind32", type=int, default=None,
                     help="A/B: Winograd kind of the 32-output-channel convs in the auto mode "
                          "(engine.WINO_KIND32: 3 or 7)")
@@ -418,6 +422,8 @@ def main():
         engine_mod.RING_FOLD = False
     if args.no_wino_th4:
         engine_mod.WINO_TH4 = {}
+    if args.wino42_levels is not None:
+        engine_mod.WINO42_LEVELS = tuple(int(v) for v in args.wino42_levels.split(",") if v and v != "none")
     if args.wino_kind32 is not None:
         engine_mod.WINO_KIND32 = args.wino_kind32
     net = Net()
@@ -557,6 +563,9 @@ def main():
                     "conv_algorithm": algo,
                     "flops_basis": ("FLOPs of the algorithm the convs run: Winograd F(2x2,3x3) = 16 multiply-adds "
                                     "per 2x2 output patch and channel pair (4/9 of the direct form's)"
+                                    + (f"; F(4,3) x F(2,3) (kind 14, grid levels {list(engine_mod.WINO42_LEVELS)}) = 24 "
+                                       "per 4x2 patch (3/9)" if args.precision == "fp32" and engine_mod.WINO42_LEVELS
+                                       else "")
                                     + (("; the 6-channel first conv runs the direct form (engine.WINO_DIRECT) and counts "
                                         "its direct-form FLOPs" if args.precision == "fp32" else
                                         "; the direct-form convs (engine.wino_f16_ok false: level 0, cout 32, cin % 16) "
@@ -584,6 +593,11 @@ def main():
                 up = tag.endswith(".up") and lvl <= eng.subpixel_max_level
                 ok = engine_mod.wino_f16_ok(cin, 4 * cout if up else cout, lvl + 1 if up else lvl)
                 return 4.0 / 9.0 if ok else 1.0
+        if args.precision == "fp32" and algo in ("winograd", "mixed") and engine_mod.WINO42_LEVELS:
+            def fscale(tag, cin, cout, lvl):  # kind 14 where engine.wino42_ok puts it
+                up = tag.endswith(".up") and lvl <= eng.subpixel_max_level
+                ok = engine_mod.wino42_ok(cin, 4 * cout if up else cout, lvl + 1 if up else lvl)
+                return 3.0 / 9.0 if ok else 4.0 / 9.0
         tlb = B * sum(roofline_bound_s(getattr(net, u), H, W, bpv, peak * 1e12, HBM_PEAK_GBS * 1e9, fscale)
                       for u in ("Flow", "refine_flow", "Mask", "final"))
         roofline["t_lb_conv_ms_per_step"] = round(1e3 * tlb, 3)

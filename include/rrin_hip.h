@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define RRIN_ABI_VERSION 17
+#define RRIN_ABI_VERSION 18
 
 #define RRIN_OK 0
 #define RRIN_E_SHAPE (-1)     /* H or W not a multiple of 16, or N < 1          */
@@ -276,7 +276,11 @@ int64_t rrin_conv_h8_ring_floats(const rrin_conv_h8_desc* d, int64_t* cnt_ints);
  * rrin_pack_conv3x3_wino_h8; cin % 16 == 0 or tail_finite; no split-K, no ring
  * fold).  0: direct form.  -1: a retired id (19, 22: ABI 16 removed the rejected
  * kinds 2, 5 and 8-13 and their configs 25-30; rrin_conv_h8_cfg_ok reports 0 and
- * rrin_conv3x3_h8_fwd returns RRIN_E_CONFIG). */
+ * rrin_conv3x3_h8_fwd returns RRIN_E_CONFIG).  14 (ABI 18, config 25): BM 32 x TH 8 on
+ * 4 waves, register U, Winograd F(4,3) x F(2,3) (patches 4 wide x 2 tall: 0.75x kind 6's
+ * MFMAs; a different rounding, not bitwise the F(2x2,3x3) kinds), packed by
+ * rrin_pack_conv3x3_wino42; cin % 8 == 0 or tail_finite; no split-K, no ring fold, the
+ * ring_full fix-up as a second launch. */
 int rrin_conv_h8_cfg_wino(int32_t cfg);
 
 /* F32R packing: [co_block][chunk of 8 ci][tap][half][bm][4] fp32 (half hh holds
@@ -295,6 +299,14 @@ int rrin_pack_conv3x3_r32(const float* w, const float* b, int32_t cout, int32_t 
 int64_t rrin_pack_conv3x3_wino_bm_floats(int32_t cout, int32_t cin, int32_t bm);
 int rrin_pack_conv3x3_wino_bm(const float* w, const float* b, int32_t cout, int32_t cin, int32_t bm,
                               const int32_t* perm, float* wpack, float* bpack);
+/* Kind-14 packing (ABI 18): U(eta, xi) = sum G2[eta][ky] G4[xi][kx] g[ky][kx] in double,
+ * rounded once to fp32 (G2 the F(2,3) matrix above, rows; G4 = F(4,3)'s [1/4 0 0; -1/6 -1/6
+ * -1/6; -1/6 1/6 -1/6; 1/24 1/12 1/6; 1/24 -1/12 1/6; 0 0 1], columns), laid out
+ * [co_block of 32][chunk of 8 ci][point 6*eta + xi (24)][half 2][co 32][4 ci].  bpack:
+ * rrin_pack_bias_floats(cout, 32) floats. */
+int64_t rrin_pack_conv3x3_wino42_floats(int32_t cout, int32_t cin);
+int rrin_pack_conv3x3_wino42(const float* w, const float* b, int32_t cout, int32_t cin, const int32_t* perm,
+                             float* wpack, float* bpack);
 int64_t rrin_pack_conv3x3_wino_floats(int32_t cout, int32_t cin);
 int rrin_pack_conv3x3_wino(const float* w, const float* b, int32_t cout, int32_t cin, const int32_t* perm,
                            float* wpack, float* bpack);

@@ -320,6 +320,10 @@ int launch_winoq(const ConvH8Args& a, int epi, int th, hipStream_t st);
 constexpr size_t kWinoCLds1 = (size_t)2048 * 16;  // TH 4: 3 x 512 stage records < 2048 exchange
 constexpr size_t kWinoCLds2 = (size_t)4096 * 16;  // TH 8: 3 x 768 < 4096
 int launch_winoc(const ConvH8Args& a, int epi, int ct, hipStream_t st);
+// the register-U tile in Winograd F(4,3) x F(2,3) (conv_winoc42.hip, kind 14): BM 32 x 32 px x
+// TH 8, 4 waves, two blocks per CU; LDS: max(3 raw stages of 768, the 4 x 16 x 64 exchange)
+constexpr size_t kWinoC42Lds = (size_t)4096 * 16;
+int launch_winoc42(const ConvH8Args& a, int epi, hipStream_t st);
 // whether rrin_conv3x3_h8_fwd runs a ring_full fix-up inside the conv's launch for tile config
 // cfg, cin input channels and precision prec (else it launches it after the conv) -- conv_f16.hip
 bool ring_in_launch_ok(int cfg, int cin, int prec);

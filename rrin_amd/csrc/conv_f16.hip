@@ -1551,22 +1551,25 @@ static const CfgH8 kCfgH8[] = {
     {64, 4, kWinoCLds1, (size_t)1 << 30, 0, true, 0, 0},
     // kWinoC1Cfg: register-U tile, BM 32 x TH 8, 4 waves of 2 patch tiles
     {32, 8, kWinoCLds2, (size_t)1 << 30, 0, true, 0, 0},
+    // kWinoC42Cfg (round 6): register-U tile in F(4,3) x F(2,3), BM 32 x TH 8 (conv_winoc42.hip)
+    {32, 8, kWinoC42Lds, (size_t)1 << 30, 0, true, 0, 0},
 };
 static constexpr int kNumCfgH8 = sizeof(kCfgH8) / sizeof(kCfgH8[0]);
-static constexpr int kWinoCfg = kNumCfgH8 - 7;
-static constexpr int kRetired19Cfg = kNumCfgH8 - 6;
-static constexpr int kWinoQCfg = kNumCfgH8 - 5;
-static constexpr int kWinoQ4Cfg = kNumCfgH8 - 4;
-static constexpr int kRetired22Cfg = kNumCfgH8 - 3;
-static constexpr int kWinoC2Cfg = kNumCfgH8 - 2;
-static constexpr int kWinoC1Cfg = kNumCfgH8 - 1;
-static_assert(kWinoCfg == 18, "the direct-form configs keep ids 0-17 (engine tile tables)");
+static constexpr int kWinoCfg = 18;
+static constexpr int kRetired19Cfg = 19;
+static constexpr int kWinoQCfg = 20;
+static constexpr int kWinoQ4Cfg = 21;
+static constexpr int kRetired22Cfg = 22;
+static constexpr int kWinoC2Cfg = 23;
+static constexpr int kWinoC1Cfg = 24;
+static constexpr int kWinoC42Cfg = 25;
+static_assert(kNumCfgH8 == 26, "config ids (engine tables, rrin_hip.h)");
 static inline bool is_winoc(int cfg) { return cfg == kWinoC2Cfg || cfg == kWinoC1Cfg; }
 // Round 6 removed the rejected Winograd tiles (kinds 2, 5, 8-13; DESIGN.md §5b-§5e keep their
 // measurements): ids 19 and 22 stay reserved (rrin_conv_h8_cfg_ok 0, RRIN_E_CONFIG), 25-30 are gone.
 static inline bool retired(int cfg) { return cfg == kRetired19Cfg || cfg == kRetired22Cfg; }
 static inline bool is_wino(int cfg) {
-  return cfg == kWinoCfg || cfg == kWinoQCfg || cfg == kWinoQ4Cfg || is_winoc(cfg);
+  return cfg == kWinoCfg || cfg == kWinoQCfg || cfg == kWinoQ4Cfg || is_winoc(cfg) || cfg == kWinoC42Cfg;
 }
 // the fp16 Winograd tile (conv_winoh.hip): kind 6
 static inline bool is_winoh(int cfg) { return cfg == kWinoC2Cfg; }
@@ -1774,7 +1777,7 @@ static int h8_prepare(const rrin_conv_h8_desc* d, ConvH8Args& a, bool need_scrat
     if (d->prec != RRIN_PREC_F32R) return RRIN_E_CONFIG;
     if ((d->cin & 3) && !d->tail_finite) return RRIN_E_CONFIG;  // stages whole records only
     // the register-U tiles stage both record groups of every chunk: they must exist
-    if (is_winoc(d->cfg) && (d->cin & 7) && !d->tail_finite) return RRIN_E_CONFIG;
+    if ((is_winoc(d->cfg) || d->cfg == kWinoC42Cfg) && (d->cin & 7) && !d->tail_finite) return RRIN_E_CONFIG;
     a.nchunks = (d->cin + 7) / 8;  // two record groups per K chunk
   }
   // the Winograd tiles stage every record group of every chunk (past cin against zero
@@ -1872,15 +1875,17 @@ extern "C" int rrin_conv_h8_cfg_th(int32_t cfg) {
 }
 // 0: direct form; Winograd tile kind: 1 BM 32 / 4 waves, 3 BM 32 / 8 waves, 4 BM 32 x TH 4 / 4 waves;
 // 6 BM 64 x TH 4 and 7 BM 32 x TH 8, register-U tiles (conv_winoc.hip; kind 6 also at fp16,
-// conv_winoh.hip).  The retired ids (19, 22) report -1.
+// conv_winoh.hip); 14 BM 32 x TH 8, the register-U tile in F(4,3) x F(2,3) (conv_winoc42.hip,
+// packed by rrin_pack_conv3x3_wino42).  The retired ids (19, 22) report -1.
 extern "C" int rrin_conv_h8_cfg_wino(int32_t cfg) {
-  return cfg == kWinoCfg     ? 1
-         : cfg == kWinoQCfg  ? 3
-         : cfg == kWinoQ4Cfg ? 4
-         : cfg == kWinoC2Cfg ? 6
-         : cfg == kWinoC1Cfg ? 7
-         : retired(cfg)      ? -1
-                             : 0;
+  return cfg == kWinoCfg      ? 1
+         : cfg == kWinoQCfg   ? 3
+         : cfg == kWinoQ4Cfg  ? 4
+         : cfg == kWinoC2Cfg  ? 6
+         : cfg == kWinoC1Cfg  ? 7
+         : cfg == kWinoC42Cfg ? 14
+         : retired(cfg)       ? -1
+                              : 0;
 }
 // Fused level-0 UNetConvBlock (conv_block0.hip): validate and launch.
 extern "C" int rrin_conv_block0_h8_fwd(const rrin_block0_h8_desc* d, void* stream) {
@@ -1993,6 +1998,7 @@ static int conv3x3_h8_launch(const rrin_conv_h8_desc* d, const ConvH8Args& a, hi
   if (is_winoh(d->cfg) && d->prec == RRIN_PREC_F16) return launch_winoh(a, d->epi_mode, st);
   if (d->cfg == kWinoC2Cfg) return launch_winoc(a, d->epi_mode, 2, st);
   if (d->cfg == kWinoC1Cfg) return launch_winoc(a, d->epi_mode, 1, st);
+  if (d->cfg == kWinoC42Cfg) return launch_winoc42(a, d->epi_mode, st);
   switch (d->cfg) {
 #define X(id, nw, wm, wn, sc, pe) \
   case id:                        \

@@ -1,0 +1,455 @@
+// Exact-fp32 3x3 conv as Winograd F(4,3) x F(2,3) on fp32 records (R32): Winograd kind 14 of
+// the record-layout conv table, the register-U structure of kind 6 (conv_winoc.hip) on patches
+// 4 outputs wide and 2 tall.  24 transform points per patch instead of F(2x2,3x3)'s 16 per 4
+// outputs: 3 MFMAs per output and input channel instead of 4 (0.75x), at the price of a 6-point
+// column transform per lane and one co tile per transform (kind 6 feeds two).
+//
+// Replaces nn.Conv2d(3, pad=1) + LeakyReLU(0.1) (unet.py:29,59-63), the fused avg_pool2d output
+// (unet.py:46), the cat by channel offset (unet.py:93) and the sub-pixel form of Upsample + up
+// conv (unet.py:77-78), as every record-layout conv.
+//
+// Transforms (1D, in double by the packer for G; the input / output ones in fp32 here):
+//   x (F(4,3)): B^T rows  v0 = 4 t0 - 5 t2 + t4        v1 = -4 (t1 + t2) + (t3 + t4)
+//                         v2 = 4 (t1 - t2) + (t4 - t3)  v3 = -2 (t1 - t3) + (t4 - t2)
+//                         v4 = 2 (t1 - t3) + (t4 - t2)  v5 = 4 t1 - 5 t3 + t5
+//               A^T rows  Q0 = (M0 + (M1 + M2)) + (M3 + M4)        Q1 = (M1 - M2) + 2 (M3 - M4)
+//                         Q2 = (M1 + M2) + 4 (M3 + M4)             Q3 = ((M1 - M2) + 8 (M3 - M4)) + M5
+//   y (F(2,3)): kind 6's (wave yw owns B^T row yw; Y0 = (Q0 + Q1) + Q2, Y1 = (Q1 - Q2) - Q3).
+// An output depends only on its 3x3 input footprint (the formulas omit the zero entries), so
+// records past the image (the last tile's rows / columns) never reach a stored output.
+//
+// Tile: BM 32 output channels x 32 px x TH 8 rows = 32 patches (8 columns x 4 rows of 4 x 2).
+// Wave yw (0-3) owns B^T_y row yw (points 6 yw .. 6 yw + 5); lane (j, hh): patch j (column
+// pc = j & 7, row pr = j >> 3) of the MFMA tile, record half hh (channels 4 hh .. + 3 of the
+// 8-channel chunk; MFMA product e contracts channels e and 4 + e).  Per wave and chunk: 24
+// MFMAs, 6 U loads (one record per 4 MFMAs), 12 window reads, ~80 VALU, 3 LDS-DMA pieces.
+// U: rrin_pack_conv3x3_wino_cfg for this kind, [cob][chunk][xi 24][hh][32 co][4 ch].
+#include "common.hpp"
+
+#ifndef RRIN_WINO42_AGPR
+#define RRIN_WINO42_AGPR 0
+#endif
+
+namespace rrin {
+
+typedef float w42f16 __attribute__((ext_vector_type(16)));
+typedef float w42f4 __attribute__((ext_vector_type(4)));
+
+struct W42 {
+  static constexpr int TH = 8;
+  static constexpr int RW = 36;                     // LDS slots per raw row (34 columns + 2 unused)
+  static constexpr int RG = (TH + 2) * RW;          // per record group
+  static constexpr int RAW = 2 * RG;                // per chunk (2 groups)
+  static constexpr int PIECES = (RAW + 255) / 256;  // DMA pieces per thread
+  static constexpr int STAGE = PIECES * 256;        // records per LDS stage (the tail is a dummy)
+  static constexpr int NS = 3;                      // stages: chunk c + 2 lands while c computes
+  static constexpr int XREC = 4 * 16 * 64;          // output-transform exchange: 4 waves x 16 records
+  static constexpr size_t LDS = (size_t)(NS * STAGE > XREC ? NS * STAGE : XREC) * 16;
+};
+static_assert(W42::LDS == kWinoC42Lds, "LDS size (common.hpp)");
+static_assert(2 * W42::LDS <= 160 * 1024, "two blocks per CU");
+
+// LDS slot of raw column col (0..33) in its row: the 8 patch columns 4 pc + k of one k are
+// consecutive slots, so a ds_read_b128 lane group (patches of 2 rows x 4 columns and their
+// neighbours, rows 72 records apart) covers the 64 banks once
+__device__ constexpr int w42_slot(int col) { return (col & 3) * 9 + (col >> 2); }
+
+__device__ inline __amdgpu_buffer_rsrc_t w42_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
+}
+
+template <int EPI>
+__global__ __launch_bounds__(256, 2) void conv3x3_winoc42_kernel(ConvH8Args a) {
+  using G = W42;
+  constexpr int TH = G::TH, RG = G::RG, RW = G::RW, STAGE = G::STAGE, P = G::PIECES;
+  extern __shared__ __attribute__((aligned(16))) uint4 smem4[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int yw = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int j = lane & 31, hh = lane >> 5;
+  const int pc = j & 7, pr = j >> 3;
+  int bid;
+  {  // XCD-aware bijective remap (conv_mfma.hip): an XCD's workgroups are consecutive tiles
+    const int nwg = (int)gridDim.x, q = nwg >> 3, r = nwg & 7;
+    const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+  }
+  const int ntiles = a.co_blocks * a.tiles_x * a.tiles_y * a.n;
+  if (bid >= ntiles) return;
+  const int nch = a.nchunks;
+  int cob, x0, y0, img;
+  {  // co-block groups as kind 6 (launch_winoc42: U of a group fits an XCD's L2)
+    const int cpg = a.cob_group > 0 ? a.cob_group : a.co_blocks;
+    const int gsz = cpg * (ntiles / a.co_blocks);
+    const int g = bid / gsz;
+    const int r = bid - g * gsz;
+    const int cg = min(cpg, a.co_blocks - g * cpg);
+    cob = g * cpg + r % cg;
+    int t = r / cg;
+    x0 = (t % a.tiles_x) * 32;
+    t /= a.tiles_x;
+    y0 = (t % a.tiles_y) * TH;
+    img = t / a.tiles_y;
+  }
+
+  // ---- raw tile: rows y0 - 1 .. y0 + TH, cols x0 - 1 .. x0 + 32 of the chunk's two record
+  // groups, buffer_load ... lds from a per-chunk base; slots past the tile re-read record 0
+  const uint4* tbase = a.src_hi + (int64_t)img * a.src_img + (int64_t)y0 * a.src_wp + x0 + (kH8PadLeft - 1);
+  uint32_t voff[P];
+#pragma unroll
+  for (int it = 0; it < P; ++it) {
+    const int idx = tid + 256 * it;
+    const int g = idx >= RG ? 1 : 0;
+    const int rem = idx < G::RAW ? idx - g * RG : 0;
+    const int r = rem / RW, pos = rem - r * RW;
+    const int m = pos / 9, q = pos - m * 9;
+    const int col = 4 * q + m;
+    const bool ok = idx < G::RAW && col < 34;
+    voff[it] = ok ? (uint32_t)((int64_t)g * a.src_gp + (int64_t)r * a.src_wp + col) * 16u : 0u;
+  }
+  const int64_t chunk_stride = 2 * a.src_gp;
+  auto issue_raw_at = [&](const uint4* base, int s) {
+    const auto rs = w42_rsrc(base);
+#pragma unroll
+    for (int it = 0; it < P; ++it)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rs, (__attribute__((address_space(3))) void*)(smem4 + s * STAGE + 256 * it + 64 * yw), 16, voff[it], 0, 0, 0);
+  };
+  const uint4* raw_next = tbase + (nch > 2 ? 2 : nch - 1) * chunk_stride;
+
+  // ---- U straight into registers: record (chunk c, xi = 6 yw + x, hh, co j) of the co block;
+  // the chunk and the point's upper part in the scalar offset, the rest < 4 KB immediate
+  const auto ur = w42_rsrc(a.w_hi + (int64_t)cob * nch * 1536);
+  const uint32_t uvoff = (uint32_t)(hh * 32 + j) * 16u;
+  auto load_u = [&](int c, int x) {
+    const int soff = c * (1536 * 16) + (6 * yw + (x & 4)) * 1024;
+    return __builtin_bit_cast(w42f4, __builtin_amdgcn_raw_buffer_load_b128(ur, uvoff + (x & 3) * 1024, soff, 0));
+  };
+
+  // ---- B operands: B^T_y row yw combines raw rows ra, rb of the patch (kind 6's rows)
+  const int ra = yw == 0 ? 0 : (yw == 2 ? 2 : 1);
+  const int rb = yw == 0 ? 2 : (yw == 1 ? 2 : (yw == 2 ? 1 : 3));
+  const float sg = yw == 1 ? 1.f : -1.f;
+  const int lbase = hh * RG + 2 * pr * RW + pc;
+  const int oa = lbase + ra * RW, ob = lbase + rb * RW;
+
+  w42f16 acc[6];
+#pragma unroll
+  for (int x = 0; x < 6; ++x) acc[x] = w42f16{};
+  w42f4 u[6];   // U of the chunk being computed (point x reloaded after its MFMAs)
+  w42f4 v[6];   // B operands of the chunk being computed
+  w42f4 d[12];  // window records of the next chunk: rows ra / rb, columns 0-5
+
+  auto read_raw = [&](int s) {
+    const uint4* rw = smem4 + s * STAGE;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      d[2 * k] = __builtin_bit_cast(w42f4, rw[oa + w42_slot(k)]);
+      d[2 * k + 1] = __builtin_bit_cast(w42f4, rw[ob + w42_slot(k)]);
+    }
+  };
+  w42f4 t[6];
+  auto rows = [&]() {
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) t[k][e] = fmaf(sg, d[2 * k + 1][e], d[2 * k][e]);
+  };
+  auto cols_a = [&]() {  // points 0-2
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[0][e] = fmaf(4.f, t[0][e], fmaf(-5.f, t[2][e], t[4][e]));
+      v[1][e] = fmaf(-4.f, t[1][e] + t[2][e], t[3][e] + t[4][e]);
+      v[2][e] = fmaf(4.f, t[1][e] - t[2][e], t[4][e] - t[3][e]);
+    }
+  };
+  auto cols_b = [&]() {  // points 3-5
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float p = t[1][e] - t[3][e], s = t[4][e] - t[2][e];
+      v[3][e] = fmaf(-2.f, p, s);
+      v[4][e] = fmaf(2.f, p, s);
+      v[5][e] = fmaf(4.f, t[1][e], fmaf(-5.f, t[3][e], t[5][e]));
+    }
+  };
+  auto mfma_point = [&](int x) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc[x] = __builtin_amdgcn_mfma_f32_32x32x2f32(u[x][e], v[x][e], acc[x], 0, 0, 0);
+  };
+  auto bar = [&]() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+  auto fence = [&]() { __builtin_amdgcn_sched_barrier(0); };
+
+  // Chunk c (U(c) in u, its B operands in v), MORE: it has a successor.  Points 0-2, each
+  // followed by the load of its U for chunk c + 1; the wait for raw(c + 1) (issued a chunk ago;
+  // U(c) pts 3-5 and U(c + 1) pts 0-2 stay in flight); the barrier; raw(c + 2) -> the free stage;
+  // chunk c + 1's window reads under points 3-4, its row combination and points 0-2, point 5,
+  // its points 3-5; U(c + 1) pts 3-5 after their MFMAs.  VMEM order per chunk: U pts 0-2,
+  // raw(c + 2), U pts 3-5 -- the same every chunk (the prologue matches it).
+  auto chunk = [&](int c, int s, const bool more) {
+#pragma unroll
+    for (int x = 0; x < 3; ++x) {
+      mfma_point(x);
+      if (more) u[x] = load_u(c + 1, x);
+      fence();
+    }
+    if (more) {
+      RRIN_VMWAIT(0, 6);
+      bar();
+      issue_raw_at(raw_next, s == 0 ? 2 : s - 1);
+      if (c + 3 < nch) raw_next += chunk_stride;
+      read_raw(s == 2 ? 0 : s + 1);
+    }
+    fence();
+    mfma_point(3);
+    if (more) u[3] = load_u(c + 1, 3);
+    fence();
+    mfma_point(4);
+    if (more) u[4] = load_u(c + 1, 4);
+    fence();
+    if (more) {
+      rows();
+      cols_a();
+    }
+    fence();
+    mfma_point(5);
+    if (more) u[5] = load_u(c + 1, 5);
+    fence();
+    if (more) cols_b();
+  };
+
+  // prologue in the steady state's VMEM order: raw(0), U(0) pts 0-2, raw(1), U(0) pts 3-5;
+  // wait for raw(0); chunk 0's B operands
+  issue_raw_at(tbase, 0);
+  vm_fence();
+#pragma unroll
+  for (int x = 0; x < 3; ++x) u[x] = load_u(0, x);
+  vm_fence();
+  issue_raw_at(nch > 1 ? tbase + chunk_stride : tbase, 1);
+  vm_fence();
+#pragma unroll
+  for (int x = 3; x < 6; ++x) u[x] = load_u(0, x);
+  vm_fence();
+  RRIN_VMWAIT(P, 6);
+  bar();
+  read_raw(0);
+  rows();
+  cols_a();
+  cols_b();
+  {
+    int s = 0;
+    for (int c = 0; c + 1 < nch; ++c) {
+      chunk(c, s, true);
+      s = s == 2 ? 0 : s + 1;
+    }
+    chunk(nch - 1, s, false);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMA past the end has landed
+  float bsv[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) bsv[i] = a.bias[cob * 32 + 8 * (i >> 2) + 4 * hh + (i & 3)];
+#if RRIN_WINO42_AGPR
+  asm volatile("" ::"a"(acc[0][0]));
+#endif
+  __syncthreads();  // every read of the stages done before the exchange reuses the LDS
+
+  // ---- output transform: Q[c] = A^T_x row c of this wave's six points, written as 16 records
+  // per lane (record k: values 4 k .. 4 k + 3 of c = k >> 2); wave yw then finishes output row
+  // r = yw & 1, columns 2 cp, 2 cp + 1 (cp = yw >> 1) of its patches from the four waves' Q
+  w42f4* X = reinterpret_cast<w42f4*>(smem4);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    w42f4 g;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int vi = 4 * k + e, c = vi >> 4, i = vi & 15;
+      const float m0 = acc[0][i], m1 = acc[1][i], m2 = acc[2][i], m3 = acc[3][i], m4 = acc[4][i], m5 = acc[5][i];
+      g[e] = c == 0   ? (m0 + (m1 + m2)) + (m3 + m4)
+             : c == 1 ? fmaf(2.f, m3 - m4, m1 - m2)
+             : c == 2 ? fmaf(4.f, m3 + m4, m1 + m2)
+                      : fmaf(8.f, m3 - m4, m1 - m2) + m5;
+    }
+    X[(yw * 16 + k) * 64 + lane] = g;
+  }
+  __syncthreads();
+  const int r = yw & 1, cp = yw >> 1;
+  float yv[2][16];
+#pragma unroll
+  for (int cc = 0; cc < 2; ++cc)
+#pragma unroll
+    for (int k4 = 0; k4 < 4; ++k4) {
+      const int k = 4 * (2 * cp + cc) + k4;
+      const w42f4 q0 = X[(0 * 16 + k) * 64 + lane];
+      const w42f4 q1 = X[(1 * 16 + k) * 64 + lane];
+      const w42f4 q2 = X[(2 * 16 + k) * 64 + lane];
+      const w42f4 q3 = X[(3 * 16 + k) * 64 + lane];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) yv[cc][4 * k4 + e] = r == 0 ? (q0[e] + q1[e]) + q2[e] : (q1[e] - q2[e]) - q3[e];
+    }
+  uint4* dst = a.dst_hi + (int64_t)img * a.dst_img;
+  auto store4 = [&](int64_t rec, const float* vv) {
+    dst[rec] = make_uint4(__float_as_uint(vv[0]), __float_as_uint(vv[1]), __float_as_uint(vv[2]), __float_as_uint(vv[3]));
+  };
+  const int y = y0 + 2 * pr + r;
+  if constexpr (EPI == RRIN_EPI_SUBPIXEL) {
+    const int HH = 2 * a.h, WW = 2 * a.w, creal = a.cout >> 2;
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc) {
+      const int x = x0 + 4 * pc + 2 * cp + cc;
+      if (cob * 32 < a.cout && y < a.h && x < a.w) {
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          const int Y = 2 * y + (qq >> 1), XX = 2 * x + (qq & 1);
+          const int64_t ri = ring_index(Y, XX, HH, WW);
+          if (ri >= 0) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              a.edge[((int64_t)img * creal + cob * 8 + 4 * hh + e) * a.ring + ri] = yv[cc][4 * qq + e];
+          } else {
+            float vv[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) vv[e] = yv[cc][4 * qq + e] + bsv[4 * qq + e];
+            store4((int64_t)(2 * cob + hh) * a.dst_gp + (int64_t)(Y + 1) * a.dst_wp + XX + kH8PadLeft, vv);
+          }
+        }
+      }
+    }
+  } else {
+    float vv[2][16];
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc) {
+      const int x = x0 + 4 * pc + 2 * cp + cc;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        float tv = yv[cc][i] + bsv[i];
+        if constexpr (EPI != RRIN_EPI_LINEAR) tv = leaky(tv, a.slope);
+        vv[cc][i] = tv;
+      }
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        if (cob * 32 + 8 * qq < a.cout && y < a.h && x < a.w) {
+          const int64_t rec = (int64_t)(cob * 8 + 2 * qq + hh) * a.dst_gp + (int64_t)(y + 1) * a.dst_wp + x + kH8PadLeft;
+          store4(rec, &vv[cc][4 * qq]);
+          if constexpr (EPI == RRIN_EPI_LEAKY_REP) {  // edge replicate into the padding ring
+            const int dy0 = y == 0 ? -1 : 0, dy1 = y == a.h - 1 ? 1 : 0;
+            const int dx0 = x == 0 ? -1 : 0, dx1 = x == a.w - 1 ? 1 : 0;
+            for (int dy = dy0; dy <= dy1; ++dy)
+              for (int dx = dx0; dx <= dx1; ++dx)
+                if (dy | dx) store4(rec + (int64_t)dy * a.dst_wp + dx, &vv[cc][4 * qq]);
+          }
+        }
+      }
+    }
+    if constexpr (EPI == RRIN_EPI_LEAKY_POOL) {
+      // rows 0 and 1 of a pool pair sit in waves yw and yw ^ 1: each wave parks its two columns,
+      // the row-0 wave writes avg = 0.25 ((Y00 + Y10) + (Y01 + Y11))
+      __syncthreads();  // every read of the Q exchange done
+#pragma unroll
+      for (int cc = 0; cc < 2; ++cc)
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          w42f4 g;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) g[e] = vv[cc][4 * qq + e];
+          X[((yw * 2 + cc) * 4 + qq) * 64 + lane] = g;
+        }
+      __syncthreads();
+      if (r == 0) {
+        const int xp = x0 + 4 * pc + 2 * cp, yp = y0 + 2 * pr;
+        uint4* pdst = a.pool_hi + (int64_t)img * a.pool_img;
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          const w42f4 y00 = X[((yw * 2 + 0) * 4 + qq) * 64 + lane];
+          const w42f4 y01 = X[((yw * 2 + 1) * 4 + qq) * 64 + lane];
+          const w42f4 y10 = X[(((yw + 1) * 2 + 0) * 4 + qq) * 64 + lane];
+          const w42f4 y11 = X[(((yw + 1) * 2 + 1) * 4 + qq) * 64 + lane];
+          if (cob * 32 + 8 * qq < a.cout && yp < a.h && xp < a.w) {
+            float s4[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) s4[e] = 0.25f * ((y00[e] + y10[e]) + (y01[e] + y11[e]));
+            const int64_t rec =
+                (int64_t)(cob * 8 + 2 * qq + hh) * a.pool_gp + (int64_t)(yp / 2 + 1) * a.pool_wp + xp / 2 + kH8PadLeft;
+            pdst[rec] = make_uint4(__float_as_uint(s4[0]), __float_as_uint(s4[1]), __float_as_uint(s4[2]),
+                                   __float_as_uint(s4[3]));
+          }
+        }
+      }
+    }
+  }
+}
+
+template <int EPI>
+static int launch_winoc42_k(const ConvH8Args& a, hipStream_t st) {
+  auto k = conv3x3_winoc42_kernel<EPI>;
+  static LdsAttr attr;
+  if (int e = attr.ensure((const void*)k, (int)W42::LDS, st)) return e;
+  const int64_t grid = (int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n;
+  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256), W42::LDS, st, a);
+  return hip_code(hipGetLastError());
+}
+
+// co-block groups whose U fits kWinoCUGroupBytes of an XCD's L2 (as launch_winoc)
+#ifndef RRIN_WINO42_UGROUP_KB
+#define RRIN_WINO42_UGROUP_KB 2048
+#endif
+int launch_winoc42(const ConvH8Args& a, int epi, hipStream_t st) {
+  ConvH8Args b = a;
+  const int64_t per_cob = (int64_t)a.nchunks * 1536 * 16;
+  b.cob_group = 0;
+  if (RRIN_WINO42_UGROUP_KB > 0 && (int64_t)a.co_blocks * per_cob > (int64_t)RRIN_WINO42_UGROUP_KB * 1024) {
+    int g = 1;
+    while (2 * g < a.co_blocks && 2 * g * per_cob <= (int64_t)RRIN_WINO42_UGROUP_KB * 1024) g *= 2;
+    b.cob_group = g;
+  }
+  switch (epi) {
+    case RRIN_EPI_LINEAR: return launch_winoc42_k<RRIN_EPI_LINEAR>(b, st);
+    case RRIN_EPI_LEAKY: return launch_winoc42_k<RRIN_EPI_LEAKY>(b, st);
+    case RRIN_EPI_LEAKY_POOL: return launch_winoc42_k<RRIN_EPI_LEAKY_POOL>(b, st);
+    case RRIN_EPI_LEAKY_REP: return launch_winoc42_k<RRIN_EPI_LEAKY_REP>(b, st);
+    case RRIN_EPI_SUBPIXEL: return launch_winoc42_k<RRIN_EPI_SUBPIXEL>(b, st);
+  }
+  return RRIN_E_ARG;
+}
+
+}  // namespace rrin
+
+using namespace rrin;
+
+// Kind-14 packing: [co block of 32][8-channel chunk][point xi = 6 eta + xi_x][record half][32 co][4 ch],
+// U(eta, xi_x) = sum G2[eta][ky] G4[xi_x][kx] g[ky][kx] in double, rounded once to fp32
+extern "C" int64_t rrin_pack_conv3x3_wino42_floats(int32_t cout, int32_t cin) {
+  if (cout < 1 || cin < 1) return RRIN_E_ARG;
+  return (int64_t)((cout + 31) / 32) * ((cin + 7) / 8) * 24 * 2 * 32 * 4;
+}
+
+extern "C" int rrin_pack_conv3x3_wino42(const float* w, const float* b, int32_t cout, int32_t cin, const int32_t* perm,
+                                        float* wpack, float* bpack) {
+  if (!w || !b || !wpack || !bpack || cout < 1 || cin < 1) return RRIN_E_ARG;
+  if (perm)
+    for (int c = 0; c < cin; ++c)
+      if (perm[c] < 0 || perm[c] >= cin) return RRIN_E_ARG;
+  static const double G2[4][3] = {{1.0, 0.0, 0.0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0.0, 0.0, 1.0}};
+  static const double G4[6][3] = {{0.25, 0.0, 0.0},
+                                  {-1.0 / 6, -1.0 / 6, -1.0 / 6},
+                                  {-1.0 / 6, 1.0 / 6, -1.0 / 6},
+                                  {1.0 / 24, 1.0 / 12, 1.0 / 6},
+                                  {1.0 / 24, -1.0 / 12, 1.0 / 6},
+                                  {0.0, 0.0, 1.0}};
+  const int cob_n = (cout + 31) / 32, nch = (cin + 7) / 8;
+  int64_t o = 0;
+  for (int cob = 0; cob < cob_n; ++cob)
+    for (int c = 0; c < nch; ++c)
+      for (int xi = 0; xi < 24; ++xi)
+        for (int hh = 0; hh < 2; ++hh)
+          for (int col = 0; col < 32; ++col)
+            for (int e = 0; e < 4; ++e) {
+              const int co = cob * 32 + col, ch = c * 8 + hh * 4 + e;
+              double u = 0.0;
+              if (co < cout && ch < cin) {
+                const float* g = w + ((int64_t)co * cin + (perm ? perm[ch] : ch)) * 9;
+                for (int ky = 0; ky < 3; ++ky)
+                  for (int kx = 0; kx < 3; ++kx) u += G2[xi / 6][ky] * G4[xi % 6][kx] * (double)g[ky * 3 + kx];
+              }
+              wpack[o++] = (float)u;
+            }
+  for (int co = 0; co < cob_n * 32; ++co) bpack[co] = co < cout ? b[co] : 0.f;
+  return 0;
+}

@@ -364,9 +364,10 @@ int conv_h8(const Plan& p, const rrin_conv_weights& cw, int cin, int cout, int e
             const rrin_edge_fix_desc* ring_full = nullptr) {
   // algorithmic FLOPs of the conv (a sub-pixel conv has 4 phase rows per real channel): 9
   // multiply-adds per output and input channel in the direct form, 4 in Winograd F(2x2,3x3)
-  // (16 per 2x2 patch)
+  // (16 per 2x2 patch), 3 in F(4,3) x F(2,3) (kind 14: 24 per 4 x 2 patch)
   const int creal = epi == RRIN_EPI_SUBPIXEL ? cout / 4 : cout;
-  const int macs = rrin_conv_h8_cfg_wino(cw.cfg) ? 4 : 9;  // Winograd: exact fp32 (F32R) or fp16 (kind 6)
+  const int wkind = rrin_conv_h8_cfg_wino(cw.cfg);
+  const int macs = wkind == 14 ? 3 : wkind ? 4 : 9;
   ProfScope ps(p.prof, st, RRIN_KIND_CONV, 2.0 * macs * cin * creal * (double)dst.g.h * dst.g.w * p.n);
   rrin_conv_h8_desc d;
   memset(&d, 0, sizeof(d));

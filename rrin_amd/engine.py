@@ -321,6 +321,17 @@ def fused_pairs(convs) -> list:
     return out
 
 
+# exact fp32: the register-U tile in Winograd F(4,3) x F(2,3) (kind 14, conv_winoc42.hip: 3
+# multiply-adds per output and input channel instead of F(2x2,3x3)'s 4, one co tile per
+# transform) on the convs of these grid levels (an up conv: its low-res grid), in every size
+# class -- never the TH-4 / split-K kinds for them, so a pair's bits stay batch-invariant.
+WINO42_LEVELS = ()
+
+
+def wino42_ok(cin: int, cout: int, level: int) -> bool:
+    return level in WINO42_LEVELS and cout % 32 == 0 and cin % 8 == 0
+
+
 def wino_f16_ok(cin: int, cout: int, level: int) -> bool:
     return WINO_F16 and level in WINO_F16_LEVELS and cout % 64 == 0 and cin % 16 == 0
 
@@ -336,6 +347,8 @@ def choose_cfg_h8(cin: int, cout: int, prec: int, level: int = 0, size: str = "l
         c = WINO_DIRECT.get((cin, cout, level))
         if c is not None and _lib.lib().rrin_conv_h8_cfg_fits(c, prec, cin):
             return c
+        if wino42_ok(cin, cout, level):
+            return wino_cfg(14)
         if split > 1:
             return wino_cfg(4)
         return wino_cfg(4 if (cin, cout, level) in WINO_TH4.get(size, ()) else wino_kind_for(cout))
@@ -545,7 +558,11 @@ class RRINEngine:
             if f32:  # fp32 records: unscaled fp32 weights (offsets in floats)
                 bp = np.empty(L.rrin_pack_bias_floats(cout, bm), np.float32)
                 pa = perm_arr.ctypes.data if perm_arr is not None else None
-                if L.rrin_conv_h8_cfg_wino(cfg) > 0:  # Winograd F(2x2,3x3): transformed weights
+                if L.rrin_conv_h8_cfg_wino(cfg) == 14:  # Winograd F(4,3) x F(2,3)
+                    wp = np.empty(L.rrin_pack_conv3x3_wino42_floats(cout, cin), np.float32)
+                    _lib.check(L.rrin_pack_conv3x3_wino42(w.ctypes.data, b.ctypes.data, cout, cin, pa,
+                                                          wp.ctypes.data, bp.ctypes.data), "rrin_pack_conv3x3_wino42")
+                elif L.rrin_conv_h8_cfg_wino(cfg) > 0:  # Winograd F(2x2,3x3): transformed weights
                     wp = np.empty(L.rrin_pack_conv3x3_wino_bm_floats(cout, cin, bm), np.float32)
                     _lib.check(L.rrin_pack_conv3x3_wino_bm(w.ctypes.data, b.ctypes.data, cout, cin, bm, pa,
                                                            wp.ctypes.data, bp.ctypes.data), "rrin_pack_conv3x3_wino_bm")

@@ -91,15 +91,17 @@ def test_wino_config_entry():
     ids = [c for c in range(lib.rrin_conv_h8_cfg_count()) if lib.rrin_conv_h8_cfg_wino(c) > 0]
     # kinds 1 (BM 32, 4 waves), 3 (BM 32, 8 waves of 4 accumulators), TH 8; 4 (kind 3's
     # arithmetic on TH 4 tiles, 4 waves); the register-U tiles 6 (BM 64 x TH 4) and 7 (BM 32 x
-    # TH 8), 4 waves.  Round 6 removed the rejected kinds 2, 5 and 8-13: ids 19 and 22 stay
-    # reserved (kind -1, never usable), 25-30 are gone.
-    assert sorted(lib.rrin_conv_h8_cfg_wino(c) for c in ids) == [1, 3, 4, 6, 7]
+    # TH 8), 4 waves; kind 14 (ABI 18, id 25): the register-U tile in F(4,3) x F(2,3), BM 32 x
+    # TH 8.  Round 6 removed the rejected kinds 2, 5 and 8-13: ids 19 and 22 stay reserved
+    # (kind -1, never usable).
+    assert sorted(lib.rrin_conv_h8_cfg_wino(c) for c in ids) == [1, 3, 4, 6, 7, 14]
     assert min(ids) == 18  # the direct-form configs keep ids 0-17 (engine tile tables)
-    assert lib.rrin_conv_h8_cfg_count() == 25
+    assert lib.rrin_conv_h8_cfg_count() == 26
+    assert lib.rrin_conv_h8_cfg_wino(25) == 14
     assert [lib.rrin_conv_h8_cfg_wino(c) for c in (19, 22)] == [-1, -1]
     assert all(lib.rrin_conv_h8_cfg_ok(c, p) == 0 for c in (19, 22) for p in range(4))
     assert {lib.rrin_conv_h8_cfg_wino(c): lib.rrin_conv_h8_cfg_bm(c) for c in ids} == {
-        1: 32, 3: 32, 4: 32, 6: 64, 7: 32}
+        1: 32, 3: 32, 4: 32, 6: 64, 7: 32, 14: 32}
     for c in ids:
         kind = lib.rrin_conv_h8_cfg_wino(c)
         assert lib.rrin_conv_h8_cfg_th(c) == {4: 4, 6: 4}.get(kind, 8)
@@ -113,6 +115,49 @@ def test_wino_config_entry():
     assert lib.rrin_pack_conv3x3_wino_bm_floats(8, 8, 48) < 0
     assert lib.rrin_pack_conv3x3_wino_h8_halves(65, 17, 64) == 2 * 2 * 16 * 2 * 64 * 8
     assert lib.rrin_pack_conv3x3_wino_h8_halves(64, 16, 32) < 0  # BM 64 only
+    assert lib.rrin_pack_conv3x3_wino42_floats(33, 9) == 2 * 2 * 24 * 2 * 32 * 4
+    assert lib.rrin_pack_conv3x3_wino42_floats(8, 0) < 0
+
+
+# F(4,3) (x) and F(2,3) (y) Winograd matrices of kind 14 (conv_winoc42.hip)
+BT4 = np.array([[4, 0, -5, 0, 1, 0], [0, -4, -4, 1, 1, 0], [0, 4, -4, -1, 1, 0], [0, -2, -1, 2, 1, 0],
+                [0, 2, -1, -2, 1, 0], [0, 4, 0, -5, 0, 1]], np.float64)
+G4 = np.array([[1 / 4, 0, 0], [-1 / 6, -1 / 6, -1 / 6], [-1 / 6, 1 / 6, -1 / 6], [1 / 24, 1 / 12, 1 / 6],
+               [1 / 24, -1 / 12, 1 / 6], [0, 0, 1]], np.float64)
+AT4 = np.array([[1, 1, 1, 1, 1, 0], [0, 1, -1, 2, -2, 0], [0, 1, 1, 4, 4, 0], [0, 1, -1, 8, -8, 1]], np.float64)
+BT2 = np.array([[1, 0, -1, 0], [0, 1, 1, 0], [0, -1, 1, 0], [0, 1, 0, -1]], np.float64)
+G2 = np.array([[1, 0, 0], [.5, .5, .5], [.5, -.5, .5], [0, 0, 1]], np.float64)
+AT2 = np.array([[1, 1, 1, 0], [0, 1, -1, -1]], np.float64)
+
+
+@pytest.mark.parametrize("cout,cin,perm", [(32, 8, False), (72, 40, True), (64, 3, False)])
+def test_pack_wino42_layout(cout, cin, perm):
+    """Kind-14 packing: [cob 32][8-ch chunk][6 eta + xi][half][32 co][4 ci] of
+    U = G2 g G4^T (double, rounded once), zero past cout / cin; and the transform pair it
+    belongs to reproduces a 3x3 correlation on a 4-tall x 6-wide window (2 x 4 outputs)."""
+    lib = _lib.lib()
+    rng = np.random.default_rng(cout * cin)
+    w = rng.standard_normal((cout, cin, 3, 3)).astype(np.float32)
+    b = rng.standard_normal(cout).astype(np.float32)
+    pa = rng.permutation(cin).astype(np.int32) if perm else None
+    wp = np.zeros(lib.rrin_pack_conv3x3_wino42_floats(cout, cin), np.float32)
+    bp = np.zeros(lib.rrin_pack_bias_floats(cout, 32), np.float32)
+    _lib.check(lib.rrin_pack_conv3x3_wino42(w.ctypes.data, b.ctypes.data, cout, cin,
+                                            pa.ctypes.data if perm else None, wp.ctypes.data, bp.ctypes.data))
+    wperm = w[:, pa] if perm else w
+    U = np.einsum("ak,oikl,bl->oiab", G2, wperm.astype(np.float64), G4).reshape(cout, cin, 24)
+    cob, nch = -(-cout // 32), -(-cin // 8)
+    want = np.zeros((cob * 32, nch * 8, 24))
+    want[:cout, :cin] = U
+    want = want.reshape(cob, 32, nch, 2, 4, 24).transpose(0, 2, 5, 3, 1, 4).reshape(-1)
+    np.testing.assert_array_equal(wp, want.astype(np.float32))
+    np.testing.assert_array_equal(bp[:cout], b)
+    # the transform: Y = AT2 [(G2 g G4^T) * (BT2 d BT4^T)] AT4^T on a 4 x 6 input window
+    d = rng.standard_normal((4, 6))
+    g = wperm[0, 0].astype(np.float64)
+    Y = AT2 @ ((G2 @ g @ G4.T) * (BT2 @ d @ BT4.T)) @ AT4.T
+    ref = np.array([[np.sum(d[r:r + 3, c:c + 3] * g) for c in range(4)] for r in range(2)])
+    np.testing.assert_allclose(Y, ref, rtol=1e-12, atol=1e-12)
 
 
 @pytest.mark.parametrize("cout,cin", [(64, 16), (72, 40), (128, 32)])
