@@ -323,13 +323,21 @@ def fused_pairs(convs) -> list:
 
 # exact fp32: the register-U tile in Winograd F(4,3) x F(2,3) (kind 14, conv_winoc42.hip: 3
 # multiply-adds per output and input channel instead of F(2x2,3x3)'s 4, one co tile per
-# transform) on the convs of these grid levels (an up conv: its low-res grid), in every size
-# class -- never the TH-4 / split-K kinds for them, so a pair's bits stay batch-invariant.
-WINO42_LEVELS = ()
+# transform) on the convs of these grid levels (an up conv: its low-res grid) that the geometry
+# rule does not split, in every size class (never the class-dependent TH-4 tiles for them), so a
+# pair's bits stay batch-invariant.
+# Per conv at 1280x720 x 2 (profiles/r06/wino42/): 0.84-0.90 of kind 6's time on every conv of
+# levels 1-4 (every epilogue, the sub-pixel up convs included) and 0.87 on the level-0 64->32
+# conv vs kind 3; the level-0 32->32 convs even (0.98-1.04) and 16->32 1.08, so level 0 takes it
+# from WINO42_MIN_CIN_L0 input channels.  Whole forward, one box interleaved: 1280x720 x 4
+# 143.1-143.7 -> 157.6-157.8 pairs/s, 640x368 x 1 338.6-339.1 -> 357.0-357.5.
+WINO42_LEVELS = (0, 1, 2, 3, 4)
+WINO42_MIN_CIN_L0 = 64
 
 
 def wino42_ok(cin: int, cout: int, level: int) -> bool:
-    return level in WINO42_LEVELS and cout % 32 == 0 and cin % 8 == 0
+    return (WINO_KIND == 0 and level in WINO42_LEVELS and cout % 32 == 0 and cin % 8 == 0
+            and (level > 0 or cin >= WINO42_MIN_CIN_L0))
 
 
 def wino_f16_ok(cin: int, cout: int, level: int) -> bool:
@@ -347,10 +355,10 @@ def choose_cfg_h8(cin: int, cout: int, prec: int, level: int = 0, size: str = "l
         c = WINO_DIRECT.get((cin, cout, level))
         if c is not None and _lib.lib().rrin_conv_h8_cfg_fits(c, prec, cin):
             return c
+        if split > 1:  # the per-image geometry split-K (kind 4) first: batch-invariant either way
+            return wino_cfg(4)
         if wino42_ok(cin, cout, level):
             return wino_cfg(14)
-        if split > 1:
-            return wino_cfg(4)
         return wino_cfg(4 if (cin, cout, level) in WINO_TH4.get(size, ()) else wino_kind_for(cout))
     if prec == _lib.PREC_F16 and wino_f16_ok(cin, cout, level):
         return wino_cfg(WINO_F16_KIND)

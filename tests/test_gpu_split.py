@@ -76,10 +76,13 @@ def test_split_net(gpu):
     """Split-K in the Net: the geometry rule (engine.geom_split, the default: 128x192
     images split their level-3/4 convs) and levels 2-4 split by the A/B override with
     every conv on a split-capable tile; each within fp32 rounding of the unsplit Net,
-    batch == per-sample bitwise with the split."""
+    batch == per-sample bitwise with the split.  The F(2x2,3x3) kinds only (engine.WINO42_LEVELS
+    off): kind 14 rounds differently from the split kinds."""
     net = make_net(gpu, stress=True)
     saved = dict(engine_mod.WINO_SPLIT_LEVELS)
     saved_geo, saved_kind = engine_mod.GEOM_SPLIT, engine_mod.WINO_KIND
+    saved42 = engine_mod.WINO42_LEVELS
+    engine_mod.WINO42_LEVELS = ()
     try:
         i0, i1 = synthetic_batch(2, 128, 192)
         i0, i1 = i0.to(gpu), i1.to(gpu)
@@ -104,4 +107,5 @@ def test_split_net(gpu):
         engine_mod.WINO_SPLIT_LEVELS.clear()
         engine_mod.WINO_SPLIT_LEVELS.update(saved)
         engine_mod.GEOM_SPLIT, engine_mod.WINO_KIND = saved_geo, saved_kind
+        engine_mod.WINO42_LEVELS = saved42
         net._engine = None
