@@ -83,11 +83,11 @@ def main():
     if a.table:
         # the conv family = every body-conv kernel (bench.py's roofline covers all 77 body
         # convs of a forward part): exact fp32 runs the Winograd tiles (kinds 3/4:
-        # conv3x3_winoq_kernel, 6/7: conv3x3_winoc_kernel) and the direct-form first conv
+        # conv3x3_winoq_kernel, 6/7: conv3x3_winoc_kernel, 14: conv3x3_winoc42_kernel) and the direct-form first conv
         # (fp16: the fused level-0 UNetConvBlock kernel runs 2 body convs per launch -- omitting it
         # dropped a third of the C3 conv bytes from the round-5 line)
         fam_name = a.family or {"fp32_planar": "conv3x3_mfma_kernel",
-                                "fp32": "conv3x3_winoq_kernel,conv3x3_winoc_kernel,conv3x3_h8_kernel",
+                                "fp32": "conv3x3_winoq_kernel,conv3x3_winoc_kernel,conv3x3_winoc42_kernel,conv3x3_h8_kernel",
                                 "fp16": "conv3x3_h8_kernel,conv3x3_winoh_kernel,conv_block0_h8_kernel"}.get(
             a.precision, "conv3x3_h8_kernel")
         names = [n for n in fam_name.split(",") if n in res]
