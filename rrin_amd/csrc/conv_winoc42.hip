@@ -29,6 +29,12 @@
 #ifndef RRIN_WINO42_AGPR
 #define RRIN_WINO42_AGPR 0
 #endif
+// A/B: 1 = point 5's MFMAs interleaved with the next chunk's row combination and points 0-2
+// transform (sched_group_barrier: 1 MFMA, then 12 VALU) instead of after them; 2 = also the
+// points 3-5 transform deferred into the next chunk, beside its point-0 MFMAs
+#ifndef RRIN_WINO42_SCHED
+#define RRIN_WINO42_SCHED 0
+#endif
 
 namespace rrin {
 
@@ -184,9 +190,24 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winoc42_kernel(ConvH8Args a) {
   // chunk c + 1's window reads under points 3-4, its row combination and points 0-2, point 5,
   // its points 3-5; U(c + 1) pts 3-5 after their MFMAs.  VMEM order per chunk: U pts 0-2,
   // raw(c + 2), U pts 3-5 -- the same every chunk (the prologue matches it).
-  auto chunk = [&](int c, int s, const bool more) {
+  auto chunk = [&](int c, int s, const bool more, const bool pend) {
+    if constexpr (RRIN_WINO42_SCHED == 2) {
+      // points 3-5's operands of this chunk (deferred from the previous one) beside point 0
+      if (pend) cols_b();
+      mfma_point(0);
+      if (pend) {
 #pragma unroll
-    for (int x = 0; x < 3; ++x) {
+        for (int k = 0; k < 4; ++k) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);
+        }
+      }
+      fence();
+      if (more) u[0] = load_u(c + 1, 0);
+      fence();
+    }
+#pragma unroll
+    for (int x = RRIN_WINO42_SCHED == 2 ? 1 : 0; x < 3; ++x) {
       mfma_point(x);
       if (more) u[x] = load_u(c + 1, x);
       fence();
@@ -205,15 +226,33 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winoc42_kernel(ConvH8Args a) {
     mfma_point(4);
     if (more) u[4] = load_u(c + 1, 4);
     fence();
-    if (more) {
-      rows();
-      cols_a();
+    if constexpr (RRIN_WINO42_SCHED >= 1) {
+      if (more) {
+        rows();
+        cols_a();
+      }
+      mfma_point(5);
+      if (more) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, 12, 0);
+        }
+      }
+      fence();
+      if (more) u[5] = load_u(c + 1, 5);
+      fence();
+    } else {
+      if (more) {
+        rows();
+        cols_a();
+      }
+      fence();
+      mfma_point(5);
+      if (more) u[5] = load_u(c + 1, 5);
+      fence();
     }
-    fence();
-    mfma_point(5);
-    if (more) u[5] = load_u(c + 1, 5);
-    fence();
-    if (more) cols_b();
+    if (RRIN_WINO42_SCHED != 2 && more) cols_b();
   };
 
   // prologue in the steady state's VMEM order: raw(0), U(0) pts 0-2, raw(1), U(0) pts 3-5;
@@ -237,10 +276,10 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winoc42_kernel(ConvH8Args a) {
   {
     int s = 0;
     for (int c = 0; c + 1 < nch; ++c) {
-      chunk(c, s, true);
+      chunk(c, s, true, c > 0);
       s = s == 2 ? 0 : s + 1;
     }
-    chunk(nch - 1, s, false);
+    chunk(nch - 1, s, false, nch > 1);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMA past the end has landed
   float bsv[16];

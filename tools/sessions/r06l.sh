@@ -38,4 +38,13 @@ for d in pmc_sq1 pmc_sq2; do
   done
 done
 head -20 $O/sum_pmc_sq1_conv3x3_winoc42_kernel.txt
+# A/B: conv_winoc42.hip under the max-ilp machine scheduler (ab/librrin_hip_w42ilp.so)
+SH="64:64:1:1,128:64:1:1,128:128:2:1,256:128:2:1,256:256:3:1,512:256:3:1,512:512:4:1,1024:512:4:1,256:512:2:4,64:32:0:1"
+run cfg_ilp 300 env RRIN_LIB_AB=ab/librrin_hip_w42ilp.so python tools/conv_lab.py cfgab --cfgs 25,23 --batch 2 --rounds 5 --shapes $SH
+run cfg_def 300 python tools/conv_lab.py cfgab --cfgs 25,23 --batch 2 --rounds 5 --shapes $SH
+HL="--steps 20 --warmup 5 --cpu-baseline off --no-alt"
+for k in 1 2; do
+run hl_def$k 200 python bench.py $HL
+run hl_ilp$k 200 env RRIN_LIB_AB=ab/librrin_hip_w42ilp.so python bench.py $HL
+done
 exit 0
