@@ -417,30 +417,17 @@ __global__ __launch_bounds__(256, 2) void conv_block0_h8_kernel(Block0Args a) {
   if (bad && a.status) *a.status = 1;
 }
 
-// CUs of the stream's device (cached per device)
-static int block0_cus(hipStream_t st) {
-  static std::atomic<int> cus[kMaxDevices];
-  const int dev = stream_device(st);
-  int ncu = cus[dev].load(std::memory_order_relaxed);
-  if (ncu <= 0) {
-    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
-    cus[dev].store(ncu, std::memory_order_relaxed);
-  }
-  return ncu;
-}
-
-#ifndef RRIN_BLOCK0_BPC
-#define RRIN_BLOCK0_BPC 0  // persistent workgroups per CU (the LDS holds two); 0: one tile per workgroup
-#endif
+// One tile per workgroup.  The kernel can walk tiles bid, bid + grid, ... with the next tile's
+// chunk 0 staged behind the current epilogue, but no build launches fewer workgroups than tiles:
+// round 5's persistent grids (RRIN_BLOCK0_BPC, kind 10) lost in the forward and kind 10 ran
+// nondeterministically, so the knob is gone and the walk never takes a second tile.
 template <bool POOL>
 static int launch_block0_k(const Block0Args& a, hipStream_t st) {
   auto k = conv_block0_h8_kernel<POOL>;
   static LdsAttr attr;
   if (int e = attr.ensure((const void*)k, (int)kB0Lds, st)) return e;
   const int64_t tiles = (int64_t)a.tiles_x * a.tiles_y * a.n;
-  const int64_t grid =
-      RRIN_BLOCK0_BPC > 0 ? std::min<int64_t>(tiles, (int64_t)RRIN_BLOCK0_BPC * block0_cus(st)) : tiles;
-  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256), kB0Lds, st, a);
+  hipLaunchKernelGGL(k, dim3((unsigned)tiles), dim3(256), kB0Lds, st, a);
   return hip_code(hipGetLastError());
 }
 
