@@ -159,6 +159,8 @@ def parse():
     ap.add_argument("--wino42-levels", default=None,
                     help="exact fp32: grid levels whose convs run Winograd F(4,3) x F(2,3) (kind 14), e.g. "
                          "'2,3' or 'none' (engine.WINO42_LEVELS)")
+    ap.add_argument("--wino42-min-cin-l0", type=int, default=None,
+                    help="A/B: smallest cin of a level-0 conv on kind 14 (engine.WINO42_MIN_CIN_L0)")
     ap.add_argument("--wino-kind32", type=int, default=None,
                     help="A/B: Winograd kind of the 32-output-channel convs in the auto mode "
                          "(engine.WINO_KIND32: 3 or 7)")
@@ -424,6 +426,8 @@ def main():
         engine_mod.WINO_TH4 = {}
     if args.wino42_levels is not None:
         engine_mod.WINO42_LEVELS = tuple(int(v) for v in args.wino42_levels.split(",") if v and v != "none")
+    if args.wino42_min_cin_l0 is not None:
+        engine_mod.WINO42_MIN_CIN_L0 = args.wino42_min_cin_l0
     if args.wino_kind32 is not None:
         engine_mod.WINO_KIND32 = args.wino_kind32
     net = Net()

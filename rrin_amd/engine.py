@@ -328,11 +328,13 @@ def fused_pairs(convs) -> list:
 # pair's bits stay batch-invariant.
 # Per conv at 1280x720 x 2 (profiles/r06/wino42/): 0.84-0.90 of kind 6's time on every conv of
 # levels 1-4 (every epilogue, the sub-pixel up convs included) and 0.87 on the level-0 64->32
-# conv vs kind 3; the level-0 32->32 convs even (0.98-1.04) and 16->32 1.08, so level 0 takes it
-# from WINO42_MIN_CIN_L0 input channels.  Whole forward, one box interleaved: 1280x720 x 4
-# 143.1-143.7 -> 157.6-157.8 pairs/s, 640x368 x 1 338.6-339.1 -> 357.0-357.5.
+# conv vs kind 3; the level-0 32->32 convs even in isolation (0.98-1.04), 16->32 1.08.  Whole
+# forward, one box interleaved: 1280x720 x 4 143.1-143.7 -> 157.6-157.8 pairs/s with level 0 from
+# cin 64, 640x368 x 1 338.6-339.1 -> 357.0-357.5; every level-0 conv with cin % 8 == 0 on kind 14
+# (WINO42_MIN_CIN_L0 16) another +0.5 % / +0.3 % (profiles/r06/r06o/: 152.6-152.7 vs 151.7-151.9
+# on a slower box, C2 356.7 vs 355.5).
 WINO42_LEVELS = (0, 1, 2, 3, 4)
-WINO42_MIN_CIN_L0 = 64
+WINO42_MIN_CIN_L0 = 16
 
 
 def wino42_ok(cin: int, cout: int, level: int) -> bool:
