@@ -576,6 +576,10 @@ def main():
                                         "count their direct-form FLOPs") if algo == "mixed" else "")
                                     if algo in ("winograd", "mixed") else "direct-form conv FLOPs (2*9*Cin*Cout*H*W)"),
                     "direct_equivalent_tflops": round(direct_fl / (conv_busy * 1e-3) / 1e12, 2),
+                    # round-5 comparable rate: every conv priced at F(2x2,3x3)'s 4/9 of the direct
+                    # FLOPs (kind 14 runs 3/9, so its own-algorithm `achieved` reads lower)
+                    "f2x2_basis_tflops": (round(direct_fl * 4 / 9 / (conv_busy * 1e-3) / 1e12, 2)
+                                          if algo in ("winograd", "mixed") else None),
                     "flops_per_launch_avg": conv_fl / max(conv_launches, 1),
                     "avg_launch_ms": conv_ms / max(conv_launches, 1),
                     "conv_busy_ms_per_step": round(conv_busy / args.steps, 3),
