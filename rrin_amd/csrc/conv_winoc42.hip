@@ -29,13 +29,6 @@
 #ifndef RRIN_WINO42_AGPR
 #define RRIN_WINO42_AGPR 0
 #endif
-// A/B: 1 = point 5's MFMAs interleaved with the next chunk's row combination and points 0-2
-// transform (sched_group_barrier: 1 MFMA, then 12 VALU) instead of after them; 2 = also the
-// points 3-5 transform deferred into the next chunk, beside its point-0 MFMAs
-#ifndef RRIN_WINO42_SCHED
-#define RRIN_WINO42_SCHED 0
-#endif
-
 namespace rrin {
 
 typedef float w42f16 __attribute__((ext_vector_type(16)));
@@ -141,7 +134,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winoc42_kernel(ConvH8Args a) {
   w42f16 acc[6];
 #pragma unroll
   for (int x = 0; x < 6; ++x) acc[x] = w42f16{};
-  w42f4 u[6];   // U of the chunk being computed (point x reloaded after its MFMAs)
+  // U of the chunk being computed (point x reloaded for the next chunk after its MFMAs; a
+  // prefetch distance of two chunks needs a second set: 256 VGPRs and spills)
+  w42f4 ua[6];
   w42f4 v[6];   // B operands of the chunk being computed
   w42f4 d[12];  // window records of the next chunk: rows ra / rb, columns 0-5
 
@@ -177,7 +172,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winoc42_kernel(ConvH8Args a) {
       v[5][e] = fmaf(4.f, t[1][e], fmaf(-5.f, t[3][e], t[5][e]));
     }
   };
-  auto mfma_point = [&](int x) {
+  auto mfma_point = [&](const w42f4(&u)[6], int x) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) acc[x] = __builtin_amdgcn_mfma_f32_32x32x2f32(u[x][e], v[x][e], acc[x], 0, 0, 0);
   };
@@ -185,31 +180,17 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winoc42_kernel(ConvH8Args a) {
   auto fence = [&]() { __builtin_amdgcn_sched_barrier(0); };
 
   // Chunk c (U(c) in u, its B operands in v), MORE: it has a successor.  Points 0-2, each
-  // followed by the load of its U for chunk c + 1; the wait for raw(c + 1) (issued a chunk ago;
-  // U(c) pts 3-5 and U(c + 1) pts 0-2 stay in flight); the barrier; raw(c + 2) -> the free stage;
-  // chunk c + 1's window reads under points 3-4, its row combination and points 0-2, point 5,
-  // its points 3-5; U(c + 1) pts 3-5 after their MFMAs.  VMEM order per chunk: U pts 0-2,
-  // raw(c + 2), U pts 3-5 -- the same every chunk (the prologue matches it).
-  auto chunk = [&](int c, int s, const bool more, const bool pend) {
-    if constexpr (RRIN_WINO42_SCHED == 2) {
-      // points 3-5's operands of this chunk (deferred from the previous one) beside point 0
-      if (pend) cols_b();
-      mfma_point(0);
-      if (pend) {
+  // followed by the load of its U for chunk c + 1; the wait for raw(c + 1) (issued a chunk ago; the
+  // previous chunk's U pts 3-5 and this chunk's U pts 0-2 stay in flight); the barrier; raw(c + 2)
+  // -> the free stage; chunk c + 1's window reads under points 3-4, its row combination and points
+  // 0-2 transform, point 5, its points 3-5 transform; U pts 3-5 after their MFMAs.  VMEM order
+  // per chunk: U pts 0-2, raw(c + 2), U pts 3-5 -- the same every chunk (the prologue matches it).
+  auto chunk = [&](int c, int s, const bool more, w42f4(&u)[6]) {
+    const int cu = c + 1;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);
-        }
-      }
-      fence();
-      if (more) u[0] = load_u(c + 1, 0);
-      fence();
-    }
-#pragma unroll
-    for (int x = RRIN_WINO42_SCHED == 2 ? 1 : 0; x < 3; ++x) {
-      mfma_point(x);
-      if (more) u[x] = load_u(c + 1, x);
+    for (int x = 0; x < 3; ++x) {
+      mfma_point(u, x);
+      if (more) u[x] = load_u(cu, x);
       fence();
     }
     if (more) {
@@ -220,52 +201,35 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winoc42_kernel(ConvH8Args a) {
       read_raw(s == 2 ? 0 : s + 1);
     }
     fence();
-    mfma_point(3);
-    if (more) u[3] = load_u(c + 1, 3);
+    mfma_point(u, 3);
+    if (more) u[3] = load_u(cu, 3);
     fence();
-    mfma_point(4);
-    if (more) u[4] = load_u(c + 1, 4);
+    mfma_point(u, 4);
+    if (more) u[4] = load_u(cu, 4);
     fence();
-    if constexpr (RRIN_WINO42_SCHED >= 1) {
-      if (more) {
-        rows();
-        cols_a();
-      }
-      mfma_point(5);
-      if (more) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x002, 12, 0);
-        }
-      }
-      fence();
-      if (more) u[5] = load_u(c + 1, 5);
-      fence();
-    } else {
-      if (more) {
-        rows();
-        cols_a();
-      }
-      fence();
-      mfma_point(5);
-      if (more) u[5] = load_u(c + 1, 5);
-      fence();
+    if (more) {
+      rows();
+      cols_a();
     }
-    if (RRIN_WINO42_SCHED != 2 && more) cols_b();
+    fence();
+    mfma_point(u, 5);
+    if (more) u[5] = load_u(cu, 5);
+    fence();
+    if (more) cols_b();
   };
+  auto next_stage = [](int s) { return s == 2 ? 0 : s + 1; };
 
   // prologue in the steady state's VMEM order: raw(0), U(0) pts 0-2, raw(1), U(0) pts 3-5;
   // wait for raw(0); chunk 0's B operands
   issue_raw_at(tbase, 0);
   vm_fence();
 #pragma unroll
-  for (int x = 0; x < 3; ++x) u[x] = load_u(0, x);
+  for (int x = 0; x < 3; ++x) ua[x] = load_u(0, x);
   vm_fence();
   issue_raw_at(nch > 1 ? tbase + chunk_stride : tbase, 1);
   vm_fence();
 #pragma unroll
-  for (int x = 3; x < 6; ++x) u[x] = load_u(0, x);
+  for (int x = 3; x < 6; ++x) ua[x] = load_u(0, x);
   vm_fence();
   RRIN_VMWAIT(P, 6);
   bar();
@@ -276,10 +240,10 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winoc42_kernel(ConvH8Args a) {
   {
     int s = 0;
     for (int c = 0; c + 1 < nch; ++c) {
-      chunk(c, s, true, c > 0);
-      s = s == 2 ? 0 : s + 1;
+      chunk(c, s, true, ua);
+      s = next_stage(s);
     }
-    chunk(nch - 1, s, false, nch > 1);
+    chunk(nch - 1, s, false, ua);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMA past the end has landed
   float bsv[16];
