@@ -131,9 +131,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winoc42_kernel(ConvH8Args a) {
   const int lbase = hh * RG + 2 * pr * RW + pc;
   const int oa = lbase + ra * RW, ob = lbase + rb * RW;
 
-  w42f16 acc[6];
-#pragma unroll
-  for (int x = 0; x < 6; ++x) acc[x] = w42f16{};
+  w42f16 acc[6];  // set by chunk 0's first MFMA of each point (C = 0: no 96 zeroing moves per tile)
   // U of the chunk being computed (point x reloaded for the next chunk after its MFMAs; a
   // prefetch distance of two chunks needs a second set: 256 VGPRs and spills)
   w42f4 ua[6];
@@ -172,9 +170,10 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winoc42_kernel(ConvH8Args a) {
       v[5][e] = fmaf(4.f, t[1][e], fmaf(-5.f, t[3][e], t[5][e]));
     }
   };
-  auto mfma_point = [&](const w42f4(&u)[6], int x) {
+  auto mfma_point = [&](const w42f4(&u)[6], int x, const bool first) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) acc[x] = __builtin_amdgcn_mfma_f32_32x32x2f32(u[x][e], v[x][e], acc[x], 0, 0, 0);
+    for (int e = 0; e < 4; ++e)
+      acc[x] = __builtin_amdgcn_mfma_f32_32x32x2f32(u[x][e], v[x][e], first && e == 0 ? w42f16{} : acc[x], 0, 0, 0);
   };
   auto bar = [&]() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
   auto fence = [&]() { __builtin_amdgcn_sched_barrier(0); };
@@ -185,11 +184,11 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winoc42_kernel(ConvH8Args a) {
   // -> the free stage; chunk c + 1's window reads under points 3-4, its row combination and points
   // 0-2 transform, point 5, its points 3-5 transform; U pts 3-5 after their MFMAs.  VMEM order
   // per chunk: U pts 0-2, raw(c + 2), U pts 3-5 -- the same every chunk (the prologue matches it).
-  auto chunk = [&](int c, int s, const bool more, w42f4(&u)[6]) {
+  auto chunk = [&](int c, int s, const bool more, const bool first, w42f4(&u)[6]) {
     const int cu = c + 1;
 #pragma unroll
     for (int x = 0; x < 3; ++x) {
-      mfma_point(u, x);
+      mfma_point(u, x, first);
       if (more) u[x] = load_u(cu, x);
       fence();
     }
@@ -201,10 +200,10 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winoc42_kernel(ConvH8Args a) {
       read_raw(s == 2 ? 0 : s + 1);
     }
     fence();
-    mfma_point(u, 3);
+    mfma_point(u, 3, first);
     if (more) u[3] = load_u(cu, 3);
     fence();
-    mfma_point(u, 4);
+    mfma_point(u, 4, first);
     if (more) u[4] = load_u(cu, 4);
     fence();
     if (more) {
@@ -212,7 +211,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winoc42_kernel(ConvH8Args a) {
       cols_a();
     }
     fence();
-    mfma_point(u, 5);
+    mfma_point(u, 5, first);
     if (more) u[5] = load_u(cu, 5);
     fence();
     if (more) cols_b();
@@ -239,11 +238,17 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winoc42_kernel(ConvH8Args a) {
   cols_b();
   {
     int s = 0;
-    for (int c = 0; c + 1 < nch; ++c) {
-      chunk(c, s, true, ua);
+    if (nch > 1) {
+      chunk(0, s, true, true, ua);
       s = next_stage(s);
+      for (int c = 1; c + 1 < nch; ++c) {
+        chunk(c, s, true, false, ua);
+        s = next_stage(s);
+      }
+      chunk(nch - 1, s, false, false, ua);
+    } else {
+      chunk(0, s, false, true, ua);
     }
-    chunk(nch - 1, s, false, ua);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMA past the end has landed
   float bsv[16];
