@@ -285,12 +285,12 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winoc42_kernel(ConvH8Args a) {
 #pragma unroll
     for (int k4 = 0; k4 < 4; ++k4) {
       const int k = 4 * (2 * cp + cc) + k4;
-      const w42f4 q0 = X[(0 * 16 + k) * 64 + lane];
+      // row 0 needs Q of waves 0-2, row 1 of waves 1-3: three reads (qo: wave 0 or 3)
+      const w42f4 qo = X[((r == 0 ? 0 : 3) * 16 + k) * 64 + lane];
       const w42f4 q1 = X[(1 * 16 + k) * 64 + lane];
       const w42f4 q2 = X[(2 * 16 + k) * 64 + lane];
-      const w42f4 q3 = X[(3 * 16 + k) * 64 + lane];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) yv[cc][4 * k4 + e] = r == 0 ? (q0[e] + q1[e]) + q2[e] : (q1[e] - q2[e]) - q3[e];
+      for (int e = 0; e < 4; ++e) yv[cc][4 * k4 + e] = r == 0 ? (qo[e] + q1[e]) + q2[e] : (q1[e] - q2[e]) - qo[e];
     }
   uint4* dst = a.dst_hi + (int64_t)img * a.dst_img;
   auto store4 = [&](int64_t rec, const float* vv) {
