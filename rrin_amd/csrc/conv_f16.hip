@@ -23,6 +23,8 @@
 #include <math.h>
 #include <string.h>
 
+#include <type_traits>
+
 #include "common.hpp"
 #include "edge_fix.hpp"
 
@@ -317,7 +319,9 @@ __global__ void RRIN_PK_CONV_ATTR __launch_bounds__(64 * NW) conv3x3_h8_kernel(C
   // 0-31 carry channels 0-7 of the chunk, lanes 32-63 channels 8-15).
   // Operands of tap t+1 are read before the MFMAs of tap t issue; after_tap(t)
   // runs behind tap t's MFMAs (SPREAD / STAGGER: DMA pieces of the next chunk).
-  auto compute_f32 = [&](int buf, int wslot, auto&& after_tap) {
+  // zc (std::true_type for the tile's first chunk): the first MFMA of each accumulator takes C = 0,
+  // so a tile starts without zeroing its accumulator registers
+  auto compute_f32 = [&](int buf, int wslot, auto&& after_tap, auto zc) {
     const uint4* si = s_in + (kNoIn ? 0 : buf) * IN_REC + (hh * ROWS + wn * WN) * H8_LC + j;
     const uint4* sw = s_w + (kNoW ? 0 : wslot) * W_REC + hh * BM + j;
     floatx4 av[2][WM], bv[2][WN];
@@ -342,16 +346,18 @@ __global__ void RRIN_PK_CONV_ATTR __launch_bounds__(64 * NW) conv3x3_h8_kernel(C
             if constexpr (kNoMfma)
               asm volatile("" ::"v"(av[s][mt][e]), "v"(bv[s][nt][e]));
             else
-              acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s][mt][e], bv[s][nt][e], acc[mt][nt], 0, 0, 0);
+              acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(
+                  av[s][mt][e], bv[s][nt][e], decltype(zc)::value && t == 0 && e == 0 ? floatx16{} : acc[mt][nt], 0, 0, 0);
           }
       after_tap(t);
     }
   };
-  auto compute = [&](int buf, int wslot, auto&& after_tap) {
+  auto compute = [&](int buf, int wslot, auto&& after_tap, auto zc) {
     if constexpr (F32) {
-      compute_f32(buf, wslot, after_tap);
+      compute_f32(buf, wslot, after_tap, zc);
       return;
     }
+    constexpr bool kZc = decltype(zc)::value;
     const uint4* si[PLANES];
     const uint4* sw[PLANES];
 #pragma unroll
@@ -396,10 +402,12 @@ __global__ void RRIN_PK_CONV_ATTR __launch_bounds__(64 * NW) conv3x3_h8_kernel(C
             }
           } else {
             if constexpr (PLANES == 2) {
-              accx[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[s][1][mt], bv[s][0][nt], accx[mt][nt], 0, 0, 0);
+              accx[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[s][1][mt], bv[s][0][nt],
+                                                                   kZc && t == 0 ? floatx16{} : accx[mt][nt], 0, 0, 0);
               accx[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[s][0][mt], bv[s][1][nt], accx[mt][nt], 0, 0, 0);
             }
-            acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[s][0][mt], bv[s][0][nt], acc[mt][nt], 0, 0, 0);
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[s][0][mt], bv[s][0][nt],
+                                                                kZc && t == 0 ? floatx16{} : acc[mt][nt], 0, 0, 0);
           }
         }
       after_tap(t);
@@ -645,18 +653,21 @@ __global__ void RRIN_PK_CONV_ATTR __launch_bounds__(64 * NW) conv3x3_h8_kernel(C
     const int ntile = tile + cgrid;
     const bool more = ntile < ntiles;
     const TileId nxt = tile_id(more ? ntile : tile);
+    if constexpr (kNoMfma || kMfma16) {  // probes: the accumulators are not written by the chunk loop's MFMAs
 #pragma unroll
-    for (int mt = 0; mt < WM; ++mt)
+      for (int mt = 0; mt < WM; ++mt)
 #pragma unroll
-      for (int nt = 0; nt < WN; ++nt)
+        for (int nt = 0; nt < WN; ++nt)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          acc[mt][nt][i] = 0.f;
-          accx[mt][nt][i] = 0.f;
-          if constexpr (kMfma16) p16[mt][nt][i >> 3][(i >> 2) & (PLANES - 1)][i & 3] = 0.f;
-        }
+          for (int i = 0; i < 16; ++i) {
+            acc[mt][nt][i] = 0.f;
+            accx[mt][nt][i] = 0.f;
+            if constexpr (kMfma16) p16[mt][nt][i >> 3][(i >> 2) & (PLANES - 1)][i & 3] = 0.f;
+          }
+    }
     if constexpr (kBias == 2) load_bias(cur.cob);
-    for (int c = 0; c < a.nchunks; ++c) {
+    // chunk 0 peeled (its MFMAs start the accumulators from C = 0), then chunks 1 .. nchunks - 1
+    auto chunk_iter = [&](const int c, auto zc) {
       // staged during this chunk: chunk c+1 of this tile, or chunk 0 of the next tile
       const bool last = c + 1 == a.nchunks;
       const bool pre = !last || more;
@@ -674,7 +685,7 @@ __global__ void RRIN_PK_CONV_ATTR __launch_bounds__(64 * NW) conv3x3_h8_kernel(C
               for (int k = 0; k < NPIECE; ++k)
                 if (t * NPIECE / kSpreadTaps <= k && k < (t + 1) * NPIECE / kSpreadTaps) issue_piece(pt, pc, buf ^ 1, k);
             }
-          });
+          }, zc);
         } else if constexpr (kStagger) {
           const bool late = __builtin_amdgcn_readfirstlane(tid) >= NT / 2;
           if (pre && !late) {
@@ -686,13 +697,13 @@ __global__ void RRIN_PK_CONV_ATTR __launch_bounds__(64 * NW) conv3x3_h8_kernel(C
 #pragma unroll
               for (int k = 0; k < NPIECE; ++k) issue_piece(pt, pc, buf ^ 1, k);
             }
-          });
+          }, zc);
         } else {
           if (pre) {
 #pragma unroll
             for (int k = 0; k < NPIECE; ++k) issue_piece(pt, pc, buf ^ 1, k);
           }
-          compute(buf, wslot, [](int) {});
+          compute(buf, wslot, [](int) {}, zc);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -701,7 +712,7 @@ __global__ void RRIN_PK_CONV_ATTR __launch_bounds__(64 * NW) conv3x3_h8_kernel(C
           load_w(pt, pc);
           load_in(pt, pc);
         }
-        compute(buf, buf, [](int) {});
+        compute(buf, buf, [](int) {}, zc);
         if (pre) {
           store_in(buf ^ 1);
           store_w(buf ^ 1);
@@ -709,7 +720,9 @@ __global__ void RRIN_PK_CONV_ATTR __launch_bounds__(64 * NW) conv3x3_h8_kernel(C
         __syncthreads();
       }
       buf ^= 1;
-    }
+    };
+    chunk_iter(0, std::true_type{});
+    for (int c = 1; c < a.nchunks; ++c) chunk_iter(c, std::false_type{});
 
     if constexpr (kMfma16) {  // probe: keep the results live (values are not the conv)
 #pragma unroll
