@@ -168,7 +168,8 @@ __global__ __launch_bounds__(256, 2) void conv_block0_h8_kernel(Block0Args a) {
   // (group hh, row m + ky, column 32 half + j + kx)
   const int a_base = hh * IR * IC + (wv >> 1) * IC + 32 * half + j;
   b0f16 acc[5];
-  auto compute_a = [&](const uint4* st, const WNext& nx) {
+  // zc (std::true_type for chunk 0): each accumulator's first MFMA takes C = 0 (no zeroing per tile)
+  auto compute_a = [&](const uint4* st, const WNext& nx, auto zc) {
     const uint4* base = st + a_base;
     b0h8 b[2][5];
     auto ld = [&](int t, int slot) {
@@ -189,7 +190,8 @@ __global__ __launch_bounds__(256, 2) void conv_block0_h8_kernel(Block0Args a) {
         if constexpr ((RRIN_B0_ABL & 1) != 0)
           asm volatile("" ::"v"(w[t]), "v"(b[t & 1][i]));
         else
-          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(w[t], b[t & 1][i], acc[i], 0, 0, 0);
+          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(w[t], b[t & 1][i],
+                                                         decltype(zc)::value && t == 0 ? b0f16{} : acc[i], 0, 0, 0);
       wload(nx, t);
       fence();  // one weight set live: tap t's replacement issues after tap t's MFMAs
     }
@@ -218,12 +220,11 @@ __global__ __launch_bounds__(256, 2) void conv_block0_h8_kernel(Block0Args a) {
   for (;;) {
     fence();
     // ---- conv a: chunk c from stage X (c even) / Y (c odd)
-#pragma unroll
-    for (int i = 0; i < 5; ++i) acc[i] = b0f16{};
-    for (int c = 0; c < nch; ++c) {
+    // chunk 0 peeled (its MFMAs start the accumulators from C = 0)
+    auto chunk_a = [&](const int c, auto zc) {
       const bool more = c + 1 < nch;
       fence();
-      compute_a((c & 1) ? stY : stX, more ? WNext{0, c + 1} : WNext{1, 0});
+      compute_a((c & 1) ? stY : stX, more ? WNext{0, c + 1} : WNext{1, 0}, zc);
       fence();
       if (more) {
         // chunk c + 1 (DMA) landed; every wave done with this chunk's stage
@@ -233,7 +234,9 @@ __global__ __launch_bounds__(256, 2) void conv_block0_h8_kernel(Block0Args a) {
         if (c + 2 < nch) issue_chunk(ibase, c + 2, (c & 1) ? stY : stX);
       }
       fence();
-    }
+    };
+    chunk_a(0, std::true_type{});
+    for (int c = 1; c < nch; ++c) chunk_a(c, std::false_type{});
     bar();  // every wave done reading the stages: Y becomes the conv-a tile, X takes the next tile
     const int ntile = tile + (int)gridDim.x;
     const bool has_next = ntile < ntiles;
@@ -286,9 +289,7 @@ __global__ __launch_bounds__(256, 2) void conv_block0_h8_kernel(Block0Args a) {
     fence();
 
     // ---- conv b: rows 4 (wv / 2) + i, column half; chunk cb = record groups 2 cb, 2 cb + 1
-    b0f16 acc2[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) acc2[i] = b0f16{};
+    b0f16 acc2[4];  // set by chunk 0's first MFMA (C = 0)
     const int b_base = hh * MR * MC + ((wv >> 1) * 4) * MC + 32 * half + j;
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb) {
@@ -313,7 +314,8 @@ __global__ __launch_bounds__(256, 2) void conv_block0_h8_kernel(Block0Args a) {
           if constexpr ((RRIN_B0_ABL & 2) != 0)
             asm volatile("" ::"v"(w[t]), "v"(b[t & 1][i]));
           else
-            acc2[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(w[t], b[t & 1][i], acc2[i], 0, 0, 0);
+            acc2[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(w[t], b[t & 1][i],
+                                                          cb == 0 && t == 0 ? b0f16{} : acc2[i], 0, 0, 0);
         wload(nx, t);
         fence();
       }
