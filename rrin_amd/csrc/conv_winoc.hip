@@ -187,12 +187,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winoc_kernel(ConvH8Args a) {
   const int oa = ra * 34, ob = rb * 34;
 
   cfloatx16 acc[CT][NT][4];
-#pragma unroll
-  for (int t = 0; t < CT; ++t)
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-      for (int x = 0; x < 4; ++x) acc[t][nt][x] = cfloatx16{};
+  // (set by chunk 0's first MFMA of each accumulator: C = 0, no zeroing per tile)
   cfloatx4 u[CT][4];              // U of the chunk being computed (point x reloaded after its MFMAs)
   cfloatx4 v[NT][4];              // B operands of the chunk being computed
   cfloatx4 d[8];                  // window records of one N tile of the next chunk
@@ -222,12 +217,13 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winoc_kernel(ConvH8Args a) {
     v[nt][2] = tr[2] - tr[1];
     v[nt][3] = tr[1] - tr[3];
   };
-  auto mfma_point = [&](int x, int nt) {
+  auto mfma_point = [&](int x, int nt, const bool first) {
 #pragma unroll
     for (int t = 0; t < CT; ++t)
 #pragma unroll
       for (int e = 0; e < 4; ++e)
-        acc[t][nt][x] = __builtin_amdgcn_mfma_f32_32x32x2f32(u[t][x][e], v[nt][x][e], acc[t][nt][x], 0, 0, 0);
+        acc[t][nt][x] = __builtin_amdgcn_mfma_f32_32x32x2f32(u[t][x][e], v[nt][x][e],
+                                                                first && e == 0 ? cfloatx16{} : acc[t][nt][x], 0, 0, 0);
   };
   auto reload_u = [&](int c, int x) {
 #pragma unroll
@@ -250,11 +246,11 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winoc_kernel(ConvH8Args a) {
   //   U pt 3 -- the same counts every chunk (the prologue matches it), so the compiler's
   //   own waits for u are 3 CT + P deep and this wait is 4 CT; a chunk past the end is
   //   never loaded: raw(nch) re-reads the last chunk into the free stage.
-  auto chunk = [&](int c, int s, const bool more) {
+  auto chunk = [&](int c, int s, const bool more, const bool first) {
 #pragma unroll
     for (int x = 0; x < 3; ++x) {
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) mfma_point(x, nt);
+      for (int nt = 0; nt < NT; ++nt) mfma_point(x, nt, first);
       if (more && !(RRIN_WINOC_ABL & 1)) reload_u(c + 1, x);
       fence();
     }
@@ -269,7 +265,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winoc_kernel(ConvH8Args a) {
     for (int nt = 0; nt < NT; ++nt) {
       if (more && !(RRIN_WINOC_ABL & 16)) read_raw(s1, nt);
       fence();
-      mfma_point(3, nt);
+      mfma_point(3, nt, first);
       fence();
       if (more) transform(nt);
     }
@@ -296,11 +292,17 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winoc_kernel(ConvH8Args a) {
   }
   {
     int s = 0;
-    for (int c = 0; c + 1 < nch; ++c) {
-      chunk(c, s, true);
-      s = s == 2 ? 0 : s + 1;
+    if (nch > 1) {  // chunk 0 peeled: its MFMAs start the accumulators from C = 0
+      chunk(0, s, true, true);
+      s = 1;
+      for (int c = 1; c + 1 < nch; ++c) {
+        chunk(c, s, true, false);
+        s = s == 2 ? 0 : s + 1;
+      }
+      chunk(nch - 1, s, false, false);
+    } else {
+      chunk(0, s, false, true);
     }
-    chunk(nch - 1, s, false);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMA past the end has landed
 #if RRIN_WINOC_CLOCK

@@ -163,12 +163,7 @@ __global__ __launch_bounds__(256, NT == 1 ? 2 : 1) void conv3x3_winoh_kernel(Con
   const int oa = ra * 34, ob = rb * 34;
 
   wfx16 acc[CT][NT][4];
-#pragma unroll
-  for (int t = 0; t < CT; ++t)
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-      for (int x = 0; x < 4; ++x) acc[t][nt][x] = wfx16{};
+  // (set by chunk 0's first MFMA of each accumulator: C = 0, no zeroing per tile)
   whx8 u[CT][4];   // U of the chunk being computed (point x reloaded after its MFMAs)
   whx8 v[NT][4];   // B operands of the chunk being computed
   whx8 d[NT][8];   // window records of the N tiles of the next chunk
@@ -198,10 +193,11 @@ __global__ __launch_bounds__(256, NT == 1 ? 2 : 1) void conv3x3_winoh_kernel(Con
     v[nt][2] = __builtin_elementwise_fma(m1, tr[1], tr[2]);
     v[nt][3] = __builtin_elementwise_fma(m1, tr[3], tr[1]);
   };
-  auto mfma_point = [&](int x, int nt) {
+  auto mfma_point = [&](int x, int nt, const bool first) {
 #pragma unroll
     for (int t = 0; t < CT; ++t)
-      acc[t][nt][x] = __builtin_amdgcn_mfma_f32_32x32x16_f16(u[t][x], v[nt][x], acc[t][nt][x], 0, 0, 0);
+      acc[t][nt][x] = __builtin_amdgcn_mfma_f32_32x32x16_f16(u[t][x], v[nt][x], first ? wfx16{} : acc[t][nt][x], 0, 0,
+                                                                  0);
   };
   auto reload_u = [&](int c, int x) {
 #pragma unroll
@@ -216,11 +212,11 @@ __global__ __launch_bounds__(256, NT == 1 ? 2 : 1) void conv3x3_winoh_kernel(Con
   // points 0-2, each followed by its U load for chunk c + 1; the wait for raw(c + 1); the
   // barrier; raw(c + 2); per N tile chunk c + 1's window reads, point 3, its transform;
   // point 3's U load.  VMEM order per chunk: U pts 0-2, raw(c + 2), U pt 3.
-  auto chunk = [&](int c, int s, const bool more) {
+  auto chunk = [&](int c, int s, const bool more, const bool first) {
 #pragma unroll
     for (int x = 0; x < 3; ++x) {
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) mfma_point(x, nt);
+      for (int nt = 0; nt < NT; ++nt) mfma_point(x, nt, first);
       if (more && !(RRIN_WINOH_ABL & 1)) reload_u(c + 1, x);
       fence();
     }
@@ -238,7 +234,7 @@ __global__ __launch_bounds__(256, NT == 1 ? 2 : 1) void conv3x3_winoh_kernel(Con
       if (more && !(RRIN_WINOH_ABL & 16)) read_raw(s1, nt);
     fence();
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) mfma_point(3, nt);
+    for (int nt = 0; nt < NT; ++nt) mfma_point(3, nt, first);
     fence();
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt)
@@ -265,11 +261,17 @@ __global__ __launch_bounds__(256, NT == 1 ? 2 : 1) void conv3x3_winoh_kernel(Con
   }
   {
     int s = 0;
-    for (int c = 0; c + 1 < nch; ++c) {
-      chunk(c, s, true);
-      s = s == 2 ? 0 : s + 1;
+    if (nch > 1) {  // chunk 0 peeled: its MFMAs start the accumulators from C = 0
+      chunk(0, s, true, true);
+      s = 1;
+      for (int c = 1; c + 1 < nch; ++c) {
+        chunk(c, s, true, false);
+        s = s == 2 ? 0 : s + 1;
+      }
+      chunk(nch - 1, s, false, false);
+    } else {
+      chunk(0, s, false, true);
     }
-    chunk(nch - 1, s, false);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMA past the end has landed
   // the epilogue's bias values, loaded now: their latency hides behind the exchange
