@@ -131,7 +131,7 @@ def parse():
     ap.add_argument("--streams", type=int, default=None,
                     help="HIP streams the rank's pairs are split over (their kernels overlap, filling each "
                          "other's launch gaps and last-wave tails; outputs are bitwise those of one stream); "
-                         "default engine.default_streams: fp16 one pair per stream up to 4, else 2")
+                         "default engine.default_streams: 2")
     ap.add_argument("--dist-init", action="store_true",
                     help="initialise torch.distributed and run the all-gather path even at WORLD_SIZE 1 "
                          "(exercises RCCL / the gather check on a single GPU)")

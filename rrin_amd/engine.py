@@ -294,15 +294,16 @@ WINO_F16_KIND = 6
 FUSE_L0 = 2
 
 
-MAX_DEFAULT_STREAMS = 4
+MAX_DEFAULT_STREAMS = 4  # the most streams a caller is expected to ask for (workspace cache sizing)
 
 
 def default_streams(precision: str, batch: int) -> int:
-    """HIP streams a forward of `batch` pairs is split over by default: fp16 one pair per stream
-    up to 4 (C3 1280x736 x 4: 488.8-489.1 pairs/s on 4 streams vs 482.1-482.3 on 2), the other
-    precisions 2 (headline 1280x720 x 4 exact fp32: 143.0-143.4 on 2 vs 141.8-142.0 on 4;
-    profiles/r05/streams_ab.txt).  The output is bitwise that of one stream either way."""
-    return max(1, min(batch, MAX_DEFAULT_STREAMS if precision == "fp16" else 2))
+    """HIP streams a forward of `batch` pairs is split over by default: 2 at every precision
+    (headline 1280x720 x 4 exact fp32: 158 vs 151 on 1 stream, 153 on 3, 155 on 4,
+    profiles/r06/r06n, r06s; fp16 C3 1280x736 x 4: 512.3-512.4 on 2 vs 507.3-507.8 on 4 and
+    487.8-488.3 on 3 since round 6's record-conv changes, profiles/r06/r06aa -- round 5 had
+    measured 4 ahead).  The output is bitwise that of one stream either way."""
+    return max(1, min(batch, 2))
 
 
 def fused_pairs(convs) -> list:

@@ -56,7 +56,7 @@ class Net(nn.Module):
         # HIP streams a batch of N >= 2 pairs is split over (pairs are
         # independent: the output is bitwise that of one stream; the parts'
         # kernels fill each other's launch gaps and tails); None: by precision
-        # and batch (engine.default_streams: fp16 up to 4, else 2)
+        # and batch (engine.default_streams: 2)
         self.streams = None
         self.register_load_state_dict_post_hook(Net._on_load)
 

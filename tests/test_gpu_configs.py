@@ -67,8 +67,8 @@ def _oracle(sd, i0, i1, t=0.5, taps=None):
 
 @pytest.fixture(scope="module")
 def c3_case():
-    """Config C3: 1280x736 (padded 720p), 4 pairs; oracle output of every pair (the fp16 forward
-    runs one pair per stream: each of the 4 streams is checked against the oracle)."""
+    """Config C3: 1280x736 (padded 720p), 4 pairs; oracle output of every pair (the forward splits
+    them over streams: every pair of every stream part is checked against the oracle)."""
     sd = keyed_state_dict(Net().state_dict())
     i0, i1 = synthetic_batch(4, 736, 1280, first_index=40)
     return sd, i0, i1, _oracle(sd, i0, i1)
@@ -83,7 +83,7 @@ def test_config_c3_1280x736x4(gpu, c3_case, precision):
         out = net(i0.to(gpu), i1.to(gpu), 0.5)
         one = net(i0[2:3].to(gpu), i1[2:3].to(gpu), 0.5)
     net.check_range()
-    for p in range(4):   # every pair (= every stream part of the fp16 forward) vs the oracle
+    for p in range(4):   # every pair (every stream part of the forward) vs the oracle
         err, psnr = err_psnr(out[p:p + 1].cpu(), ref[p:p + 1])
         if precision == "fp16":
             assert err <= 1e-2 and psnr >= 45, f"C3 fp16 pair {p}: max-abs {err:.3e} psnr {psnr:.1f}"

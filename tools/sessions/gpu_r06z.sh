@@ -35,7 +35,7 @@ if [[ $STEPS == *pmc* ]]; then
   run c3_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/c3_fetch -o run -- $C3P
   run c3_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/c3_write -o run -- $C3P
   python3 tools/pmc_summary.py --fetch $O/c3_fetch --write $O/c3_write --steps 3 --out $O/traffic_c3.json \
-    --table profiles/pmc_traffic.json --precision fp16 --config 1280x736x4s4 > $O/pmc_summary_c3.txt 2>&1; tail -2 $O/pmc_summary_c3.txt
+    --table profiles/pmc_traffic.json --precision fp16 --config 1280x736x4s2 > $O/pmc_summary_c3.txt 2>&1; tail -2 $O/pmc_summary_c3.txt
   cp profiles/pmc_traffic.json $O/pmc_traffic.json
 fi
 [[ $STEPS == *bench* ]] && run bench 400 python bench.py && run bench_2 300 python bench.py --steps 20 --warmup 5 --cpu-baseline off --no-alt
