@@ -289,9 +289,11 @@ WINO_F16_KIND = 6
 # 6-16-channel input) fused; 2: also the last up block's conv_block (conv a 64 -> 32).  In
 # isolation at 1280x736 x 2 the fused down block takes 108 vs 121 us, the fused up block 159 vs
 # 150 us (its recomputed halo, 1.29x conv a's MACs, costs more than the HBM round trip it saves;
-# profiles/r05/block0/); in the two-stream C3 forward mode 2 measured best: 480.0-481.7 pairs/s
-# vs 478.2-479.6 (mode 1) and 474.5-475.7 (unfused), C5 within noise (56.6-56.9).
-FUSE_L0 = 2
+# profiles/r05/block0/); in round 5's C3 forward (4 streams) mode 2 measured best: 480.0-481.7
+# pairs/s vs 478.2-479.6 (mode 1) and 474.5-475.7 (unfused), C5 within noise (56.6-56.9).  On the
+# round-6 schedule (2 streams for fp16) mode 1 leads: 514.1-514.9 vs 511.5-512.9 (mode 2) and
+# 509.2-509.6 (unfused), one box interleaved (profiles/r06/r06ac/).
+FUSE_L0 = 1
 
 
 MAX_DEFAULT_STREAMS = 4  # the most streams a caller is expected to ask for (workspace cache sizing)
