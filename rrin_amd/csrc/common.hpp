@@ -321,8 +321,8 @@ constexpr size_t kWinoCLds1 = (size_t)2048 * 16;  // TH 4: 3 x 512 stage records
 constexpr size_t kWinoCLds2 = (size_t)4096 * 16;  // TH 8: 3 x 768 < 4096
 int launch_winoc(const ConvH8Args& a, int epi, int ct, hipStream_t st);
 // the register-U tile in Winograd F(4,3) x F(2,3) (conv_winoc42.hip, kind 14): BM 32 x 32 px x
-// TH 8, 4 waves, two blocks per CU; LDS: max(3 raw stages of 768, the 4 x 16 x 64 exchange)
-constexpr size_t kWinoC42Lds = (size_t)4096 * 16;
+// TH 8, 4 waves, two blocks per CU; LDS: max(3 raw stages of 768, the 4 x 16 x 65 exchange)
+constexpr size_t kWinoC42Lds = (size_t)4160 * 16;
 int launch_winoc42(const ConvH8Args& a, int epi, hipStream_t st);
 // whether rrin_conv3x3_h8_fwd runs a ring_full fix-up inside the conv's launch for tile config
 // cfg, cin input channels and precision prec (else it launches it after the conv) -- conv_f16.hip

@@ -42,7 +42,8 @@ struct W42 {
   static constexpr int PIECES = (RAW + 255) / 256;  // DMA pieces per thread
   static constexpr int STAGE = PIECES * 256;        // records per LDS stage (the tail is a dummy)
   static constexpr int NS = 3;                      // stages: chunk c + 2 lands while c computes
-  static constexpr int XREC = 4 * 16 * 64;          // output-transform exchange: 4 waves x 16 records
+  static constexpr int XP = 65;                     // exchange pitch in records (64 lanes + 1)
+  static constexpr int XREC = 4 * 16 * XP;          // output-transform exchange: 4 waves x 16 records
   static constexpr size_t LDS = (size_t)(NS * STAGE > XREC ? NS * STAGE : XREC) * 16;
 };
 static_assert(W42::LDS == kWinoC42Lds, "LDS size (common.hpp)");
@@ -259,9 +260,15 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winoc42_kernel(ConvH8Args a) {
 #endif
   __syncthreads();  // every read of the stages done before the exchange reuses the LDS
 
-  // ---- output transform: Q[c] = A^T_x row c of this wave's six points, written as 16 records
-  // per lane (record k: values 4 k .. 4 k + 3 of c = k >> 2); wave yw then finishes output row
-  // r = yw & 1, columns 2 cp, 2 cp + 1 (cp = yw >> 1) of its patches from the four waves' Q
+  // ---- output transform: Q[c] = A^T_x row c of this wave's six points, 16 records per lane
+  // (record k: values 4 k .. 4 k + 3 of c = k >> 2) into X[wave][record][lane] (pitch XP = 65
+  // records: the gather below reads 16 distinct 4-bank slots per ds_read_b128 lane group).  Wave
+  // yw then finishes patch row yw: lane (xo = lane & 31, hh) takes pixel column x0 + xo (patch
+  // xo >> 2, column xo & 3) of output rows y0 + 2 yw and + 1 from the four waves' Q with kind 6's
+  // A^T_y, so each store instruction writes 32 consecutive pixels of a record group (the
+  // patch-per-lane layout wrote 16 B of every 64 B: the stores were a quarter of a short-K
+  // tile's time)
+  constexpr int XP = G::XP;
   w42f4* X = reinterpret_cast<w42f4*>(smem4);
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
@@ -275,33 +282,35 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winoc42_kernel(ConvH8Args a) {
              : c == 2 ? fmaf(4.f, m3 + m4, m1 + m2)
                       : fmaf(8.f, m3 - m4, m1 - m2) + m5;
     }
-    X[(yw * 16 + k) * 64 + lane] = g;
+    X[(yw * 16 + k) * XP + lane] = g;
   }
   __syncthreads();
-  const int r = yw & 1, cp = yw >> 1;
-  float yv[2][16];
+  const int xo = lane & 31, cx = xo & 3;
+  const int src = (xo >> 2) + 8 * yw + 32 * hh;  // the lane of the MFMA layout holding this patch
+  float yv[2][16];                               // rows 0 / 1 of the patch row, 16 channels
 #pragma unroll
-  for (int cc = 0; cc < 2; ++cc)
+  for (int k4 = 0; k4 < 4; ++k4) {
+    const int k = 4 * cx + k4;
+    const w42f4 q0 = X[(0 * 16 + k) * XP + src];
+    const w42f4 q1 = X[(1 * 16 + k) * XP + src];
+    const w42f4 q2 = X[(2 * 16 + k) * XP + src];
+    const w42f4 q3 = X[(3 * 16 + k) * XP + src];
 #pragma unroll
-    for (int k4 = 0; k4 < 4; ++k4) {
-      const int k = 4 * (2 * cp + cc) + k4;
-      // row 0 needs Q of waves 0-2, row 1 of waves 1-3: three reads (qo: wave 0 or 3)
-      const w42f4 qo = X[((r == 0 ? 0 : 3) * 16 + k) * 64 + lane];
-      const w42f4 q1 = X[(1 * 16 + k) * 64 + lane];
-      const w42f4 q2 = X[(2 * 16 + k) * 64 + lane];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) yv[cc][4 * k4 + e] = r == 0 ? (qo[e] + q1[e]) + q2[e] : (q1[e] - q2[e]) - qo[e];
+    for (int e = 0; e < 4; ++e) {
+      yv[0][4 * k4 + e] = (q0[e] + q1[e]) + q2[e];
+      yv[1][4 * k4 + e] = (q1[e] - q2[e]) - q3[e];
     }
+  }
   uint4* dst = a.dst_hi + (int64_t)img * a.dst_img;
   auto store4 = [&](int64_t rec, const float* vv) {
     dst[rec] = make_uint4(__float_as_uint(vv[0]), __float_as_uint(vv[1]), __float_as_uint(vv[2]), __float_as_uint(vv[3]));
   };
-  const int y = y0 + 2 * pr + r;
+  const int x = x0 + xo, yb = y0 + 2 * yw;
   if constexpr (EPI == RRIN_EPI_SUBPIXEL) {
     const int HH = 2 * a.h, WW = 2 * a.w, creal = a.cout >> 2;
 #pragma unroll
-    for (int cc = 0; cc < 2; ++cc) {
-      const int x = x0 + 4 * pc + 2 * cp + cc;
+    for (int r = 0; r < 2; ++r) {
+      const int y = yb + r;
       if (cob * 32 < a.cout && y < a.h && x < a.w) {
 #pragma unroll
         for (int qq = 0; qq < 4; ++qq) {
@@ -310,11 +319,11 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winoc42_kernel(ConvH8Args a) {
           if (ri >= 0) {
 #pragma unroll
             for (int e = 0; e < 4; ++e)
-              a.edge[((int64_t)img * creal + cob * 8 + 4 * hh + e) * a.ring + ri] = yv[cc][4 * qq + e];
+              a.edge[((int64_t)img * creal + cob * 8 + 4 * hh + e) * a.ring + ri] = yv[r][4 * qq + e];
           } else {
             float vv[4];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) vv[e] = yv[cc][4 * qq + e] + bsv[4 * qq + e];
+            for (int e = 0; e < 4; ++e) vv[e] = yv[r][4 * qq + e] + bsv[4 * qq + e];
             store4((int64_t)(2 * cob + hh) * a.dst_gp + (int64_t)(Y + 1) * a.dst_wp + XX + kH8PadLeft, vv);
           }
         }
@@ -323,61 +332,48 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winoc42_kernel(ConvH8Args a) {
   } else {
     float vv[2][16];
 #pragma unroll
-    for (int cc = 0; cc < 2; ++cc) {
-      const int x = x0 + 4 * pc + 2 * cp + cc;
+    for (int r = 0; r < 2; ++r) {
+      const int y = yb + r;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        float tv = yv[cc][i] + bsv[i];
+        float tv = yv[r][i] + bsv[i];
         if constexpr (EPI != RRIN_EPI_LINEAR) tv = leaky(tv, a.slope);
-        vv[cc][i] = tv;
+        vv[r][i] = tv;
       }
 #pragma unroll
       for (int qq = 0; qq < 4; ++qq) {
         if (cob * 32 + 8 * qq < a.cout && y < a.h && x < a.w) {
           const int64_t rec = (int64_t)(cob * 8 + 2 * qq + hh) * a.dst_gp + (int64_t)(y + 1) * a.dst_wp + x + kH8PadLeft;
-          store4(rec, &vv[cc][4 * qq]);
+          store4(rec, &vv[r][4 * qq]);
           if constexpr (EPI == RRIN_EPI_LEAKY_REP) {  // edge replicate into the padding ring
             const int dy0 = y == 0 ? -1 : 0, dy1 = y == a.h - 1 ? 1 : 0;
             const int dx0 = x == 0 ? -1 : 0, dx1 = x == a.w - 1 ? 1 : 0;
             for (int dy = dy0; dy <= dy1; ++dy)
               for (int dx = dx0; dx <= dx1; ++dx)
-                if (dy | dx) store4(rec + (int64_t)dy * a.dst_wp + dx, &vv[cc][4 * qq]);
+                if (dy | dx) store4(rec + (int64_t)dy * a.dst_wp + dx, &vv[r][4 * qq]);
           }
         }
       }
     }
     if constexpr (EPI == RRIN_EPI_LEAKY_POOL) {
-      // rows 0 and 1 of a pool pair sit in waves yw and yw ^ 1: each wave parks its two columns,
-      // the row-0 wave writes avg = 0.25 ((Y00 + Y10) + (Y01 + Y11))
-      __syncthreads();  // every read of the Q exchange done
+      // a pool pair: rows yb, yb + 1 in this lane, columns x, x + 1 in lanes xo, xo ^ 1 (DPP
+      // quad_perm [1, 0, 3, 2]); the even lane writes avg = 0.25 ((Y00 + Y10) + (Y01 + Y11))
+      const int yp = yb;
+      uint4* pdst = a.pool_hi + (int64_t)img * a.pool_img;
 #pragma unroll
-      for (int cc = 0; cc < 2; ++cc)
+      for (int qq = 0; qq < 4; ++qq) {
+        float s4[4];
 #pragma unroll
-        for (int qq = 0; qq < 4; ++qq) {
-          w42f4 g;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) g[e] = vv[cc][4 * qq + e];
-          X[((yw * 2 + cc) * 4 + qq) * 64 + lane] = g;
+        for (int e = 0; e < 4; ++e) {
+          const float col = vv[0][4 * qq + e] + vv[1][4 * qq + e];
+          const float nb = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(col), 0xB1, 0xF, 0xF, false));
+          s4[e] = 0.25f * (col + nb);
         }
-      __syncthreads();
-      if (r == 0) {
-        const int xp = x0 + 4 * pc + 2 * cp, yp = y0 + 2 * pr;
-        uint4* pdst = a.pool_hi + (int64_t)img * a.pool_img;
-#pragma unroll
-        for (int qq = 0; qq < 4; ++qq) {
-          const w42f4 y00 = X[((yw * 2 + 0) * 4 + qq) * 64 + lane];
-          const w42f4 y01 = X[((yw * 2 + 1) * 4 + qq) * 64 + lane];
-          const w42f4 y10 = X[(((yw + 1) * 2 + 0) * 4 + qq) * 64 + lane];
-          const w42f4 y11 = X[(((yw + 1) * 2 + 1) * 4 + qq) * 64 + lane];
-          if (cob * 32 + 8 * qq < a.cout && yp < a.h && xp < a.w) {
-            float s4[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) s4[e] = 0.25f * ((y00[e] + y10[e]) + (y01[e] + y11[e]));
-            const int64_t rec =
-                (int64_t)(cob * 8 + 2 * qq + hh) * a.pool_gp + (int64_t)(yp / 2 + 1) * a.pool_wp + xp / 2 + kH8PadLeft;
-            pdst[rec] = make_uint4(__float_as_uint(s4[0]), __float_as_uint(s4[1]), __float_as_uint(s4[2]),
-                                   __float_as_uint(s4[3]));
-          }
+        if ((xo & 1) == 0 && cob * 32 + 8 * qq < a.cout && yp < a.h && x < a.w) {
+          const int64_t rec =
+              (int64_t)(cob * 8 + 2 * qq + hh) * a.pool_gp + (int64_t)(yp / 2 + 1) * a.pool_wp + x / 2 + kH8PadLeft;
+          pdst[rec] = make_uint4(__float_as_uint(s4[0]), __float_as_uint(s4[1]), __float_as_uint(s4[2]),
+                                 __float_as_uint(s4[3]));
         }
       }
     }
