@@ -47,7 +47,7 @@ if [[ $STEPS == *prof* ]]; then
   run prof 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --cpu-baseline off --no-alt
   python3 tools/kernel_family_stats.py $O/prof/run_kernel_stats.csv $O/prof/run_kernel_trace.csv auto conv3x3_winoc42_kernel conv3x3_winoq_kernel --ms-per-step $(msps $O/prof.log) > $O/kernel_family.txt 2>&1; echo "family rc=$?"; tail -4 $O/kernel_family.txt
   run prof_c3 300 rocprofv3 --kernel-trace --stats -d $O/prof_c3 -o run --output-format csv -- python3 bench.py --height 736 --width 1280 --batch 4 --precision fp16 --steps 5 --warmup 2 --cpu-baseline off --no-alt
-  python3 tools/kernel_family_stats.py $O/prof_c3/run_kernel_stats.csv $O/prof_c3/run_kernel_trace.csv auto conv3x3_h8_kernel conv_block0_h8_kernel conv3x3_winoh_kernel --parts 4 --ms-per-step $(msps $O/prof_c3.log) > $O/kernel_family_c3.txt 2>&1; echo "family c3 rc=$?"; tail -5 $O/kernel_family_c3.txt
+  python3 tools/kernel_family_stats.py $O/prof_c3/run_kernel_stats.csv $O/prof_c3/run_kernel_trace.csv auto conv3x3_h8_kernel conv_block0_h8_kernel conv3x3_winoh_kernel --parts 2 --ms-per-step $(msps $O/prof_c3.log) > $O/kernel_family_c3.txt 2>&1; echo "family c3 rc=$?"; tail -5 $O/kernel_family_c3.txt
 fi
 if [[ $STEPS == *sq* ]]; then
   B2="python3 bench.py --steps 2 --warmup 1 --cpu-baseline off --no-prof --no-alt"
