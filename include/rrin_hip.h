@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define RRIN_ABI_VERSION 18
+#define RRIN_ABI_VERSION 19
 
 #define RRIN_OK 0
 #define RRIN_E_SHAPE (-1)     /* H or W not a multiple of 16, or N < 1          */
@@ -282,6 +282,11 @@ int64_t rrin_conv_h8_ring_floats(const rrin_conv_h8_desc* d, int64_t* cnt_ints);
  * rrin_pack_conv3x3_wino42; cin % 8 == 0 or tail_finite; no split-K, no ring fold, the
  * ring_full fix-up as a second launch. */
 int rrin_conv_h8_cfg_wino(int32_t cfg);
+/* ABI 19: kind 14's tile geometry, process-wide: 0 (default) picks per launch the one needing
+ * fewer rounds of 512 resident workgroups, 1 always 32 px x 8 rows, 2 always 16 px x 16 rows.
+ * Both compute every output from the same patch with the same arithmetic: the outputs are the
+ * same bits whatever the policy.  Returns the previous policy, RRIN_E_ARG outside 0-2. */
+int rrin_conv_h8_set_wino42_geom(int32_t mode);
 
 /* F32R packing: [co_block][chunk of 8 ci][tap][half][bm][4] fp32 (half hh holds
  * input channels chunk*8 + 4*hh .. +3), unscaled; pass as whi (wlo NULL,

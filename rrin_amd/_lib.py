@@ -9,7 +9,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-ABI_VERSION = 18
+ABI_VERSION = 19
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "librrin_hip.so")
 # A/B sessions only (tools/sessions/): another build of the same library, e.g. ab/librrin_hip_X.so
 if os.environ.get("RRIN_LIB_AB"):
@@ -175,6 +175,7 @@ SIGNATURES = {
     "rrin_pack_conv3x3_wino": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p,
                                          C.c_void_p]),
     "rrin_pack_conv3x3_wino42_floats": (C.c_int64, [C.c_int32, C.c_int32]),
+    "rrin_conv_h8_set_wino42_geom": (C.c_int, [C.c_int32]),
     "rrin_pack_conv3x3_wino42": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p,
                                            C.c_void_p]),
     "rrin_pack_conv3x3_wino_h8_halves": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32]),

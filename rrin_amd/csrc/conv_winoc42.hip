@@ -34,9 +34,22 @@ namespace rrin {
 typedef float w42f16 __attribute__((ext_vector_type(16)));
 typedef float w42f4 __attribute__((ext_vector_type(4)));
 
+// Tile geometry PCW: 8 -> 32 px x 8 rows (8 x 4 patches), 4 -> 16 px x 16 rows (4 x 8 patches).
+// Every output comes from the same patch, transforms and MFMA column arithmetic in both, so the
+// geometry changes no bit of the result (tests/test_gpu_wino42.py); launch_winoc42 picks the one
+// with fewer workgroup rounds (the 16 x 16 tile fits the level-4 grids, 80 x 45 at 1280 x 720).
+template <int PCW_>
 struct W42 {
-  static constexpr int TH = 8;
-  static constexpr int RW = 36;                     // LDS slots per raw row (34 columns + 2 unused)
+  static constexpr int PCW = PCW_;                  // patch columns per tile
+  static constexpr int PRW = 32 / PCW;              // patch rows per tile
+  static constexpr int TW = 4 * PCW;                // output columns
+  static constexpr int TH = 2 * PRW;                // output rows
+  static constexpr int RC = TW + 2;                 // raw columns
+  static constexpr int WM = (RC + 3) / 4;           // slots per column residue (w42_slot)
+  // LDS slots per raw row: >= 4 WM, and 2 RW = 8 (PCW 8) or 4 / 12 (PCW 4) mod 16 records so a
+  // ds_read_b128 group of 16 lanes (PCW columns x 16 / PCW rows) covers the 64 banks once
+  static constexpr int RW = PCW == 8 ? 36 : 22;
+  static_assert(RW >= 4 * WM, "raw row slots");
   static constexpr int RG = (TH + 2) * RW;          // per record group
   static constexpr int RAW = 2 * RG;                // per chunk (2 groups)
   static constexpr int PIECES = (RAW + 255) / 256;  // DMA pieces per thread
@@ -46,27 +59,28 @@ struct W42 {
   static constexpr int XREC = 4 * 16 * XP;          // output-transform exchange: 4 waves x 16 records
   static constexpr size_t LDS = (size_t)(NS * STAGE > XREC ? NS * STAGE : XREC) * 16;
 };
-static_assert(W42::LDS == kWinoC42Lds, "LDS size (common.hpp)");
-static_assert(2 * W42::LDS <= 160 * 1024, "two blocks per CU");
+static_assert(W42<8>::LDS == kWinoC42Lds && W42<4>::LDS == kWinoC42Lds, "LDS size (common.hpp)");
+static_assert(2 * kWinoC42Lds <= 160 * 1024, "two blocks per CU");
 
-// LDS slot of raw column col (0..33) in its row: the 8 patch columns 4 pc + k of one k are
-// consecutive slots, so a ds_read_b128 lane group (patches of 2 rows x 4 columns and their
-// neighbours, rows 72 records apart) covers the 64 banks once
-__device__ constexpr int w42_slot(int col) { return (col & 3) * 9 + (col >> 2); }
+// LDS slot of raw column col (0 .. RC - 1) in its row: the PCW patch columns 4 pc + k of one k
+// are consecutive slots, so a ds_read_b128 lane group (16 patches and their neighbours) covers
+// the 64 banks once
+template <int WM>
+__device__ constexpr int w42_slot(int col) { return (col & 3) * WM + (col >> 2); }
 
 __device__ inline __amdgpu_buffer_rsrc_t w42_rsrc(const void* base) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
 }
 
-template <int EPI>
+template <int EPI, int PCW>
 __global__ __launch_bounds__(256, 2) void conv3x3_winoc42_kernel(ConvH8Args a) {
-  using G = W42;
-  constexpr int TH = G::TH, RG = G::RG, RW = G::RW, STAGE = G::STAGE, P = G::PIECES;
+  using G = W42<PCW>;
+  constexpr int TH = G::TH, TW = G::TW, RG = G::RG, RW = G::RW, STAGE = G::STAGE, P = G::PIECES, WM = G::WM;
   extern __shared__ __attribute__((aligned(16))) uint4 smem4[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int yw = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int j = lane & 31, hh = lane >> 5;
-  const int pc = j & 7, pr = j >> 3;
+  const int pc = j % PCW, pr = j / PCW;
   int bid;
   {  // XCD-aware bijective remap (conv_mfma.hip): an XCD's workgroups are consecutive tiles
     const int nwg = (int)gridDim.x, q = nwg >> 3, r = nwg & 7;
@@ -85,25 +99,28 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winoc42_kernel(ConvH8Args a) {
     const int cg = min(cpg, a.co_blocks - g * cpg);
     cob = g * cpg + r % cg;
     int t = r / cg;
-    x0 = (t % a.tiles_x) * 32;
+    x0 = (t % a.tiles_x) * TW;
     t /= a.tiles_x;
     y0 = (t % a.tiles_y) * TH;
     img = t / a.tiles_y;
   }
 
-  // ---- raw tile: rows y0 - 1 .. y0 + TH, cols x0 - 1 .. x0 + 32 of the chunk's two record
+  // ---- raw tile: rows y0 - 1 .. y0 + TH, cols x0 - 1 .. x0 + TW of the chunk's two record
   // groups, buffer_load ... lds from a per-chunk base; slots past the tile re-read record 0
   const uint4* tbase = a.src_hi + (int64_t)img * a.src_img + (int64_t)y0 * a.src_wp + x0 + (kH8PadLeft - 1);
-  uint32_t voff[P];
+  // (a fixed bound: an array sized by the dependent P and captured by the lambda below drops the
+  // kernel's host stub without a diagnostic -- hipcc 7.2)
+  static_assert(P <= 4, "DMA pieces");
+  uint32_t voff[4];
 #pragma unroll
   for (int it = 0; it < P; ++it) {
     const int idx = tid + 256 * it;
     const int g = idx >= RG ? 1 : 0;
     const int rem = idx < G::RAW ? idx - g * RG : 0;
     const int r = rem / RW, pos = rem - r * RW;
-    const int m = pos / 9, q = pos - m * 9;
+    const int m = pos / WM, q = pos - m * WM;
     const int col = 4 * q + m;
-    const bool ok = idx < G::RAW && col < 34;
+    const bool ok = idx < G::RAW && m < 4 && col < G::RC;
     voff[it] = ok ? (uint32_t)((int64_t)g * a.src_gp + (int64_t)r * a.src_wp + col) * 16u : 0u;
   }
   const int64_t chunk_stride = 2 * a.src_gp;
@@ -143,8 +160,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winoc42_kernel(ConvH8Args a) {
     const uint4* rw = smem4 + s * STAGE;
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
-      d[2 * k] = __builtin_bit_cast(w42f4, rw[oa + w42_slot(k)]);
-      d[2 * k + 1] = __builtin_bit_cast(w42f4, rw[ob + w42_slot(k)]);
+      d[2 * k] = __builtin_bit_cast(w42f4, rw[oa + w42_slot<WM>(k)]);
+      d[2 * k + 1] = __builtin_bit_cast(w42f4, rw[ob + w42_slot<WM>(k)]);
     }
   };
   w42f4 t[6];
@@ -263,9 +280,10 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winoc42_kernel(ConvH8Args a) {
   // ---- output transform: Q[c] = A^T_x row c of this wave's six points, 16 records per lane
   // (record k: values 4 k .. 4 k + 3 of c = k >> 2) into X[wave][record][lane] (pitch XP = 65
   // records: the gather below reads 16 distinct 4-bank slots per ds_read_b128 lane group).  Wave
-  // yw then finishes patch row yw: lane (xo = lane & 31, hh) takes pixel column x0 + xo (patch
-  // xo >> 2, column xo & 3) of output rows y0 + 2 yw and + 1 from the four waves' Q with kind 6's
-  // A^T_y, so each store instruction writes 32 consecutive pixels of a record group (the
+  // yw then finishes patch row prw = yw (PCW 8; PCW 4: rows 2 yw and 2 yw + 1 in lanes 0-15 and
+  // 16-31): lane (xo, hh) takes pixel column x0 + xo (patch xo >> 2, column xo & 3) of output rows
+  // y0 + 2 prw and + 1 from the four waves' Q with kind 6's A^T_y, so each store instruction
+  // writes runs of TW consecutive pixels of a record group (the
   // patch-per-lane layout wrote 16 B of every 64 B: the stores were a quarter of a short-K
   // tile's time)
   constexpr int XP = G::XP;
@@ -285,8 +303,10 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winoc42_kernel(ConvH8Args a) {
     X[(yw * 16 + k) * XP + lane] = g;
   }
   __syncthreads();
-  const int xo = lane & 31, cx = xo & 3;
-  const int src = (xo >> 2) + 8 * yw + 32 * hh;  // the lane of the MFMA layout holding this patch
+  constexpr int NPR = 32 / TW;  // patch rows a wave finishes
+  const int xo = lane & (TW - 1), cx = xo & 3;
+  const int prw = yw * NPR + (NPR == 1 ? 0 : (lane >> 4) & 1);
+  const int src = (xo >> 2) + PCW * prw + 32 * hh;  // the lane of the MFMA layout holding this patch
   float yv[2][16];                               // rows 0 / 1 of the patch row, 16 channels
 #pragma unroll
   for (int k4 = 0; k4 < 4; ++k4) {
@@ -305,7 +325,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winoc42_kernel(ConvH8Args a) {
   auto store4 = [&](int64_t rec, const float* vv) {
     dst[rec] = make_uint4(__float_as_uint(vv[0]), __float_as_uint(vv[1]), __float_as_uint(vv[2]), __float_as_uint(vv[3]));
   };
-  const int x = x0 + xo, yb = y0 + 2 * yw;
+  const int x = x0 + xo, yb = y0 + 2 * prw;
   if constexpr (EPI == RRIN_EPI_SUBPIXEL) {
     const int HH = 2 * a.h, WW = 2 * a.w, creal = a.cout >> 2;
 #pragma unroll
@@ -380,15 +400,21 @@ __global__ __launch_bounds__(256, 2) void conv3x3_winoc42_kernel(ConvH8Args a) {
   }
 }
 
-template <int EPI>
+template <int EPI, int PCW>
 static int launch_winoc42_k(const ConvH8Args& a, hipStream_t st) {
-  auto k = conv3x3_winoc42_kernel<EPI>;
+  auto k = conv3x3_winoc42_kernel<EPI, PCW>;
   static LdsAttr attr;
-  if (int e = attr.ensure((const void*)k, (int)W42::LDS, st)) return e;
+  if (int e = attr.ensure((const void*)k, (int)kWinoC42Lds, st)) return e;
   const int64_t grid = (int64_t)a.co_blocks * a.tiles_x * a.tiles_y * a.n;
-  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256), W42::LDS, st, a);
+  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256), kWinoC42Lds, st, a);
   return hip_code(hipGetLastError());
 }
+
+// geometry policy (rrin_conv_h8_set_wino42_geom): 0 auto, 1 32 x 8 tiles, 2 16 x 16 tiles
+#ifndef RRIN_WINO42_GEOM_DEFAULT
+#define RRIN_WINO42_GEOM_DEFAULT 0  // A/B builds (tools/build_wino_variant.sh): another start policy
+#endif
+static std::atomic<int> g_wino42_geom{RRIN_WINO42_GEOM_DEFAULT};
 
 // co-block groups whose U fits kWinoCUGroupBytes of an XCD's L2 (as launch_winoc)
 #ifndef RRIN_WINO42_UGROUP_KB
@@ -403,12 +429,29 @@ int launch_winoc42(const ConvH8Args& a, int epi, hipStream_t st) {
     while (2 * g < a.co_blocks && 2 * g * per_cob <= (int64_t)RRIN_WINO42_UGROUP_KB * 1024) g *= 2;
     b.cob_group = g;
   }
-  switch (epi) {
-    case RRIN_EPI_LINEAR: return launch_winoc42_k<RRIN_EPI_LINEAR>(b, st);
-    case RRIN_EPI_LEAKY: return launch_winoc42_k<RRIN_EPI_LEAKY>(b, st);
-    case RRIN_EPI_LEAKY_POOL: return launch_winoc42_k<RRIN_EPI_LEAKY_POOL>(b, st);
-    case RRIN_EPI_LEAKY_REP: return launch_winoc42_k<RRIN_EPI_LEAKY_REP>(b, st);
-    case RRIN_EPI_SUBPIXEL: return launch_winoc42_k<RRIN_EPI_SUBPIXEL>(b, st);
+  // the 16 x 16 tile when it needs fewer rounds of the 512 resident workgroups (two per CU):
+  // 1280 x 720's level 4 (80 x 45) is 576 tiles of 32 x 8 (1.1 rounds, 28 % of the area past
+  // the image) but 480 of 16 x 16; elsewhere the 32 x 8 tile (10 raw rows per 8, not 18 per 16)
+  const int64_t per_tile = (int64_t)a.co_blocks * a.n;
+  const int64_t wide = per_tile * a.tiles_x * a.tiles_y;
+  const int64_t tall = per_tile * ((a.w + 15) / 16) * ((a.h + 15) / 16);
+  const int mode = g_wino42_geom.load(std::memory_order_relaxed);
+  const bool use_tall = mode == 2 || (mode == 0 && (tall + 511) / 512 < (wide + 511) / 512);
+  if (use_tall) {
+    b.tiles_x = (a.w + 15) / 16;
+    b.tiles_y = (a.h + 15) / 16;
+  }
+  switch (epi * 2 + (use_tall ? 1 : 0)) {
+    case 2 * RRIN_EPI_LINEAR: return launch_winoc42_k<RRIN_EPI_LINEAR, 8>(b, st);
+    case 2 * RRIN_EPI_LINEAR + 1: return launch_winoc42_k<RRIN_EPI_LINEAR, 4>(b, st);
+    case 2 * RRIN_EPI_LEAKY: return launch_winoc42_k<RRIN_EPI_LEAKY, 8>(b, st);
+    case 2 * RRIN_EPI_LEAKY + 1: return launch_winoc42_k<RRIN_EPI_LEAKY, 4>(b, st);
+    case 2 * RRIN_EPI_LEAKY_POOL: return launch_winoc42_k<RRIN_EPI_LEAKY_POOL, 8>(b, st);
+    case 2 * RRIN_EPI_LEAKY_POOL + 1: return launch_winoc42_k<RRIN_EPI_LEAKY_POOL, 4>(b, st);
+    case 2 * RRIN_EPI_LEAKY_REP: return launch_winoc42_k<RRIN_EPI_LEAKY_REP, 8>(b, st);
+    case 2 * RRIN_EPI_LEAKY_REP + 1: return launch_winoc42_k<RRIN_EPI_LEAKY_REP, 4>(b, st);
+    case 2 * RRIN_EPI_SUBPIXEL: return launch_winoc42_k<RRIN_EPI_SUBPIXEL, 8>(b, st);
+    case 2 * RRIN_EPI_SUBPIXEL + 1: return launch_winoc42_k<RRIN_EPI_SUBPIXEL, 4>(b, st);
   }
   return RRIN_E_ARG;
 }
@@ -416,6 +459,13 @@ int launch_winoc42(const ConvH8Args& a, int epi, hipStream_t st) {
 }  // namespace rrin
 
 using namespace rrin;
+
+// Kind-14 tile geometry policy (process-wide; results are the same bits either way): 0 auto
+// (fewer workgroup rounds), 1 always 32 x 8, 2 always 16 x 16.  Returns the previous policy.
+extern "C" int rrin_conv_h8_set_wino42_geom(int32_t mode) {
+  if (mode < 0 || mode > 2) return RRIN_E_ARG;
+  return g_wino42_geom.exchange(mode);
+}
 
 // Kind-14 packing: [co block of 32][8-channel chunk][point xi = 6 eta + xi_x][record half][32 co][4 ch],
 // U(eta, xi_x) = sum G2[eta][ky] G4[xi_x][kx] g[ky][kx] in double, rounded once to fp32

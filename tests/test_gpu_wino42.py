@@ -101,3 +101,51 @@ def test_kind14_conv_bitwise_beside_side_stream_conv(gpu):
         torch.cuda.synchronize(gpu)
         bad += sum(int(not torch.equal(o.hi, ref.hi)) for o in outs)
     assert bad == 0, f"{bad}/32 convs differ from the serial result"
+
+
+
+@pytest.fixture
+def geom():
+    """Sets kind 14's tile-geometry policy (rrin_conv_h8_set_wino42_geom) and restores auto."""
+    lib = _lib.lib()
+    yield lambda mode: lib.rrin_conv_h8_set_wino42_geom(mode)
+    lib.rrin_conv_h8_set_wino42_geom(0)
+
+
+@pytest.mark.parametrize("epi", [_lib.EPI_LINEAR, _lib.EPI_LEAKY, _lib.EPI_LEAKY_POOL, _lib.EPI_LEAKY_REP,
+                                 _lib.EPI_SUBPIXEL])
+@pytest.mark.parametrize("n,cin,cout,h,w", [(2, 256, 64, 46, 82), (1, 64, 32, 17, 50), (2, 512, 64, 46, 80)])
+def test_kind14_geometries_bitwise(gpu, geom, epi, n, cin, cout, h, w):
+    """The 32 x 8 and 16 x 16 tiles give the same bits (so the launcher's geometry policy may
+    follow the grid and the batch without breaking batch invariance), on ragged grids, every
+    epilogue; the 16 x 16 result also against float64."""
+    if epi == _lib.EPI_LEAKY_POOL and (h % 2 or w % 2):
+        pytest.skip("pool needs even sizes")
+    torch.manual_seed(cin + h + epi)
+    x = torch.rand(n, cin, h, w, device=gpu) * 2 - 1
+    src = H8Tensor.from_nchw(x, R32)
+    sub = epi == _lib.EPI_SUBPIXEL
+    wt, b = keyed_conv(cin, cout, "geo_sub" if sub else "geo")
+    if sub:
+        replicate_ring(src)
+    outs = []
+    for mode in (1, 2):
+        assert geom(mode) in (0, 1, 2)
+        if sub:
+            dst = subpixel_upconv(src, wt, b, cfg42(), R32, dst=H8Tensor(n, 2 * cout, 2 * h, 2 * w, gpu, R32))
+            outs.append([dst.hi.clone()])
+            continue
+        kw = dict(dst=H8Tensor(n, 2 * cout, h, w, gpu, R32), dst_off=cout) if epi == _lib.EPI_LEAKY_POOL else {}
+        dst, pool = conv_h8(src, wt, b, cfg42(), R32, epi=epi, **kw)
+        outs.append([dst.hi.clone()] + ([pool.hi.clone()] if epi == _lib.EPI_LEAKY_POOL else []))
+    for a_, b_ in zip(*outs):
+        assert torch.equal(a_, b_)
+    if epi == _lib.EPI_LEAKY:
+        ref = ref_conv(x, wt, b, 0.1)
+        np.testing.assert_allclose(dst.to_nchw().cpu().double().numpy(), ref.numpy(), **TOL42)
+
+
+def test_kind14_geometry_policy(gpu, geom):
+    """The setter returns the previous policy and rejects modes outside 0-2."""
+    assert geom(3) < 0 and geom(-1) < 0
+    assert geom(2) == 0 and geom(1) == 2 and geom(0) == 1
