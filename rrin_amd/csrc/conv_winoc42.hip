@@ -18,11 +18,12 @@
 // An output depends only on its 3x3 input footprint (the formulas omit the zero entries), so
 // records past the image (the last tile's rows / columns) never reach a stored output.
 //
-// Tile: BM 32 output channels x 32 px x TH 8 rows = 32 patches (8 columns x 4 rows of 4 x 2).
-// Wave yw (0-3) owns B^T_y row yw (points 6 yw .. 6 yw + 5); lane (j, hh): patch j (column
-// pc = j & 7, row pr = j >> 3) of the MFMA tile, record half hh (channels 4 hh .. + 3 of the
-// 8-channel chunk; MFMA product e contracts channels e and 4 + e).  Per wave and chunk: 24
-// MFMAs, 6 U loads (one record per 4 MFMAs), 12 window reads, ~80 VALU, 3 LDS-DMA pieces.
+// Tile: BM 32 output channels x 32 patches of 4 x 2: 32 px x 8 rows (8 columns x 4 rows of
+// patches) or 16 px x 16 rows (4 x 8; W42<PCW>).  Wave yw (0-3) owns B^T_y row yw (points
+// 6 yw .. 6 yw + 5); lane (j, hh): patch j (column pc = j % PCW, row pr = j / PCW) of the MFMA
+// tile, record half hh (channels 4 hh .. + 3 of the 8-channel chunk; MFMA product e contracts
+// channels e and 4 + e).  Per wave and chunk: 24 MFMAs, 6 U loads (one record per 4 MFMAs),
+// 12 window reads, ~80 VALU, 3 (32 x 8) or 4 (16 x 16) LDS-DMA pieces.
 // U: rrin_pack_conv3x3_wino_cfg for this kind, [cob][chunk][xi 24][hh][32 co][4 ch].
 #include "common.hpp"
 
