@@ -105,6 +105,21 @@ def test_batch_size_bitwise_640x368(gpu, nets, precision):
         net.precision = "fp32"
 
 
+def test_batch_size_bitwise_1280x720_fp32(gpu, nets):
+    """At the headline size kind 14's launcher picks the 16 x 16 tile for the level-4 convs of a
+    two-pair call (480 workgroups, one round) and the 32 x 8 tile for a one-pair call: a pair's
+    bits must still not depend on its batch (the geometries are bitwise equal per output)."""
+    net = nets["stress"]
+    net.precision = "fp32"
+    i0, i1 = synthetic_batch(2, 720, 1280, first_index=60)
+    i0, i1 = i0.to(gpu), i1.to(gpu)
+    eng = net.engine()
+    with torch.no_grad():
+        two = eng.forward(i0, i1, 0.5, streams=1)
+        ones = torch.cat([eng.forward(i0[k:k + 1], i1[k:k + 1], 0.5) for k in range(2)])
+    assert torch.equal(two, ones)
+
+
 @pytest.mark.parametrize("precision", ["fp32_split16", "fp16", "fp32", "fp32_planar"])
 def test_streams_split_is_bitwise(gpu, nets, precision):
     """The batch split over several HIP streams (engine.forward(streams=k)) gives the
