@@ -161,9 +161,9 @@ def parse():
                          "'2,3' or 'none' (engine.WINO42_LEVELS)")
     ap.add_argument("--wino42-min-cin-l0", type=int, default=None,
                     help="A/B: smallest cin of a level-0 conv on kind 14 (engine.WINO42_MIN_CIN_L0)")
-    ap.add_argument("--wino42-geom", type=int, default=None, choices=(0, 1, 2),
-                    help="A/B: kind 14's tile geometry (rrin_conv_h8_set_wino42_geom: 0 auto, 1 32x8, 2 16x16; "
-                         "the same output bits)")
+    ap.add_argument("--wino42-geom", type=int, default=None, choices=(0, 1, 2, 3),
+                    help="A/B: kind 14's tile geometry (rrin_conv_h8_set_wino42_geom: 0 auto, 1 32x8, 2 16x16, "
+                         "3 32x8 one workgroup per tile; the same output bits)")
     ap.add_argument("--wino-kind32", type=int, default=None,
                     help="A/B: Winograd kind of the 32-output-channel convs in the auto mode "
                          "(engine.WINO_KIND32: 3 or 7)")

@@ -283,9 +283,11 @@ int64_t rrin_conv_h8_ring_floats(const rrin_conv_h8_desc* d, int64_t* cnt_ints);
  * ring_full fix-up as a second launch. */
 int rrin_conv_h8_cfg_wino(int32_t cfg);
 /* ABI 19: kind 14's tile geometry, process-wide: 0 (default) picks per launch the one needing
- * fewer rounds of 512 resident workgroups, 1 always 32 px x 8 rows, 2 always 16 px x 16 rows.
- * Both compute every output from the same patch with the same arithmetic: the outputs are the
- * same bits whatever the policy.  Returns the previous policy, RRIN_E_ARG outside 0-2. */
+ * fewer rounds of 512 resident workgroups, and persistent workgroups for short K (<= 8 chunks)
+ * on large grids; 1 always 32 px x 8 rows (persistent where eligible); 2 always 16 px x 16 rows;
+ * 3 always 32 x 8, one workgroup per tile.  Every policy computes each output from the same patch
+ * with the same arithmetic: the outputs are the same bits.  Returns the previous policy,
+ * RRIN_E_ARG outside 0-3. */
 int rrin_conv_h8_set_wino42_geom(int32_t mode);
 
 /* F32R packing: [co_block][chunk of 8 ci][tap][half][bm][4] fp32 (half hh holds

@@ -146,6 +146,39 @@ def test_kind14_geometries_bitwise(gpu, geom, epi, n, cin, cout, h, w):
 
 
 def test_kind14_geometry_policy(gpu, geom):
-    """The setter returns the previous policy and rejects modes outside 0-2."""
-    assert geom(3) < 0 and geom(-1) < 0
-    assert geom(2) == 0 and geom(1) == 2 and geom(0) == 1
+    """The setter returns the previous policy and rejects modes outside 0-3."""
+    assert geom(4) < 0 and geom(-1) < 0
+    assert geom(2) == 0 and geom(3) == 2 and geom(1) == 3 and geom(0) == 1
+
+
+@pytest.mark.parametrize("epi", [_lib.EPI_LINEAR, _lib.EPI_LEAKY, _lib.EPI_LEAKY_POOL, _lib.EPI_LEAKY_REP,
+                                 _lib.EPI_SUBPIXEL])
+@pytest.mark.parametrize("n,cin,cout,h,w", [(2, 64, 32, 360, 640), (2, 32, 64, 183, 650), (1, 8, 32, 720, 1280)])
+def test_kind14_persistent_bitwise(gpu, geom, epi, n, cin, cout, h, w):
+    """Short K on a large grid runs persistent workgroups (the next tile's first raw chunks in
+    flight under this tile's epilogue, two-phase exchange): the same bits as one workgroup per
+    tile (policy 3), every epilogue, ragged grids; and the persistent result against float64."""
+    if epi == _lib.EPI_LEAKY_POOL and (h % 2 or w % 2):
+        pytest.skip("pool needs even sizes")
+    torch.manual_seed(cin + h + epi + 7)
+    x = torch.rand(n, cin, h, w, device=gpu) * 2 - 1
+    src = H8Tensor.from_nchw(x, R32)
+    sub = epi == _lib.EPI_SUBPIXEL
+    wt, b = keyed_conv(cin, cout, "pers_sub" if sub else "pers")
+    if sub:
+        replicate_ring(src)
+    outs = []
+    for mode in (3, 0):
+        assert geom(mode) in (0, 1, 2, 3)
+        if sub:
+            dst = subpixel_upconv(src, wt, b, cfg42(), R32, dst=H8Tensor(n, 2 * cout, 2 * h, 2 * w, gpu, R32))
+            outs.append([dst.hi.clone()])
+            continue
+        kw = dict(dst=H8Tensor(n, 2 * cout, h, w, gpu, R32), dst_off=cout) if epi == _lib.EPI_LEAKY_POOL else {}
+        dst, pool = conv_h8(src, wt, b, cfg42(), R32, epi=epi, **kw)
+        outs.append([dst.hi.clone()] + ([pool.hi.clone()] if epi == _lib.EPI_LEAKY_POOL else []))
+    for a_, b_ in zip(*outs):
+        assert torch.equal(a_, b_)
+    if epi == _lib.EPI_LEAKY and n * h * w <= 2 * 360 * 640:
+        ref = ref_conv(x, wt, b, 0.1)
+        np.testing.assert_allclose(dst.to_nchw().cpu().double().numpy(), ref.numpy(), **TOL42)
