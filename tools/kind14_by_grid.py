@@ -16,15 +16,17 @@ def main(path, steps):
         total += d
         name = r["Kernel_Name"]
         if "conv3x3_winoc42_kernel" in name:
-            epi, pcw = name.split("<")[1].split(">")[0].split(",")
-            key = (int(epi), int(pcw), int(r["Grid_Size_X"]) // int(r["Workgroup_Size_X"]))
+            targs = [t.strip() for t in name.split("<")[1].split(">")[0].split(",")]
+            persist = len(targs) > 2 and targs[2] == "true"
+            key = (int(targs[0]), int(targs[1]) * (-1 if persist else 1),
+                   int(r["Grid_Size_X"]) // int(r["Workgroup_Size_X"]))
             agg[key][0] += 1
             agg[key][1] += d
     k14 = sum(v[1] for v in agg.values())
     print(f"all kernels {total / steps:.3f} ms/step (sum of durations), kind 14 {k14 / steps:.3f}")
-    print("epi  PCW  workgroups  launches/step  ms/step  share of kind 14  avg us")
+    print("epi  PCW (-8: persistent)  workgroups  launches/step  ms/step  share of kind 14  avg us")
     for (epi, pcw, wg), (n, ms) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
-        print(f"{epi:3d} {pcw:4d} {wg:11d} {n / steps:14.1f} {ms / steps:8.3f} {ms / k14:17.3f} {1000 * ms / n:7.1f}")
+        print(f"{epi:3d} {pcw:4d}                  {wg:11d} {n / steps:14.1f} {ms / steps:8.3f} {ms / k14:17.3f} {1000 * ms / n:7.1f}")
 
 
 if __name__ == "__main__":
