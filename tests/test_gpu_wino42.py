@@ -67,13 +67,15 @@ def test_kind14_subpixel(gpu, n, cin, cout, sh, sw):
         assert not dst.to_nchw(cout, cout).any()
 
 
-def test_kind14_conv_bitwise_beside_side_stream_conv(gpu):
-    """A kind-14 conv (cin 256, a level-3 grid) repeated 32 times is bitwise the same whether or
-    not an LDS-DMA + MFMA conv loops on another stream: a counted wait that retires the wrong
-    loads reads a stage before it lands and shows up as run-to-run differences."""
+@pytest.mark.parametrize("n,cin,cout,h,w", [(2, 256, 256, 92, 160), (2, 64, 32, 360, 640)])
+def test_kind14_conv_bitwise_beside_side_stream_conv(gpu, n, cin, cout, h, w):
+    """A kind-14 conv (cin 256 on a level-3 grid; cin 64 on a level-1 grid: the persistent
+    short-K launch, its next tile's prologue in flight under the epilogue) repeated 32 times is
+    bitwise the same whether or not an LDS-DMA + MFMA conv loops on another stream: a counted
+    wait that retires the wrong loads reads a stage before it lands and shows up as run-to-run
+    differences."""
     from tests import hip_helpers as H
     from tests.test_gpu_concurrency import side_conv
-    n, cin, cout, h, w = 2, 256, 256, 92, 160
     x = H8Tensor.from_nchw(torch.rand(n, cin, h, w, device=gpu) * 2 - 1, R32)
     wt, b = keyed_conv(cin, cout, "conc42")
     cfg = cfg42()
